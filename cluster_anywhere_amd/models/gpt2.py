@@ -1,0 +1,130 @@
+"""GPT-2 family (124M … 1.5B "XL") built on the gfx950 kernels.
+
+Pre-LN transformer. The residual stream is carried as (h, pending_delta) so every
+``h = h + delta; a = LN(h)`` pair is ONE fused ``add_layer_norm`` kernel. MLP
+bias+GELU is one fused kernel (dbias fused in backward); the LM head is tied to
+the token embedding, the vocab is padded to a multiple of 64 for the GEMMs and
+the fused cross-entropy masks the padding. GEMMs are plain hipBLASLt
+(``F.linear``); attention goes through :func:`ops.attention`.
+
+This is the model behind the headline benchmark (Ray Train
+TorchTrainer DDP GPT-2-XL tokens/s).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import add_layer_norm, attention, bias_gelu, cross_entropy, layer_norm
+
+
+@dataclass
+class GPT2Config:
+    vocab_size: int = 50257
+    n_positions: int = 1024
+    n_layer: int = 48
+    n_head: int = 25
+    n_embd: int = 1600
+    ln_eps: float = 1e-5
+    pad_vocab_to: int = 64
+
+    @property
+    def padded_vocab(self) -> int:
+        m = self.pad_vocab_to
+        return (self.vocab_size + m - 1) // m * m
+
+    @staticmethod
+    def named(name: str) -> "GPT2Config":
+        presets = {
+            "gpt2": dict(n_layer=12, n_head=12, n_embd=768),
+            "gpt2-medium": dict(n_layer=24, n_head=16, n_embd=1024),
+            "gpt2-large": dict(n_layer=36, n_head=20, n_embd=1280),
+            "gpt2-xl": dict(n_layer=48, n_head=25, n_embd=1600),
+            "gpt2-tiny": dict(n_layer=2, n_head=4, n_embd=128, n_positions=128, vocab_size=512),
+        }
+        return GPT2Config(**presets[name])
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        d = cfg.n_embd
+        self.n_head = cfg.n_head
+        self.eps = cfg.ln_eps
+        self.ln1_w = nn.Parameter(torch.ones(d))
+        self.ln1_b = nn.Parameter(torch.zeros(d))
+        self.attn_w = nn.Parameter(torch.empty(3 * d, d))
+        self.attn_b = nn.Parameter(torch.zeros(3 * d))
+        self.proj_w = nn.Parameter(torch.empty(d, d))
+        self.proj_b = nn.Parameter(torch.zeros(d))
+        self.ln2_w = nn.Parameter(torch.ones(d))
+        self.ln2_b = nn.Parameter(torch.zeros(d))
+        self.fc_w = nn.Parameter(torch.empty(4 * d, d))
+        self.fc_b = nn.Parameter(torch.zeros(4 * d))
+        self.fc2_w = nn.Parameter(torch.empty(d, 4 * d))
+        self.fc2_b = nn.Parameter(torch.zeros(d))
+        std = 0.02
+        nn.init.normal_(self.attn_w, std=std)
+        nn.init.normal_(self.fc_w, std=std)
+        nn.init.normal_(self.proj_w, std=std / math.sqrt(2 * cfg.n_layer))
+        nn.init.normal_(self.fc2_w, std=std / math.sqrt(2 * cfg.n_layer))
+
+    def forward(self, h, delta):
+        if delta is None:
+            a = layer_norm(h, self.ln1_w, self.ln1_b, self.eps)
+        else:
+            h, a = add_layer_norm(h, delta, self.ln1_w, self.ln1_b, self.eps)
+        qkv = F.linear(a, self.attn_w, self.attn_b)
+        y = attention(qkv, self.n_head, causal=True)
+        attn_out = F.linear(y, self.proj_w, self.proj_b)
+        h, m = add_layer_norm(h, attn_out, self.ln2_w, self.ln2_b, self.eps)
+        u = bias_gelu(F.linear(m, self.fc_w), self.fc_b)
+        return h, F.linear(u, self.fc2_w, self.fc2_b)
+
+
+class GPT2(nn.Module):
+    def __init__(self, cfg: GPT2Config):
+        super().__init__()
+        self.cfg = cfg
+        self.wte = nn.Parameter(torch.empty(cfg.padded_vocab, cfg.n_embd))
+        self.wpe = nn.Parameter(torch.empty(cfg.n_positions, cfg.n_embd))
+        nn.init.normal_(self.wte, std=0.02)
+        nn.init.normal_(self.wpe, std=0.01)
+        with torch.no_grad():
+            self.wte[cfg.vocab_size :].zero_()
+        self.blocks = nn.ModuleList([Block(cfg) for _ in range(cfg.n_layer)])
+        self.lnf_w = nn.Parameter(torch.ones(cfg.n_embd))
+        self.lnf_b = nn.Parameter(torch.zeros(cfg.n_embd))
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    def hidden(self, idx):
+        B, T = idx.shape
+        h = F.embedding(idx, self.wte) + self.wpe[:T]
+        delta = None
+        for blk in self.blocks:
+            h, delta = blk(h, delta)
+        _, hf = add_layer_norm(h, delta, self.lnf_w, self.lnf_b, self.cfg.ln_eps)
+        return hf
+
+    def forward(self, idx, targets=None):
+        hf = self.hidden(idx)
+        B, T, D = hf.shape
+        logits = F.linear(hf.reshape(B * T, D), self.wte)  # [B*T, Vpad]
+        if targets is None:
+            return logits.view(B, T, -1)[..., : self.cfg.vocab_size]
+        losses = cross_entropy(logits, targets.reshape(-1), self.cfg.vocab_size)
+        valid = (targets.reshape(-1) >= 0).sum().clamp(min=1)
+        return losses.sum() / valid
+
+    def flops_per_token(self, seq_len: int) -> float:
+        """Training FLOPs/token (fwd+bwd = 3x fwd), PaLM-style accounting incl. attention."""
+        c = self.cfg
+        n = sum(p.numel() for n_, p in self.named_parameters() if n_ != "wpe")
+        attn = 12 * c.n_layer * c.n_embd * seq_len / 2  # causal: half the score matrix
+        return 6 * n + attn

@@ -1,0 +1,62 @@
+"""LayerNorm (optionally fused with the residual add) backed by ``layernorm.hip``."""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from ._lib import kernels, use_gpu_kernel
+
+
+def layer_norm_ref(x, g, b, eps=1e-5):
+    return F.layer_norm(x.float(), (x.shape[-1],), g.float(), b.float(), eps).to(x.dtype)
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, res, g, b, eps):
+        C = kernels()
+        x = x.contiguous()
+        if res is not None:
+            res = res.contiguous()
+        y, mean, rstd, s = C.layernorm_fwd(x, res, g, b, eps)
+        saved = s if res is not None else x
+        ctx.save_for_backward(saved, g, mean, rstd)
+        ctx.has_res = res is not None
+        if res is not None:
+            return s, y
+        return y
+
+    @staticmethod
+    def backward(ctx, *grads):
+        C = kernels()
+        saved, g, mean, rstd = ctx.saved_tensors
+        if ctx.has_res:
+            ds, dy = grads
+            dres = ds.contiguous() if ds is not None else None
+        else:
+            (dy,) = grads
+            dres = None
+        if dy is None:
+            dy = torch.zeros_like(saved)
+        dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres)
+        if ctx.has_res:
+            return dx, dx, dg, db, None
+        return dx, None, dg, db, None
+
+
+def layer_norm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e-5):
+    if use_gpu_kernel(x, g, b) and x.dtype == torch.bfloat16:
+        return _LayerNormFn.apply(x, None, g, b, eps)
+    return F.layer_norm(x, (x.shape[-1],), g, b, eps)
+
+
+def add_layer_norm(
+    x: torch.Tensor, res: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e-5
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Return ``(s, LN(s))`` with ``s = x + res`` in one HBM pass."""
+    if use_gpu_kernel(x, res, g, b) and x.dtype == torch.bfloat16:
+        return _LayerNormFn.apply(x, res, g, b, eps)
+    s = x + res
+    return s, F.layer_norm(s, (s.shape[-1],), g, b, eps)

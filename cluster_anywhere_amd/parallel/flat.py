@@ -1,0 +1,115 @@
+"""Flat parameter / gradient storage.
+
+Every trainable parameter of a module becomes a view into ONE contiguous
+compute-dtype buffer (bf16 on MI355X), its ``.grad`` a view into ONE contiguous
+gradient buffer, and the optimizer state (fp32 master, Adam moments) lives in
+matching flat fp32 buffers. This gives:
+
+* one fused AdamW launch for the whole model (``adamw.hip``),
+* gradient buckets that are plain slices of the grad buffer, so the RCCL
+  all-reduce / reduce-scatter reads the grads in place (no pack/unpack copies),
+* one ``memset`` to zero all gradients.
+
+Each parameter slice is aligned to 64 elements (128 B for bf16) so the 16-byte
+vector kernels never straddle two parameters and a per-8-element weight-decay
+mask is exact. The total is padded to a multiple of ``pad_multiple`` so a
+reduce-scatter shards evenly.
+
+Reference parity: the role of ``python/ray/train/torch/train_loop_utils.py:162``
+(`prepare_model` → DDP with `gradient_as_bucket_view`).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+ALIGN = 64
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class ParamSlot:
+    name: str
+    param: torch.nn.Parameter
+    offset: int
+    numel: int
+    decay: bool
+
+
+def default_decay_rule(name: str, p: torch.Tensor) -> bool:
+    """GPT-style: decay matrices/embeddings, not biases or norm gains."""
+    return p.dim() >= 2
+
+
+class FlatParamSpace:
+    def __init__(
+        self,
+        module: torch.nn.Module,
+        dtype: Optional[torch.dtype] = None,
+        grad_dtype: Optional[torch.dtype] = None,
+        pad_multiple: int = ALIGN,
+        decay_rule: Callable[[str, torch.Tensor], bool] = default_decay_rule,
+        master_fp32: bool = True,
+        align: int = ALIGN,
+    ):
+        align = max(ALIGN, align)
+        assert align % 8 == 0
+        seen = set()
+        named = []
+        for n, p in module.named_parameters():
+            if not p.requires_grad or id(p) in seen:
+                continue
+            seen.add(id(p))
+            named.append((n, p))
+        if not named:
+            raise ValueError("module has no trainable parameters")
+        device = named[0][1].device
+        self.dtype = dtype or named[0][1].dtype
+        self.grad_dtype = grad_dtype or self.dtype
+        off = 0
+        self.slots: List[ParamSlot] = []
+        for n, p in named:
+            self.slots.append(ParamSlot(n, p, off, p.numel(), decay_rule(n, p)))
+            off = _round_up(off + p.numel(), align)
+        self.align = align
+        self.numel = _round_up(off, max(pad_multiple, align))
+        self.device = device
+
+        self.param_buffer = torch.zeros(self.numel, dtype=self.dtype, device=device)
+        self.grad_buffer = torch.zeros(self.numel, dtype=self.grad_dtype, device=device)
+        master = torch.zeros(self.numel, dtype=torch.float32, device=device) if master_fp32 else None
+        mask = torch.zeros(self.numel // 8, dtype=torch.uint8, device=device)
+        with torch.no_grad():
+            for s in self.slots:
+                src = s.param.detach()
+                if master is not None:
+                    master[s.offset : s.offset + s.numel].copy_(src.reshape(-1).float())
+                view = self.param_buffer[s.offset : s.offset + s.numel].view_as(src)
+                view.copy_(src)
+                s.param.data = view
+                s.param.grad = self.grad_buffer[s.offset : s.offset + s.numel].view_as(src)
+                if s.decay:
+                    a, b = s.offset // 8, (s.offset + s.numel + 7) // 8
+                    mask[a:b] = 1
+        self.master = master
+        self.wd_mask = mask
+
+    def zero_grad(self):
+        self.grad_buffer.zero_()
+        # autograd may have replaced .grad (e.g. after set_to_none elsewhere): re-bind views
+        for s in self.slots:
+            g = s.param.grad
+            if g is None or g.data_ptr() != self.grad_buffer[s.offset :].data_ptr():
+                s.param.grad = self.grad_buffer[s.offset : s.offset + s.numel].view_as(s.param)
+
+    def param_index(self) -> Dict[int, ParamSlot]:
+        return {id(s.param): s for s in self.slots}
+
+    def sync_params_from_master(self):
+        with torch.no_grad():
+            self.param_buffer.copy_(self.master.to(self.dtype))

@@ -1,0 +1,113 @@
+// Fused bias + GELU(tanh) forward and backward (GPT-2 MLP), bf16 I/O.
+//   fwd: y = gelu(h + b)                               (one read of h, one write)
+//   bwd: dh = dy * gelu'(h + b);  db = sum_rows dh     (dbias fused: per-thread
+//        column accumulators over a row slab -> fp32 partials -> column reduce)
+// 16-byte (8 x bf16) vector accesses everywhere (CDNA guideline 13).
+#include "common.h"
+
+namespace caamd {
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
+  return 0.5f * x * (1.f + t);
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float u = k0 * (x + k1 * x * x * x);
+  const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
+}
+
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16* __restrict__ h,
+                                                            const bf16* __restrict__ b,
+                                                            bf16* __restrict__ y, int64_t nvec,
+                                                            int ncv) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cv = (int)(i % ncv);
+    float hv[8], bv[8], o[8];
+    load8(h + i * 8, hv);
+    if (b) load8(b + cv * 8, bv);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bv[j] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = gelu_tanh(hv[j] + bv[j]);
+    store8(y + i * 8, o);
+  }
+}
+
+// grid: x = ceil(ncv / 256) column tiles, y = row slabs.
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
+    const bf16* __restrict__ dy, const bf16* __restrict__ h, const bf16* __restrict__ b,
+    bf16* __restrict__ dh, float* __restrict__ partial, int rows, int ncv, int rows_per) {
+  const int cv = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cv >= ncv) return;
+  const int N = ncv * 8;
+  float bv[8], acc[8];
+  if (b) load8(b + cv * 8, bv);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    acc[j] = 0.f;
+    if (!b) bv[j] = 0.f;
+  }
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(rows, r0 + rows_per);
+  for (int r = r0; r < r1; ++r) {
+    const size_t off = (size_t)r * N + cv * 8;
+    float hv[8], dv[8], o[8];
+    load8(h + off, hv);
+    load8(dy + off, dv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = dv[j] * gelu_tanh_grad(hv[j] + bv[j]);
+      acc[j] += o[j];
+    }
+    store8(dh + off, o);
+  }
+  if (partial) {
+    float* p = partial + (size_t)blockIdx.y * N + cv * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) p[j] = acc[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void colsum_f32_to_bf16_kernel(const float* __restrict__ partial,
+                                                                 int nblk, int ncol,
+                                                                 bf16* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  float acc = 0.f;
+  for (int r = 0; r < nblk; ++r) acc += partial[(size_t)r * ncol + c];
+  out[c] = (bf16)acc;
+}
+
+void bias_gelu_fwd_launch(const bf16* h, const bf16* b, bf16* y, int64_t rows, int N,
+                          hipStream_t st) {
+  const int64_t nvec = rows * (int64_t)N / 8;
+  hipLaunchKernelGGL(bias_gelu_fwd_kernel, dim3(ew_grid(nvec, 256)), dim3(256), 0, st, h, b, y,
+                     nvec, N / 8);
+}
+
+int bias_gelu_bwd_slabs(int rows) {
+  int s = (rows + 63) / 64;  // 64 rows per slab
+  return s < 1 ? 1 : s;
+}
+
+void bias_gelu_bwd_launch(const bf16* dy, const bf16* h, const bf16* b, bf16* dh, float* partial,
+                          bf16* db, int rows, int N, hipStream_t st) {
+  const int ncv = N / 8;
+  const int slabs = bias_gelu_bwd_slabs(rows);
+  const int rows_per = (rows + slabs - 1) / slabs;
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((ncv + 255) / 256, slabs), dim3(256), 0, st, dy, h,
+                     b, dh, partial, rows, ncv, rows_per);
+  if (db)
+    hipLaunchKernelGGL(colsum_f32_to_bf16_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
+                       partial, slabs, N, db);
+}
+
+}  // namespace caamd

@@ -1,0 +1,297 @@
+// Python bindings for the gfx950 kernels (torch tensors in, HIP launches on the
+// current torch HIP stream out). Every entry point validates device, dtype,
+// contiguity and shape on the host BEFORE launching, so a bad call raises a
+// Python error instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+namespace caamd {
+typedef __bf16 bf16;
+void ln_fwd_launch(const bf16*, const bf16*, bf16*, const bf16*, const bf16*, bf16*, float*, float*,
+                   int, int, float, hipStream_t);
+void ln_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, const float*, const bf16*,
+                   bf16*, float*, bf16*, bf16*, int, int, hipStream_t);
+int ln_nv_for(int D);
+int ln_bwd_num_blocks(int rows);
+void bias_gelu_fwd_launch(const bf16*, const bf16*, bf16*, int64_t, int, hipStream_t);
+void bias_gelu_bwd_launch(const bf16*, const bf16*, const bf16*, bf16*, float*, bf16*, int, int,
+                          hipStream_t);
+int bias_gelu_bwd_slabs(int rows);
+void xent_fwd_launch(const bf16*, const int64_t*, float*, float*, int, int, int, hipStream_t);
+void xent_bwd_launch(bf16*, const int64_t*, const float*, const float*, int, int, int, hipStream_t);
+void grad_sumsq_launch(const void*, bool, int64_t, float*, hipStream_t);
+void adamw_launch(float*, float*, float*, const void*, bool, bf16*, int64_t, float, float, float,
+                  float, float, float, float, float, float, const float*, const uint8_t*,
+                  hipStream_t);
+void gae_launch(const float*, const float*, const float*, float*, float*, int, int, float, float,
+                hipStream_t);
+void vtrace_launch(const float*, const float*, const float*, const float*, const float*, float*,
+                   float*, int, int, float, float, hipStream_t);
+}  // namespace caamd
+
+using at::Tensor;
+
+#define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype")
+#define CHECK_BF16(t) \
+  CHECK_GPU(t);       \
+  CHECK_CONTIG(t);    \
+  CHECK_DT(t, at::kBFloat16)
+#define CHECK_F32(t) \
+  CHECK_GPU(t);      \
+  CHECK_CONTIG(t);   \
+  CHECK_DT(t, at::kFloat)
+
+static inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+static inline caamd::bf16* bp(const Tensor& t) { return reinterpret_cast<caamd::bf16*>(t.data_ptr()); }
+static inline caamd::bf16* bp_opt(const c10::optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? bp(*t) : nullptr;
+}
+
+// ---- LayerNorm -------------------------------------------------------------
+// returns (y, mean, rstd, s) where s = x + res when res is given (else undefined)
+std::vector<Tensor> layernorm_fwd(const Tensor& x, const c10::optional<Tensor>& res,
+                                  const Tensor& g, const Tensor& b, double eps) {
+  CHECK_BF16(x);
+  CHECK_BF16(g);
+  CHECK_BF16(b);
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0, "layernorm: D must be a multiple of 8");
+  TORCH_CHECK(caamd::ln_nv_for(D) > 0, "layernorm: D too large (max 4096)");
+  TORCH_CHECK(g.numel() == D && b.numel() == D, "layernorm: weight/bias size mismatch");
+  const int rows = (int)(x.numel() / D);
+  Tensor s;
+  if (res.has_value() && res->defined()) {
+    CHECK_BF16(*res);
+    TORCH_CHECK(res->sizes() == x.sizes(), "layernorm: residual shape mismatch");
+    s = at::empty_like(x);
+  }
+  auto y = at::empty_like(x);
+  auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  if (rows > 0)
+    caamd::ln_fwd_launch(bp(x), bp_opt(res), s.defined() ? bp(s) : nullptr, bp(g), bp(b), bp(y),
+                         mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, D, (float)eps,
+                         cur_stream());
+  return {y, mean, rstd, s};
+}
+
+// returns (dx, dg, db); dx += dres when dres given
+std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& g,
+                                  const Tensor& mean, const Tensor& rstd,
+                                  const c10::optional<Tensor>& dres) {
+  CHECK_BF16(dy);
+  CHECK_BF16(x);
+  CHECK_BF16(g);
+  CHECK_F32(mean);
+  CHECK_F32(rstd);
+  TORCH_CHECK(dy.sizes() == x.sizes(), "layernorm_bwd: dy/x shape mismatch");
+  const int D = (int)x.size(-1);
+  const int rows = (int)(x.numel() / D);
+  TORCH_CHECK(mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: stats size");
+  if (dres.has_value() && dres->defined()) {
+    CHECK_BF16(*dres);
+    TORCH_CHECK(dres->sizes() == x.sizes(), "layernorm_bwd: dres shape mismatch");
+  }
+  auto dx = at::empty_like(x);
+  auto dg = at::empty_like(g);
+  auto db = at::empty_like(g);
+  const int nblk = caamd::ln_bwd_num_blocks(rows);
+  auto partial = at::empty({nblk, 2, D}, x.options().dtype(at::kFloat));
+  if (rows > 0)
+    caamd::ln_bwd_launch(bp(dy), bp(x), bp(g), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                         bp_opt(dres), bp(dx), partial.data_ptr<float>(), bp(dg), bp(db), rows, D,
+                         cur_stream());
+  else {
+    dg.zero_();
+    db.zero_();
+  }
+  return {dx, dg, db};
+}
+
+// ---- bias + GELU -------------------------------------------------------------
+Tensor bias_gelu_fwd(const Tensor& h, const c10::optional<Tensor>& b) {
+  CHECK_BF16(h);
+  const int N = (int)h.size(-1);
+  TORCH_CHECK(N % 8 == 0, "bias_gelu: last dim must be a multiple of 8");
+  if (b.has_value() && b->defined()) {
+    CHECK_BF16(*b);
+    TORCH_CHECK(b->numel() == N, "bias_gelu: bias size mismatch");
+  }
+  auto y = at::empty_like(h);
+  const int64_t rows = h.numel() / N;
+  if (rows > 0) caamd::bias_gelu_fwd_launch(bp(h), bp_opt(b), bp(y), rows, N, cur_stream());
+  return y;
+}
+
+std::vector<Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& h,
+                                  const c10::optional<Tensor>& b) {
+  CHECK_BF16(dy);
+  CHECK_BF16(h);
+  TORCH_CHECK(dy.sizes() == h.sizes(), "bias_gelu_bwd: shape mismatch");
+  const int N = (int)h.size(-1);
+  TORCH_CHECK(N % 8 == 0, "bias_gelu_bwd: last dim must be a multiple of 8");
+  const int64_t rows64 = h.numel() / N;
+  TORCH_CHECK(rows64 < (1ll << 31), "bias_gelu_bwd: too many rows");
+  const int rows = (int)rows64;
+  const bool has_b = b.has_value() && b->defined();
+  if (has_b) CHECK_BF16(*b);
+  auto dh = at::empty_like(h);
+  Tensor db, partial;
+  if (has_b) {
+    db = at::empty_like(*b);
+    partial = at::empty({caamd::bias_gelu_bwd_slabs(rows), N}, h.options().dtype(at::kFloat));
+  }
+  if (rows > 0)
+    caamd::bias_gelu_bwd_launch(bp(dy), bp(h), bp_opt(b), bp(dh),
+                                has_b ? partial.data_ptr<float>() : nullptr,
+                                has_b ? bp(db) : nullptr, rows, N, cur_stream());
+  return {dh, db};
+}
+
+// ---- cross entropy -----------------------------------------------------------
+// logits [N, stride] bf16 (columns >= V are padding), target [N] int64.
+std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& target, int64_t V) {
+  CHECK_BF16(logits);
+  CHECK_GPU(target);
+  CHECK_CONTIG(target);
+  CHECK_DT(target, at::kLong);
+  TORCH_CHECK(logits.dim() == 2, "xent: logits must be 2-D");
+  const int rows = (int)logits.size(0), stride = (int)logits.size(1);
+  TORCH_CHECK(stride % 8 == 0, "xent: row stride must be a multiple of 8");
+  TORCH_CHECK(V > 0 && V <= stride, "xent: bad vocab size");
+  TORCH_CHECK(target.numel() == rows, "xent: target size mismatch");
+  auto loss = at::empty({rows}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({rows}, logits.options().dtype(at::kFloat));
+  if (rows > 0)
+    caamd::xent_fwd_launch(bp(logits), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                           lse.data_ptr<float>(), rows, (int)V, stride, cur_stream());
+  return {loss, lse};
+}
+
+// In place: logits <- dlogits.
+void xent_bwd_(Tensor& logits, const Tensor& target, const Tensor& lse, const Tensor& dl,
+               int64_t V) {
+  CHECK_BF16(logits);
+  CHECK_F32(lse);
+  CHECK_F32(dl);
+  CHECK_DT(target, at::kLong);
+  const int rows = (int)logits.size(0), stride = (int)logits.size(1);
+  TORCH_CHECK(stride % 8 == 0 && V <= stride, "xent_bwd: bad stride/V");
+  TORCH_CHECK(target.numel() == rows && lse.numel() == rows && dl.numel() == rows,
+              "xent_bwd: size mismatch");
+  if (rows > 0)
+    caamd::xent_bwd_launch(bp(logits), target.data_ptr<int64_t>(), lse.data_ptr<float>(),
+                           dl.data_ptr<float>(), rows, (int)V, stride, cur_stream());
+}
+
+// ---- optimizer ---------------------------------------------------------------
+void grad_sumsq(const Tensor& g, Tensor& out) {
+  CHECK_GPU(g);
+  CHECK_CONTIG(g);
+  CHECK_F32(out);
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat,
+              "grad_sumsq: grad must be bf16 or fp32");
+  TORCH_CHECK(g.numel() % 8 == 0, "grad_sumsq: numel must be a multiple of 8");
+  if (g.numel() > 0)
+    caamd::grad_sumsq_launch(g.data_ptr(), g.scalar_type() == at::kBFloat16, g.numel(),
+                             out.data_ptr<float>(), cur_stream());
+}
+
+void adamw_step(Tensor& p, Tensor& m, Tensor& v, const Tensor& g,
+                const c10::optional<Tensor>& pbf, double lr, double beta1, double beta2,
+                double eps, double wd, int64_t step, double inv_world, double max_norm,
+                const c10::optional<Tensor>& sumsq, const c10::optional<Tensor>& wd_mask) {
+  CHECK_F32(p);
+  CHECK_F32(m);
+  CHECK_F32(v);
+  CHECK_GPU(g);
+  CHECK_CONTIG(g);
+  const int64_t n = p.numel();
+  TORCH_CHECK(m.numel() == n && v.numel() == n && g.numel() == n, "adamw: size mismatch");
+  TORCH_CHECK(n % 8 == 0, "adamw: numel must be a multiple of 8 (pad the flat buffer)");
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 || g.scalar_type() == at::kFloat,
+              "adamw: grad must be bf16 or fp32");
+  if (pbf.has_value() && pbf->defined()) {
+    CHECK_BF16(*pbf);
+    TORCH_CHECK(pbf->numel() == n, "adamw: bf16 copy size mismatch");
+  }
+  const float* ss = nullptr;
+  if (sumsq.has_value() && sumsq->defined()) {
+    CHECK_F32(*sumsq);
+    ss = sumsq->data_ptr<float>();
+  }
+  const uint8_t* mask = nullptr;
+  if (wd_mask.has_value() && wd_mask->defined()) {
+    CHECK_GPU(*wd_mask);
+    CHECK_CONTIG(*wd_mask);
+    CHECK_DT(*wd_mask, at::kByte);
+    TORCH_CHECK(wd_mask->numel() == n / 8, "adamw: wd_mask must have numel/8 entries");
+    mask = wd_mask->data_ptr<uint8_t>();
+  }
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  if (n > 0)
+    caamd::adamw_launch(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                        g.data_ptr(), g.scalar_type() == at::kBFloat16, bp_opt(pbf), n, (float)lr,
+                        (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
+                        (float)inv_world, (float)max_norm, ss, mask, cur_stream());
+}
+
+// ---- RL returns (time-major [T, B], fp32) ----------------------------------------
+std::vector<Tensor> gae(const Tensor& rewards, const Tensor& values, const Tensor& nonterminal,
+                        double gamma, double lam) {
+  CHECK_F32(rewards);
+  CHECK_F32(values);
+  CHECK_F32(nonterminal);
+  TORCH_CHECK(rewards.dim() == 2, "gae: rewards must be [T, B]");
+  const int T = (int)rewards.size(0), B = (int)rewards.size(1);
+  TORCH_CHECK(values.dim() == 2 && values.size(0) == T + 1 && values.size(1) == B,
+              "gae: values must be [T+1, B]");
+  TORCH_CHECK(nonterminal.sizes() == rewards.sizes(), "gae: nonterminal must be [T, B]");
+  auto adv = at::empty_like(rewards), tgt = at::empty_like(rewards);
+  if (T > 0 && B > 0)
+    caamd::gae_launch(rewards.data_ptr<float>(), values.data_ptr<float>(),
+                      nonterminal.data_ptr<float>(), adv.data_ptr<float>(), tgt.data_ptr<float>(),
+                      T, B, (float)gamma, (float)lam, cur_stream());
+  return {adv, tgt};
+}
+
+std::vector<Tensor> vtrace(const Tensor& log_rhos, const Tensor& discounts, const Tensor& rewards,
+                           const Tensor& values, const Tensor& bootstrap, double clip_rho,
+                           double clip_pg_rho) {
+  CHECK_F32(log_rhos);
+  CHECK_F32(discounts);
+  CHECK_F32(rewards);
+  CHECK_F32(values);
+  CHECK_F32(bootstrap);
+  TORCH_CHECK(log_rhos.dim() == 2, "vtrace: inputs must be [T, B]");
+  const int T = (int)log_rhos.size(0), B = (int)log_rhos.size(1);
+  TORCH_CHECK(discounts.sizes() == log_rhos.sizes() && rewards.sizes() == log_rhos.sizes() &&
+                  values.sizes() == log_rhos.sizes(),
+              "vtrace: shape mismatch");
+  TORCH_CHECK(bootstrap.numel() == B, "vtrace: bootstrap must be [B]");
+  auto vs = at::empty_like(values), pg = at::empty_like(values);
+  if (T > 0 && B > 0)
+    caamd::vtrace_launch(log_rhos.data_ptr<float>(), discounts.data_ptr<float>(),
+                         rewards.data_ptr<float>(), values.data_ptr<float>(),
+                         bootstrap.data_ptr<float>(), vs.data_ptr<float>(), pg.data_ptr<float>(),
+                         T, B, (float)clip_rho, (float)clip_pg_rho, cur_stream());
+  return {vs, pg};
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "cluster_anywhere_amd gfx950 HIP kernels";
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("bias_gelu_fwd", &bias_gelu_fwd);
+  m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd_", &xent_bwd_);
+  m.def("grad_sumsq", &grad_sumsq);
+  m.def("adamw_step", &adamw_step);
+  m.def("gae", &gae);
+  m.def("vtrace", &vtrace);
+}
