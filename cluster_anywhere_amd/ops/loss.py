@@ -40,7 +40,12 @@ class _XentFn(torch.autograd.Function):
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor, vocab: int = None) -> torch.Tensor:
     """Per-row loss; ignore_index is any negative target."""
     vocab = vocab or logits.shape[-1]
-    if use_gpu_kernel(logits, target) and logits.dtype == torch.bfloat16 and logits.is_contiguous():
+    if (
+        use_gpu_kernel(logits, target)
+        and logits.dtype == torch.bfloat16
+        and logits.is_contiguous()
+        and logits.shape[-1] % 8 == 0
+    ):
         return _XentFn.apply(logits, target.contiguous().long(), vocab)
     t = target.clone()
     t[t < 0] = -100

@@ -76,15 +76,8 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void colsum_f32_to_bf16_kernel(const float* __restrict__ partial,
-                                                                 int nblk, int ncol,
-                                                                 bf16* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncol) return;
-  float acc = 0.f;
-  for (int r = 0; r < nblk; ++r) acc += partial[(size_t)r * ncol + c];
-  out[c] = (bf16)acc;
-}
+void colsum_bf16_launch(const float* partial, int nrow, int ncol, int split, bf16* o0, bf16* o1,
+                        hipStream_t st);
 
 void bias_gelu_fwd_launch(const bf16* h, const bf16* b, bf16* y, int64_t rows, int N,
                           hipStream_t st) {
@@ -105,9 +98,7 @@ void bias_gelu_bwd_launch(const bf16* dy, const bf16* h, const bf16* b, bf16* dh
   const int rows_per = (rows + slabs - 1) / slabs;
   hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((ncv + 255) / 256, slabs), dim3(256), 0, st, dy, h,
                      b, dh, partial, rows, ncv, rows_per);
-  if (db)
-    hipLaunchKernelGGL(colsum_f32_to_bf16_kernel, dim3((N + 255) / 256), dim3(256), 0, st,
-                       partial, slabs, N, db);
+  if (db) colsum_bf16_launch(partial, slabs, N, N, db, db, st);
 }
 
 }  // namespace caamd

@@ -35,14 +35,26 @@ using at::Tensor;
 #define CHECK_GPU(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_DT(t, dt) TORCH_CHECK((t).scalar_type() == (dt), #t " has wrong dtype")
-#define CHECK_BF16(t) \
-  CHECK_GPU(t);       \
-  CHECK_CONTIG(t);    \
-  CHECK_DT(t, at::kBFloat16)
-#define CHECK_F32(t) \
-  CHECK_GPU(t);      \
-  CHECK_CONTIG(t);   \
-  CHECK_DT(t, at::kFloat)
+#define CHECK_BF16(t)          \
+  do {                         \
+    CHECK_GPU(t);              \
+    CHECK_CONTIG(t);           \
+    CHECK_DT(t, at::kBFloat16); \
+  } while (0)
+#define CHECK_F32(t)       \
+  do {                     \
+    CHECK_GPU(t);          \
+    CHECK_CONTIG(t);       \
+    CHECK_DT(t, at::kFloat); \
+  } while (0)
+
+// Every launch is followed by a check so a rejected launch (bad LDS size,
+// bad grid) raises instead of leaving outputs silently unwritten.
+#define LAUNCH_CHECK()                                                              \
+  do {                                                                              \
+    hipError_t e_ = hipGetLastError();                                              \
+    TORCH_CHECK(e_ == hipSuccess, "HIP kernel launch failed: ", hipGetErrorString(e_)); \
+  } while (0)
 
 static inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 static inline caamd::bf16* bp(const Tensor& t) { return reinterpret_cast<caamd::bf16*>(t.data_ptr()); }
@@ -75,6 +87,7 @@ std::vector<Tensor> layernorm_fwd(const Tensor& x, const c10::optional<Tensor>& 
     caamd::ln_fwd_launch(bp(x), bp_opt(res), s.defined() ? bp(s) : nullptr, bp(g), bp(b), bp(y),
                          mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, D, (float)eps,
                          cur_stream());
+    LAUNCH_CHECK();
   return {y, mean, rstd, s};
 }
 
@@ -100,11 +113,12 @@ std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tenso
   auto db = at::empty_like(g);
   const int nblk = caamd::ln_bwd_num_blocks(rows);
   auto partial = at::empty({nblk, 2, D}, x.options().dtype(at::kFloat));
-  if (rows > 0)
+  if (rows > 0) {
     caamd::ln_bwd_launch(bp(dy), bp(x), bp(g), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                          bp_opt(dres), bp(dx), partial.data_ptr<float>(), bp(dg), bp(db), rows, D,
                          cur_stream());
-  else {
+    LAUNCH_CHECK();
+  } else {
     dg.zero_();
     db.zero_();
   }
@@ -123,6 +137,7 @@ Tensor bias_gelu_fwd(const Tensor& h, const c10::optional<Tensor>& b) {
   auto y = at::empty_like(h);
   const int64_t rows = h.numel() / N;
   if (rows > 0) caamd::bias_gelu_fwd_launch(bp(h), bp_opt(b), bp(y), rows, N, cur_stream());
+  LAUNCH_CHECK();
   return y;
 }
 
@@ -148,6 +163,7 @@ std::vector<Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& h,
     caamd::bias_gelu_bwd_launch(bp(dy), bp(h), bp_opt(b), bp(dh),
                                 has_b ? partial.data_ptr<float>() : nullptr,
                                 has_b ? bp(db) : nullptr, rows, N, cur_stream());
+    LAUNCH_CHECK();
   return {dh, db};
 }
 
@@ -168,6 +184,7 @@ std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& target, int64_t
   if (rows > 0)
     caamd::xent_fwd_launch(bp(logits), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
                            lse.data_ptr<float>(), rows, (int)V, stride, cur_stream());
+    LAUNCH_CHECK();
   return {loss, lse};
 }
 
@@ -185,6 +202,7 @@ void xent_bwd_(Tensor& logits, const Tensor& target, const Tensor& lse, const Te
   if (rows > 0)
     caamd::xent_bwd_launch(bp(logits), target.data_ptr<int64_t>(), lse.data_ptr<float>(),
                            dl.data_ptr<float>(), rows, (int)V, stride, cur_stream());
+    LAUNCH_CHECK();
 }
 
 // ---- optimizer ---------------------------------------------------------------
@@ -198,6 +216,7 @@ void grad_sumsq(const Tensor& g, Tensor& out) {
   if (g.numel() > 0)
     caamd::grad_sumsq_launch(g.data_ptr(), g.scalar_type() == at::kBFloat16, g.numel(),
                              out.data_ptr<float>(), cur_stream());
+    LAUNCH_CHECK();
 }
 
 void adamw_step(Tensor& p, Tensor& m, Tensor& v, const Tensor& g,
@@ -238,6 +257,7 @@ void adamw_step(Tensor& p, Tensor& m, Tensor& v, const Tensor& g,
                         g.data_ptr(), g.scalar_type() == at::kBFloat16, bp_opt(pbf), n, (float)lr,
                         (float)beta1, (float)beta2, (float)eps, (float)wd, (float)bc1, (float)bc2,
                         (float)inv_world, (float)max_norm, ss, mask, cur_stream());
+    LAUNCH_CHECK();
 }
 
 // ---- RL returns (time-major [T, B], fp32) ----------------------------------------
@@ -256,6 +276,7 @@ std::vector<Tensor> gae(const Tensor& rewards, const Tensor& values, const Tenso
     caamd::gae_launch(rewards.data_ptr<float>(), values.data_ptr<float>(),
                       nonterminal.data_ptr<float>(), adv.data_ptr<float>(), tgt.data_ptr<float>(),
                       T, B, (float)gamma, (float)lam, cur_stream());
+    LAUNCH_CHECK();
   return {adv, tgt};
 }
 
@@ -279,7 +300,58 @@ std::vector<Tensor> vtrace(const Tensor& log_rhos, const Tensor& discounts, cons
                          rewards.data_ptr<float>(), values.data_ptr<float>(),
                          bootstrap.data_ptr<float>(), vs.data_ptr<float>(), pg.data_ptr<float>(),
                          T, B, (float)clip_rho, (float)clip_pg_rho, cur_stream());
+    LAUNCH_CHECK();
   return {vs, pg};
+}
+
+// ---- flash attention (packed qkv [B, T, 3*H*D]) ---------------------------------
+namespace caamd {
+void fa_fwd_launch(const bf16*, bf16*, float*, int, int, int, int, int, hipStream_t);
+void fa_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, float*, bf16*, int, int,
+                   int, int, int, hipStream_t);
+}
+
+static void fa_check_qkv(const Tensor& qkv, int64_t H, int& B, int& T, int& D) {
+  CHECK_BF16(qkv);
+  TORCH_CHECK(qkv.dim() == 3, "flash_attn: qkv must be [B, T, 3*H*D]");
+  B = (int)qkv.size(0);
+  T = (int)qkv.size(1);
+  TORCH_CHECK(qkv.size(2) % (3 * H) == 0, "flash_attn: last dim must be 3*H*D");
+  D = (int)(qkv.size(2) / (3 * H));
+  TORCH_CHECK(D == 64 || D == 128, "flash_attn: head dim must be 64 or 128");
+}
+
+std::vector<Tensor> flash_attn_fwd(const Tensor& qkv, int64_t H, bool causal) {
+  int B, T, D;
+  fa_check_qkv(qkv, H, B, T, D);
+  auto out = at::empty({B, T, H * D}, qkv.options());
+  auto lse = at::empty({B, H, T}, qkv.options().dtype(at::kFloat));
+  if (B > 0 && T > 0)
+    caamd::fa_fwd_launch(bp(qkv), bp(out), lse.data_ptr<float>(), B, T, (int)H, D, causal ? 1 : 0,
+                         cur_stream());
+    LAUNCH_CHECK();
+  return {out, lse};
+}
+
+Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, const Tensor& lse,
+                      int64_t H, bool causal) {
+  int B, T, D;
+  fa_check_qkv(qkv, H, B, T, D);
+  CHECK_BF16(out);
+  CHECK_BF16(dout);
+  CHECK_F32(lse);
+  TORCH_CHECK(out.dim() == 3 && out.size(0) == B && out.size(1) == T && out.size(2) == H * D,
+              "flash_attn_bwd: out shape");
+  TORCH_CHECK(dout.sizes() == out.sizes(), "flash_attn_bwd: dout shape");
+  TORCH_CHECK(lse.numel() == (int64_t)B * H * T, "flash_attn_bwd: lse shape");
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty_like(lse);
+  if (B > 0 && T > 0)
+    caamd::fa_bwd_launch(bp(qkv), bp(out), bp(dout), lse.data_ptr<float>(),
+                         delta.data_ptr<float>(), bp(dqkv), B, T, (int)H, D, causal ? 1 : 0,
+                         cur_stream());
+    LAUNCH_CHECK();
+  return dqkv;
 }
 
 PYBIND11_MODULE(_C, m) {
@@ -294,4 +366,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("adamw_step", &adamw_step);
   m.def("gae", &gae);
   m.def("vtrace", &vtrace);
+  m.def("flash_attn_fwd", &flash_attn_fwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd);
 }

@@ -78,33 +78,32 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   }
 }
 
+// 8 waves (512 threads) per block; g lives in LDS (not VGPRs); x/dy are read
+// twice per row (stats pass, then dx pass — the second read hits L1/L2) so only
+// the dgamma/dbeta accumulators occupy registers -> >= 4 waves/SIMD resident.
 template <int NV, bool HAS_DRES>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(
+__global__ __launch_bounds__(512) void ln_bwd_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ g,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const bf16* __restrict__ dres, bf16* __restrict__ dx, float* __restrict__ partial,
     int rows, int D) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // 2*D floats
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // 3*D floats
+  float* red = smem;         // [2D] dgamma | dbeta
+  float* gl = smem + 2 * D;  // [D] gamma
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nchunk = D >> 3;
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) red[i] = 0.f;
-  float gg[NV][8], dg[NV][8], db[NV][8];
+  for (int i = threadIdx.x; i < D; i += blockDim.x) gl[i] = (float)g[i];
+  __syncthreads();
+  float dg[NV][8], db[NV][8];
 #pragma unroll
-  for (int c = 0; c < NV; ++c) {
-    const int ch = lane + c * 64;
-    if (ch < nchunk) load8(g + ch * 8, gg[c]);
+  for (int c = 0; c < NV; ++c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dg[c][j] = 0.f;
-      db[c][j] = 0.f;
-      if (ch >= nchunk) gg[c][j] = 0.f;
-    }
-  }
+    for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
   const float inv_d = 1.f / (float)D;
-  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+  for (int row = blockIdx.x * 8 + wave; row < rows; row += gridDim.x * 8) {
     const size_t base = (size_t)row * D;
     const float mu = mean[row], rs = rstd[row];
-    float xh[NV][8], gdy[NV][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
@@ -115,11 +114,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         load8(dy + base + ch * 8, dv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          xh[c][j] = (xv[j] - mu) * rs;
-          gdy[c][j] = dv[j] * gg[c][j];
-          s1 += gdy[c][j];
-          s2 += gdy[c][j] * xh[c][j];
-          dg[c][j] += dv[j] * xh[c][j];
+          const float xh = (xv[j] - mu) * rs;
+          const float gd = dv[j] * gl[ch * 8 + j];
+          s1 += gd;
+          s2 += gd * xh;
+          dg[c][j] += dv[j] * xh;
           db[c][j] += dv[j];
         }
       }
@@ -129,9 +128,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     for (int c = 0; c < NV; ++c) {
       const int ch = lane + c * 64;
       if (ch < nchunk) {
-        float o[8];
+        float xv[8], dv[8], o[8];
+        load8(x + base + ch * 8, xv);
+        load8(dy + base + ch * 8, dv);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rs * (gdy[c][j] - m1 - xh[c][j] * m2);
+        for (int j = 0; j < 8; ++j)
+          o[j] = rs * (dv[j] * gl[ch * 8 + j] - m1 - (xv[j] - mu) * rs * m2);
         if (HAS_DRES) {
           float t[8];
           load8(dres + base + ch * 8, t);
@@ -142,7 +144,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
     }
   }
-  __syncthreads();
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
     const int ch = lane + c * 64;
@@ -159,17 +160,43 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) out[i] = red[i];
 }
 
-// out[c] = sum_b partial[b][c] for c < ncol; written as bf16 split in two
-// destination arrays (first D columns -> o0, next D -> o1).
-__global__ __launch_bounds__(256) void colsum_to_bf16_kernel(
-    const float* __restrict__ partial, int nblk, int D, bf16* __restrict__ o0,
-    bf16* __restrict__ o1) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * D) return;
+// Column sum of an fp32 [nrow, ncol] slab -> bf16, split at column `split`
+// (columns < split -> o0[c], the rest -> o1[c - split]). One block = 64 columns
+// x 16 waves; wave w sums rows w, w+16, ... with 8 loads in flight; LDS merge.
+__global__ __launch_bounds__(1024) void colsum_bf16_kernel(const float* __restrict__ partial,
+                                                           int nrow, int ncol, int split,
+                                                           bf16* __restrict__ o0,
+                                                           bf16* __restrict__ o1) {
+  __shared__ float red[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 64 + lane;
   float acc = 0.f;
-  for (int b = 0; b < nblk; ++b) acc += partial[(size_t)b * 2 * D + c];
-  if (c < D) o0[c] = (bf16)acc;
-  else o1[c - D] = (bf16)acc;
+  if (c < ncol) {
+    int r = wave;
+    for (; r + 7 * 16 < nrow; r += 8 * 16) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = partial[(size_t)(r + u * 16) * ncol + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; r < nrow; r += 16) acc += partial[(size_t)r * ncol + c];
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < ncol) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) s += red[w][lane];
+    if (c < split) o0[c] = (bf16)s;
+    else o1[c - split] = (bf16)s;
+  }
+}
+
+void colsum_bf16_launch(const float* partial, int nrow, int ncol, int split, bf16* o0, bf16* o1,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((ncol + 63) / 64), dim3(1024), 0, st, partial, nrow,
+                     ncol, split, o0, o1);
 }
 
 template <int NV>
@@ -189,8 +216,8 @@ template <int NV>
 static void ln_bwd_dispatch(const bf16* dy, const bf16* x, const bf16* g, const float* mean,
                             const float* rstd, const bf16* dres, bf16* dx, float* partial,
                             int nblk, int rows, int D, hipStream_t st) {
-  dim3 grid(nblk), block(256);
-  size_t lds = (size_t)2 * D * sizeof(float);
+  dim3 grid(nblk), block(512);
+  size_t lds = (size_t)3 * D * sizeof(float);
   if (dres)
     hipLaunchKernelGGL((ln_bwd_kernel<NV, true>), grid, block, lds, st, dy, x, g, mean, rstd, dres,
                        dx, partial, rows, D);
@@ -209,7 +236,7 @@ int ln_nv_for(int D) {
 }
 
 int ln_bwd_num_blocks(int rows) {
-  int nb = (rows + 3) / 4;
+  int nb = (rows + 7) / 8;
   return nb < 512 ? nb : 512;
 }
 
@@ -233,8 +260,7 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
     case 4: ln_bwd_dispatch<4>(dy, x, g, mean, rstd, dres, dx, partial, nblk, rows, D, st); break;
     case 8: ln_bwd_dispatch<8>(dy, x, g, mean, rstd, dres, dx, partial, nblk, rows, D, st); break;
   }
-  hipLaunchKernelGGL(colsum_to_bf16_kernel, dim3((2 * D + 255) / 256), dim3(256), 0, st, partial,
-                     nblk, D, dg, db);
+  colsum_bf16_launch(partial, nblk, 2 * D, D, dg, db, st);
 }
 
 }  // namespace caamd

@@ -177,3 +177,33 @@ def test_gpt2_gpu_matches_fp32_reference_loss():
     mg = mg.cuda().bfloat16()
     got = mg(x[:, :-1].cuda(), x[:, 1:].cuda()).item()
     assert abs(got - ref) < 0.05 * abs(ref), (got, ref)
+
+
+@pytest.mark.parametrize(
+    "B,T,H,D,causal",
+    [(2, 128, 3, 64, True), (1, 1024, 25, 64, True), (2, 256, 2, 128, True),
+     (1, 100, 2, 64, True), (2, 192, 2, 64, False), (1, 77, 1, 128, False)],
+)
+def test_flash_attention_fwd_bwd(C, B, T, H, D, causal):
+    from cluster_anywhere_amd.ops.attention import attention_ref
+    from cluster_anywhere_amd.ops.flash import flash_attention_lse, flash_attention_qkv
+
+    torch.manual_seed(7)
+    qkv = torch.randn(B, T, 3 * H * D, device="cuda", dtype=torch.bfloat16).requires_grad_()
+    out = flash_attention_qkv(qkv, H, causal)
+    dout = torch.randn_like(out)
+    out.backward(dout)
+    qf = qkv.detach().float().requires_grad_()
+    q, k, v = qf.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)
+    ref = attention_ref(q, k, v, causal)  # [B, H, T, D] fp32
+    ref_o = ref.transpose(1, 2).reshape(B, T, H * D)
+    ref_o.backward(dout.float())
+    assert _rel(out, ref_o) < 2e-2, _rel(out, ref_o)
+    g, gr = qkv.grad.view(B, T, 3, H, D), qf.grad.view(B, T, 3, H, D)
+    for i, name in enumerate("qkv"):
+        assert _rel(g[:, :, i], gr[:, :, i]) < 3e-2, (name, _rel(g[:, :, i], gr[:, :, i]))
+    _, lse = flash_attention_lse(qkv.detach(), H, causal)
+    s = (q.detach() @ k.detach().transpose(-1, -2)) / D ** 0.5
+    if causal:
+        s = s.masked_fill(~torch.ones(T, T, dtype=torch.bool, device="cuda").tril(), float("-inf"))
+    assert torch.allclose(lse, torch.logsumexp(s, -1), atol=2e-2, rtol=1e-3)
