@@ -31,6 +31,9 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// raw v_exp_f32 (no denormal range fix-up: softmax probabilities that small are 0 anyway)
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -217,30 +220,30 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16* __restrict__
 #pragma unroll
       for (int qs = 0; qs < kQS; ++qs) {
         const int q = q0w + qs * 32 + r;
+        if (need_mask) {  // branch-free selects (v_cndmask), only on diagonal / tail tiles
+          const int lim = causal ? min(q, T - 1) : T - 1;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+              sacc[qs][kb][i] = (k0 + kb * 32 + crow(i, h) > lim) ? -INFINITY : sacc[qs][kb][i];
+        }
         float mx4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float v = sacc[qs][kb][i] * scale_log2;
-            if (need_mask) {
-              const int key = k0 + kb * 32 + crow(i, h);
-              if (key >= T || (causal && key > q)) v = -INFINITY;
-            }
-            sacc[qs][kb][i] = v;
-            mx4[i & 3] = fmaxf(mx4[i & 3], v);
-          }
+          for (int i = 0; i < 16; ++i) mx4[i & 3] = fmaxf(mx4[i & 3], sacc[qs][kb][i]);
         float mx = fmaxf(fmaxf(mx4[0], mx4[1]), fmaxf(mx4[2], mx4[3]));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;  // scale > 0 commutes with max
         const float mnew = fmaxf(m[qs], mx);
         const float muse = mnew == -INFINITY ? 0.f : mnew;
-        const float alpha = exp2f(m[qs] - muse);
+        const float alpha = fexp2(m[qs] - muse);
         float rs4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            const float p = exp2f(sacc[qs][kb][i] - muse);
+            const float p = fexp2(__builtin_fmaf(sacc[qs][kb][i], scale_log2, -muse));
             sacc[qs][kb][i] = p;
             rs4[i & 3] += p;
           }
@@ -389,13 +392,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fa_bwd_dq_kernel(
 #pragma unroll
         for (int qs = 0; qs < kQS; ++qs) {
           const int q = q0w + qs * 32 + r;
+          const int lim = q >= T ? -1 : (causal ? min(q, T - 1) : T - 1);
 #pragma unroll
           for (int i = 0; i < 16; ++i) {
-            float p = exp2f(sacc[qs][i] * scale_log2 - lse2[qs]);
-            if (need_mask) {
-              const int key = k0 + kb * 32 + crow(i, h);
-              if (key >= T || (causal && key > q) || q >= T) p = 0.f;
-            }
+            float p = fexp2(__builtin_fmaf(sacc[qs][i], scale_log2, -lse2[qs]));
+            if (need_mask) p = (k0 + kb * 32 + crow(i, h) > lim) ? 0.f : p;
             sacc[qs][i] = p * (dp[qs][i] - dlt[qs]);  // dS^T
           }
         }
@@ -547,10 +548,11 @@ __global__ __launch_bounds__(256, D == 64 ? 2 : 1) void fa_bwd_dkdv_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             const int i = 4 * g + j;
-            float p = exp2f(sacc[qh][i] * scale_log2 - l4[j]);
+            float p = fexp2(__builtin_fmaf(sacc[qh][i], scale_log2, -l4[j]));
             if (need_mask) {
               const int qq = q0 + qi + j;
-              if (qq >= T || !kv || (causal && key > qq)) p = 0.f;
+              const bool bad = (qq >= T) | (!kv) | ((causal != 0) & (key > qq));
+              p = bad ? 0.f : p;
             }
             sacc[qh][i] = p;
             dp[qh][i] = p * (dp[qh][i] - d4[j]);
