@@ -1,0 +1,391 @@
+"""Public Core API (reference: python/ray/_private/worker.py — init :1275,
+shutdown :1884, get :2667, put :2803, wait :2868, get_actor :3013, kill :3048,
+cancel :3079, remote :3256; python/ray/_private/state.py — nodes, timeline,
+cluster_resources, available_resources)."""
+from __future__ import annotations
+
+import atexit
+import inspect
+import json
+import os
+import shutil
+import socket
+import tempfile
+import threading
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+from . import context
+from .object_ref import ObjectRef
+
+_head = None
+_init_lock = threading.RLock()
+_session = {}
+
+LOCAL_MODE = 2
+SCRIPT_MODE = 0
+WORKER_MODE = 1
+
+
+def detect_gpus() -> List[int]:
+    """MI355X GPUs visible to this process, without initialising HIP.
+
+    Reads the KFD topology (a node with simd_count > 0 is a GPU agent) and
+    honours ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CAAMD_NUM_GPUS.
+    """
+    if "CAAMD_NUM_GPUS" in os.environ:
+        return list(range(int(os.environ["CAAMD_NUM_GPUS"])))
+    n = 0
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for d in sorted(os.listdir(base), key=lambda x: int(x) if x.isdigit() else 0):
+            try:
+                with open(os.path.join(base, d, "properties")) as f:
+                    props = dict(line.split() for line in f if len(line.split()) == 2)
+                if int(props.get("simd_count", "0")) > 0:
+                    n += 1
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        n = 0
+    ids = list(range(n))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None and v != "":
+            sel = [int(x) for x in v.split(",") if x.strip().isdigit()]
+            ids = [i for i in sel if i < max(n, len(sel))] if n else sel
+            ids = list(range(len(ids)))  # re-indexed inside this process
+            break
+    return ids
+
+
+def _default_cpus() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _default_store_bytes() -> int:
+    try:
+        import psutil
+
+        avail = psutil.virtual_memory().available
+    except Exception:
+        avail = 8 << 30
+    try:
+        shm = shutil.disk_usage("/dev/shm").free
+    except OSError:
+        shm = avail
+    return int(max(64 << 20, min(avail * 0.3, shm * 0.8, 200 << 30)))
+
+
+class RayContext(dict):
+    """Returned by init(): address info (dict-like, like the reference's RayContext)."""
+
+    def __init__(self, info):
+        super().__init__(info)
+        self.address_info = info
+        self.dashboard_url = info.get("webui_url")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        shutdown()
+
+    def disconnect(self):
+        shutdown()
+
+
+def is_initialized() -> bool:
+    return context.worker is not None or context.local_mode
+
+
+def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
+         num_gpus: Optional[int] = None, resources: Optional[Dict[str, float]] = None,
+         object_store_memory: Optional[int] = None, local_mode: bool = False,
+         ignore_reinit_error: bool = False, namespace: Optional[str] = None,
+         runtime_env: Optional[dict] = None, include_dashboard: Optional[bool] = None,
+         dashboard_host: str = "127.0.0.1", dashboard_port: Optional[int] = None,
+         job_config=None, logging_level=None, log_to_driver: bool = True,
+         _temp_dir: Optional[str] = None, _node_ip_address: str = "127.0.0.1",
+         **kwargs) -> RayContext:
+    global _head
+    with _init_lock:
+        if is_initialized():
+            if ignore_reinit_error:
+                return RayContext(dict(_session))
+            raise RuntimeError("Maybe you called init twice by accident? "
+                               "Pass ignore_reinit_error=True to ignore this.")
+        if local_mode:
+            context.local_mode = True
+            from .local_mode import reset_local
+
+            reset_local()
+            _session.clear()
+            _session.update({"node_id": "local", "address": "local"})
+            return RayContext(dict(_session))
+        address = address or os.environ.get("CAAMD_ADDRESS") or os.environ.get("RAY_ADDRESS")
+        if address == "local":
+            address = None
+        from .worker import CoreWorker
+
+        job_id = os.urandom(4)
+        if address is None:
+            from .head import Head
+
+            sess = f"session_{time.strftime('%Y%m%d-%H%M%S')}_{os.getpid()}_{uuid.uuid4().hex[:6]}"
+            root = _temp_dir or os.path.join(tempfile.gettempdir(), "caamd")
+            session_dir = os.path.join(root, sess)
+            gpus = detect_gpus()
+            if num_gpus is not None:
+                gpus = list(range(num_gpus))
+            res = {"CPU": float(num_cpus if num_cpus is not None else _default_cpus())}
+            if gpus:
+                res["GPU"] = float(len(gpus))
+            res["memory"] = float(_mem_bytes())
+            store_bytes = int(object_store_memory or _default_store_bytes())
+            res["object_store_memory"] = float(store_bytes)
+            node_id = os.urandom(16)
+            res[f"node:{_node_ip_address}"] = 1.0
+            res["node:__internal_head__"] = 1.0
+            for k, v in (resources or {}).items():
+                res[k] = float(v)
+            store_name = f"/caamd_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+            head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
+                        namespace=namespace or "default",
+                        worker_env=_worker_env_from(runtime_env),
+                        listen_tcp=kwargs.get("_listen_tcp"))
+            head.start()
+            _head = head
+            address = head.sock_path
+            try:
+                os.makedirs(root, exist_ok=True)
+                with open(os.path.join(root, "latest_address"), "w") as f:
+                    f.write(head.tcp_address or head.sock_path)
+            except OSError:
+                pass
+        elif address == "auto":
+            root = _temp_dir or os.path.join(tempfile.gettempdir(), "caamd")
+            with open(os.path.join(root, "latest_address")) as f:
+                address = f.read().strip()
+        cw = CoreWorker(address, "driver", os.urandom(16), job_id=job_id)
+        cw.namespace = namespace or cw.namespace
+        context.worker = cw
+        _session.clear()
+        _session.update({"address": address, "node_id": cw.node_hex, "session_dir": cw.session_dir,
+                         "namespace": cw.namespace, "job_id": job_id.hex(),
+                         "object_store_address": getattr(cw.store, "name", ""),
+                         "webui_url": None, "gcs_address": address})
+        if runtime_env:
+            _session["runtime_env"] = runtime_env
+        if include_dashboard:
+            from ..dashboard import start_dashboard
+
+            _session["webui_url"] = start_dashboard(dashboard_host, dashboard_port or 8265)
+        return RayContext(dict(_session))
+
+
+def _mem_bytes():
+    try:
+        import psutil
+
+        return psutil.virtual_memory().total
+    except Exception:
+        return 16 << 30
+
+
+def _worker_env_from(renv):
+    env = {}
+    if renv:
+        for k, v in (renv.get("env_vars") or {}).items():
+            env[k] = str(v)
+        env["CAAMD_RUNTIME_ENV"] = json.dumps(renv)
+    return env
+
+
+def _ensure_init():
+    if not is_initialized():
+        init()
+
+
+def shutdown(_exiting_interpreter: bool = False):
+    global _head
+    with _init_lock:
+        if context.local_mode:
+            context.local_mode = False
+            from .local_mode import reset_local
+
+            reset_local()
+        w = context.worker
+        context.worker = None
+        if w is not None:
+            try:
+                w.close()
+            except Exception:
+                pass
+        if _head is not None:
+            _head.shutdown()
+            _head = None
+        _session.clear()
+
+
+atexit.register(lambda: shutdown(True))
+
+
+def _w():
+    _ensure_init()
+    return context.worker
+
+
+def put(value, *, _owner=None) -> ObjectRef:
+    if context.local_mode:
+        from .local_mode import local_put
+
+        return local_put(value)
+    return _w().put(value)
+
+
+def get(object_refs, *, timeout: Optional[float] = None):
+    if context.local_mode:
+        from .local_mode import local_get
+
+        return local_get(object_refs)
+    from .object_ref import ObjectRefGenerator
+
+    if isinstance(object_refs, ObjectRefGenerator):
+        object_refs = list(object_refs)
+    if isinstance(object_refs, (list, tuple)):
+        return _w().get(list(object_refs), timeout=timeout)
+    if not isinstance(object_refs, ObjectRef):
+        from ..dag.compiled import CompiledDAGRef
+
+        if isinstance(object_refs, CompiledDAGRef):
+            return object_refs.get(timeout)
+        raise TypeError(f"get() expects an ObjectRef or a list of ObjectRefs, got {type(object_refs)}")
+    return _w().get(object_refs, timeout=timeout)
+
+
+def wait(object_refs: List[ObjectRef], *, num_returns: int = 1, timeout: Optional[float] = None,
+         fetch_local: bool = True):
+    if isinstance(object_refs, ObjectRef):
+        raise TypeError("wait() expected a list of ObjectRef")
+    if context.local_mode:
+        return list(object_refs)[:num_returns], list(object_refs)[num_returns:]
+    return _w().wait(list(object_refs), num_returns=num_returns, timeout=timeout, fetch_local=fetch_local)
+
+
+def remote(*args, **kwargs):
+    """``@remote`` / ``@remote(num_cpus=..., ...)`` for functions and classes."""
+    from .actor import ActorClass
+    from .remote_function import RemoteFunction
+
+    def make(obj, opts):
+        if inspect.isclass(obj):
+            return ActorClass(obj, opts)
+        if callable(obj):
+            return RemoteFunction(obj, opts)
+        raise TypeError("@remote can only decorate functions or classes")
+
+    if len(args) == 1 and not kwargs and callable(args[0]):
+        return make(args[0], {})
+    if args:
+        raise TypeError("@remote takes keyword arguments only, e.g. @remote(num_gpus=1)")
+    return lambda obj: make(obj, kwargs)
+
+
+def get_actor(name: str, namespace: Optional[str] = None):
+    from .actor import ActorHandle
+
+    w = _w()
+    res = w.request(lambda r: ("check_name", r, namespace or w.namespace, name))
+    if res is None:
+        raise ValueError(f"Failed to look up actor with name '{name}'.")
+    return ActorHandle(res[0], res[1] or {})
+
+
+def kill(actor, *, no_restart: bool = True):
+    from .actor import ActorHandle
+
+    if not isinstance(actor, ActorHandle):
+        raise ValueError("kill() only supports actor handles")
+    if context.local_mode:
+        return
+    _w().send(("kill_actor", actor._actor_id, no_restart))
+
+
+def cancel(ref, *, force: bool = False, recursive: bool = True):
+    from .object_ref import ObjectRefGenerator
+
+    if isinstance(ref, ObjectRefGenerator):
+        tid = ref._task_id
+    elif isinstance(ref, ObjectRef):
+        tid = ref.binary()[:16]
+    else:
+        raise TypeError("cancel() expects an ObjectRef")
+    if context.local_mode:
+        return
+    _w().send(("cancel", tid, force, recursive))
+
+
+def free(refs):
+    _w().free(refs)
+
+
+def _state(what, arg=None):
+    w = _w()
+    return w.request(lambda r: ("state", r, what, arg))
+
+
+def nodes():
+    return _state("nodes")
+
+
+def cluster_resources():
+    return _state("cluster_resources")
+
+
+def available_resources():
+    return _state("available_resources")
+
+
+def available_resources_per_node():
+    return _state("available_per_node")
+
+
+def get_gpu_ids():
+    ctx = context.current_task()
+    if ctx is not None and ctx.gpu_ids is not None:
+        return list(range(len(ctx.gpu_ids))) if os.environ.get("ROCR_VISIBLE_DEVICES") else ctx.gpu_ids
+    env = os.environ.get("CAAMD_GPU_IDS", "")
+    return [int(x) for x in env.split(",") if x]
+
+
+def timeline(filename: Optional[str] = None):
+    """Chrome-trace events of task execution (reference: state.py:965)."""
+    ev = _state("events")
+    starts = {}
+    out = []
+    for e in ev:
+        if e[0] == "start":
+            starts[e[1]] = e
+        elif e[0] == "end" and e[1] in starts:
+            s = starts.pop(e[1])
+            out.append({"cat": "task", "name": s[2], "ph": "X", "ts": s[3] * 1e6,
+                        "dur": (e[3] - s[3]) * 1e6, "pid": "node", "tid": s[4] or 0,
+                        "args": {"task_id": e[1].hex()}})
+    if filename:
+        with open(filename, "w") as f:
+            json.dump(out, f)
+        return None
+    return out
+
+
+def show_in_dashboard(message: str, key: str = "", dtype: str = "text"):
+    pass
+
+
+def head():
+    return _head

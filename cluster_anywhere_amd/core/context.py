@@ -1,0 +1,27 @@
+"""Process-global runtime state: the connected CoreWorker (driver or worker) and
+the task-execution context used by ``get_runtime_context()``."""
+from __future__ import annotations
+
+import threading
+
+worker = None  # CoreWorker of this process, or None when not initialised
+local_mode = False
+
+_tls = threading.local()
+
+
+class TaskContext:
+    __slots__ = ("task_id", "actor_id", "fn_name", "attempt", "gpu_ids", "resources", "pg",
+                 "actor_name", "cancelled")
+
+    def __init__(self, **kw):
+        for s in self.__slots__:
+            setattr(self, s, kw.get(s))
+
+
+def current_task() -> "TaskContext":
+    return getattr(_tls, "ctx", None)
+
+
+def set_current_task(ctx):
+    _tls.ctx = ctx

@@ -1,0 +1,1332 @@
+"""The head: GCS tables + raylet scheduling loop + object directory + worker pool.
+
+Reference roles: ``src/ray/gcs/gcs_server`` (actor / node / job / placement-group
+tables, internal KV, health checks) and ``src/ray/raylet`` (NodeManager,
+LocalTaskManager, WorkerPool, DependencyManager, WaitManager). Here they are one
+single-threaded event loop (selectors) so all control state is mutated without
+locks; resource accounting and placement are done by the native
+``ClusterScheduler`` and object payloads live in the native shared-memory
+``ObjectStore`` (workers read/write it directly; only small objects are inlined
+in control messages).
+
+The head runs as a thread inside the driver (``init()``) or as a standalone
+process (``python -m cluster_anywhere_amd.core.head``) that drivers and other
+nodes connect to over TCP.
+"""
+from __future__ import annotations
+
+import collections
+import os
+import selectors
+import signal
+import socket
+import subprocess
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Dict, List, Optional, Set
+
+from . import serialization
+from .ids import ObjectID
+from .protocol import Conn, ConnectionClosed
+
+INLINE_MAX = int(os.environ.get("CAAMD_INLINE_MAX", str(100 * 1024)))
+
+# task kinds
+NORMAL, ACTOR_CREATE, ACTOR_METHOD = 0, 1, 2
+# object states
+PENDING, READY, FREED = 0, 1, 2
+
+
+class TaskSpec:
+    """Everything the head needs to schedule, run, retry and report a task."""
+
+    __slots__ = (
+        "task_id", "kind", "fn_id", "fn_name", "args", "kwargs", "arg_refs", "num_returns",
+        "return_ids", "resources", "strategy", "max_retries", "retry_exceptions", "owner",
+        "actor_id", "method", "actor_opts", "runtime_env", "name", "job_id", "attempt",
+        "generator", "node", "worker", "gpu_ids", "state", "submit_time", "start_time",
+        "acquired", "pg_id", "cancelled", "parent", "concurrency_group", "pinned_refs",
+        "blocked",
+    )
+
+    def __init__(self, **kw):
+        for s in self.__slots__:
+            setattr(self, s, kw.get(s))
+        self.attempt = self.attempt or 0
+        self.arg_refs = self.arg_refs or []
+        self.resources = self.resources or {}
+        self.cancelled = False
+
+
+class ObjEntry:
+    __slots__ = ("state", "inline", "size", "node", "refcount", "pins", "waiters", "contained",
+                 "is_error", "owner_task", "spilled_path", "gen_end")
+
+    def __init__(self):
+        self.state = PENDING
+        self.inline = None
+        self.size = 0
+        self.node = None
+        self.refcount = 0
+        self.pins = 0
+        self.waiters = []
+        self.contained = ()
+        self.is_error = False
+        self.owner_task = None
+        self.spilled_path = None
+        self.gen_end = None
+
+
+class WorkerInfo:
+    __slots__ = ("worker_id", "conn", "pid", "node", "gpu_key", "idle", "actor_id", "task",
+                 "proc", "fns", "alive", "kind", "started", "tasks_inflight", "env_key", "client_id")
+
+    def __init__(self, **kw):
+        for s in self.__slots__:
+            setattr(self, s, kw.get(s))
+        self.fns = set()
+        self.tasks_inflight = {}
+
+
+class ActorInfo:
+    __slots__ = ("actor_id", "spec", "state", "worker", "name", "namespace", "restarts_left",
+                 "max_task_retries", "queue", "inflight", "node", "gpu_ids", "acquired",
+                 "class_name", "lifetime", "death_cause", "num_restarts", "owner", "pid")
+
+    def __init__(self, **kw):
+        for s in self.__slots__:
+            setattr(self, s, kw.get(s))
+        self.queue = collections.deque()
+        self.inflight = {}
+        self.num_restarts = 0
+
+
+class Head:
+    def __init__(self, session_dir: str, node_id: bytes, resources: Dict[str, float],
+                 store_name: str, store_capacity: int, gpu_ids: List[int],
+                 listen_tcp: Optional[str] = None, namespace: str = "default",
+                 worker_env: Optional[Dict[str, str]] = None, prestart: int = 0,
+                 spill_dir: Optional[str] = None):
+        from .. import _native
+
+        self.session_dir = session_dir
+        os.makedirs(session_dir, exist_ok=True)
+        self.node_id = node_id
+        self.store_name = store_name
+        self.store = _native.ObjectStore(store_name, store_capacity, 1 << 18, True)
+        self.sched = _native.ClusterScheduler(0.5)
+        self.sched.add_node(node_id.hex(), resources)
+        self.node_resources = {node_id.hex(): dict(resources)}
+        self.free_gpus = {node_id.hex(): list(gpu_ids)}
+        self.node_info = {node_id.hex(): {"NodeID": node_id.hex(), "Alive": True,
+                                          "NodeManagerAddress": "127.0.0.1",
+                                          "Resources": dict(resources), "local": True}}
+        self.namespace = namespace
+        self.worker_env = worker_env or {}
+        self.spill_dir = spill_dir or os.path.join(session_dir, "spill")
+        self.sock_path = os.path.join(session_dir, "head.sock")
+        self.sel = selectors.DefaultSelector()
+        self.lsock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        try:
+            os.unlink(self.sock_path)
+        except FileNotFoundError:
+            pass
+        self.lsock.bind(self.sock_path)
+        self.lsock.listen(1024)
+        self.lsock.setblocking(False)
+        self.sel.register(self.lsock, selectors.EVENT_READ, ("listen", None))
+        self.tcp_address = None
+        if listen_tcp:
+            host, port = listen_tcp.rsplit(":", 1)
+            self.tsock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            self.tsock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            self.tsock.bind((host, int(port)))
+            self.tsock.listen(1024)
+            self.tsock.setblocking(False)
+            self.tcp_address = f"{host}:{self.tsock.getsockname()[1]}"
+            self.sel.register(self.tsock, selectors.EVENT_READ, ("listen", None))
+        # wakeup pipe for cross-thread calls
+        self._wr, self._ww = socket.socketpair()
+        self._wr.setblocking(False)
+        self.sel.register(self._wr, selectors.EVENT_READ, ("wake", None))
+        self._calls = collections.deque()
+
+        self.objects: Dict[bytes, ObjEntry] = {}
+        self.tasks: Dict[bytes, TaskSpec] = {}
+        self.waiting_deps: Dict[bytes, Set[bytes]] = {}  # task -> unresolved object ids
+        self.dep_index: Dict[bytes, List[bytes]] = collections.defaultdict(list)
+        # ready tasks grouped by scheduling class (demand + strategy), like the
+        # reference's per-SchedulingClass queues: a blocked class costs O(1) per pass
+        self.ready_queues: Dict[tuple, collections.deque] = {}
+        self.infeasible: List[TaskSpec] = []
+        self.workers: Dict[bytes, WorkerInfo] = {}
+        self.conn_worker: Dict[Conn, WorkerInfo] = {}
+        self.clients: Dict[Conn, dict] = {}
+        self.idle: Dict[tuple, List[WorkerInfo]] = collections.defaultdict(list)
+        self.starting: Dict[tuple, int] = collections.defaultdict(int)
+        self.pending_spawn: Dict[bytes, tuple] = {}
+        self.actors: Dict[bytes, ActorInfo] = {}
+        self.named_actors: Dict[tuple, bytes] = {}
+        self.kv: Dict[tuple, bytes] = {}
+        self.functions: Dict[bytes, bytes] = {}
+        self.pgs: Dict[bytes, dict] = {}
+        self.pending_pgs: List[bytes] = []
+        self.gen_waiters: Dict[bytes, list] = collections.defaultdict(list)
+        self.events: collections.deque = collections.deque(maxlen=200000)
+        self.jobs: Dict[bytes, dict] = {}
+        self.max_workers = int(max(4, resources.get("CPU", 1) * 4))
+        self.running = True
+        self.thread = None
+        self._prestart = prestart
+        self.cpu_count = resources.get("CPU", 1)
+        self._last_health = time.time()
+
+    # ------------------------------------------------------------------ loop
+    def start(self):
+        self.thread = threading.Thread(target=self._loop, name="caamd-head", daemon=True)
+        self.thread.start()
+        for _ in range(self._prestart):
+            self.call(lambda: self._spawn_worker(self.node_id.hex(), ()))
+
+    def call(self, fn):
+        """Run ``fn`` on the head thread (fire-and-forget)."""
+        self._calls.append(fn)
+        try:
+            self._ww.send(b"x")
+        except OSError:
+            pass
+
+    def call_sync(self, fn, timeout=30):
+        ev = threading.Event()
+        box = {}
+
+        def run():
+            try:
+                box["v"] = fn()
+            except BaseException as e:  # pragma: no cover
+                box["e"] = e
+            ev.set()
+
+        self.call(run)
+        if not ev.wait(timeout):
+            raise TimeoutError("head did not answer")
+        if "e" in box:
+            raise box["e"]
+        return box.get("v")
+
+    def _loop(self):
+        while self.running:
+            try:
+                events = self.sel.select(timeout=0.2)
+            except OSError:
+                break
+            for key, _ in events:
+                kind, data = key.data
+                if kind == "listen":
+                    try:
+                        s, _ = key.fileobj.accept()
+                    except OSError:
+                        continue
+                    s.setblocking(True)
+                    c = Conn(s)
+                    s.setblocking(False)
+                    self.clients[c] = {"id": None}
+                    self.sel.register(s, selectors.EVENT_READ, ("conn", c))
+                elif kind == "wake":
+                    try:
+                        self._wr.recv(4096)
+                    except OSError:
+                        pass
+                elif kind == "conn":
+                    self._on_readable(data)
+            while self._calls:
+                fn = self._calls.popleft()
+                try:
+                    fn()
+                except Exception:
+                    traceback.print_exc()
+            now = time.time()
+            if now - self._last_health > 1.0:
+                self._last_health = now
+                self._health_check()
+
+    def _on_readable(self, c: Conn):
+        try:
+            data = c.sock.recv(1 << 20)
+        except BlockingIOError:
+            return
+        except OSError:
+            data = b""
+        if not data:
+            self._on_disconnect(c)
+            return
+        for msg in c.feed(data):
+            try:
+                self._dispatch(c, msg)
+            except Exception:
+                traceback.print_exc()
+
+    def _send(self, c: Conn, msg):
+        if c is None or c.closed:
+            return
+        try:
+            c.sock.setblocking(True)
+            c.send(msg)
+        except ConnectionClosed:
+            pass
+        finally:
+            try:
+                c.sock.setblocking(False)
+            except OSError:
+                pass
+
+    # -------------------------------------------------------------- dispatch
+    def _dispatch(self, c: Conn, msg):
+        t = msg[0]
+        h = getattr(self, "_h_" + t, None)
+        if h is None:
+            raise ValueError(f"unknown message {t}")
+        h(c, *msg[1:])
+
+    def _reply(self, c, req, value):
+        self._send(c, ("reply", req, value))
+
+    def _h_register(self, c, kind, worker_id, pid, node_hex, extra):
+        self.clients[c] = {"id": worker_id, "kind": kind, "pid": pid, "node": node_hex}
+        self._send(c, ("registered", {"store_name": self.store_name,
+                                      "node_id": node_hex or self.node_id.hex(),
+                                      "namespace": self.namespace,
+                                      "session_dir": self.session_dir}))
+        if kind == "worker":
+            w = self.workers.get(worker_id)
+            if w is None:
+                w = WorkerInfo(worker_id=worker_id, pid=pid, node=node_hex,
+                               gpu_key=tuple(extra.get("gpu_ids", ())), kind="worker")
+                self.workers[worker_id] = w
+            w.conn = c
+            w.alive = True
+            w.started = time.time()
+            w.client_id = worker_id
+            self.conn_worker[c] = w
+            key = (w.node, w.gpu_key)
+            self.starting[key] = max(0, self.starting[key] - 1)
+            pending = self.pending_spawn.pop(worker_id, None)
+            if pending and pending[0] == "actor":
+                self._start_actor_on(self.actors[pending[1]], w)
+            else:
+                w.idle = True
+                self.idle[key].append(w)
+                self._schedule()
+        elif kind == "driver":
+            self.jobs.setdefault(extra.get("job_id", b""), {"start": time.time(), "pid": pid,
+                                                             "driver": worker_id})
+
+    # ------------------------------------------------------------ functions/kv
+    def _h_fn(self, c, fn_id, blob):
+        self.functions[fn_id] = blob
+
+    def _h_kv(self, c, req, op, ns, key, value, overwrite):
+        k = (ns, key)
+        if op == "put":
+            existed = k in self.kv
+            if overwrite or not existed:
+                self.kv[k] = value
+            self._reply(c, req, not existed)
+        elif op == "get":
+            self._reply(c, req, self.kv.get(k))
+        elif op == "del":
+            if key.endswith(b"*"):
+                n = 0
+                for kk in [kk for kk in self.kv if kk[0] == ns and kk[1].startswith(key[:-1])]:
+                    del self.kv[kk]
+                    n += 1
+                self._reply(c, req, n)
+            else:
+                self._reply(c, req, 1 if self.kv.pop(k, None) is not None else 0)
+        elif op == "exists":
+            self._reply(c, req, k in self.kv)
+        elif op == "keys":
+            self._reply(c, req, [kk[1] for kk in self.kv if kk[0] == ns and kk[1].startswith(key)])
+
+    # ------------------------------------------------------------------ objects
+    def _obj(self, oid) -> ObjEntry:
+        e = self.objects.get(oid)
+        if e is None:
+            e = ObjEntry()
+            self.objects[oid] = e
+        return e
+
+    def _h_put(self, c, oid, inline, size, node_hex, contained, is_error=False):
+        e = self._obj(oid)
+        e.refcount += 1
+        self._seal_object(oid, inline, size, node_hex, contained, is_error)
+
+    def _seal_object(self, oid, inline, size, node_hex, contained, is_error=False):
+        e = self._obj(oid)
+        if e.state == READY:
+            return
+        e.state = READY
+        e.inline = inline
+        e.size = size
+        e.node = node_hex
+        e.is_error = is_error
+        e.contained = tuple(contained or ())
+        for r in e.contained:
+            self._obj(r).pins += 1
+        waiters, e.waiters = e.waiters, []
+        for w in waiters:
+            w(oid)
+        self._maybe_free(oid)
+
+    def _h_addref(self, c, oids):
+        for o in oids:
+            self._obj(o).refcount += 1
+
+    def _h_decref(self, c, oids):
+        for o in oids:
+            e = self.objects.get(o)
+            if e is None:
+                continue
+            e.refcount -= 1
+            self._maybe_free(o)
+
+    def _maybe_free(self, oid):
+        e = self.objects.get(oid)
+        if e is None or e.refcount > 0 or e.pins > 0 or e.state != READY or e.waiters:
+            return
+        if e.owner_task is not None:
+            t = self.tasks.get(e.owner_task)
+            if t is not None and t.state in ("pending", "running"):
+                return
+        del self.objects[oid]
+        if e.inline is None and e.spilled_path is None:
+            try:
+                self.store.remove(oid)
+            except Exception:
+                pass
+        if e.spilled_path:
+            try:
+                os.unlink(e.spilled_path)
+            except OSError:
+                pass
+        for r in e.contained:
+            ce = self.objects.get(r)
+            if ce is not None:
+                ce.pins -= 1
+                self._maybe_free(r)
+
+    def _obj_payload(self, oid):
+        e = self.objects.get(oid)
+        if e is None:
+            return ("lost", None)
+        if e.inline is not None:
+            return ("err" if e.is_error else "inline", e.inline)
+        if e.spilled_path is not None:
+            self._restore(oid, e)
+        return ("err_store" if e.is_error else "store", e.size)
+
+    def _restore(self, oid, e):
+        with open(e.spilled_path, "rb") as f:
+            data = f.read()
+        off = self.store.create(oid, len(data), 0)
+        if off < 0:
+            self._evict(len(data))
+            off = self.store.create(oid, len(data), 0)
+        if off >= 0:
+            self.store.buffer(off, len(data), False)[:] = data
+            self.store.seal(oid)
+            os.unlink(e.spilled_path)
+            e.spilled_path = None
+        else:
+            e.inline = data  # last resort: serve through the control plane
+
+    def _evict(self, need):
+        """Spill least-recently-used sealed objects to disk until ``need`` fits."""
+        os.makedirs(self.spill_dir, exist_ok=True)
+        freed = 0
+        for oid in self.store.lru_candidates(256):
+            e = self.objects.get(oid)
+            if e is None:
+                continue
+            pb = self.store.get_pinned(oid)
+            if pb is None:
+                continue
+            path = os.path.join(self.spill_dir, oid.hex())
+            with open(path, "wb") as f:
+                f.write(memoryview(pb))
+            del pb
+            self.store.remove(oid)
+            e.spilled_path = path
+            freed += e.size
+            self.events.append(("spill", oid.hex(), e.size, time.time()))
+            if freed >= need and self.store.largest_free() >= need:
+                break
+        return freed
+
+    def _h_evict(self, c, req, need):
+        self._reply(c, req, self._evict(need))
+
+    def _h_get(self, c, req, oids, timeout):
+        """Reply when every object is ready (or on timeout with what is ready)."""
+        missing = set()
+        for o in oids:
+            e = self._obj(o)
+            if e.state != READY:
+                missing.add(o)
+        if not missing:
+            self._reply(c, req, [(o, *self._obj_payload(o)) for o in oids])
+            return
+        state = {"missing": missing, "done": False}
+
+        def on_ready(oid):
+            state["missing"].discard(oid)
+            if not state["missing"] and not state["done"]:
+                state["done"] = True
+                self._reply(c, req, [(o, *self._obj_payload(o)) for o in oids])
+
+        for o in missing:
+            self._obj(o).waiters.append(on_ready)
+        if timeout is not None and timeout >= 0:
+            def on_timeout():
+                if not state["done"]:
+                    state["done"] = True
+                    for o in list(state["missing"]):
+                        e = self.objects.get(o)
+                        if e is not None and on_ready in e.waiters:
+                            e.waiters.remove(on_ready)
+                    self._reply(c, req, None)
+            self._timer(timeout, on_timeout)
+
+    def _h_wait(self, c, req, oids, num_returns, timeout):
+        ready = [o for o in oids if self._obj(o).state == READY]
+        if len(ready) >= num_returns or timeout == 0:
+            self._reply(c, req, ready[: max(num_returns, 0)] if len(ready) >= num_returns else ready)
+            return
+        state = {"ready": set(ready), "done": False}
+
+        def finish():
+            if state["done"]:
+                return
+            state["done"] = True
+            for o in oids:
+                e = self.objects.get(o)
+                if e is not None and on_ready in e.waiters:
+                    e.waiters.remove(on_ready)
+            rs = [o for o in oids if o in state["ready"]]
+            self._reply(c, req, rs[:num_returns])
+
+        def on_ready(oid):
+            state["ready"].add(oid)
+            if len(state["ready"]) >= num_returns:
+                finish()
+
+        for o in oids:
+            if o not in state["ready"]:
+                self._obj(o).waiters.append(on_ready)
+        if timeout is not None and timeout >= 0:
+            self._timer(timeout, finish)
+
+    def _timer(self, delay, fn):
+        def fire():
+            time.sleep(delay)
+            self.call(fn)
+
+        threading.Thread(target=fire, daemon=True).start()
+
+    def _h_free(self, c, oids):
+        for o in oids:
+            e = self.objects.get(o)
+            if e is not None:
+                e.refcount = 0
+                e.pins = 0
+                self._maybe_free(o)
+
+    # -------------------------------------------------------------------- tasks
+    def _h_submit(self, c, spec: TaskSpec):
+        spec.owner = self.clients.get(c, {}).get("id")
+        spec.state = "pending"
+        spec.submit_time = time.time()
+        self.tasks[spec.task_id] = spec
+        for i, oid in enumerate(spec.return_ids or ()):
+            e = self._obj(oid)
+            e.refcount += 1
+            e.owner_task = spec.task_id
+        self.events.append(("submit", spec.task_id, spec.fn_name, spec.submit_time))
+        for r in spec.arg_refs:
+            self._obj(r).pins += 1
+        for r in spec.pinned_refs or ():
+            self._obj(r).pins += 1
+        if spec.kind == ACTOR_CREATE:
+            self._register_actor(spec, c)
+        self._enqueue_when_ready(spec)
+
+    def _enqueue_when_ready(self, spec):
+        unresolved = {r for r in spec.arg_refs if self._obj(r).state != READY}
+        if not unresolved:
+            self._on_deps_ready(spec)
+            return
+        self.waiting_deps[spec.task_id] = unresolved
+
+        def on_ready(oid, tid=spec.task_id):
+            s = self.waiting_deps.get(tid)
+            if s is None:
+                return
+            s.discard(oid)
+            if not s:
+                del self.waiting_deps[tid]
+                t = self.tasks.get(tid)
+                if t is not None and not t.cancelled:
+                    self._on_deps_ready(t)
+
+        for r in unresolved:
+            self._obj(r).waiters.append(on_ready)
+
+    def _on_deps_ready(self, spec):
+        # a dependency that failed poisons the task (reference: task dependency errors)
+        for r in spec.arg_refs:
+            e = self.objects.get(r)
+            if e is not None and e.is_error:
+                pass  # the worker re-raises the stored error when it resolves the arg
+        if spec.kind == ACTOR_METHOD:
+            a = self.actors.get(spec.actor_id)
+            if a is None:
+                self._fail_task(spec, ("ActorDiedError", "actor not found"))
+                return
+            a.queue.append(spec)
+            self._pump_actor(a)
+        else:
+            self._enqueue_ready(spec)
+            self._schedule()
+
+    def _demand(self, spec):
+        d = dict(spec.resources)
+        st = spec.strategy
+        if st and st[0] == "pg":
+            _, pg_id, bidx = st[:3]
+            pg_hex = pg_id.hex()
+            nd = {}
+            for k, v in d.items():
+                if v <= 0:
+                    continue
+                if bidx is None or bidx < 0:
+                    nd[f"{k}_group_{pg_hex}"] = v
+                else:
+                    nd[f"{k}_group_{bidx}_{pg_hex}"] = v
+            if not nd:
+                nd = ({f"bundle_group_{pg_hex}": 0.001} if bidx is None or bidx < 0
+                      else {f"bundle_group_{bidx}_{pg_hex}": 0.001})
+            return nd
+        return d
+
+    def _enqueue_ready(self, spec):
+        key = (tuple(sorted(spec.resources.items())), spec.strategy, spec.kind == ACTOR_CREATE)
+        q = self.ready_queues.get(key)
+        if q is None:
+            q = self.ready_queues[key] = collections.deque()
+        q.append(spec)
+
+    def _schedule(self):
+        if not self.ready_queues:
+            return
+        for key in list(self.ready_queues):
+            q = self.ready_queues[key]
+            while q:
+                spec = q[0]
+                if spec.cancelled:
+                    q.popleft()
+                    continue
+                if self._try_place(spec):
+                    q.popleft()
+                else:
+                    break
+            if not q:
+                del self.ready_queues[key]
+
+    def _try_place(self, spec) -> bool:
+        demand = self._demand(spec)
+        st = spec.strategy or ("default",)
+        if st[0] == "pg" and spec.strategy[1] not in self.pgs:
+            self._fail_task(spec, ("TaskPlacementGroupRemoved", "placement group was removed"))
+            return True
+        strategy, aff, soft = 0, "", False
+        if st[0] == "spread":
+            strategy = 1
+        elif st[0] == "node":
+            strategy, aff, soft = 2, st[1], bool(st[2])
+        node = self.sched.pick_node(demand, strategy, aff, soft, self.node_id.hex())
+        if node == "!":
+            if spec not in self.infeasible:
+                self.infeasible.append(spec)
+                self.events.append(("infeasible", spec.task_id, spec.fn_name, time.time()))
+            return True  # parked
+        if node == "":
+            return False
+        ngpu = int(round(spec.resources.get("GPU", 0)))
+        gpu_ids = ()
+        if ngpu > 0:
+            free = self.free_gpus.get(node, [])
+            if len(free) < ngpu:
+                return False
+            gpu_ids = tuple(free[:ngpu])
+        if spec.kind == ACTOR_CREATE:
+            if not self.sched.acquire(node, demand):
+                return False
+            if gpu_ids:
+                for g in gpu_ids:
+                    self.free_gpus[node].remove(g)
+            spec.acquired = (node, demand)
+            spec.gpu_ids = gpu_ids
+            a = self.actors[spec.actor_id]
+            a.node, a.gpu_ids, a.acquired = node, gpu_ids, (node, demand)
+            wid = os.urandom(16)
+            self.pending_spawn[wid] = ("actor", spec.actor_id)
+            self._spawn_worker(node, gpu_ids, worker_id=wid, env=spec.runtime_env)
+            return True
+        key = (node, gpu_ids)
+        idle = self.idle.get(key)
+        w = None
+        while idle:
+            cand = idle.pop()
+            if cand.alive and cand.idle:
+                w = cand
+                break
+        if w is None:
+            if self.starting[key] < max(1, int(self.cpu_count)) and self._num_workers(node) < self.max_workers:
+                self._spawn_worker(node, gpu_ids)
+            return False
+        if not self.sched.acquire(node, demand):
+            w.idle = True
+            self.idle[key].append(w)
+            return False
+        if gpu_ids:
+            for g in gpu_ids:
+                self.free_gpus[node].remove(g)
+        spec.acquired = (node, demand)
+        spec.gpu_ids = gpu_ids
+        self._dispatch_to(w, spec)
+        return True
+
+    def _num_workers(self, node):
+        return sum(1 for w in self.workers.values() if w.node == node and w.alive) + sum(
+            v for (n, _), v in self.starting.items() if n == node)
+
+    def _spawn_worker(self, node, gpu_ids, worker_id=None, env=None):
+        worker_id = worker_id or os.urandom(16)
+        key = (node, tuple(gpu_ids))
+        self.starting[key] += 1
+        e = dict(os.environ)
+        e.update(self.worker_env)
+        e["CAAMD_HEAD"] = self.sock_path if node == self.node_id.hex() else (self.tcp_address or "")
+        e["CAAMD_WORKER_ID"] = worker_id.hex()
+        e["CAAMD_NODE_ID"] = node
+        e["CAAMD_GPU_IDS"] = ",".join(str(g) for g in gpu_ids)
+        if gpu_ids:
+            e["ROCR_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpu_ids)
+        elif "CAAMD_KEEP_GPU_VISIBLE" not in e:
+            pass
+        renv = env or {}
+        for k, v in (renv.get("env_vars") or {}).items():
+            e[k] = str(v)
+        if renv:
+            import json
+
+            e["CAAMD_RUNTIME_ENV"] = json.dumps(renv)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
+        log = open(os.path.join(self.session_dir, f"worker-{worker_id.hex()[:8]}.log"), "ab")
+        proc = subprocess.Popen([sys.executable, "-m", "cluster_anywhere_amd.core.worker_main"],
+                                env=e, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                                cwd=os.getcwd())
+        log.close()
+        w = WorkerInfo(worker_id=worker_id, pid=proc.pid, node=node, gpu_key=tuple(gpu_ids),
+                       kind="worker", proc=proc, alive=False)
+        self.workers[worker_id] = w
+        return w
+
+    def _dispatch_to(self, w: WorkerInfo, spec: TaskSpec):
+        w.idle = False
+        w.task = spec.task_id
+        spec.worker = w.worker_id
+        spec.node = w.node
+        spec.state = "running"
+        spec.start_time = time.time()
+        self.events.append(("start", spec.task_id, spec.fn_name, spec.start_time, w.pid))
+        w.tasks_inflight[spec.task_id] = spec
+        self._send(w.conn, ("execute", self._exec_payload(w, spec)))
+
+    def _exec_payload(self, w, spec):
+        fn_blob = None
+        if spec.fn_id is not None and spec.fn_id not in w.fns:
+            fn_blob = self.functions.get(spec.fn_id)
+            w.fns.add(spec.fn_id)
+        resolved = {}
+        for r in spec.arg_refs:
+            resolved[r] = self._obj_payload(r)
+        return (spec, fn_blob, resolved)
+
+    def _h_fetch_fn(self, c, req, fn_id):
+        self._reply(c, req, self.functions.get(fn_id))
+
+    def _h_task_done(self, c, task_id, results, error_kind, retryable):
+        spec = self.tasks.get(task_id)
+        w = self.conn_worker.get(c)
+        if w is not None:
+            w.tasks_inflight.pop(task_id, None)
+        if spec is None:
+            return
+        self.events.append(("end", task_id, spec.fn_name, time.time(), w.pid if w else None))
+        if error_kind == "app" and retryable and spec.attempt < (spec.max_retries or 0) and not spec.cancelled:
+            spec.attempt += 1
+            self._release(spec)
+            self._finish_worker(w, spec)
+            spec.state = "pending"
+            self._on_deps_ready(spec)
+            return
+        spec.state = "finished" if not error_kind else "failed"
+        for (oid, inline, size, node_hex, contained, is_err) in results:
+            self._seal_object(oid, inline, size, node_hex, contained, is_err)
+        if spec.generator is not None:
+            self._gen_end(task_id, len(results) if spec.generator == "dynamic" else None)
+        self._release(spec)
+        if spec.kind == ACTOR_METHOD:
+            a = self.actors.get(spec.actor_id)
+            if a is not None:
+                a.inflight.pop(task_id, None)
+                self._pump_actor(a)
+        elif spec.kind == ACTOR_CREATE:
+            a = self.actors.get(spec.actor_id)
+            if a is not None:
+                if error_kind:
+                    a.state = "DEAD"
+                    a.death_cause = "creation task failed"
+                    self._fail_actor_queue(a, "ActorDiedError", "actor constructor raised")
+                    self._kill_worker(a.worker)
+                else:
+                    a.state = "ALIVE"
+                    self._pump_actor(a)
+        else:
+            self._finish_worker(w, spec)
+        self._task_cleanup(spec)
+        self._schedule()
+
+    def _task_cleanup(self, spec):
+        if spec.kind == ACTOR_CREATE:
+            return  # creation args stay pinned for restarts; released when the actor dies
+        for r in list(spec.arg_refs) + list(spec.pinned_refs or ()):
+            e = self.objects.get(r)
+            if e is not None:
+                e.pins -= 1
+                self._maybe_free(r)
+        for oid in spec.return_ids or ():
+            self._maybe_free(oid)
+        if spec.kind != ACTOR_CREATE:
+            self.tasks.pop(spec.task_id, None)
+
+    def _finish_worker(self, w, spec):
+        if w is None or not w.alive or w.actor_id is not None:
+            return
+        w.task = None
+        w.idle = True
+        self.idle[(w.node, w.gpu_key)].append(w)
+
+    def _release(self, spec):
+        if spec.acquired and spec.kind != ACTOR_CREATE:
+            node, demand = spec.acquired
+            self.sched.release(node, demand)
+            for g in spec.gpu_ids or ():
+                self.free_gpus[node].append(g)
+            spec.acquired = None
+            self._retry_pending_pgs()
+            self._retry_infeasible()
+
+    def _retry_infeasible(self):
+        if not self.infeasible:
+            return
+        still = []
+        for spec in self.infeasible:
+            node = self.sched.pick_node(self._demand(spec), 0, "", False, "")
+            if node == "!":
+                still.append(spec)
+            else:
+                self._enqueue_ready(spec)
+        self.infeasible = still
+
+    def _fail_task(self, spec, err):
+        from ..exceptions import (ActorDiedError, TaskCancelledError, TaskPlacementGroupRemoved,
+                                  WorkerCrashedError, RayError)
+
+        kind, msg = err
+        cls = {"ActorDiedError": ActorDiedError, "TaskCancelledError": TaskCancelledError,
+               "WorkerCrashedError": WorkerCrashedError,
+               "TaskPlacementGroupRemoved": TaskPlacementGroupRemoved}.get(kind, RayError)
+        exc = cls(msg) if cls is not TaskCancelledError else TaskCancelledError(spec.task_id.hex(), msg)
+        blob = serialization.serialize(exc).to_bytes()
+        spec.state = "failed"
+        for oid in spec.return_ids or ():
+            self._seal_object(oid, blob, len(blob), None, (), True)
+        if spec.generator is not None:
+            self._gen_end(spec.task_id, 0, error=blob)
+        self._release(spec)
+        self._task_cleanup(spec)
+
+    # ----------------------------------------------------------- generators
+    def _h_gen_item(self, c, task_id, index, oid, inline, size, node_hex, contained, is_err=False):
+        self._obj(oid).refcount += 1  # held by the generator object on the owner side
+        self._seal_object(oid, inline, size, node_hex, contained, is_err)
+        for cb in list(self.gen_waiters.get((task_id, index), [])):
+            cb()
+        self.gen_waiters.pop((task_id, index), None)
+
+    def _gen_end(self, task_id, count, error=None):
+        key = ("__gen_end__", task_id)
+        self.kv[key] = (count, error)
+        for k in [k for k in self.gen_waiters if k[0] == task_id]:
+            for cb in self.gen_waiters.pop(k):
+                cb()
+
+    def _h_gen_next(self, c, req, task_id, index):
+        oid = ObjectID.for_task_return(task_id, index)
+
+        def answer():
+            e = self.objects.get(oid)
+            if e is not None and e.state == READY:
+                self._reply(c, req, ("item", oid))
+                return True
+            end = self.kv.get(("__gen_end__", task_id))
+            if end is not None:
+                count, err = end
+                if err is not None and index == 0:
+                    self._reply(c, req, ("error", err))
+                else:
+                    self._reply(c, req, ("end", None))
+                return True
+            return False
+
+        if not answer():
+            self.gen_waiters[(task_id, index)].append(answer)
+
+    # ------------------------------------------------------------------ actors
+    def _register_actor(self, spec, c):
+        opts = spec.actor_opts or {}
+        a = ActorInfo(actor_id=spec.actor_id, spec=spec, state="PENDING_CREATION",
+                      name=opts.get("name"), namespace=opts.get("namespace") or self.namespace,
+                      restarts_left=opts.get("max_restarts", 0) or 0,
+                      max_task_retries=opts.get("max_task_retries", 0) or 0,
+                      class_name=spec.fn_name, lifetime=opts.get("lifetime"),
+                      owner=self.clients.get(c, {}).get("id"))
+        self.actors[spec.actor_id] = a
+        if a.name:
+            self.named_actors[(a.namespace, a.name)] = spec.actor_id
+
+    def _h_check_name(self, c, req, namespace, name):
+        aid = self.named_actors.get((namespace or self.namespace, name))
+        if aid is not None and self.actors.get(aid) and self.actors[aid].state != "DEAD":
+            a = self.actors[aid]
+            self._reply(c, req, (aid, a.spec.actor_opts.get("handle_meta")))
+        else:
+            self._reply(c, req, None)
+
+    def _start_actor_on(self, a: ActorInfo, w: WorkerInfo):
+        w.actor_id = a.actor_id
+        w.idle = False
+        a.worker = w.worker_id
+        a.pid = w.pid
+        spec = a.spec
+        spec.worker = w.worker_id
+        spec.node = w.node
+        spec.state = "running"
+        spec.start_time = time.time()
+        a.state = "PENDING_CREATION" if a.num_restarts == 0 else "RESTARTING"
+        self.events.append(("start", spec.task_id, spec.fn_name, spec.start_time, w.pid))
+        w.tasks_inflight[spec.task_id] = spec
+        self._send(w.conn, ("execute", self._exec_payload(w, spec)))
+
+    def _pump_actor(self, a: ActorInfo):
+        if a.state == "DEAD":
+            self._fail_actor_queue(a, "ActorDiedError", a.death_cause or "actor is dead")
+            return
+        if a.state != "ALIVE":
+            return
+        w = self.workers.get(a.worker)
+        if w is None or not w.alive:
+            return
+        batch = []
+        while a.queue:
+            spec = a.queue.popleft()
+            if spec.cancelled:
+                continue
+            spec.worker = w.worker_id
+            spec.node = w.node
+            spec.state = "running"
+            spec.start_time = time.time()
+            a.inflight[spec.task_id] = spec
+            w.tasks_inflight[spec.task_id] = spec
+            self.events.append(("start", spec.task_id, spec.fn_name, spec.start_time, w.pid))
+            batch.append(("execute", self._exec_payload(w, spec)))
+        if batch and w.conn is not None:
+            try:
+                w.conn.sock.setblocking(True)
+                w.conn.send_many(batch)
+            except ConnectionClosed:
+                pass
+            finally:
+                try:
+                    w.conn.sock.setblocking(False)
+                except OSError:
+                    pass
+
+    def _fail_actor_queue(self, a, kind, msg):
+        while a.queue:
+            self._fail_task(a.queue.popleft(), (kind, msg))
+        for tid, spec in list(a.inflight.items()):
+            self._fail_task(spec, (kind, msg))
+        a.inflight.clear()
+
+    def _h_kill_actor(self, c, actor_id, no_restart):
+        a = self.actors.get(actor_id)
+        if a is None:
+            return
+        if no_restart:
+            a.restarts_left = 0
+        a.death_cause = "killed by ray.kill"
+        self._kill_worker(a.worker)
+
+    def _kill_worker(self, worker_id):
+        w = self.workers.get(worker_id)
+        if w is None:
+            return
+        try:
+            os.kill(w.pid, signal.SIGKILL)
+        except (ProcessLookupError, TypeError):
+            pass
+
+    def _h_actor_exit(self, c, actor_id):
+        a = self.actors.get(actor_id)
+        if a is not None:
+            a.restarts_left = 0
+            a.death_cause = "exit_actor() was called"
+
+    def _on_actor_worker_death(self, a: ActorInfo, w: WorkerInfo):
+        if a.acquired:
+            node, demand = a.acquired
+            if a.restarts_left == 0 or a.restarts_left is None:
+                self.sched.release(node, demand)
+                for g in a.gpu_ids or ():
+                    self.free_gpus[node].append(g)
+                a.acquired = None
+        if a.restarts_left and a.restarts_left != 0 and a.state != "DEAD":
+            if a.restarts_left > 0:
+                a.restarts_left -= 1
+            a.num_restarts += 1
+            a.state = "RESTARTING"
+            retry = a.max_task_retries != 0
+            for tid, spec in list(a.inflight.items()):
+                if retry:
+                    a.queue.appendleft(spec)
+                else:
+                    self._fail_task(spec, ("ActorDiedError", "actor died while running the task"))
+            a.inflight.clear()
+            wid = os.urandom(16)
+            self.pending_spawn[wid] = ("actor", a.actor_id)
+            self._spawn_worker(a.node, a.gpu_ids or (), worker_id=wid, env=a.spec.runtime_env)
+            return
+        a.state = "DEAD"
+        a.death_cause = a.death_cause or "the actor's worker process died"
+        self._fail_actor_queue(a, "ActorDiedError", a.death_cause)
+        if a.name:
+            self.named_actors.pop((a.namespace, a.name), None)
+        spec = a.spec
+        if spec is not None:
+            for r in list(spec.arg_refs) + list(spec.pinned_refs or ()):
+                e = self.objects.get(r)
+                if e is not None:
+                    e.pins -= 1
+                    self._maybe_free(r)
+            spec.arg_refs = []
+            spec.pinned_refs = []
+
+    # ------------------------------------------------------------ disconnects
+    def _on_disconnect(self, c: Conn):
+        try:
+            self.sel.unregister(c.sock)
+        except (KeyError, ValueError):
+            pass
+        c.close()
+        info = self.clients.pop(c, {})
+        w = self.conn_worker.pop(c, None)
+        if w is None:
+            if info.get("kind") == "driver":
+                self._on_driver_exit(info.get("id"))
+            return
+        w.alive = False
+        w.idle = False
+        try:
+            if w.proc is not None:
+                w.proc.wait(timeout=1)
+        except Exception:
+            pass
+        if w.actor_id is not None:
+            a = self.actors.get(w.actor_id)
+            if a is not None and a.worker == w.worker_id:
+                self._on_actor_worker_death(a, w)
+        for tid, spec in list(w.tasks_inflight.items()):
+            if spec.kind != NORMAL:
+                continue
+            self._release(spec)
+            if spec.cancelled:
+                self._fail_task(spec, ("TaskCancelledError", "task was cancelled"))
+            elif spec.attempt < (spec.max_retries if spec.max_retries is not None else 3):
+                spec.attempt += 1
+                spec.state = "pending"
+                self._enqueue_ready(spec)
+            else:
+                self._fail_task(spec, ("WorkerCrashedError", "the worker died while running the task"))
+        w.tasks_inflight.clear()
+        self.workers.pop(w.worker_id, None)
+        self._schedule()
+
+    def _on_driver_exit(self, driver_id):
+        # non-detached actors owned by the driver die with it (reference: actor lifetimes)
+        for a in list(self.actors.values()):
+            if a.owner == driver_id and a.lifetime != "detached" and a.state != "DEAD":
+                a.restarts_left = 0
+                a.death_cause = "owner exited"
+                self._kill_worker(a.worker)
+
+    def _health_check(self):
+        for w in list(self.workers.values()):
+            if w.proc is not None and w.proc.poll() is not None and not w.alive and w.conn is None:
+                # died before registering
+                key = (w.node, w.gpu_key)
+                self.starting[key] = max(0, self.starting[key] - 1)
+                self.workers.pop(w.worker_id, None)
+                pending = self.pending_spawn.pop(w.worker_id, None)
+                if pending and pending[0] == "actor":
+                    a = self.actors.get(pending[1])
+                    if a is not None:
+                        a.state = "DEAD"
+                        a.death_cause = "worker process failed to start (see session logs)"
+                        self._fail_actor_queue(a, "ActorDiedError", a.death_cause)
+                self._schedule()
+
+    # ------------------------------------------------ blocked in ray.get
+    def _h_blocked(self, c, task_id):
+        """A worker blocked in get() lends its CPUs back (reference: raylet
+        HandleNotifyWorkerBlocked) so nested tasks cannot deadlock the node."""
+        spec = self.tasks.get(task_id)
+        if spec is None or spec.kind != NORMAL or not spec.acquired or spec.blocked:
+            return
+        node, demand = spec.acquired
+        cpu = {k: v for k, v in demand.items() if k == "CPU" or k.startswith("CPU_group_")}
+        if cpu:
+            self.sched.release(node, cpu)
+            spec.blocked = cpu
+            self._schedule()
+
+    def _h_unblocked(self, c, task_id):
+        spec = self.tasks.get(task_id)
+        if spec is None or not spec.blocked:
+            return
+        node, _ = spec.acquired
+        # take the CPUs back even if that oversubscribes the node for a moment
+        self.sched.release(node, {k: -v for k, v in spec.blocked.items()})
+        spec.blocked = None
+
+    # ------------------------------------------------------------------ cancel
+    def _h_cancel(self, c, task_id, force, recursive):
+        spec = self.tasks.get(task_id)
+        if spec is None:
+            return
+        spec.cancelled = True
+        if spec.state == "pending":
+            self.waiting_deps.pop(task_id, None)
+            if spec.kind == ACTOR_METHOD:
+                a = self.actors.get(spec.actor_id)
+                if a is not None and spec in a.queue:
+                    a.queue.remove(spec)
+            self._fail_task(spec, ("TaskCancelledError", "task was cancelled before it ran"))
+        elif spec.state == "running":
+            w = self.workers.get(spec.worker)
+            if w is None:
+                return
+            if force and spec.kind == NORMAL:
+                self._kill_worker(w.worker_id)
+            else:
+                self._send(w.conn, ("cancel", task_id))
+
+    # ------------------------------------------------------- placement groups
+    def _h_pg_create(self, c, pg_id, bundles, strategy, name, ready_oid, lifetime):
+        codes = {"PACK": 0, "SPREAD": 1, "STRICT_PACK": 2, "STRICT_SPREAD": 3}
+        self.pgs[pg_id] = {"bundles": bundles, "strategy": strategy, "name": name, "state": "PENDING",
+                           "nodes": None, "ready_oid": ready_oid, "code": codes[strategy],
+                           "lifetime": lifetime}
+        self._obj(ready_oid).refcount += 1
+        if not self.sched.pg_feasible(bundles, codes[strategy]):
+            self.pgs[pg_id]["state"] = "INFEASIBLE"
+        self.pending_pgs.append(pg_id)
+        self._retry_pending_pgs()
+
+    def _retry_pending_pgs(self):
+        still = []
+        for pg_id in self.pending_pgs:
+            pg = self.pgs.get(pg_id)
+            if pg is None:
+                continue
+            nodes = self.sched.reserve_pg(pg_id.hex(), pg["bundles"], pg["code"])
+            if nodes or not pg["bundles"]:
+                pg["nodes"] = nodes
+                pg["state"] = "CREATED"
+                blob = serialization.serialize(True).to_bytes()
+                self._seal_object(pg["ready_oid"], blob, len(blob), None, ())
+                self._schedule()
+            else:
+                still.append(pg_id)
+        self.pending_pgs = still
+
+    def _h_pg_remove(self, c, pg_id):
+        pg = self.pgs.pop(pg_id, None)
+        if pg is None:
+            return
+        if pg_id in self.pending_pgs:
+            self.pending_pgs.remove(pg_id)
+        # actors placed in the group die with it (reference: ActorPlacementGroupRemoved)
+        for a in list(self.actors.values()):
+            st = a.spec.strategy if a.spec else None
+            if st and st[0] == "pg" and st[1] == pg_id and a.state != "DEAD":
+                a.restarts_left = 0
+                a.death_cause = "placement group removed"
+                if a.acquired:
+                    a.acquired = None  # group resources vanish with the group
+                self._kill_worker(a.worker)
+        self.sched.remove_pg(pg_id.hex())
+        self._retry_pending_pgs()
+        self._schedule()
+
+    def _h_pg_table(self, c, req, pg_id):
+        def fmt(pid, pg):
+            return {"placement_group_id": pid.hex(), "name": pg["name"], "strategy": pg["strategy"],
+                    "state": pg["state"], "bundles": {i: b for i, b in enumerate(pg["bundles"])},
+                    "bundles_to_node_id": {i: n for i, n in enumerate(pg["nodes"] or [])}}
+        if pg_id is not None:
+            pg = self.pgs.get(pg_id)
+            self._reply(c, req, fmt(pg_id, pg) if pg else None)
+        else:
+            self._reply(c, req, {pid.hex(): fmt(pid, pg) for pid, pg in self.pgs.items()})
+
+    def _h_pg_by_name(self, c, req, name):
+        for pid, pg in self.pgs.items():
+            if pg["name"] == name:
+                self._reply(c, req, (pid, pg["bundles"], pg["strategy"]))
+                return
+        self._reply(c, req, None)
+
+    # ------------------------------------------------------------- state API
+    def _h_state(self, c, req, what, arg):
+        self._reply(c, req, self.state(what, arg))
+
+    def state(self, what, arg=None):
+        if what == "cluster_resources":
+            return self.sched.cluster_total()
+        if what == "available_resources":
+            return {k: v for k, v in self.sched.cluster_available().items()}
+        if what == "available_per_node":
+            return {n: self.sched.available(n) for n in self.sched.nodes()}
+        if what == "nodes":
+            out = []
+            for n, info in self.node_info.items():
+                d = dict(info)
+                d["Resources"] = self.sched.total(n)
+                out.append(d)
+            return out
+        if what == "actors":
+            return [{"actor_id": a.actor_id.hex(), "class_name": a.class_name, "state": a.state,
+                     "name": a.name or "", "namespace": a.namespace, "pid": a.pid,
+                     "node_id": a.node, "num_restarts": a.num_restarts,
+                     "death_cause": a.death_cause} for a in self.actors.values()]
+        if what == "tasks":
+            return [{"task_id": t.task_id.hex(), "name": t.fn_name, "state": t.state,
+                     "kind": ["NORMAL_TASK", "ACTOR_CREATION_TASK", "ACTOR_TASK"][t.kind],
+                     "node_id": t.node, "attempt": t.attempt} for t in self.tasks.values()]
+        if what == "objects":
+            return [{"object_id": o.hex(), "state": ["PENDING", "READY", "FREED"][e.state],
+                     "size": e.size, "inline": e.inline is not None, "ref_count": e.refcount,
+                     "pins": e.pins, "spilled": e.spilled_path is not None}
+                    for o, e in self.objects.items()]
+        if what == "workers":
+            return [{"worker_id": w.worker_id.hex(), "pid": w.pid, "node_id": w.node,
+                     "alive": w.alive, "idle": w.idle, "actor_id": w.actor_id.hex() if w.actor_id else None,
+                     "gpu_ids": list(w.gpu_key or ())} for w in self.workers.values()]
+        if what == "placement_groups":
+            return [{"placement_group_id": p.hex(), "name": g["name"], "state": g["state"],
+                     "strategy": g["strategy"], "bundles": g["bundles"]} for p, g in self.pgs.items()]
+        if what == "jobs":
+            return [{"job_id": j.hex() if isinstance(j, bytes) else str(j), **v} for j, v in self.jobs.items()]
+        if what == "events":
+            return list(self.events)
+        if what == "store":
+            return {"capacity": self.store.capacity, "used": self.store.used,
+                    "num_objects": self.store.num_objects}
+        if what == "actor":
+            a = self.actors.get(arg)
+            return None if a is None else {"state": a.state, "name": a.name, "pid": a.pid,
+                                           "num_restarts": a.num_restarts}
+        if what == "named_actors":
+            return [(ns, n) for (ns, n), aid in self.named_actors.items()
+                    if self.actors.get(aid) and self.actors[aid].state != "DEAD"]
+        raise ValueError(what)
+
+    # -------------------------------------------------------------- nodes
+    def _h_add_node(self, c, req, node_hex, resources, gpu_ids, address):
+        self.sched.add_node(node_hex, resources)
+        self.free_gpus[node_hex] = list(gpu_ids)
+        self.node_info[node_hex] = {"NodeID": node_hex, "Alive": True, "NodeManagerAddress": address,
+                                    "Resources": dict(resources), "local": False}
+        self._reply(c, req, True)
+        self._retry_pending_pgs()
+        self._retry_infeasible()
+        self._schedule()
+
+    def _h_remove_node(self, c, node_hex):
+        self.sched.set_alive(node_hex, False)
+        if node_hex in self.node_info:
+            self.node_info[node_hex]["Alive"] = False
+
+    # -------------------------------------------------------------- shutdown
+    def shutdown(self):
+        if not self.running:
+            return
+        self.running = False
+        for w in list(self.workers.values()):
+            try:
+                if w.conn is not None:
+                    w.conn.close()
+            except Exception:
+                pass
+            try:
+                if w.pid:
+                    os.kill(w.pid, signal.SIGKILL)
+            except (ProcessLookupError, TypeError):
+                pass
+        for w in list(self.workers.values()):
+            try:
+                if w.proc is not None:
+                    w.proc.wait(timeout=2)
+            except Exception:
+                pass
+        try:
+            self._ww.send(b"x")
+        except OSError:
+            pass
+        if self.thread is not None:
+            self.thread.join(timeout=5)
+        try:
+            self.lsock.close()
+            os.unlink(self.sock_path)
+        except OSError:
+            pass
+        try:
+            self.store.unlink()
+        except Exception:
+            pass

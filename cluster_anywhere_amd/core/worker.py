@@ -1,0 +1,648 @@
+"""CoreWorker: the per-process client of the head (reference role:
+src/ray/core_worker/core_worker.cc + python/ray/_private/worker.py).
+
+Owns the control connection, the ordered reference-count stream, object
+put/get/wait against the shared-memory store, task submission, and (in worker
+processes) task execution: normal tasks, actor construction and actor methods
+(sequential, threaded via ``max_concurrency`` or asyncio for ``async def``
+methods), streaming / dynamic generators, cancellation and error propagation.
+"""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures
+import ctypes
+import hashlib
+import inspect
+import itertools
+import os
+import queue
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Dict, List, Optional
+
+from . import context, serialization
+from .head import ACTOR_CREATE, ACTOR_METHOD, INLINE_MAX, NORMAL, TaskSpec
+from .ids import ObjectID
+from .object_ref import DynamicObjectRefGenerator, ObjectRef, ObjectRefGenerator
+from .protocol import ConnectionClosed, connect
+
+
+class RefCounter:
+    """Process-local counts; 0->1 borrow announcements and 1->0 releases are
+    queued IN ORDER and flushed ahead of the next control message."""
+
+    def __init__(self):
+        self.counts: Dict[bytes, int] = {}
+        self.lock = threading.Lock()
+        self.ops: List[tuple] = []
+
+    def add(self, oid: bytes, announce: bool):
+        with self.lock:
+            c = self.counts.get(oid, 0)
+            self.counts[oid] = c + 1
+            if c == 0 and announce:
+                self.ops.append(("a", oid))
+
+    def remove(self, oid: bytes):
+        with self.lock:
+            c = self.counts.get(oid)
+            if c is None:
+                return
+            if c <= 1:
+                del self.counts[oid]
+                self.ops.append(("d", oid))
+            else:
+                self.counts[oid] = c - 1
+
+    def drain(self):
+        with self.lock:
+            ops, self.ops = self.ops, []
+        msgs = []
+        for kind, group in itertools.groupby(ops, key=lambda x: x[0]):
+            ids = [o for _, o in group]
+            msgs.append(("addref" if kind == "a" else "decref", ids))
+        return msgs
+
+
+class _Cancelled(BaseException):
+    pass
+
+
+class CoreWorker:
+    def __init__(self, address: str, kind: str, worker_id: bytes, node_hex: str = "",
+                 job_id: bytes = b"\x00\x00\x00\x01", extra: Optional[dict] = None):
+        self.address = address
+        self.kind = kind
+        self.worker_id = worker_id
+        self.job_id = job_id
+        self.conn = connect(address)
+        self.refs = RefCounter()
+        self.send_lock = threading.Lock()
+        self._req = itertools.count(1)
+        self.pending: Dict[int, concurrent.futures.Future] = {}
+        self.task_queue: "queue.Queue" = queue.Queue()
+        self.fn_cache: Dict[bytes, Any] = {}
+        self.sent_fns = set()
+        self.running_tasks: Dict[bytes, threading.Thread] = {}
+        self.cancelled_tasks = set()
+        self.actor_instance = None
+        self.actor_id = None
+        self.actor_opts = {}
+        self.async_loop = None
+        self.thread_pool = None
+        self.alive = True
+        self.conn.send(("register", kind, worker_id, os.getpid(), node_hex, dict(extra or {}, job_id=job_id)))
+        msg = self.conn.recv()
+        assert msg[0] == "registered", msg
+        info = msg[1]
+        self.node_hex = info["node_id"]
+        self.namespace = info["namespace"]
+        self.session_dir = info["session_dir"]
+        from .. import _native
+
+        self.store = _native.ObjectStore(info["store_name"], 0, 0, False)
+        self._reader = threading.Thread(target=self._read_loop, name="caamd-reader", daemon=True)
+        self._reader.start()
+        self._flusher = threading.Thread(target=self._flush_loop, name="caamd-flush", daemon=True)
+        self._flusher.start()
+
+    # ------------------------------------------------------------- transport
+    def send(self, msg):
+        # borrow announcements go BEFORE the message, releases AFTER it: a message
+        # may pin objects (task_done with nested refs, submit args) whose last
+        # local reference died while it was being built.
+        with self.send_lock:
+            ops = self.refs.drain()
+            if ops:
+                adds = [m for m in ops if m[0] == "addref"]
+                decs = [m for m in ops if m[0] == "decref"]
+                self.conn.send_many(adds + [msg] + decs)
+            else:
+                self.conn.send(msg)
+
+    def request(self, build, timeout=None):
+        req = next(self._req)
+        fut = concurrent.futures.Future()
+        self.pending[req] = fut
+        self.send(build(req))
+        try:
+            return fut.result(timeout)
+        finally:
+            self.pending.pop(req, None)
+
+    def request_async(self, build) -> concurrent.futures.Future:
+        req = next(self._req)
+        fut = concurrent.futures.Future()
+        self.pending[req] = fut
+        fut.add_done_callback(lambda f, r=req: self.pending.pop(r, None))
+        self.send(build(req))
+        return fut
+
+    def _flush_loop(self):
+        while self.alive:
+            time.sleep(0.05)
+            if self.refs.ops:
+                try:
+                    with self.send_lock:
+                        ops = self.refs.drain()
+                        if ops:
+                            self.conn.send_many(ops)
+                except (ConnectionClosed, OSError):
+                    return
+
+    def _read_loop(self):
+        while self.alive:
+            try:
+                msg = self.conn.recv()
+            except (ConnectionClosed, OSError):
+                self.alive = False
+                for f in list(self.pending.values()):
+                    if not f.done():
+                        f.set_exception(ConnectionError("connection to the head was lost"))
+                self.task_queue.put(None)
+                return
+            t = msg[0]
+            if t == "reply":
+                f = self.pending.get(msg[1])
+                if f is not None and not f.done():
+                    f.set_result(msg[2])
+            elif t == "execute":
+                self._on_execute(msg[1])
+            elif t == "cancel":
+                self._on_cancel(msg[1])
+            elif t == "exit":
+                self.task_queue.put(None)
+
+    def close(self):
+        self.alive = False
+        try:
+            with self.send_lock:
+                ops = self.refs.drain()
+                if ops:
+                    self.conn.send_many(ops)
+        except Exception:
+            pass
+        self.conn.close()
+
+    # ------------------------------------------------------------- objects
+    def _store(self, oid: bytes, so) -> tuple:
+        """-> (inline_bytes | None, size, node_hex | None)."""
+        size = so.total_bytes
+        if size <= INLINE_MAX:
+            return so.to_bytes(), size, None
+        off = self.store.create(oid, size, 0)
+        if off == -1:
+            self.request(lambda r: ("evict", r, size))
+            off = self.store.create(oid, size, 0)
+        if off < 0:
+            from ..exceptions import ObjectStoreFullError
+
+            raise ObjectStoreFullError(
+                f"object of {size} bytes does not fit in the object store "
+                f"(capacity {self.store.capacity}, used {self.store.used})")
+        so.write_into(self.store.buffer(off, size, False))
+        self.store.seal(oid)
+        return None, size, self.node_hex
+
+    def put(self, value, _owner_ref=True) -> ObjectRef:
+        if isinstance(value, ObjectRef):
+            raise TypeError("Calling put() on an ObjectRef is not allowed")
+        so = serialization.serialize(value)
+        oid = ObjectID.for_put(self.worker_id)
+        inline, size, node = self._store(oid, so)
+        self.send(("put", oid, inline, size, node, so.contained_refs, False))
+        return ObjectRef(oid, _owned=True)
+
+    def _materialize(self, oid, kind, payload):
+        from ..exceptions import ObjectLostError
+
+        if kind == "inline":
+            return serialization.deserialize(payload)
+        if kind == "store":
+            pb = self.store.get_pinned(oid)
+            if pb is None:
+                raise ObjectLostError(oid.hex(), "object is not in the local object store")
+            return serialization.deserialize(memoryview(pb))
+        if kind in ("err", "err_store"):
+            if kind == "err":
+                err = serialization.deserialize(payload)
+            else:
+                err = serialization.deserialize(memoryview(self.store.get_pinned(oid)))
+            raise _as_raisable(err)
+        if kind == "lost":
+            raise ObjectLostError(oid.hex())
+        raise RuntimeError(kind)
+
+    def get(self, refs, timeout=None):
+        from ..exceptions import GetTimeoutError
+
+        single = isinstance(refs, ObjectRef)
+        if single:
+            refs = [refs]
+        for r in refs:
+            if not isinstance(r, ObjectRef):
+                raise TypeError(f"get() expects ObjectRefs, got {type(r).__name__}")
+        ids = [r.binary() for r in refs]
+        blocked = self._maybe_blocked(True)
+        try:
+            res = self.request(lambda req: ("get", req, ids, timeout))
+        finally:
+            if blocked:
+                self._maybe_blocked(False)
+        if res is None:
+            raise GetTimeoutError(f"get() timed out after {timeout}s")
+        out = [self._materialize(o, k, p) for (o, k, p) in res]
+        return out[0] if single else out
+
+    def get_future(self, ref: ObjectRef) -> concurrent.futures.Future:
+        out = concurrent.futures.Future()
+        inner = self.request_async(lambda req: ("get", req, [ref.binary()], None))
+
+        def done(f):
+            try:
+                res = f.result()
+                o, k, p = res[0]
+                out.set_result(self._materialize(o, k, p))
+            except BaseException as e:
+                out.set_exception(e)
+
+        inner.add_done_callback(done)
+        return out
+
+    def wait(self, refs, num_returns=1, timeout=None, fetch_local=True):
+        ids = [r.binary() for r in refs]
+        if len(set(ids)) != len(ids):
+            raise ValueError("wait() requires a list of unique object refs")
+        if num_returns > len(ids):
+            raise ValueError("num_returns cannot exceed the number of refs")
+        blocked = self._maybe_blocked(True)
+        try:
+            ready = set(self.request(lambda req: ("wait", req, ids, num_returns, timeout)))
+        finally:
+            if blocked:
+                self._maybe_blocked(False)
+        r = [x for x in refs if x.binary() in ready]
+        nr = [x for x in refs if x.binary() not in ready]
+        return r, nr
+
+    def _maybe_blocked(self, on: bool) -> bool:
+        ctx = context.current_task()
+        if self.kind != "worker" or ctx is None or ctx.actor_id is not None:
+            return False
+        self.send(("blocked" if on else "unblocked", ctx.task_id))
+        return True
+
+    def free(self, refs):
+        self.send(("free", [r.binary() for r in refs]))
+
+    def gen_next(self, task_id, index):
+        return self.request(lambda req: ("gen_next", req, task_id, index))
+
+    # ------------------------------------------------------------- submission
+    def register_function(self, fn_id: bytes, blob_fn):
+        if fn_id not in self.sent_fns:
+            self.send(("fn", fn_id, blob_fn()))
+            self.sent_fns.add(fn_id)
+
+    def _pack_args(self, args, kwargs):
+        arg_refs, pinned = [], []
+        keep = []
+
+        def pack(v):
+            if isinstance(v, ObjectRef):
+                arg_refs.append(v.binary())
+                keep.append(v)
+                return ("r", v.binary())
+            so = serialization.serialize(v)
+            pinned.extend(so.contained_refs)
+            if so.total_bytes > INLINE_MAX:
+                ref = self.put(v)
+                keep.append(ref)
+                arg_refs.append(ref.binary())
+                return ("r", ref.binary())
+            return ("v", so.to_bytes())
+
+        pa = [pack(a) for a in args]
+        pk = {k: pack(v) for k, v in kwargs.items()}
+        return pa, pk, arg_refs, pinned, keep
+
+    def submit(self, kind, fn_id, fn_name, args, kwargs, num_returns=1, resources=None,
+               strategy=None, max_retries=0, retry_exceptions=False, actor_id=None, method=None,
+               actor_opts=None, runtime_env=None, name=None, concurrency_group=None):
+        task_id = os.urandom(16)
+        pa, pk, arg_refs, pinned, keep = self._pack_args(args, kwargs)
+        generator = None
+        if num_returns == "streaming":
+            generator = "streaming"
+            return_ids = []
+        elif num_returns == "dynamic":
+            generator = "dynamic"
+            return_ids = [ObjectID.for_task_return(task_id, 0)]
+        else:
+            return_ids = [ObjectID.for_task_return(task_id, i) for i in range(int(num_returns))]
+        ctx = context.current_task()
+        spec = TaskSpec(task_id=task_id, kind=kind, fn_id=fn_id, fn_name=fn_name, args=pa,
+                        kwargs=pk, arg_refs=arg_refs, pinned_refs=pinned, num_returns=num_returns,
+                        return_ids=return_ids, resources=resources or {}, strategy=strategy,
+                        max_retries=max_retries, retry_exceptions=retry_exceptions,
+                        actor_id=actor_id, method=method, actor_opts=actor_opts,
+                        runtime_env=runtime_env, name=name, job_id=self.job_id,
+                        generator=generator, parent=ctx.task_id if ctx else None,
+                        concurrency_group=concurrency_group)
+        self.send(("submit", spec))
+        del keep
+        if generator == "streaming":
+            return ObjectRefGenerator(task_id)
+        refs = [ObjectRef(o, _owned=True) for o in return_ids]
+        return refs
+
+    # ------------------------------------------------------------- execution
+    def _on_execute(self, payload):
+        spec, fn_blob, resolved = payload
+        if fn_blob is not None and spec.fn_id not in self.fn_cache:
+            self.fn_cache[spec.fn_id] = serialization.loads_function(fn_blob)
+        if spec.kind == ACTOR_METHOD and self.actor_instance is not None:
+            if self.async_loop is not None:
+                asyncio.run_coroutine_threadsafe(self._run_async(payload), self.async_loop)
+                return
+            if self.thread_pool is not None:
+                self.thread_pool.submit(self.execute, payload)
+                return
+        self.task_queue.put(payload)
+
+    def _on_cancel(self, task_id):
+        self.cancelled_tasks.add(task_id)
+        t = self.running_tasks.get(task_id)
+        if isinstance(t, threading.Thread):
+            ctypes.pythonapi.PyThreadState_SetAsyncExc(ctypes.c_ulong(t.ident), ctypes.py_object(_Cancelled))
+        elif t is not None and hasattr(t, "cancel"):
+            self.async_loop.call_soon_threadsafe(t.cancel)
+
+    def _resolve_args(self, spec, resolved):
+        def unpack(a):
+            if a[0] == "v":
+                return serialization.deserialize(a[1])
+            kind, payload = resolved[a[1]]
+            return self._materialize(a[1], kind, payload)
+
+        args = [unpack(a) for a in spec.args]
+        kwargs = {k: unpack(v) for k, v in spec.kwargs.items()}
+        return args, kwargs
+
+    def _function(self, spec):
+        fn = self.fn_cache.get(spec.fn_id)
+        if fn is None:
+            blob = self.request(lambda r: ("fetch_fn", r, spec.fn_id))
+            fn = serialization.loads_function(blob)
+            self.fn_cache[spec.fn_id] = fn
+        return fn
+
+    def _set_ctx(self, spec):
+        gpu_env = os.environ.get("CAAMD_GPU_IDS", "")
+        context.set_current_task(context.TaskContext(
+            task_id=spec.task_id, actor_id=self.actor_id if spec.kind != NORMAL else None,
+            fn_name=spec.fn_name, attempt=spec.attempt,
+            gpu_ids=[int(g) for g in gpu_env.split(",") if g != ""],
+            resources=spec.resources, pg=spec.strategy if spec.strategy and spec.strategy[0] == "pg" else None,
+        ))
+
+    def execute(self, payload):
+        spec, _, resolved = payload
+        self.running_tasks[spec.task_id] = threading.current_thread()
+        self._set_ctx(spec)
+        error_kind, retryable = None, False
+        try:
+            if spec.task_id in self.cancelled_tasks:
+                raise _Cancelled()
+            try:
+                args, kwargs = self._resolve_args(spec, resolved)
+            except Exception as dep_err:
+                from ..exceptions import RayError
+
+                if isinstance(dep_err, RayError):
+                    # a failed dependency: propagate the ORIGINAL error unchanged
+                    results = self._error_results(spec, dep_err, raw=True)
+                    self.running_tasks.pop(spec.task_id, None)
+                    self._reply_done(spec, results, "dep", False)
+                    context.set_current_task(None)
+                    return
+                raise
+            if spec.kind == ACTOR_CREATE:
+                cls = self._function(spec)
+                self.actor_id = spec.actor_id
+                self.actor_opts = spec.actor_opts or {}
+                context.current_task().actor_id = spec.actor_id
+                self.actor_instance = cls(*args, **kwargs)
+                self._setup_actor_concurrency(cls)
+                result = None
+            elif spec.kind == ACTOR_METHOD:
+                if self.actor_instance is None:
+                    raise RuntimeError("actor is not initialised")
+                if spec.method == "__ray_terminate__":
+                    self._exit_actor_after = True
+                    result = None
+                else:
+                    result = getattr(self.actor_instance, spec.method)(*args, **kwargs)
+            else:
+                result = self._function(spec)(*args, **kwargs)
+            results = self._package_results(spec, result)
+        except _Cancelled:
+            from ..exceptions import TaskCancelledError
+
+            results = self._error_results(spec, TaskCancelledError(spec.task_id.hex()), raw=True)
+            error_kind = "cancel"
+        except SystemExit as e:
+            if getattr(e, "_caamd_exit_actor", False):
+                results = self._package_results(spec, None)
+                self._reply_done(spec, results, None, False)
+                self.running_tasks.pop(spec.task_id, None)
+                self.send(("actor_exit", self.actor_id))
+                self._hard_exit()
+            results = self._error_results(spec, e)
+            error_kind = "app"
+        except BaseException as e:  # noqa
+            results = self._error_results(spec, e)
+            error_kind = "app"
+            retryable = _retryable(spec.retry_exceptions, e)
+        self.running_tasks.pop(spec.task_id, None)
+        if spec.task_id in self.cancelled_tasks and error_kind is None:
+            from ..exceptions import TaskCancelledError
+
+            results = self._error_results(spec, TaskCancelledError(spec.task_id.hex()), raw=True)
+            error_kind = "cancel"
+        self.cancelled_tasks.discard(spec.task_id)
+        self._reply_done(spec, results, error_kind, retryable)
+        context.set_current_task(None)
+        if getattr(self, "_exit_actor_after", False):
+            self._hard_exit()
+
+    def _hard_exit(self):
+        try:
+            self.close()
+        finally:
+            os._exit(0)
+
+    def _reply_done(self, spec, results, error_kind, retryable):
+        try:
+            self.send(("task_done", spec.task_id, results, error_kind, retryable))
+        except ConnectionClosed:
+            pass
+
+    def _setup_actor_concurrency(self, cls):
+        is_async = any(inspect.iscoroutinefunction(m) or inspect.isasyncgenfunction(m)
+                       for _, m in inspect.getmembers(cls, predicate=inspect.isfunction))
+        mc = self.actor_opts.get("max_concurrency")
+        if is_async:
+            self.async_loop = asyncio.new_event_loop()
+            self._async_sem = None
+            limit = mc or 1000
+            th = threading.Thread(target=self._run_loop, args=(limit,), daemon=True)
+            th.start()
+        elif mc and mc > 1:
+            self.thread_pool = concurrent.futures.ThreadPoolExecutor(mc)
+
+    def _run_loop(self, limit):
+        asyncio.set_event_loop(self.async_loop)
+        self._async_sem = asyncio.Semaphore(limit)
+        self.async_loop.run_forever()
+
+    async def _run_async(self, payload):
+        spec, _, resolved = payload
+        while self._async_sem is None:
+            await asyncio.sleep(0.001)
+        async with self._async_sem:
+            self._set_ctx(spec)
+            error_kind, retryable = None, False
+            task = asyncio.current_task()
+            self.running_tasks[spec.task_id] = task
+            try:
+                args, kwargs = self._resolve_args(spec, resolved)
+                m = getattr(self.actor_instance, spec.method)
+                if inspect.isasyncgenfunction(m):
+                    items = []
+                    async for x in m(*args, **kwargs):
+                        items.append(x)
+                    result = items
+                    if spec.generator is not None:
+                        result = iter(items)
+                else:
+                    result = m(*args, **kwargs)
+                    if inspect.isawaitable(result):
+                        result = await result
+                results = self._package_results(spec, result)
+            except asyncio.CancelledError:
+                from ..exceptions import TaskCancelledError
+
+                results = self._error_results(spec, TaskCancelledError(spec.task_id.hex()), raw=True)
+                error_kind = "cancel"
+            except SystemExit as e:
+                if getattr(e, "_caamd_exit_actor", False):
+                    self._reply_done(spec, self._package_results(spec, None), None, False)
+                    self.send(("actor_exit", self.actor_id))
+                    self._hard_exit()
+                results = self._error_results(spec, e)
+                error_kind = "app"
+            except BaseException as e:  # noqa
+                results = self._error_results(spec, e)
+                error_kind = "app"
+                retryable = _retryable(spec.retry_exceptions, e)
+            self.running_tasks.pop(spec.task_id, None)
+            self._reply_done(spec, results, error_kind, retryable)
+
+    def _package_results(self, spec, result):
+        if spec.generator == "streaming":
+            return self._stream(spec, result)
+        if spec.generator == "dynamic":
+            refs = []
+            for i, item in enumerate(result):
+                oid = ObjectID.for_task_return(spec.task_id, i + 1)
+                so = serialization.serialize(item)
+                inline, size, node = self._store(oid, so)
+                self.send(("put", oid, inline, size, node, so.contained_refs, False))
+                refs.append(ObjectRef(oid, _owned=True))
+            result = DynamicObjectRefGenerator(refs)
+            return [self._result_entry(spec.return_ids[0], result)]
+        n = spec.num_returns
+        if n == 1:
+            return [self._result_entry(spec.return_ids[0], result)]
+        if n == 0:
+            return []
+        vals = tuple(result) if result is not None else None
+        if vals is None or len(vals) != n:
+            raise ValueError(f"task declared num_returns={n} but returned {result!r}")
+        return [self._result_entry(o, v) for o, v in zip(spec.return_ids, vals)]
+
+    def _stream(self, spec, gen):
+        i = 0
+        try:
+            for item in gen:
+                oid = ObjectID.for_task_return(spec.task_id, i)
+                so = serialization.serialize(item)
+                inline, size, node = self._store(oid, so)
+                self.send(("gen_item", spec.task_id, i, oid, inline, size, node, so.contained_refs, False))
+                i += 1
+        except BaseException as e:  # noqa
+            from ..exceptions import RayTaskError
+
+            err = RayTaskError.from_exception(spec.fn_name, e)
+            oid = ObjectID.for_task_return(spec.task_id, i)
+            blob = serialization.serialize(err).to_bytes()
+            self.send(("gen_item", spec.task_id, i, oid, blob, len(blob), None, [], True))
+        return []
+
+    def _result_entry(self, oid, value):
+        if isinstance(value, ObjectRef):
+            # returning a ref: the result object holds the ref (nested)
+            pass
+        so = serialization.serialize(value)
+        inline, size, node = self._store(oid, so)
+        return (oid, inline, size, node, so.contained_refs, False)
+
+    def _error_results(self, spec, exc, raw=False):
+        from ..exceptions import RayTaskError
+
+        err = exc if raw else RayTaskError.from_exception(
+            f"{spec.fn_name}" + (f".{spec.method}" if spec.method else ""), exc)
+        blob = serialization.serialize(err).to_bytes()
+        ids = list(spec.return_ids or [])
+        if spec.generator == "streaming":
+            oid = ObjectID.for_task_return(spec.task_id, 0)
+            self.send(("gen_item", spec.task_id, 0, oid, blob, len(blob), None, [], True))
+            return []
+        return [(oid, blob, len(blob), None, [], True) for oid in ids]
+
+    # ------------------------------------------------------------- worker main
+    def run_worker_loop(self):
+        while True:
+            item = self.task_queue.get()
+            if item is None:
+                break
+            self.execute(item)
+
+
+def _retryable(retry_exceptions, e) -> bool:
+    if retry_exceptions is True:
+        return True
+    if isinstance(retry_exceptions, (list, tuple)):
+        return isinstance(e, tuple(retry_exceptions))
+    return False
+
+
+def _as_raisable(err):
+    from ..exceptions import RayTaskError
+
+    if isinstance(err, RayTaskError):
+        return err.as_instanceof_cause()
+    return err
+
+
+def function_id(fn) -> bytes:
+    name = f"{getattr(fn, '__module__', '')}.{getattr(fn, '__qualname__', repr(fn))}"
+    try:
+        src = inspect.getsource(fn)
+    except Exception:
+        src = ""
+    return hashlib.blake2b((name + src + str(id(fn))).encode(), digest_size=16).digest()

@@ -1,0 +1,142 @@
+"""Lazy task DAGs (reference: python/ray/dag/): ``f.bind(...)``, ``Cls.bind(...)``,
+``actor.method.bind(...)``, ``InputNode``, ``MultiOutputNode``; ``dag.execute(x)``
+submits the graph as ordinary tasks (ObjectRefs flow between nodes, so the
+scheduler overlaps independent branches); ``dag.experimental_compile()`` builds a
+:class:`~cluster_anywhere_amd.dag.compiled.CompiledDAG` that re-executes the same
+actor pipeline with pre-resolved handles and no per-call graph walk."""
+from __future__ import annotations
+
+from typing import Any, Dict, List
+
+
+class DAGNode:
+    def __init__(self, args, kwargs):
+        self._args = tuple(args)
+        self._kwargs = dict(kwargs)
+
+    def _children(self):
+        out = [a for a in self._args if isinstance(a, DAGNode)]
+        out += [v for v in self._kwargs.values() if isinstance(v, DAGNode)]
+        return out
+
+    def _resolve_args(self, cache, inp):
+        a = [x._exec(cache, inp) if isinstance(x, DAGNode) else x for x in self._args]
+        k = {n: (v._exec(cache, inp) if isinstance(v, DAGNode) else v) for n, v in self._kwargs.items()}
+        return a, k
+
+    def _exec(self, cache, inp):
+        key = id(self)
+        if key not in cache:
+            cache[key] = self._run(cache, inp)
+        return cache[key]
+
+    def _run(self, cache, inp):  # pragma: no cover
+        raise NotImplementedError
+
+    def execute(self, *args, **kwargs):
+        inp = InputValue(args, kwargs)
+        return self._exec({}, inp)
+
+    def experimental_compile(self, **kw):
+        from .compiled import CompiledDAG
+
+        return CompiledDAG(self, **kw)
+
+
+class InputValue:
+    def __init__(self, args, kwargs):
+        self.args, self.kwargs = args, kwargs
+
+
+class InputNode(DAGNode):
+    def __init__(self):
+        super().__init__((), {})
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *e):
+        return False
+
+    def _run(self, cache, inp):
+        if len(inp.args) == 1 and not inp.kwargs:
+            return inp.args[0]
+        return inp.args if inp.args else inp.kwargs
+
+    def __getitem__(self, key):
+        return InputAttributeNode(self, key)
+
+    def __getattr__(self, key):
+        if key.startswith("_"):
+            raise AttributeError(key)
+        return InputAttributeNode(self, key)
+
+
+class InputAttributeNode(DAGNode):
+    def __init__(self, parent, key):
+        super().__init__((), {})
+        self._parent, self._key = parent, key
+
+    def _run(self, cache, inp):
+        if isinstance(self._key, int):
+            return inp.args[self._key]
+        return inp.kwargs[self._key] if self._key in inp.kwargs else getattr(inp.args[0], self._key)
+
+
+class FunctionNode(DAGNode):
+    def __init__(self, rf, args, kwargs, options):
+        super().__init__(args, kwargs)
+        self._rf = rf
+        self._options = options
+
+    def _run(self, cache, inp):
+        a, k = self._resolve_args(cache, inp)
+        return self._rf.remote(*a, **k)
+
+
+class ClassNode(DAGNode):
+    def __init__(self, ac, args, kwargs):
+        super().__init__(args, kwargs)
+        self._ac = ac
+        self._handle = None
+
+    def _run(self, cache, inp):
+        if self._handle is None:
+            a, k = self._resolve_args(cache, inp)
+            self._handle = self._ac.remote(*a, **k)
+        return self._handle
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        node = self
+
+        class _M:
+            def bind(_, *args, **kwargs):
+                return ClassMethodNode(node, name, args, kwargs, 1)
+
+        return _M()
+
+
+class ClassMethodNode(DAGNode):
+    def __init__(self, target, method, args, kwargs, num_returns):
+        super().__init__(args, kwargs)
+        self._target = target
+        self._method = method
+        self._num_returns = num_returns
+
+    def _run(self, cache, inp):
+        h = self._target._exec(cache, inp) if isinstance(self._target, DAGNode) else self._target
+        a, k = self._resolve_args(cache, inp)
+        return getattr(h, self._method).remote(*a, **k)
+
+
+class MultiOutputNode(DAGNode):
+    def __init__(self, outputs: List[DAGNode]):
+        super().__init__(tuple(outputs), {})
+
+    def _run(self, cache, inp):
+        return [x._exec(cache, inp) if isinstance(x, DAGNode) else x for x in self._args]
+
+
+__all__ = ["DAGNode", "InputNode", "FunctionNode", "ClassNode", "ClassMethodNode", "MultiOutputNode"]

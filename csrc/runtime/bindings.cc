@@ -1,0 +1,106 @@
+// pybind11 bindings of the native runtime: object store + cluster scheduler.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "object_store.h"
+#include "scheduler.h"
+
+namespace py = pybind11;
+using namespace caamd_rt;
+
+// A sealed object's payload exported through the Python buffer protocol. It
+// holds a pin on the object for as long as any memoryview / numpy array /
+// torch tensor derived from it is alive; the pin is dropped in the destructor,
+// which is what lets the store defer freeing deleted-but-still-viewed objects.
+struct PinnedBuffer {
+  std::shared_ptr<ObjectStore> store;
+  std::string id;
+  uint64_t off, size, meta;
+  ~PinnedBuffer() {
+    if (store) store->unpin(id);
+  }
+};
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "cluster_anywhere_amd native runtime (object store, scheduler)";
+
+  py::class_<PinnedBuffer>(m, "PinnedBuffer", py::buffer_protocol())
+      .def_buffer([](PinnedBuffer& b) -> py::buffer_info {
+        return py::buffer_info(b.store->base() + b.off, 1, py::format_descriptor<uint8_t>::format(),
+                               1, {(ssize_t)b.size}, {1}, /*readonly=*/true);
+      })
+      .def_readonly("size", &PinnedBuffer::size)
+      .def_readonly("meta", &PinnedBuffer::meta);
+
+  py::class_<ObjectStore, std::shared_ptr<ObjectStore>>(m, "ObjectStore")
+      .def(py::init<const std::string&, uint64_t, uint64_t, bool>(), py::arg("name"),
+           py::arg("capacity") = 0, py::arg("table_capacity") = 1 << 16, py::arg("create") = false)
+      .def("create",
+           [](ObjectStore& s, py::bytes id, uint64_t size, uint64_t meta) {
+             py::gil_scoped_release g;
+             return s.create(std::string(id), size, meta);
+           },
+           py::arg("id"), py::arg("size"), py::arg("meta") = 0)
+      .def("seal", [](ObjectStore& s, py::bytes id) { return s.seal(std::string(id)); })
+      .def("lookup",
+           [](ObjectStore& s, py::bytes id, bool pin) -> py::object {
+             uint64_t off, size, meta;
+             if (!s.lookup(std::string(id), &off, &size, &meta, pin)) return py::none();
+             return py::make_tuple(off, size, meta);
+           },
+           py::arg("id"), py::arg("pin") = false)
+      .def("unpin", [](ObjectStore& s, py::bytes id) { s.unpin(std::string(id)); })
+      .def("get_pinned",
+           [](std::shared_ptr<ObjectStore> s, py::bytes id) -> py::object {
+             uint64_t off, size, meta;
+             std::string sid(id);
+             if (!s->lookup(sid, &off, &size, &meta, true)) return py::none();
+             auto pb = new PinnedBuffer{s, sid, off, size, meta};
+             return py::cast(pb, py::return_value_policy::take_ownership);
+           })
+      .def("contains", [](ObjectStore& s, py::bytes id) { return s.contains(std::string(id)); })
+      .def("remove", [](ObjectStore& s, py::bytes id) { return s.remove(std::string(id)); })
+      .def("abort", [](ObjectStore& s, py::bytes id) { return s.abort(std::string(id)); })
+      .def("buffer",
+           [](ObjectStore& s, uint64_t off, uint64_t size, bool readonly) {
+             return py::memoryview::from_memory(s.base() + off, (ssize_t)size, readonly);
+           },
+           py::arg("offset"), py::arg("size"), py::arg("readonly") = true)
+      .def("address", [](ObjectStore& s, uint64_t off) { return (uintptr_t)(s.base() + off); })
+      .def("lru_candidates",
+           [](ObjectStore& s, uint64_t n) {
+             std::vector<py::bytes> out;
+             for (auto& x : s.lru_candidates(n)) out.emplace_back(x);
+             return out;
+           })
+      .def("list_ids",
+           [](ObjectStore& s) {
+             std::vector<py::bytes> out;
+             for (auto& x : s.list_ids()) out.emplace_back(x);
+             return out;
+           })
+      .def("largest_free", &ObjectStore::largest_free)
+      .def("unlink", &ObjectStore::unlink)
+      .def_property_readonly("capacity", &ObjectStore::capacity)
+      .def_property_readonly("used", &ObjectStore::used)
+      .def_property_readonly("num_objects", &ObjectStore::num_objects)
+      .def_property_readonly("name", &ObjectStore::name);
+
+  py::class_<ClusterScheduler>(m, "ClusterScheduler")
+      .def(py::init<double>(), py::arg("spread_threshold") = 0.5)
+      .def("add_node", &ClusterScheduler::add_node)
+      .def("remove_node", &ClusterScheduler::remove_node)
+      .def("set_alive", &ClusterScheduler::set_alive)
+      .def("total", &ClusterScheduler::total)
+      .def("available", &ClusterScheduler::available)
+      .def("cluster_total", &ClusterScheduler::cluster_total)
+      .def("cluster_available", &ClusterScheduler::cluster_available)
+      .def("nodes", &ClusterScheduler::nodes)
+      .def("pick_node", &ClusterScheduler::pick_node, py::arg("demand"), py::arg("strategy") = 0,
+           py::arg("affinity_node") = "", py::arg("soft") = false, py::arg("preferred_node") = "")
+      .def("acquire", &ClusterScheduler::acquire)
+      .def("release", &ClusterScheduler::release)
+      .def("reserve_pg", &ClusterScheduler::reserve_pg)
+      .def("remove_pg", &ClusterScheduler::remove_pg)
+      .def("pg_feasible", &ClusterScheduler::pg_feasible);
+}

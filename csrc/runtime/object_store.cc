@@ -1,0 +1,333 @@
+#include "object_store.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <stdexcept>
+
+namespace caamd_rt {
+
+static constexpr uint64_t kMagic = 0x43414d444f424a31ull;  // "CAMDOBJ1"
+static constexpr uint64_t kMinBlock = 128;
+
+static inline uint64_t round_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+static inline uint64_t hash_id(const uint8_t* id) {
+  uint64_t h = 1469598103934665603ull;
+  for (int i = 0; i < kIdBytes; ++i) {
+    h ^= id[i];
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+ObjectStore::ObjectStore(const std::string& name, uint64_t capacity, uint64_t table_capacity,
+                         bool create)
+    : name_(name) {
+  if (create) {
+    uint64_t tc = 1;
+    while (tc < table_capacity) tc <<= 1;
+    const uint64_t table_off = round_up(sizeof(Header), 4096);
+    const uint64_t data_off = round_up(table_off + tc * sizeof(ObjectEntry), 4096);
+    const uint64_t data_size = round_up(std::max<uint64_t>(capacity, 1 << 20), kAlign);
+    map_size_ = data_off + data_size;
+    shm_unlink(name.c_str());
+    fd_ = shm_open(name.c_str(), O_CREAT | O_RDWR | O_EXCL, 0600);
+    if (fd_ < 0) throw std::runtime_error("shm_open(create) failed: " + std::string(strerror(errno)));
+    if (ftruncate(fd_, (off_t)map_size_) != 0) {
+      close(fd_);
+      shm_unlink(name.c_str());
+      throw std::runtime_error("ftruncate failed: " + std::string(strerror(errno)));
+    }
+    base_ = (uint8_t*)mmap(nullptr, map_size_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);
+    if (base_ == MAP_FAILED) throw std::runtime_error("mmap failed");
+    hdr_ = reinterpret_cast<Header*>(base_);
+    hdr_->total_size = map_size_;
+    hdr_->table_offset = table_off;
+    hdr_->table_capacity = tc;
+    hdr_->data_offset = data_off;
+    hdr_->data_size = data_size;
+    hdr_->used_bytes = 0;
+    hdr_->num_objects = 0;
+    hdr_->tick = 0;
+    pthread_mutexattr_t a;
+    pthread_mutexattr_init(&a);
+    pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
+    pthread_mutexattr_setrobust(&a, PTHREAD_MUTEX_ROBUST);
+    pthread_mutex_init(&hdr_->mu, &a);
+    pthread_mutexattr_destroy(&a);
+    table_ = reinterpret_cast<ObjectEntry*>(base_ + table_off);
+    // one free block spanning the data region
+    BlockHdr* b = B(data_off);
+    b->size = data_size;
+    b->prev_size = 0;
+    b->free = 1;
+    b->next_free = b->prev_free = 0;
+    hdr_->free_head = data_off;
+    __atomic_store_n(&hdr_->magic, kMagic, __ATOMIC_RELEASE);
+  } else {
+    fd_ = shm_open(name.c_str(), O_RDWR, 0600);
+    if (fd_ < 0) throw std::runtime_error("shm_open(attach) failed: " + std::string(strerror(errno)));
+    struct stat st;
+    fstat(fd_, &st);
+    map_size_ = (uint64_t)st.st_size;
+    base_ = (uint8_t*)mmap(nullptr, map_size_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);
+    if (base_ == MAP_FAILED) throw std::runtime_error("mmap failed");
+    hdr_ = reinterpret_cast<Header*>(base_);
+    if (__atomic_load_n(&hdr_->magic, __ATOMIC_ACQUIRE) != kMagic)
+      throw std::runtime_error("object store arena has a bad magic");
+    table_ = reinterpret_cast<ObjectEntry*>(base_ + hdr_->table_offset);
+  }
+}
+
+ObjectStore::~ObjectStore() {
+  if (base_ && base_ != MAP_FAILED) munmap(base_, map_size_);
+  if (fd_ >= 0) close(fd_);
+}
+
+void ObjectStore::unlink() { shm_unlink(name_.c_str()); }
+
+void ObjectStore::lock() {
+  int r = pthread_mutex_lock(&hdr_->mu);
+  if (r == EOWNERDEAD) pthread_mutex_consistent(&hdr_->mu);  // a worker died holding it
+}
+void ObjectStore::unlock() { pthread_mutex_unlock(&hdr_->mu); }
+
+ObjectEntry* ObjectStore::find(const uint8_t* id, bool for_insert) {
+  const uint64_t mask = hdr_->table_capacity - 1;
+  uint64_t i = hash_id(id) & mask;
+  ObjectEntry* tomb = nullptr;
+  for (uint64_t n = 0; n <= mask; ++n, i = (i + 1) & mask) {
+    ObjectEntry* e = &table_[i];
+    if (e->state == 0) return for_insert ? (tomb ? tomb : e) : nullptr;
+    if (e->state == 3) {
+      if (!tomb) tomb = e;
+      continue;
+    }
+    if (memcmp(e->id, id, kIdBytes) == 0) return e;
+  }
+  return for_insert ? tomb : nullptr;
+}
+
+void ObjectStore::fl_insert(uint64_t blk) {
+  BlockHdr* b = B(blk);
+  b->free = 1;
+  b->prev_free = 0;
+  b->next_free = hdr_->free_head;
+  if (hdr_->free_head) B(hdr_->free_head)->prev_free = blk;
+  hdr_->free_head = blk;
+}
+
+void ObjectStore::fl_remove(uint64_t blk) {
+  BlockHdr* b = B(blk);
+  if (b->prev_free) B(b->prev_free)->next_free = b->next_free;
+  else hdr_->free_head = b->next_free;
+  if (b->next_free) B(b->next_free)->prev_free = b->prev_free;
+  b->free = 0;
+  b->next_free = b->prev_free = 0;
+}
+
+uint64_t ObjectStore::alloc(uint64_t size) {
+  const uint64_t need = std::max(kMinBlock, round_up(size + sizeof(BlockHdr), kAlign));
+  const uint64_t end = hdr_->data_offset + hdr_->data_size;
+  // best fit among the first few candidates (bounded scan keeps it O(1)-ish)
+  uint64_t best = 0, best_size = ~0ull;
+  int scanned = 0;
+  for (uint64_t f = hdr_->free_head; f; f = B(f)->next_free) {
+    const uint64_t s = B(f)->size;
+    if (s >= need && s < best_size) {
+      best = f;
+      best_size = s;
+      if (s - need < kMinBlock) break;
+    }
+    if (best && ++scanned > 64) break;
+  }
+  if (!best) return 0;
+  fl_remove(best);
+  BlockHdr* b = B(best);
+  if (b->size - need >= kMinBlock) {
+    const uint64_t rest = best + need;
+    BlockHdr* r = B(rest);
+    r->size = b->size - need;
+    r->prev_size = need;
+    const uint64_t nxt = rest + r->size;
+    if (nxt < end) B(nxt)->prev_size = r->size;
+    b->size = need;
+    fl_insert(rest);
+  }
+  b->free = 0;
+  hdr_->used_bytes += b->size;
+  return best;
+}
+
+void ObjectStore::free_block(uint64_t blk) {
+  const uint64_t end = hdr_->data_offset + hdr_->data_size;
+  BlockHdr* b = B(blk);
+  hdr_->used_bytes -= b->size;
+  // coalesce with next
+  uint64_t nxt = blk + b->size;
+  if (nxt < end && B(nxt)->free) {
+    fl_remove(nxt);
+    b->size += B(nxt)->size;
+  }
+  // coalesce with prev
+  if (b->prev_size) {
+    const uint64_t prv = blk - b->prev_size;
+    if (B(prv)->free) {
+      fl_remove(prv);
+      B(prv)->size += b->size;
+      blk = prv;
+      b = B(prv);
+    }
+  }
+  nxt = blk + b->size;
+  if (nxt < end) B(nxt)->prev_size = b->size;
+  fl_insert(blk);
+}
+
+int64_t ObjectStore::create(const std::string& id, uint64_t size, uint64_t meta) {
+  if (id.size() != kIdBytes) throw std::invalid_argument("object id must be 24 bytes");
+  lock();
+  ObjectEntry* e = find((const uint8_t*)id.data(), true);
+  if (!e) {
+    unlock();
+    return -3;  // table full
+  }
+  if (e->state == 1 || e->state == 2 || e->state == 4) {
+    if (memcmp(e->id, id.data(), kIdBytes) == 0) {
+      unlock();
+      return -2;
+    }
+  }
+  const uint64_t blk = alloc(size);
+  if (!blk) {
+    unlock();
+    return -1;
+  }
+  memcpy(e->id, id.data(), kIdBytes);
+  e->offset = blk + sizeof(BlockHdr);
+  e->size = size;
+  e->meta = meta;
+  e->state = 1;
+  e->pins = 0;
+  e->lru = ++hdr_->tick;
+  hdr_->num_objects++;
+  const int64_t off = (int64_t)e->offset;
+  unlock();
+  return off;
+}
+
+bool ObjectStore::seal(const std::string& id) {
+  lock();
+  ObjectEntry* e = find((const uint8_t*)id.data(), false);
+  bool ok = e && e->state == 1;
+  if (ok) __atomic_store_n(&e->state, 2u, __ATOMIC_RELEASE);
+  unlock();
+  return ok;
+}
+
+bool ObjectStore::lookup(const std::string& id, uint64_t* off, uint64_t* size, uint64_t* meta,
+                         bool pin) {
+  lock();
+  ObjectEntry* e = find((const uint8_t*)id.data(), false);
+  bool ok = e && e->state == 2;
+  if (ok) {
+    *off = e->offset;
+    *size = e->size;
+    *meta = e->meta;
+    e->lru = ++hdr_->tick;
+    if (pin) e->pins++;
+  }
+  unlock();
+  return ok;
+}
+
+void ObjectStore::unpin(const std::string& id) {
+  lock();
+  ObjectEntry* e = find((const uint8_t*)id.data(), false);
+  if (e && e->pins > 0) {
+    e->pins--;
+    if (e->pins == 0 && e->state == 4) {  // deletion was deferred while readers held views
+      free_block(e->offset - sizeof(BlockHdr));
+      e->state = 3;
+    }
+  }
+  unlock();
+}
+
+bool ObjectStore::contains(const std::string& id) {
+  lock();
+  ObjectEntry* e = find((const uint8_t*)id.data(), false);
+  bool ok = e && e->state == 2;
+  unlock();
+  return ok;
+}
+
+bool ObjectStore::remove(const std::string& id) {
+  lock();
+  ObjectEntry* e = find((const uint8_t*)id.data(), false);
+  bool ok = e != nullptr && e->state != 4;
+  if (ok) {
+    hdr_->num_objects--;
+    if (e->pins > 0) {
+      e->state = 4;  // zombie: freed by the last unpin
+    } else {
+      free_block(e->offset - sizeof(BlockHdr));
+      e->state = 3;
+    }
+  }
+  unlock();
+  return ok;
+}
+
+bool ObjectStore::abort(const std::string& id) {
+  lock();
+  ObjectEntry* e = find((const uint8_t*)id.data(), false);
+  bool ok = e && e->state == 1;
+  if (ok) {
+    free_block(e->offset - sizeof(BlockHdr));
+    e->state = 3;
+    hdr_->num_objects--;
+  }
+  unlock();
+  return ok;
+}
+
+std::vector<std::string> ObjectStore::lru_candidates(uint64_t max_count) {
+  std::vector<std::pair<uint64_t, std::string>> c;
+  lock();
+  for (uint64_t i = 0; i < hdr_->table_capacity; ++i) {
+    ObjectEntry* e = &table_[i];
+    if (e->state == 2 && e->pins == 0)
+      c.emplace_back(e->lru, std::string((const char*)e->id, kIdBytes));
+  }
+  unlock();
+  std::sort(c.begin(), c.end());
+  std::vector<std::string> out;
+  for (size_t i = 0; i < c.size() && i < max_count; ++i) out.push_back(c[i].second);
+  return out;
+}
+
+std::vector<std::string> ObjectStore::list_ids() {
+  std::vector<std::string> out;
+  lock();
+  for (uint64_t i = 0; i < hdr_->table_capacity; ++i)
+    if (table_[i].state == 2) out.emplace_back((const char*)table_[i].id, kIdBytes);
+  unlock();
+  return out;
+}
+
+uint64_t ObjectStore::largest_free() {
+  lock();
+  uint64_t m = 0;
+  for (uint64_t f = hdr_->free_head; f; f = B(f)->next_free) m = std::max(m, B(f)->size);
+  unlock();
+  return m > sizeof(BlockHdr) ? m - sizeof(BlockHdr) : 0;
+}
+
+}  // namespace caamd_rt

