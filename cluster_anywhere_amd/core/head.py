@@ -722,11 +722,13 @@ class Head:
         e["CAAMD_WORKER_ID"] = worker_id.hex()
         e["CAAMD_NODE_ID"] = node
         e["CAAMD_GPU_IDS"] = ",".join(str(g) for g in gpu_ids)
-        if gpu_ids:
-            e["ROCR_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpu_ids)
-        elif "CAAMD_KEEP_GPU_VISIBLE" not in e:
-            pass
         renv = env or {}
+        noset = (renv.get("env_vars") or {}).get("CAAMD_NOSET_ROCR_VISIBLE_DEVICES")
+        if gpu_ids and not noset:
+            # isolate the worker to its GPUs before HIP initialises (reference:
+            # accelerators/amd_gpu.py ROCR_VISIBLE_DEVICES). Train worker groups opt
+            # out (NOSET) so RCCL sees every peer GPU of the node for xGMI P2P.
+            e["ROCR_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpu_ids)
         for k, v in (renv.get("env_vars") or {}).items():
             e[k] = str(v)
         if renv:
@@ -735,6 +737,9 @@ class Head:
             e["CAAMD_RUNTIME_ENV"] = json.dumps(renv)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
+        # workers import user code the way the driver does (reference: the driver's
+        # code search path is propagated through the job config)
+        e["CAAMD_SYS_PATH"] = os.pathsep.join(p for p in sys.path if p and os.path.isdir(p))
         log = open(os.path.join(self.session_dir, f"worker-{worker_id.hex()[:8]}.log"), "ab")
         proc = subprocess.Popen([sys.executable, "-m", "cluster_anywhere_amd.core.worker_main"],
                                 env=e, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,

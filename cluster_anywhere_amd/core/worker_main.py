@@ -36,6 +36,9 @@ def _apply_runtime_env(renv: dict):
 
 def main():
     _die_with_parent()
+    for p in reversed(os.environ.get("CAAMD_SYS_PATH", "").split(os.pathsep)):
+        if p and p not in sys.path:
+            sys.path.insert(1, p)
     renv = os.environ.get("CAAMD_RUNTIME_ENV")
     if renv:
         _apply_runtime_env(json.loads(renv))

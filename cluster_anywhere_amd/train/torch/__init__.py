@@ -1,0 +1,222 @@
+"""PyTorch-ROCm training (reference: python/ray/train/torch/: torch_trainer.py:11,
+config.py:36/66, train_loop_utils.py: get_device :46, prepare_model :162,
+prepare_data_loader :204, accelerate :278, prepare_optimizer :299, backward :312,
+enable_reproducibility :322).
+
+MI355X specifics: the process group is RCCL (``"nccl"``) over xGMI with
+``HSA_ENABLE_IPC_MODE_LEGACY=0`` (dmabuf IPC); ``prepare_model`` uses DDP buckets
+sized for per-link-bound xGMI rings (64 MiB, gradients as bucket views);
+``prepare_data_parallel_step`` returns the fused fast path (flat bf16 weights +
+fp32 master, bucketed all-reduce or ZeRO-1, one fused HIP AdamW launch).
+"""
+from __future__ import annotations
+
+import os
+import random
+from datetime import timedelta
+from typing import Any, Dict, Optional
+
+from ..checkpoint import Checkpoint
+from ..config import RunConfig, ScalingConfig
+from ..session import get_context
+from ..trainer import Backend, DataParallelTrainer, Result
+
+
+class TorchConfig(Backend):
+    def __init__(self, backend: Optional[str] = None, init_method: str = "env", timeout_s: int = 1800):
+        self.backend = backend
+        self.init_method = init_method
+        self.timeout_s = timeout_s
+
+    def on_start(self, rank, world_size, master_addr, master_port, device_id):
+        import torch
+        import torch.distributed as dist
+
+        backend = self.backend
+        if device_id is not None and torch.cuda.is_available():
+            torch.cuda.set_device(int(device_id))
+        if backend is None:
+            backend = "nccl" if (device_id is not None and torch.cuda.is_available()) else "gloo"
+        if dist.is_initialized():
+            return
+        kw = {}
+        if backend == "nccl" and device_id is not None:
+            kw["device_id"] = torch.device("cuda", int(device_id))
+        dist.init_process_group(backend, init_method=f"tcp://{master_addr}:{master_port}", rank=rank,
+                                world_size=world_size, timeout=timedelta(seconds=self.timeout_s), **kw)
+
+    def on_shutdown(self):
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+
+
+class TorchTrainer(DataParallelTrainer):
+    _default_backend = TorchConfig
+
+    def __init__(self, train_loop_per_worker, *, train_loop_config=None, torch_config=None,
+                 scaling_config=None, run_config=None, datasets=None, dataset_config=None,
+                 resume_from_checkpoint=None, metadata=None):
+        super().__init__(train_loop_per_worker, train_loop_config=train_loop_config,
+                         backend_config=torch_config or TorchConfig(), scaling_config=scaling_config,
+                         run_config=run_config, datasets=datasets, dataset_config=dataset_config,
+                         resume_from_checkpoint=resume_from_checkpoint, metadata=metadata)
+
+    def _fit_spmd(self):
+        import torch
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            lr = int(os.environ.get("LOCAL_RANK", "0"))
+            if torch.cuda.is_available():
+                torch.cuda.set_device(lr)
+                os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+                dist.init_process_group("nccl", device_id=torch.device("cuda", lr))
+            else:
+                dist.init_process_group("gloo")
+        return super()._fit_spmd()
+
+
+def get_device():
+    import torch
+
+    if torch.cuda.is_available():
+        ids = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
+        if ids and not os.environ.get("ROCR_VISIBLE_DEVICES"):
+            return torch.device("cuda", ids[0])
+        if "LOCAL_RANK" in os.environ and not ids:
+            return torch.device("cuda", int(os.environ["LOCAL_RANK"]) % torch.cuda.device_count())
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def get_devices():
+    return [get_device()]
+
+
+def prepare_model(model, move_to_device: bool = True, parallel_strategy: Optional[str] = "ddp",
+                  parallel_strategy_kwargs: Optional[Dict[str, Any]] = None):
+    import torch
+    import torch.distributed as dist
+
+    dev = get_device()
+    if move_to_device:
+        model = model.to(dev)
+    if not dist.is_initialized() or dist.get_world_size() == 1 or parallel_strategy is None:
+        return model
+    kw = dict(parallel_strategy_kwargs or {})
+    if parallel_strategy == "fsdp":
+        from torch.distributed.fsdp import FullyShardedDataParallel as FSDP
+
+        return FSDP(model, device_id=dev if dev.type == "cuda" else None, **kw)
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    kw.setdefault("bucket_cap_mb", float(os.environ.get("CAAMD_BUCKET_MB", "64")))
+    kw.setdefault("gradient_as_bucket_view", True)
+    if dev.type == "cuda":
+        kw.setdefault("device_ids", [dev.index])
+    return DDP(model, **kw)
+
+
+def prepare_data_parallel_step(model, **kwargs):
+    """The fused MI355X training step (see :class:`cluster_anywhere_amd.train.loop.DataParallelStep`)."""
+    from ..loop import DataParallelStep
+
+    return DataParallelStep(model.to(get_device()), **kwargs)
+
+
+class _DeviceLoader:
+    """Wraps a DataLoader: moves every batch to the device on a side HIP stream,
+    one batch ahead, so host->HBM copies overlap compute."""
+
+    def __init__(self, loader, device):
+        self.loader = loader
+        self.device = device
+
+    def __len__(self):
+        return len(self.loader)
+
+    def _move(self, b):
+        import torch
+
+        if isinstance(b, torch.Tensor):
+            return b.to(self.device, non_blocking=True)
+        if isinstance(b, (list, tuple)):
+            return type(b)(self._move(x) for x in b)
+        if isinstance(b, dict):
+            return {k: self._move(v) for k, v in b.items()}
+        return b
+
+    def __iter__(self):
+        import torch
+
+        if self.device.type != "cuda":
+            for b in self.loader:
+                yield self._move(b)
+            return
+        stream = torch.cuda.Stream(self.device)
+        it = iter(self.loader)
+        nxt = None
+        try:
+            with torch.cuda.stream(stream):
+                nxt = self._move(next(it))
+        except StopIteration:
+            return
+        while nxt is not None:
+            torch.cuda.current_stream(self.device).wait_stream(stream)
+            cur = nxt
+            try:
+                with torch.cuda.stream(stream):
+                    nxt = self._move(next(it))
+            except StopIteration:
+                nxt = None
+            yield cur
+
+
+def prepare_data_loader(data_loader, add_dist_sampler: bool = True, move_to_device: bool = True,
+                        auto_transfer: bool = True):
+    import torch
+    import torch.distributed as dist
+    from torch.utils.data import DataLoader, DistributedSampler
+
+    if add_dist_sampler and dist.is_initialized() and dist.get_world_size() > 1 and \
+            not isinstance(getattr(data_loader, "sampler", None), DistributedSampler):
+        sampler = DistributedSampler(data_loader.dataset, shuffle=isinstance(
+            data_loader.sampler, torch.utils.data.RandomSampler))
+        data_loader = DataLoader(data_loader.dataset, batch_size=data_loader.batch_size, sampler=sampler,
+                                 num_workers=data_loader.num_workers, collate_fn=data_loader.collate_fn,
+                                 pin_memory=torch.cuda.is_available(), drop_last=data_loader.drop_last)
+    if move_to_device:
+        return _DeviceLoader(data_loader, get_device())
+    return data_loader
+
+
+def prepare_optimizer(optimizer):
+    return optimizer
+
+
+def backward(tensor):
+    tensor.backward()
+
+
+def accelerate(amp: bool = False):
+    pass
+
+
+def enable_reproducibility(seed: int = 0):
+    import numpy as np
+    import torch
+
+    torch.manual_seed(seed)
+    random.seed(seed)
+    np.random.seed(seed)
+    torch.use_deterministic_algorithms(True, warn_only=True)
+
+
+__all__ = ["TorchTrainer", "TorchConfig", "get_device", "get_devices", "prepare_model",
+           "prepare_data_loader", "prepare_optimizer", "prepare_data_parallel_step", "backward",
+           "accelerate", "enable_reproducibility"]

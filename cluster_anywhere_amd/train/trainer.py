@@ -1,0 +1,441 @@
+"""Trainers and the training worker group (reference: python/ray/train/
+base_trainer.py, data_parallel_trainer.py:26, _internal/backend_executor.py:69,
+_internal/worker_group.py:102).
+
+``DataParallelTrainer.fit()``:
+  1. reserves one placement-group bundle per worker (PACK by default, so a
+     node's GPUs are used together and RCCL rings stay on xGMI),
+  2. starts one ``_TrainWorker`` actor per bundle; GPU workers see every GPU
+     of their node (device = their assigned id) so RCCL can use peer xGMI links,
+  3. runs the backend's process-group setup (torch: ``init_process_group``
+     over RCCL on GPUs / gloo on CPUs, 127.0.0.1 / node address rendezvous),
+  4. runs ``train_loop_per_worker`` in every worker, streaming ``report()``ed
+     metrics + persisted checkpoints back to the driver,
+  5. on worker failure restarts the whole group from the latest checkpoint up
+     to ``FailureConfig.max_failures`` times.
+
+When the process is already one rank of a torch.distributed job
+(``torchrun``/``python -m torch.distributed.run`` sets WORLD_SIZE / RANK), ``fit()``
+runs the loop in-process on that rank ("SPMD mode") — same session, report and
+checkpoint semantics, no actors.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import socket
+import threading
+import time
+import traceback
+import uuid
+from typing import Any, Callable, Dict, List, Optional
+
+from ..core import api as core
+from .checkpoint import Checkpoint
+from .config import CheckpointConfig, DataConfig, FailureConfig, RunConfig, ScalingConfig
+from .session import TrainContext, _Session, init_session, shutdown_session
+
+
+class TrainingFailedError(RuntimeError):
+    pass
+
+
+class Result:
+    def __init__(self, metrics=None, checkpoint=None, error=None, path=None, metrics_history=None,
+                 best_checkpoints=None):
+        self.metrics = metrics or {}
+        self.checkpoint = checkpoint
+        self.error = error
+        self.path = path
+        self._history = metrics_history or []
+        self.best_checkpoints = best_checkpoints or []
+        self.filesystem = None
+
+    @property
+    def metrics_dataframe(self):
+        import pandas as pd
+
+        return pd.DataFrame(self._history)
+
+    @property
+    def config(self):
+        return self.metrics.get("config")
+
+    def __repr__(self):
+        return f"Result(metrics={self.metrics}, path={self.path}, checkpoint={self.checkpoint}, error={self.error!r})"
+
+    @classmethod
+    def from_path(cls, path: str) -> "Result":
+        hist = []
+        p = os.path.join(path, "result.json")
+        if os.path.exists(p):
+            with open(p) as f:
+                hist = [json.loads(l) for l in f if l.strip()]
+        ckpts = sorted(d for d in os.listdir(path) if d.startswith("checkpoint_"))
+        ck = Checkpoint(os.path.join(path, ckpts[-1])) if ckpts else None
+        return cls(hist[-1] if hist else {}, ck, None, path, hist)
+
+
+class Backend:
+    """Process-group hooks run inside every worker (reference: train/backend.py)."""
+
+    def on_start(self, rank, world_size, master_addr, master_port, device_id):
+        pass
+
+    def on_shutdown(self):
+        pass
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _TrainWorker:
+    def __init__(self):
+        self.thread = None
+        self.session = None
+        self.error = None
+        self.done = False
+        self.backend = None
+
+    def node_info(self):
+        gpus = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
+        return {"node_id": os.environ.get("CAAMD_NODE_ID", "local"), "gpu_ids": gpus,
+                "port": _free_port(), "addr": "127.0.0.1", "pid": os.getpid()}
+
+    def setup(self, backend, rank, world_size, local_rank, local_world_size, node_rank,
+              master_addr, master_port, device_id):
+        os.environ.update({
+            "RANK": str(rank), "WORLD_SIZE": str(world_size), "LOCAL_RANK": str(local_rank),
+            "LOCAL_WORLD_SIZE": str(local_world_size), "NODE_RANK": str(node_rank),
+            "MASTER_ADDR": master_addr, "MASTER_PORT": str(master_port),
+            "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+        })
+        self.backend = backend
+        backend.on_start(rank, world_size, master_addr, master_port, device_id)
+        return True
+
+    def run(self, fn, config, ckpt_path, shards, ctx_kwargs, run_dir, ckpt_index):
+        ckpt = Checkpoint(ckpt_path) if ckpt_path else None
+        self.session = _Session(TrainContext(**ctx_kwargs), ckpt, shards, run_dir, ckpt_index)
+        init_session(self.session)
+
+        def target():
+            try:
+                import inspect
+
+                if len(inspect.signature(fn).parameters) == 0:
+                    fn()
+                else:
+                    fn(config if config is not None else {})
+            except BaseException as e:  # noqa
+                from ..exceptions import RayTaskError
+
+                self.error = RayTaskError.from_exception("train_loop_per_worker", e)
+            finally:
+                self.done = True
+
+        self.thread = threading.Thread(target=target, name="train-loop", daemon=True)
+        self.thread.start()
+        return True
+
+    def poll(self, timeout=0.5):
+        out = []
+        s = self.session
+        deadline = time.time() + timeout
+        while True:
+            try:
+                out.append(s.reports.get(timeout=max(0.0, min(0.05, deadline - time.time()))))
+                while True:
+                    out.append(s.reports.get_nowait())
+            except Exception:
+                pass
+            if out or self.done or time.time() >= deadline:
+                break
+        done = self.done and s.reports.empty()
+        return out, done, self.error
+
+    def shutdown(self):
+        try:
+            if self.backend is not None:
+                self.backend.on_shutdown()
+        finally:
+            shutdown_session()
+        return True
+
+
+class DataParallelTrainer:
+    _default_backend = Backend
+
+    def __init__(self, train_loop_per_worker: Callable, *, train_loop_config: Optional[Dict] = None,
+                 backend_config: Optional[Backend] = None, scaling_config: Optional[ScalingConfig] = None,
+                 run_config: Optional[RunConfig] = None, datasets: Optional[Dict[str, Any]] = None,
+                 dataset_config: Optional[DataConfig] = None,
+                 resume_from_checkpoint: Optional[Checkpoint] = None,
+                 metadata: Optional[Dict[str, Any]] = None):
+        self.train_loop_per_worker = train_loop_per_worker
+        self.train_loop_config = train_loop_config
+        self.backend = backend_config or self._default_backend()
+        self.scaling_config = scaling_config or ScalingConfig(num_workers=1)
+        self.run_config = run_config or RunConfig()
+        self.datasets = datasets or {}
+        self.dataset_config = dataset_config or DataConfig()
+        self.resume_from_checkpoint = resume_from_checkpoint
+        self.metadata = metadata or {}
+
+    # ------------------------------------------------------------------ helpers
+    def _run_dir(self):
+        name = self.run_config.name or f"{type(self).__name__}_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
+        self.run_config.name = name
+        d = os.path.join(self.run_config.storage_path, name)
+        os.makedirs(d, exist_ok=True)
+        return d
+
+    def _split_datasets(self, n):
+        shards = [dict() for _ in range(n)]
+        split = self.dataset_config.datasets_to_split
+        for name, ds in self.datasets.items():
+            if split == "all" or (isinstance(split, list) and name in split):
+                parts = ds.streaming_split(n, equal=True) if hasattr(ds, "streaming_split") else [ds] * n
+            else:
+                parts = [ds] * n
+            for i in range(n):
+                shards[i][name] = parts[i]
+        return shards
+
+    @staticmethod
+    def _spmd_env() -> bool:
+        return "WORLD_SIZE" in os.environ and "RANK" in os.environ and not os.environ.get("CAAMD_WORKER_ID")
+
+    # ---------------------------------------------------------------- SPMD mode
+    def _fit_spmd(self) -> Result:
+        rank = int(os.environ["RANK"])
+        world = int(os.environ["WORLD_SIZE"])
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        run_dir = self._run_dir()
+        ctx = TrainContext(world, rank, local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", world)),
+                           int(os.environ.get("GROUP_RANK", "0")), self.run_config.name,
+                           self.run_config.name, "spmd", self.run_config.storage_path, self.metadata, run_dir)
+        shards = self._split_datasets(world)[rank] if self.datasets else {}
+        s = _Session(ctx, self.resume_from_checkpoint, shards, run_dir if rank == 0 else "", 0)
+        init_session(s)
+        history, last, ckpt = [], {}, None
+        error = None
+        try:
+            import inspect
+
+            fn = self.train_loop_per_worker
+            if len(inspect.signature(fn).parameters) == 0:
+                fn()
+            else:
+                fn(self.train_loop_config or {})
+        except BaseException as e:  # noqa
+            error = e
+        finally:
+            shutdown_session()
+        while not s.reports.empty():
+            _, m, p = s.reports.get()
+            history.append(m)
+            last = m
+            if p:
+                ckpt = Checkpoint(p)
+        if error is not None:
+            raise error
+        return Result(last, ckpt, None, run_dir, history)
+
+    # ------------------------------------------------------------ actor mode
+    def fit(self) -> Result:
+        if self._spmd_env():
+            return self._fit_spmd()
+        core._ensure_init()
+        run_dir = self._run_dir()
+        fc: FailureConfig = self.run_config.failure_config
+        failures = 0
+        latest_ckpt = self.resume_from_checkpoint
+        history: List[dict] = []
+        kept: List[tuple] = []
+        ckpt_index = 0
+        last_metrics: Dict[str, Any] = {}
+        while True:
+            try:
+                res = self._run_attempt(run_dir, latest_ckpt, ckpt_index)
+            except _AttemptFailed as af:
+                history.extend(af.history)
+                if af.history:
+                    last_metrics = af.history[-1]
+                for m, p in af.ckpts:
+                    latest_ckpt = Checkpoint(p)
+                    kept = self._track_checkpoint(kept, m, p)
+                ckpt_index = af.ckpt_index
+                failures += 1
+                if fc.max_failures >= 0 and failures > fc.max_failures:
+                    err = TrainingFailedError(f"Training failed after {failures} attempt(s): {af.error}")
+                    err.__cause__ = af.error if isinstance(af.error, BaseException) else None
+                    result = Result(last_metrics, latest_ckpt, err, run_dir, history,
+                                    [(Checkpoint(p), m) for m, p in kept])
+                    self._write_history(run_dir, history)
+                    raise err
+                continue
+            hist, ckpts, ckpt_index = res
+            history.extend(hist)
+            for m, p in ckpts:
+                latest_ckpt = Checkpoint(p)
+                kept = self._track_checkpoint(kept, m, p)
+            if hist:
+                last_metrics = hist[-1]
+            break
+        self._write_history(run_dir, history)
+        return Result(last_metrics, latest_ckpt, None, run_dir, history,
+                      [(Checkpoint(p), m) for m, p in kept])
+
+    def _write_history(self, run_dir, history):
+        try:
+            with open(os.path.join(run_dir, "result.json"), "w") as f:
+                for m in history:
+                    f.write(json.dumps({k: v for k, v in m.items() if _jsonable(v)}) + "\n")
+        except OSError:
+            pass
+
+    def _track_checkpoint(self, kept, metrics, path):
+        cc: CheckpointConfig = self.run_config.checkpoint_config
+        kept = [k for k in kept if k[1] != path] + [(metrics, path)]
+        if cc.num_to_keep is not None and len(kept) > cc.num_to_keep:
+            attr = cc.checkpoint_score_attribute
+            if attr:
+                rev = cc.checkpoint_score_order == "max"
+                order = sorted(kept, key=lambda x: x[0].get(attr, float("-inf") if rev else float("inf")),
+                               reverse=rev)
+            else:
+                order = list(reversed(kept))
+            keep, drop = order[: cc.num_to_keep], order[cc.num_to_keep:]
+            latest = kept[-1]
+            if latest not in keep:  # never delete the newest (needed for restore)
+                drop = [d for d in drop if d is not latest]
+                keep.append(latest)
+            for m, p in drop:
+                shutil.rmtree(p, ignore_errors=True)
+            kept = [k for k in kept if k in keep]
+        return kept
+
+    def _run_attempt(self, run_dir, ckpt, ckpt_index):
+        from ..core.actor import ActorClass
+        from ..exceptions import RayActorError
+        from ..util.placement_group import placement_group, remove_placement_group
+        from ..util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+        sc = self.scaling_config
+        n = sc.total_workers
+        bundles = sc.as_placement_group_bundles()
+        pg = placement_group(bundles, strategy=sc.placement_strategy)
+        ready, _ = core.wait([pg.ready()], timeout=float(os.environ.get("CAAMD_TRAIN_PG_TIMEOUT", "600")))
+        if not ready:
+            remove_placement_group(pg)
+            raise RuntimeError(f"could not reserve {n} training workers with {bundles[0]} each "
+                               f"(cluster: {core.available_resources()})")
+        res = sc._resources_per_worker_not_none
+        Worker = ActorClass(_TrainWorker, {})
+        workers = []
+        for i in range(n):
+            opts = dict(num_cpus=res.get("CPU", 1), num_gpus=res.get("GPU", 0),
+                        resources={k: v for k, v in res.items() if k not in ("CPU", "GPU")},
+                        scheduling_strategy=PlacementGroupSchedulingStrategy(pg, i),
+                        runtime_env={"env_vars": {"CAAMD_NOSET_ROCR_VISIBLE_DEVICES": "1",
+                                                  "HSA_ENABLE_IPC_MODE_LEGACY": "0"}})
+            workers.append(Worker.options(**opts).remote())
+        history, ckpts = [], []
+        try:
+            infos = core.get([w.node_info.remote() for w in workers], timeout=600)
+            # ranks: group workers by node (node_rank order of first appearance)
+            nodes = []
+            for inf in infos:
+                if inf["node_id"] not in nodes:
+                    nodes.append(inf["node_id"])
+            local_counts = {nd: 0 for nd in nodes}
+            local_world = {nd: sum(1 for x in infos if x["node_id"] == nd) for nd in nodes}
+            master = infos[0]
+            setups = []
+            ranks = []
+            for rank, (w, inf) in enumerate(zip(workers, infos)):
+                nd = inf["node_id"]
+                lr = local_counts[nd]
+                local_counts[nd] += 1
+                dev = inf["gpu_ids"][0] if inf["gpu_ids"] else None
+                ranks.append((rank, lr, local_world[nd], nodes.index(nd)))
+                setups.append(w.setup.remote(self.backend, rank, n, lr, local_world[nd], nodes.index(nd),
+                                             master["addr"], master["port"], dev))
+            core.get(setups, timeout=900)
+            shards = self._split_datasets(n)
+            runs = []
+            for (rank, lr, lw, nr), w in zip(ranks, workers):
+                ctx = dict(world_size=n, world_rank=rank, local_rank=lr, local_world_size=lw,
+                           node_rank=nr, experiment_name=self.run_config.name,
+                           trial_name=self.run_config.name, trial_id=uuid.uuid4().hex[:8],
+                           storage_path=self.run_config.storage_path, metadata=self.metadata,
+                           trial_dir=run_dir)
+                runs.append(w.run.remote(self.train_loop_per_worker, self.train_loop_config,
+                                         ckpt.path if ckpt else None, shards[rank], ctx, run_dir,
+                                         ckpt_index))
+            core.get(runs, timeout=600)
+            done = [False] * n
+            callbacks = self.run_config.callbacks or []
+            while not all(done):
+                polls = core.get([w.poll.remote(0.5) for w in workers])
+                err = None
+                round_reports = {}
+                for i, (reports, d, e) in enumerate(polls):
+                    done[i] = d
+                    if e is not None and err is None:
+                        err = e
+                    for (rank, m, p) in reports:
+                        round_reports.setdefault(rank, []).append((m, p))
+                # rank 0 metrics define the result; a checkpoint reported by any rank counts
+                all_paths = {}
+                for rank, items in round_reports.items():
+                    for k, (m, p) in enumerate(items):
+                        if p:
+                            all_paths.setdefault(k, p)
+                for k, (m, p) in enumerate(round_reports.get(0, [])):
+                    path = p or all_paths.get(k)
+                    history.append(m)
+                    if path:
+                        ckpts.append((m, path))
+                        ckpt_index += 1
+                    for cb in callbacks:
+                        if hasattr(cb, "on_report"):
+                            cb.on_report(m)
+                if err is not None:
+                    raise _AttemptFailed(err, history, ckpts, ckpt_index)
+            core.get([w.shutdown.remote() for w in workers], timeout=60)
+            return history, ckpts, ckpt_index
+        except RayActorError as e:
+            raise _AttemptFailed(e, history, ckpts, ckpt_index)
+        finally:
+            for w in workers:
+                try:
+                    core.kill(w)
+                except Exception:
+                    pass
+            remove_placement_group(pg)
+            time.sleep(0.05)
+
+
+class _AttemptFailed(Exception):
+    def __init__(self, error, history, ckpts, ckpt_index):
+        super().__init__(str(error))
+        self.error = error
+        self.history = history
+        self.ckpts = ckpts
+        self.ckpt_index = ckpt_index
+
+
+def _jsonable(v):
+    try:
+        json.dumps(v)
+        return True
+    except TypeError:
+        return False

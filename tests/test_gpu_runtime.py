@@ -1,0 +1,78 @@
+"""Runtime on a real MI355X: GPU actors (ROCR_VISIBLE_DEVICES isolation, HIP
+kernels inside workers), GPU tensors through the object store, and TorchTrainer
+in actor mode driving the fused GPT-2 step on the GPU."""
+import pytest
+import torch
+
+import cluster_anywhere_amd as ray
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=4)
+    yield
+    ray.shutdown()
+
+
+def test_gpu_actor_runs_hip_kernels(cluster):
+    @ray.remote(num_gpus=1)
+    class G:
+        def info(self):
+            import os
+
+            import torch
+
+            from cluster_anywhere_amd.ops import layer_norm
+
+            x = torch.randn(16, 1600, device="cuda", dtype=torch.bfloat16)
+            g = torch.ones(1600, device="cuda", dtype=torch.bfloat16)
+            b = torch.zeros(1600, device="cuda", dtype=torch.bfloat16)
+            y = layer_norm(x, g, b)
+            ref = torch.nn.functional.layer_norm(x.float(), (1600,))
+            err = (y.float() - ref).abs().max().item()
+            return (torch.cuda.device_count(), os.environ.get("ROCR_VISIBLE_DEVICES"),
+                    ray.get_gpu_ids(), err)
+
+    n, vis, ids, err = ray.get(G.remote().info.remote(), timeout=300)
+    assert n == 1 and vis is not None and len(ids) == 1
+    assert err < 0.05
+
+
+def test_gpu_tensor_roundtrip(cluster):
+    @ray.remote(num_gpus=1)
+    def make():
+        import torch
+
+        return torch.arange(1000, device="cuda", dtype=torch.float32)
+
+    t = ray.get(make.remote(), timeout=300)
+    assert t.is_cuda and float(t.sum()) == sum(range(1000))
+
+
+def test_torch_trainer_gpu_actor_mode(cluster, tmp_path):
+    from cluster_anywhere_amd import train
+    from cluster_anywhere_amd.train import RunConfig, ScalingConfig
+    from cluster_anywhere_amd.train.torch import TorchTrainer, get_device, prepare_data_parallel_step
+
+    def loop(cfg):
+        import torch
+
+        from cluster_anywhere_amd.models.gpt2 import GPT2, GPT2Config
+
+        torch.manual_seed(0)
+        mc = GPT2Config.named("gpt2-tiny")
+        step = prepare_data_parallel_step(GPT2(mc), lr=1e-3)
+        dev = get_device()
+        x = torch.randint(0, mc.vocab_size, (4, 65), device=dev)
+        for i in range(cfg["steps"]):
+            loss = step(x[:, :-1], x[:, 1:])
+            train.report({"loss": float(loss), "device": str(dev)})
+
+    r = TorchTrainer(loop, train_loop_config={"steps": 20},
+                     scaling_config=ScalingConfig(num_workers=1, use_gpu=True),
+                     run_config=RunConfig(name="gpu", storage_path=str(tmp_path))).fit()
+    df = r.metrics_dataframe
+    assert r.metrics["device"].startswith("cuda")
+    assert df["loss"].iloc[-1] < df["loss"].iloc[0] - 1.0
