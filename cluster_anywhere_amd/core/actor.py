@@ -62,10 +62,25 @@ class ActorMethod:
         return ClassMethodNode(self._handle, self._name, args, kwargs, self._num_returns)
 
 
+HANDLE_SUFFIX = b"\xac" * 8
+
+
+def handle_ref_id(actor_id: bytes) -> bytes:
+    """Object id whose reference count tracks the live handles of an actor."""
+    return actor_id + HANDLE_SUFFIX
+
+
 class ActorHandle:
-    def __init__(self, actor_id: bytes, meta: Dict[str, Any]):
+    """Handle to an actor. Holds a reference on the actor's handle-object so an
+    unnamed, non-detached actor is terminated (after its queued calls) once no
+    handle to it is left anywhere (reference: actor handle ref-counting)."""
+
+    def __init__(self, actor_id: bytes, meta: Dict[str, Any], _owned: bool = False, _ref=None):
+        from .object_ref import ObjectRef
+
         self._actor_id = actor_id
         self._meta = meta
+        self._ref = _ref if _ref is not None else ObjectRef(handle_ref_id(actor_id), _owned=_owned)
 
     @property
     def _ray_actor_id(self):
@@ -98,7 +113,9 @@ class ActorHandle:
         return refs
 
     def __reduce__(self):
-        return (ActorHandle, (self._actor_id, self._meta))
+        # the ObjectRef travels with the handle: it is recorded as a contained
+        # reference, so the actor stays alive while the handle is in flight
+        return (_rebuild_handle, (self._actor_id, self._meta, self._ref))
 
     def __repr__(self):
         return f"Actor({self._meta.get('class_name')}, {self._actor_id.hex()})"
@@ -108,6 +125,10 @@ class ActorHandle:
 
     def __hash__(self):
         return hash(self._actor_id)
+
+
+def _rebuild_handle(actor_id, meta, ref):
+    return ActorHandle(actor_id, meta, _ref=ref)
 
 
 class _ReadyMixin:
@@ -178,7 +199,7 @@ class ActorClass:
                  resources=opt_utils.resource_demand(o, actor=True),
                  strategy=opt_utils.strategy_tuple(o), actor_id=actor_id, actor_opts=actor_opts,
                  runtime_env=o.get("runtime_env"), max_retries=0)
-        return ActorHandle(actor_id, meta)
+        return ActorHandle(actor_id, meta, _owned=True)
 
     def bind(self, *args, **kwargs):
         from ..dag import ClassNode

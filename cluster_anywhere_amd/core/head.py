@@ -174,6 +174,7 @@ class Head:
         self.pgs: Dict[bytes, dict] = {}
         self.pending_pgs: List[bytes] = []
         self.gen_waiters: Dict[bytes, list] = collections.defaultdict(list)
+        self.handle_objs: Dict[bytes, bytes] = {}  # handle object id -> actor id
         self.events: collections.deque = collections.deque(maxlen=200000)
         self.jobs: Dict[bytes, dict] = {}
         self.max_workers = int(max(4, resources.get("CPU", 1) * 4))
@@ -401,6 +402,10 @@ class Head:
             if t is not None and t.state in ("pending", "running"):
                 return
         del self.objects[oid]
+        aid = self.handle_objs.pop(oid, None)
+        if aid is not None:
+            self._on_handles_gone(aid)
+            return
         if e.inline is None and e.spilled_path is None:
             try:
                 self.store.remove(oid)
@@ -924,6 +929,13 @@ class Head:
         self.actors[spec.actor_id] = a
         if a.name:
             self.named_actors[(a.namespace, a.name)] = spec.actor_id
+        # the creator's handle: an always-READY object whose refcount = live handles
+        hid = spec.actor_id + b"\xac" * 8
+        he = self._obj(hid)
+        he.refcount += 1
+        he.state = READY
+        he.inline = b""
+        self.handle_objs[hid] = spec.actor_id
 
     def _h_check_name(self, c, req, namespace, name):
         aid = self.named_actors.get((namespace or self.namespace, name))
@@ -988,6 +1000,22 @@ class Head:
         for tid, spec in list(a.inflight.items()):
             self._fail_task(spec, (kind, msg))
         a.inflight.clear()
+
+    def _on_handles_gone(self, actor_id):
+        """No handle left: terminate an unnamed, non-detached actor once its queued
+        calls have run (a __ray_terminate__ call appended to its queue)."""
+        a = self.actors.get(actor_id)
+        if a is None or a.name or a.lifetime == "detached" or a.state == "DEAD":
+            return
+        a.restarts_left = 0
+        a.death_cause = "all references to the actor were removed"
+        term = TaskSpec(task_id=os.urandom(16), kind=ACTOR_METHOD, fn_name="__ray_terminate__",
+                        args=[], kwargs={}, arg_refs=[], num_returns=0, return_ids=[],
+                        actor_id=actor_id, method="__ray_terminate__", max_retries=0)
+        term.state = "pending"
+        self.tasks[term.task_id] = term
+        a.queue.append(term)
+        self._pump_actor(a)
 
     def _h_kill_actor(self, c, actor_id, no_restart):
         a = self.actors.get(actor_id)

@@ -95,7 +95,8 @@ def test_cross_entropy(C, rows, V, stride):
     (ref * w).sum().backward()
     assert torch.allclose(loss, ref, atol=2e-2, rtol=1e-2)
     assert _rel(lg.grad[:, :V], lf.grad) < 2e-2
-    assert lg.grad[:, V:].abs().max().item() == 0
+    if V < stride:
+        assert lg.grad[:, V:].abs().max().item() == 0
     assert lg.grad[0].abs().max().item() == 0
 
 
