@@ -1,0 +1,37 @@
+"""Distributed streaming datasets (reference: python/ray/data/)."""
+from . import preprocessors
+from .aggregate import AbsMax, AggregateFn, Count, Max, Mean, Min, Std, Sum
+from .context import DataContext
+from .dataset import ActorPoolStrategy, Dataset, GroupedData, MaterializedDataset, Schema, TaskPoolStrategy
+from .iterator import DataIterator
+from .read_api import (
+    from_arrow,
+    from_arrow_refs,
+    from_blocks,
+    from_huggingface,
+    from_items,
+    from_numpy,
+    from_numpy_refs,
+    from_pandas,
+    from_pandas_refs,
+    from_torch,
+    range,
+    range_tensor,
+    read_binary_files,
+    read_csv,
+    read_datasource,
+    read_images,
+    read_json,
+    read_numpy,
+    read_parquet,
+    read_text,
+)
+
+__all__ = [
+    "Dataset", "MaterializedDataset", "GroupedData", "DataIterator", "DataContext", "Schema",
+    "ActorPoolStrategy", "TaskPoolStrategy", "AggregateFn", "Count", "Sum", "Min", "Max", "Mean",
+    "Std", "AbsMax", "range", "range_tensor", "from_items", "from_blocks", "from_numpy",
+    "from_pandas", "from_arrow", "from_numpy_refs", "from_pandas_refs", "from_arrow_refs",
+    "from_torch", "from_huggingface", "read_parquet", "read_csv", "read_json", "read_text",
+    "read_numpy", "read_binary_files", "read_images", "read_datasource", "preprocessors",
+]

@@ -1,0 +1,37 @@
+"""DataContext (reference: python/ray/data/context.py)."""
+from __future__ import annotations
+
+import os
+import threading
+from dataclasses import dataclass, field
+
+
+@dataclass
+class DataContext:
+    target_max_block_size: int = 128 * 1024 * 1024
+    target_min_block_size: int = 1 * 1024 * 1024
+    max_tasks_in_flight_per_op: int = int(os.environ.get("CAAMD_DATA_MAX_INFLIGHT", "0"))
+    actor_max_tasks_in_flight: int = 2
+    execution_preserve_order: bool = True
+    enable_progress_bars: bool = False
+    read_op_min_num_blocks: int = 8
+    eager_free: bool = True
+    verbose_stats_logs: bool = False
+
+    _lock = threading.Lock()
+    _current = None
+
+    @staticmethod
+    def get_current() -> "DataContext":
+        with DataContext._lock:
+            if DataContext._current is None:
+                DataContext._current = DataContext()
+            return DataContext._current
+
+    @staticmethod
+    def _set_current(ctx: "DataContext"):
+        DataContext._current = ctx
+
+    @property
+    def execution_options(self):
+        return self

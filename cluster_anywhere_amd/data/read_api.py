@@ -1,0 +1,244 @@
+"""Dataset creation (reference: python/ray/data/read_api.py: range :228,
+range_tensor :280, from_items :145, read_parquet :776, read_csv :1393,
+read_json :1248, read_text :1562, read_numpy :1786, read_binary_files :2151,
+read_images :955, from_pandas :2658, from_numpy :2780, from_arrow :2866,
+from_torch :3262, from_huggingface :3058)."""
+from __future__ import annotations
+
+import glob
+import math
+import os
+from typing import Any, Dict, List, Optional, Union
+
+import numpy as np
+
+from . import block as B
+from .dataset import Dataset
+
+
+def _default_blocks(n_rows: int, override: Optional[int]) -> int:
+    if override:
+        return max(1, int(override))
+    try:
+        from ..core.api import cluster_resources
+
+        cpus = int(cluster_resources().get("CPU", 4))
+    except Exception:
+        cpus = 4
+    return max(1, min(n_rows, max(2 * cpus, 8), 200)) if n_rows else 1
+
+
+def _chunks(n: int, k: int):
+    import builtins
+
+    per = [n // k + (1 if i < n % k else 0) for i in builtins.range(k)]
+    s = 0
+    for p in per:
+        yield s, s + p
+        s += p
+
+
+def range(n: int, *, override_num_blocks: Optional[int] = None, parallelism: int = -1) -> Dataset:
+    k = _default_blocks(n, override_num_blocks or (parallelism if parallelism > 0 else None))
+    reads = [(lambda s=s, e=e: {"id": np.arange(s, e, dtype=np.int64)}) for s, e in _chunks(n, k)]
+    return Dataset(("read", reads))
+
+
+def range_tensor(n: int, *, shape=(1,), override_num_blocks: Optional[int] = None, parallelism: int = -1) -> Dataset:
+    k = _default_blocks(n, override_num_blocks or (parallelism if parallelism > 0 else None))
+    shape = tuple(shape)
+
+    def mk(s, e):
+        a = np.arange(s, e, dtype=np.int64).reshape((-1,) + (1,) * len(shape))
+        return {"data": np.broadcast_to(a, (e - s,) + shape).copy()}
+
+    return Dataset(("read", [(lambda s=s, e=e: mk(s, e)) for s, e in _chunks(n, k)]))
+
+
+def from_items(items: List[Any], *, override_num_blocks: Optional[int] = None, parallelism: int = -1) -> Dataset:
+    from ..core.api import put
+
+    k = _default_blocks(len(items), override_num_blocks or (parallelism if parallelism > 0 else None))
+    refs = []
+    for s, e in _chunks(len(items), k):
+        b = B.from_rows(items[s:e])
+        refs.append((put(b), {"num_rows": B.num_rows(b), "size_bytes": B.size_bytes(b),
+                              "schema": B.schema_of(b)}))
+    return Dataset(("refs", refs))
+
+
+def from_blocks(blocks: List[Dict[str, np.ndarray]]) -> Dataset:
+    from ..core.api import put
+
+    return Dataset(("refs", [(put(b), {"num_rows": B.num_rows(b), "size_bytes": B.size_bytes(b),
+                                       "schema": B.schema_of(b)}) for b in blocks]))
+
+
+def from_numpy(ndarrays) -> Dataset:
+    arrs = ndarrays if isinstance(ndarrays, list) else [ndarrays]
+    return from_blocks([{"data": np.asarray(a)} for a in arrs])
+
+
+def from_pandas(dfs) -> Dataset:
+    dfs = dfs if isinstance(dfs, list) else [dfs]
+    return from_blocks([B.from_batch(df) for df in dfs])
+
+
+def from_arrow(tables) -> Dataset:
+    tables = tables if isinstance(tables, list) else [tables]
+    return from_blocks([B.from_batch(t) for t in tables])
+
+
+def from_numpy_refs(refs) -> Dataset:
+    from ..core.api import get
+
+    return from_numpy(get(refs))
+
+
+def from_pandas_refs(refs) -> Dataset:
+    from ..core.api import get
+
+    return from_pandas(get(refs))
+
+
+def from_arrow_refs(refs) -> Dataset:
+    from ..core.api import get
+
+    return from_arrow(get(refs))
+
+
+def from_torch(dataset) -> Dataset:
+    return from_items([{"item": dataset[i]} for i in builtins_range(len(dataset))])
+
+
+def from_huggingface(dataset, **kw) -> Dataset:
+    if hasattr(dataset, "to_pandas"):
+        return from_pandas(dataset.to_pandas())
+    return from_items(list(dataset))
+
+
+def builtins_range(n):
+    import builtins
+
+    return builtins.range(n)
+
+
+def _expand(paths, exts=None) -> List[str]:
+    if isinstance(paths, str):
+        paths = [paths]
+    out = []
+    for p in paths:
+        if os.path.isdir(p):
+            for root, _, files in os.walk(p):
+                for f in sorted(files):
+                    if exts is None or any(f.endswith(e) for e in exts):
+                        out.append(os.path.join(root, f))
+        elif any(ch in p for ch in "*?["):
+            out.extend(sorted(glob.glob(p)))
+        else:
+            out.append(p)
+    if not out:
+        raise ValueError(f"no input files found in {paths}")
+    return out
+
+
+def _file_ds(files, reader, **kw) -> Dataset:
+    ds = Dataset(("read", [(lambda f=f: reader(f)) for f in files]))
+    ds._input_files = files
+    return ds
+
+
+def read_parquet(paths, *, columns: Optional[List[str]] = None, filter=None, **kw) -> Dataset:
+    files = _expand(paths, [".parquet"])
+
+    def rd(f):
+        import pyarrow.parquet as pq
+
+        return B.from_batch(pq.read_table(f, columns=columns, filters=filter))
+
+    return _file_ds(files, rd)
+
+
+def read_csv(paths, **arrow_csv_args) -> Dataset:
+    files = _expand(paths, [".csv", ".csv.gz"])
+
+    def rd(f):
+        import pyarrow.csv as pcsv
+
+        return B.from_batch(pcsv.read_csv(f))
+
+    return _file_ds(files, rd)
+
+
+def read_json(paths, *, lines: bool = True, **kw) -> Dataset:
+    files = _expand(paths, [".json", ".jsonl"])
+
+    def rd(f):
+        import pandas as pd
+
+        try:
+            return B.from_batch(pd.read_json(f, lines=True))
+        except ValueError:
+            return B.from_batch(pd.read_json(f))
+
+    return _file_ds(files, rd)
+
+
+def read_text(paths, *, encoding: str = "utf-8", drop_empty_lines: bool = True, **kw) -> Dataset:
+    files = _expand(paths)
+
+    def rd(f):
+        with open(f, encoding=encoding) as fh:
+            lines = [l.rstrip("\n") for l in fh]
+        if drop_empty_lines:
+            lines = [l for l in lines if l.strip()]
+        return {"text": np.asarray(lines, dtype=object)}
+
+    return _file_ds(files, rd)
+
+
+def read_numpy(paths, **kw) -> Dataset:
+    files = _expand(paths, [".npy"])
+    return _file_ds(files, lambda f: {"data": np.load(f, allow_pickle=False)})
+
+
+def read_binary_files(paths, *, include_paths: bool = False, **kw) -> Dataset:
+    files = _expand(paths)
+
+    def rd(f):
+        with open(f, "rb") as fh:
+            data = fh.read()
+        b = {"bytes": np.asarray([data], dtype=object)}
+        if include_paths:
+            b["path"] = np.asarray([f], dtype=object)
+        return b
+
+    return _file_ds(files, rd)
+
+
+def read_images(paths, *, size=None, mode=None, include_paths: bool = False, **kw) -> Dataset:
+    files = _expand(paths, [".png", ".jpg", ".jpeg", ".bmp", ".gif", ".npy"])
+
+    def rd(f):
+        if f.endswith(".npy"):
+            img = np.load(f, allow_pickle=False)
+        else:
+            from PIL import Image  # optional dependency
+
+            im = Image.open(f)
+            if mode:
+                im = im.convert(mode)
+            if size:
+                im = im.resize(size[::-1])
+            img = np.asarray(im)
+        b = {"image": img[None]}
+        if include_paths:
+            b["path"] = np.asarray([f], dtype=object)
+        return b
+
+    return _file_ds(files, rd)
+
+
+def read_datasource(datasource, *, parallelism: int = -1, **kw) -> Dataset:
+    tasks = datasource.get_read_tasks(parallelism if parallelism > 0 else 8)
+    return Dataset(("read", [(lambda t=t: B.concat([B.from_batch(x) for x in t()])) for t in tasks]))

@@ -20,6 +20,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import add_layer_norm, attention, bias_gelu, cross_entropy, layer_norm
+from ..ops.linear import linear
 
 
 @dataclass
@@ -78,12 +79,12 @@ class Block(nn.Module):
             a = layer_norm(h, self.ln1_w, self.ln1_b, self.eps)
         else:
             h, a = add_layer_norm(h, delta, self.ln1_w, self.ln1_b, self.eps)
-        qkv = F.linear(a, self.attn_w, self.attn_b)
+        qkv = linear(a, self.attn_w, self.attn_b)
         y = attention(qkv, self.n_head, causal=True)
-        attn_out = F.linear(y, self.proj_w, self.proj_b)
+        attn_out = linear(y, self.proj_w, self.proj_b)
         h, m = add_layer_norm(h, attn_out, self.ln2_w, self.ln2_b, self.eps)
-        u = bias_gelu(F.linear(m, self.fc_w), self.fc_b)
-        return h, F.linear(u, self.fc2_w, self.fc2_b)
+        u = bias_gelu(linear(m, self.fc_w), self.fc_b)
+        return h, linear(u, self.fc2_w, self.fc2_b)
 
 
 class GPT2(nn.Module):

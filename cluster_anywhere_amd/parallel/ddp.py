@@ -85,6 +85,7 @@ class BucketedDDP:
         self._owner = owner
         for s in slots:
             self._hooks.append(s.param.register_post_accumulate_grad_hook(self._on_grad))
+            s.param._ca_grad_ready = self._on_grad  # fused layers signal readiness directly
 
     def _global_src(self):
         if self.pg is None:

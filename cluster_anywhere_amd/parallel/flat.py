@@ -93,6 +93,8 @@ class FlatParamSpace:
                 view.copy_(src)
                 s.param.data = view
                 s.param.grad = self.grad_buffer[s.offset : s.offset + s.numel].view_as(src)
+                # fused layers (ops.linear) accumulate straight into this view
+                s.param.main_grad = s.param.grad
                 if s.decay:
                     a, b = s.offset // 8, (s.offset + s.numel + 7) // 8
                     mask[a:b] = 1

@@ -99,6 +99,8 @@ class Zero1Reducer:
         )
         self._next = 0
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._on_grad) for s in slots]
+        for s in slots:
+            s.param._ca_grad_ready = self._on_grad
 
     # -- backward-side -------------------------------------------------------------
     def start(self):

@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
   }
   const int r0 = blockIdx.y * rows_per;
   const int r1 = min(rows, r0 + rows_per);
+#pragma unroll 4
   for (int r = r0; r < r1; ++r) {
     const size_t off = (size_t)r * N + cv * 8;
     float hv[8], dv[8], o[8];
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(
 }
 
 void colsum_bf16_launch(const float* partial, int nrow, int ncol, int split, bf16* o0, bf16* o1,
-                        hipStream_t st);
+                        hipStream_t st, int accumulate);
 
 void bias_gelu_fwd_launch(const bf16* h, const bf16* b, bf16* y, int64_t rows, int N,
                           hipStream_t st) {
@@ -98,7 +99,42 @@ void bias_gelu_bwd_launch(const bf16* dy, const bf16* h, const bf16* b, bf16* dh
   const int rows_per = (rows + slabs - 1) / slabs;
   hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((ncv + 255) / 256, slabs), dim3(256), 0, st, dy, h,
                      b, dh, partial, rows, ncv, rows_per);
-  if (db) colsum_bf16_launch(partial, slabs, N, N, db, db, st);
+  if (db) colsum_bf16_launch(partial, slabs, N, N, db, db, st, 0);
+}
+
+// dbias = sum over rows of dy [rows, N] (bf16) -> fp32 slab partials -> bf16,
+// optionally accumulated into an existing gradient (the flat main-grad buffer).
+__global__ __launch_bounds__(256) void rowsum_partial_kernel(const bf16* __restrict__ dy,
+                                                             float* __restrict__ partial, int rows,
+                                                             int ncv, int rows_per) {
+  const int cv = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cv >= ncv) return;
+  const int N = ncv * 8;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(rows, r0 + rows_per);
+#pragma unroll 4
+  for (int r = r0; r < r1; ++r) {
+    float v[8];
+    load8(dy + (size_t)r * N + cv * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += v[j];
+  }
+  float* p = partial + (size_t)blockIdx.y * N + cv * 8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) p[j] = acc[j];
+}
+
+void bias_grad_launch(const bf16* dy, float* partial, bf16* out, int rows, int N, int accumulate,
+                      hipStream_t st) {
+  const int ncv = N / 8;
+  const int slabs = bias_gelu_bwd_slabs(rows);
+  const int rows_per = (rows + slabs - 1) / slabs;
+  hipLaunchKernelGGL(rowsum_partial_kernel, dim3((ncv + 255) / 256, slabs), dim3(256), 0, st, dy,
+                     partial, rows, ncv, rows_per);
+  colsum_bf16_launch(partial, slabs, N, N, out, out, st, accumulate);
 }
 
 }  // namespace caamd

@@ -167,6 +167,28 @@ std::vector<Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& h,
   return {dh, db};
 }
 
+// ---- bias gradient (column sum of dy), optionally accumulated in place -----------
+namespace caamd {
+void bias_grad_launch(const bf16*, float*, bf16*, int, int, int, hipStream_t);
+}
+
+void bias_grad_(const Tensor& dy2d, Tensor& out, bool accumulate) {
+  CHECK_BF16(dy2d);
+  CHECK_BF16(out);
+  TORCH_CHECK(dy2d.dim() == 2, "bias_grad: dy must be 2-D");
+  const int rows = (int)dy2d.size(0), N = (int)dy2d.size(1);
+  TORCH_CHECK(N % 8 == 0, "bias_grad: N must be a multiple of 8");
+  TORCH_CHECK(out.numel() == N, "bias_grad: out size mismatch");
+  auto partial = at::empty({caamd::bias_gelu_bwd_slabs(rows), N}, dy2d.options().dtype(at::kFloat));
+  if (rows > 0) {
+    caamd::bias_grad_launch(bp(dy2d), partial.data_ptr<float>(), bp(out), rows, N, accumulate ? 1 : 0,
+                            cur_stream());
+    LAUNCH_CHECK();
+  } else if (!accumulate) {
+    out.zero_();
+  }
+}
+
 // ---- cross entropy -----------------------------------------------------------
 // logits [N, stride] bf16 (columns >= V are padding), target [N] int64.
 std::vector<Tensor> xent_fwd(const Tensor& logits, const Tensor& target, int64_t V) {
@@ -360,6 +382,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
+  m.def("bias_grad_", &bias_grad_);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd_", &xent_bwd_);
   m.def("grad_sumsq", &grad_sumsq);

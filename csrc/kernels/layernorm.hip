@@ -78,72 +78,103 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   }
 }
 
-// 8 waves (512 threads) per block; g lives in LDS (not VGPRs); x/dy are read
-// twice per row (stats pass, then dx pass — the second read hits L1/L2) so only
-// the dgamma/dbeta accumulators occupy registers -> >= 4 waves/SIMD resident.
+// Backward in ONE HBM pass: a wave owns TWO rows at a time (two independent
+// load -> cross-lane-reduction -> store chains hide each other's latency), keeps
+// both rows' x and dy as packed bf16 in VGPRs between the statistics and the dx
+// pass, and accumulates dgamma/dbeta of its columns in fp32 registers across
+// the rows it visits (merged per block with LDS atomics at the end).
 template <int NV, bool HAS_DRES>
-__global__ __launch_bounds__(512) void ln_bwd_kernel(
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ g,
     const float* __restrict__ mean, const float* __restrict__ rstd,
     const bf16* __restrict__ dres, bf16* __restrict__ dx, float* __restrict__ partial,
     int rows, int D) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // 3*D floats
-  float* red = smem;         // [2D] dgamma | dbeta
-  float* gl = smem + 2 * D;  // [D] gamma
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2D] dgamma | dbeta
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nchunk = D >> 3;
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) red[i] = 0.f;
-  for (int i = threadIdx.x; i < D; i += blockDim.x) gl[i] = (float)g[i];
-  __syncthreads();
+  bf16x8 gv[NV];
   float dg[NV][8], db[NV][8];
 #pragma unroll
-  for (int c = 0; c < NV; ++c)
+  for (int c = 0; c < NV; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nchunk) gv[c] = *reinterpret_cast<const bf16x8*>(g + ch * 8);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      if (ch >= nchunk) gv[c][j] = (bf16)0.f;
+      dg[c][j] = db[c][j] = 0.f;
+    }
+  }
   const float inv_d = 1.f / (float)D;
-  for (int row = blockIdx.x * 8 + wave; row < rows; row += gridDim.x * 8) {
-    const size_t base = (size_t)row * D;
-    const float mu = mean[row], rs = rstd[row];
-    float s1 = 0.f, s2 = 0.f;
+  const int stride = gridDim.x * 4;
+  for (int r0 = blockIdx.x * 4 + wave; r0 < rows; r0 += 2 * stride) {
+    const int r1 = r0 + stride;
+    const bool v1 = r1 < rows;
+    const size_t b0 = (size_t)r0 * D, b1 = (size_t)(v1 ? r1 : r0) * D;
+    bf16x8 xa[NV], da[NV], xb[NV], dbb[NV];
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int ch = lane + c * 64;
       if (ch < nchunk) {
-        float xv[8], dv[8];
-        load8(x + base + ch * 8, xv);
-        load8(dy + base + ch * 8, dv);
+        xa[c] = *reinterpret_cast<const bf16x8*>(x + b0 + ch * 8);
+        da[c] = *reinterpret_cast<const bf16x8*>(dy + b0 + ch * 8);
+        xb[c] = *reinterpret_cast<const bf16x8*>(x + b1 + ch * 8);
+        dbb[c] = *reinterpret_cast<const bf16x8*>(dy + b1 + ch * 8);
+      }
+    }
+    const float mua = mean[r0], rsa = rstd[r0];
+    const float mub = mean[v1 ? r1 : r0], rsb = rstd[v1 ? r1 : r0];
+    float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nchunk) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float xh = (xv[j] - mu) * rs;
-          const float gd = dv[j] * gl[ch * 8 + j];
-          s1 += gd;
-          s2 += gd * xh;
-          dg[c][j] += dv[j] * xh;
-          db[c][j] += dv[j];
+          const float gj = (float)gv[c][j];
+          const float dva = (float)da[c][j], xha = ((float)xa[c][j] - mua) * rsa;
+          const float dvb = v1 ? (float)dbb[c][j] : 0.f, xhb = ((float)xb[c][j] - mub) * rsb;
+          s1a += dva * gj;
+          s2a += dva * gj * xha;
+          s1b += dvb * gj;
+          s2b += dvb * gj * xhb;
+          dg[c][j] += dva * xha + dvb * xhb;
+          db[c][j] += dva + dvb;
         }
       }
     }
-    const float m1 = wave_sum(s1) * inv_d, m2 = wave_sum(s2) * inv_d;
+    s1a = wave_sum(s1a);
+    s2a = wave_sum(s2a);
+    s1b = wave_sum(s1b);
+    s2b = wave_sum(s2b);
+    const float m1a = s1a * inv_d, m2a = s2a * inv_d, m1b = s1b * inv_d, m2b = s2b * inv_d;
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int ch = lane + c * 64;
       if (ch < nchunk) {
-        float xv[8], dv[8], o[8];
-        load8(x + base + ch * 8, xv);
-        load8(dy + base + ch * 8, dv);
+        float oa[8], ob[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          o[j] = rs * (dv[j] * gl[ch * 8 + j] - m1 - (xv[j] - mu) * rs * m2);
-        if (HAS_DRES) {
-          float t[8];
-          load8(dres + base + ch * 8, t);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += t[j];
+        for (int j = 0; j < 8; ++j) {
+          const float gj = (float)gv[c][j];
+          oa[j] = rsa * ((float)da[c][j] * gj - m1a - ((float)xa[c][j] - mua) * rsa * m2a);
+          ob[j] = rsb * ((float)dbb[c][j] * gj - m1b - ((float)xb[c][j] - mub) * rsb * m2b);
         }
-        store8(dx + base + ch * 8, o);
+        if (HAS_DRES) {
+          float ta[8], tb[8];
+          load8(dres + b0 + ch * 8, ta);
+          if (v1) load8(dres + b1 + ch * 8, tb);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            oa[j] += ta[j];
+            if (v1) ob[j] += tb[j];
+          }
+        }
+        store8(dx + b0 + ch * 8, oa);
+        if (v1) store8(dx + b1 + ch * 8, ob);
       }
     }
   }
+  __syncthreads();
 #pragma unroll
   for (int c = 0; c < NV; ++c) {
     const int ch = lane + c * 64;
@@ -166,7 +197,7 @@ __global__ __launch_bounds__(512) void ln_bwd_kernel(
 __global__ __launch_bounds__(1024) void colsum_bf16_kernel(const float* __restrict__ partial,
                                                            int nrow, int ncol, int split,
                                                            bf16* __restrict__ o0,
-                                                           bf16* __restrict__ o1) {
+                                                           bf16* __restrict__ o1, int accumulate) {
   __shared__ float red[16][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int c = blockIdx.x * 64 + lane;
@@ -188,15 +219,16 @@ __global__ __launch_bounds__(1024) void colsum_bf16_kernel(const float* __restri
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < 16; ++w) s += red[w][lane];
-    if (c < split) o0[c] = (bf16)s;
-    else o1[c - split] = (bf16)s;
+    bf16* dst = c < split ? o0 + c : o1 + (c - split);
+    if (accumulate) s += (float)*dst;  // accumulate into an existing (main) gradient
+    *dst = (bf16)s;
   }
 }
 
 void colsum_bf16_launch(const float* partial, int nrow, int ncol, int split, bf16* o0, bf16* o1,
-                        hipStream_t st) {
+                        hipStream_t st, int accumulate) {
   hipLaunchKernelGGL(colsum_bf16_kernel, dim3((ncol + 63) / 64), dim3(1024), 0, st, partial, nrow,
-                     ncol, split, o0, o1);
+                     ncol, split, o0, o1, accumulate);
 }
 
 template <int NV>
@@ -216,8 +248,8 @@ template <int NV>
 static void ln_bwd_dispatch(const bf16* dy, const bf16* x, const bf16* g, const float* mean,
                             const float* rstd, const bf16* dres, bf16* dx, float* partial,
                             int nblk, int rows, int D, hipStream_t st) {
-  dim3 grid(nblk), block(512);
-  size_t lds = (size_t)3 * D * sizeof(float);
+  dim3 grid(nblk), block(256);
+  size_t lds = (size_t)2 * D * sizeof(float);
   if (dres)
     hipLaunchKernelGGL((ln_bwd_kernel<NV, true>), grid, block, lds, st, dy, x, g, mean, rstd, dres,
                        dx, partial, rows, D);
@@ -260,7 +292,7 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
     case 4: ln_bwd_dispatch<4>(dy, x, g, mean, rstd, dres, dx, partial, nblk, rows, D, st); break;
     case 8: ln_bwd_dispatch<8>(dy, x, g, mean, rstd, dres, dx, partial, nblk, rows, D, st); break;
   }
-  colsum_bf16_launch(partial, nblk, 2 * D, D, dg, db, st);
+  colsum_bf16_launch(partial, nblk, 2 * D, D, dg, db, st, 0);
 }
 
 }  // namespace caamd

@@ -164,6 +164,25 @@ def test_gpt2_train_step_gpu():
     assert last < first - 1.0, (first, last)
 
 
+def test_main_grad_path_matches_autograd():
+    """Fused main-grad linears + flat buffer == plain autograd gradients."""
+    from cluster_anywhere_amd.models.gpt2 import GPT2, GPT2Config
+    from cluster_anywhere_amd.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(0)
+    cfg = GPT2Config.named("gpt2-tiny")
+    ref = GPT2(cfg).cuda().bfloat16()
+    fused = GPT2(cfg).cuda()
+    fused.load_state_dict({k: v.float() for k, v in ref.state_dict().items()})
+    flat = FlatParamSpace(fused, dtype=torch.bfloat16)
+    x = torch.randint(0, cfg.vocab_size, (2, 65), device="cuda")
+    ref(x[:, :-1], x[:, 1:]).backward()
+    flat.zero_grad()
+    fused(x[:, :-1], x[:, 1:]).backward()
+    for (n, p), (_, q) in zip(ref.named_parameters(), fused.named_parameters()):
+        assert _rel(q.main_grad, p.grad) < 3e-2, (n, _rel(q.main_grad, p.grad))
+
+
 def test_gpt2_gpu_matches_fp32_reference_loss():
     """bf16 model on GPU (HIP kernels) vs fp32 CPU reference: same initial loss."""
     from cluster_anywhere_amd.models.gpt2 import GPT2, GPT2Config
