@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-xl")
-    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("CAAMD_MBS", "8")))
+    ap.add_argument("--micro-batch", type=int, default=int(os.environ.get("CAAMD_MBS", "32")))
     ap.add_argument("--seq-len", type=int, default=1024)
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--zero", type=int, default=int(os.environ.get("CAAMD_ZERO", "1")),

@@ -406,7 +406,9 @@ class DataParallelTrainer:
                         ckpts.append((m, path))
                         ckpt_index += 1
                     for cb in callbacks:
-                        if hasattr(cb, "on_report"):
+                        if hasattr(cb, "on_report_with_checkpoint"):
+                            cb.on_report_with_checkpoint(m, path)
+                        elif hasattr(cb, "on_report"):
                             cb.on_report(m)
                 if err is not None:
                     raise _AttemptFailed(err, history, ckpts, ckpt_index)
