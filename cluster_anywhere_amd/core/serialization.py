@@ -127,6 +127,8 @@ class _Pickler(pickle.Pickler):
 
             if isinstance(obj, torch.Tensor) and not isinstance(obj, torch.nn.Parameter):
                 return _reduce_torch(obj)
+        if type(obj).__name__ == "State" and mod == "starlette.datastructures":
+            return (type(obj), (dict(obj._state),))
         return NotImplemented
 
 
@@ -146,6 +148,9 @@ class _CloudPickler(cloudpickle.CloudPickler):
 
             if isinstance(obj, torch.Tensor) and not isinstance(obj, torch.nn.Parameter):
                 return _reduce_torch(obj)
+        if type(obj).__name__ == "State" and type(obj).__module__ == "starlette.datastructures":
+            # starlette's State.__getattr__ recurses when unpickled attribute-by-attribute
+            return (type(obj), (dict(obj._state),))
         return super().reducer_override(obj)
 
 

@@ -521,7 +521,19 @@ class CoreWorker:
             try:
                 args, kwargs = self._resolve_args(spec, resolved)
                 m = getattr(self.actor_instance, spec.method)
-                if inspect.isasyncgenfunction(m):
+                if inspect.isasyncgenfunction(m) and spec.generator == "streaming":
+                    # stream items to the owner as they are produced
+                    i = 0
+                    try:
+                        async for x in m(*args, **kwargs):
+                            self._stream_item(spec, i, x)
+                            i += 1
+                    except asyncio.CancelledError:
+                        raise
+                    except BaseException as e:  # noqa
+                        self._stream_error(spec, i, e)
+                    result = iter(())
+                elif inspect.isasyncgenfunction(m):
                     items = []
                     async for x in m(*args, **kwargs):
                         items.append(x)
@@ -575,22 +587,28 @@ class CoreWorker:
             raise ValueError(f"task declared num_returns={n} but returned {result!r}")
         return [self._result_entry(o, v) for o, v in zip(spec.return_ids, vals)]
 
+    def _stream_item(self, spec, i, item):
+        oid = ObjectID.for_task_return(spec.task_id, i)
+        so = serialization.serialize(item)
+        inline, size, node = self._store(oid, so)
+        self.send(("gen_item", spec.task_id, i, oid, inline, size, node, so.contained_refs, False))
+
+    def _stream_error(self, spec, i, e):
+        from ..exceptions import RayTaskError
+
+        err = RayTaskError.from_exception(spec.fn_name, e)
+        oid = ObjectID.for_task_return(spec.task_id, i)
+        blob = serialization.serialize(err).to_bytes()
+        self.send(("gen_item", spec.task_id, i, oid, blob, len(blob), None, [], True))
+
     def _stream(self, spec, gen):
         i = 0
         try:
             for item in gen:
-                oid = ObjectID.for_task_return(spec.task_id, i)
-                so = serialization.serialize(item)
-                inline, size, node = self._store(oid, so)
-                self.send(("gen_item", spec.task_id, i, oid, inline, size, node, so.contained_refs, False))
+                self._stream_item(spec, i, item)
                 i += 1
         except BaseException as e:  # noqa
-            from ..exceptions import RayTaskError
-
-            err = RayTaskError.from_exception(spec.fn_name, e)
-            oid = ObjectID.for_task_return(spec.task_id, i)
-            blob = serialization.serialize(err).to_bytes()
-            self.send(("gen_item", spec.task_id, i, oid, blob, len(blob), None, [], True))
+            self._stream_error(spec, i, e)
         return []
 
     def _result_entry(self, oid, value):

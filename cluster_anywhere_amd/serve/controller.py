@@ -1,0 +1,342 @@
+"""Serve controller actor (reference: python/ray/serve/_private/controller.py,
+deployment_state.py, application_state.py, autoscaling_state.py).
+
+A named, detached, threaded actor that owns every application's deployments
+and replicas. A reconcile thread (every 100 ms):
+  * starts replicas up to the target count and promotes them to RUNNING once
+    their ``ready()`` completes,
+  * drains + kills surplus replicas (graceful ``prepare_for_shutdown``),
+  * health-checks RUNNING replicas and replaces dead ones,
+  * runs the autoscaling policy from replica-reported ongoing requests.
+Handles and the HTTP proxy read ``(version, replicas)`` snapshots; the version
+bumps on every membership change so clients refresh only when needed."""
+from __future__ import annotations
+
+import threading
+import time
+import traceback
+import uuid
+from typing import Any, Dict, List, Optional
+
+from ..core import api as core
+from .config import DeploymentConfig
+
+CONTROLLER_NAME = "SERVE_CONTROLLER"
+NAMESPACE = "serve"
+
+
+class _ReplicaState:
+    def __init__(self, tag, handle):
+        self.tag = tag
+        self.handle = handle
+        self.state = "STARTING"
+        self.ready_ref = handle.ready.remote()
+        self.health_ref = None
+        self.health_sent = 0.0
+        self.metrics = {"ongoing": 0, "models": []}
+        self.metrics_ref = None
+        self.started = time.time()
+        self.stop_ref = None
+
+
+class _DeploymentState:
+    def __init__(self, app: str, name: str, target, init_args, init_kwargs, config: DeploymentConfig):
+        self.app = app
+        self.name = name
+        self.target = target
+        self.init_args = init_args
+        self.init_kwargs = init_kwargs
+        self.config = config
+        self.target_replicas = config.initial_replicas()
+        self.replicas: List[_ReplicaState] = []
+        self.version = 0
+        self.counter = 0
+        self.error: Optional[str] = None
+        self.scale_since: Optional[float] = None
+        self.scale_dir = 0
+        self.metric_hist: List[tuple] = []
+        self.deleting = False
+
+    def running(self):
+        return [r for r in self.replicas if r.state == "RUNNING"]
+
+    def status(self):
+        if self.error:
+            return "DEPLOY_FAILED"
+        run = len(self.running())
+        if run == self.target_replicas and all(r.state == "RUNNING" for r in self.replicas):
+            return "HEALTHY"
+        return "UPDATING" if run < self.target_replicas else "DOWNSCALING"
+
+
+class ServeController:
+    def __init__(self, http_options=None):
+        self.apps: Dict[str, Dict[str, Any]] = {}  # name -> {route_prefix, ingress, deployments{}}
+        self.lock = threading.RLock()
+        self.http_options = http_options
+        self.proxy = None
+        self.proxy_port = None
+        self._orphans: List[_DeploymentState] = []
+        self.alive = True
+        self.thread = threading.Thread(target=self._loop, name="serve-reconcile", daemon=True)
+        self.thread.start()
+
+    # ------------------------------------------------------------- public API
+    def deploy_application(self, name: str, route_prefix: Optional[str], ingress: str,
+                           deployments: List[Dict]):
+        with self.lock:
+            old = self.apps.get(name)
+            new_deps = {}
+            for d in deployments:
+                cfg: DeploymentConfig = d["config"]
+                prev = old["deployments"].get(d["name"]) if old else None
+                if prev is not None and prev.config.version is not None and prev.config.version == cfg.version \
+                        and prev.target is not None:
+                    # same code version: in-place reconfigure / rescale
+                    if cfg.user_config != prev.config.user_config:
+                        for r in prev.replicas:
+                            r.handle.reconfigure.remote(cfg.user_config)
+                    prev.config = cfg
+                    if cfg.autoscaling_config is None:
+                        prev.target_replicas = cfg.initial_replicas()
+                    new_deps[d["name"]] = prev
+                    continue
+                if prev is not None:
+                    prev.deleting = True  # old replicas drain below
+                    self._orphans.append(prev)
+                new_deps[d["name"]] = _DeploymentState(name, d["name"], d["target"], d["args"], d["kwargs"], cfg)
+            if old:
+                for dn, st in old["deployments"].items():
+                    if dn not in new_deps:
+                        st.deleting = True
+                        self._orphans.append(st)
+            self.apps[name] = {"route_prefix": route_prefix, "ingress": ingress, "deployments": new_deps,
+                               "created": time.time()}
+        return True
+
+    def delete_application(self, name: str):
+        with self.lock:
+            app = self.apps.pop(name, None)
+            if app:
+                for st in app["deployments"].values():
+                    st.deleting = True
+                    self._orphans.append(st)
+        return True
+
+    def get_replicas(self, app: str, deployment: str):
+        with self.lock:
+            a = self.apps.get(app)
+            if a is None or deployment not in a["deployments"]:
+                return None
+            st = a["deployments"][deployment]
+            return (st.version, [(r.tag, r.handle, list(r.metrics.get("models", []))) for r in st.running()],
+                    st.config.max_ongoing_requests)
+
+    def get_routes(self):
+        with self.lock:
+            return {a["route_prefix"]: (name, a["ingress"]) for name, a in self.apps.items()
+                    if a["route_prefix"] is not None}
+
+    def get_ingress(self, app: str):
+        with self.lock:
+            a = self.apps.get(app)
+            return a["ingress"] if a else None
+
+    def list_apps(self):
+        with self.lock:
+            return list(self.apps.keys())
+
+    def status(self):
+        with self.lock:
+            out = {}
+            for name, a in self.apps.items():
+                deps = {}
+                for dn, st in a["deployments"].items():
+                    deps[dn] = {"status": st.status(), "target_replicas": st.target_replicas,
+                                "running_replicas": len(st.running()),
+                                "replica_states": {r.tag: r.state for r in st.replicas},
+                                "message": st.error or ""}
+                sts = [d["status"] for d in deps.values()]
+                if any(s == "DEPLOY_FAILED" for s in sts):
+                    ast = "DEPLOY_FAILED"
+                elif all(s == "HEALTHY" for s in sts):
+                    ast = "RUNNING"
+                else:
+                    ast = "DEPLOYING"
+                out[name] = {"status": ast, "route_prefix": a["route_prefix"], "deployments": deps}
+            return out
+
+    def set_proxy(self, proxy, port):
+        self.proxy, self.proxy_port = proxy, port
+        return True
+
+    def get_proxy(self):
+        return self.proxy, self.proxy_port
+
+    def record_handle_metrics(self, app, deployment, queued):
+        with self.lock:
+            a = self.apps.get(app)
+            if a and deployment in a["deployments"]:
+                a["deployments"][deployment].handle_queued = queued
+        return True
+
+    def shutdown(self):
+        with self.lock:
+            for name in list(self.apps):
+                self.delete_application(name)
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            with self.lock:
+                if not self._orphans:
+                    break
+            time.sleep(0.05)
+        if self.proxy is not None:
+            try:
+                core.kill(self.proxy)
+            except Exception:
+                pass
+            self.proxy = None
+        self.alive = False
+        return True
+
+    # --------------------------------------------------------------- reconcile
+    def _loop(self):
+        while self.alive:
+            try:
+                with self.lock:
+                    for a in list(self.apps.values()):
+                        for st in a["deployments"].values():
+                            self._reconcile(st)
+                    for st in list(self._orphans):
+                        self._reconcile(st)
+                        if not st.replicas:
+                            self._orphans.remove(st)
+            except Exception:  # keep the control loop alive
+                traceback.print_exc()
+            time.sleep(0.1)
+
+    def _start_replica(self, st: _DeploymentState):
+        from ..core.actor import ActorClass
+        from .replica import ServeReplica
+
+        st.counter += 1
+        tag = f"{st.app}#{st.name}#{uuid.uuid4().hex[:6]}"
+        opts = dict(st.config.ray_actor_options or {})
+        opts.setdefault("num_cpus", 0)
+        opts["max_concurrency"] = max(16, st.config.max_ongoing_requests * 2)
+        opts["max_restarts"] = 0
+        Replica = ActorClass(ServeReplica, {})
+        h = Replica.options(**opts).remote(st.app, st.name, tag, st.target, st.init_args, st.init_kwargs,
+                                           st.config.user_config, st.config.max_ongoing_requests)
+        st.replicas.append(_ReplicaState(tag, h))
+
+    def _stop_replica(self, st: _DeploymentState, r: _ReplicaState):
+        if r.state != "STOPPING":
+            r.state = "STOPPING"
+            st.version += 1
+            r.stop_ref = r.handle.prepare_for_shutdown.remote(st.config.graceful_shutdown_timeout_s,
+                                                             st.config.graceful_shutdown_wait_loop_s)
+            r.stop_deadline = time.time() + st.config.graceful_shutdown_timeout_s + 2
+
+    def _reconcile(self, st: _DeploymentState):
+        from ..exceptions import RayActorError, RayError
+
+        now = time.time()
+        # promote / fail starting replicas
+        for r in list(st.replicas):
+            if r.state == "STARTING":
+                ready, _ = core.wait([r.ready_ref], timeout=0)
+                if ready:
+                    try:
+                        core.get(r.ready_ref)
+                        r.state = "RUNNING"
+                        st.version += 1
+                        st.error = None
+                    except RayError as e:
+                        st.error = f"replica {r.tag} failed to start: {e}"
+                        st.replicas.remove(r)
+                        self._kill(r)
+            elif r.state == "STOPPING":
+                ready, _ = core.wait([r.stop_ref], timeout=0)
+                if ready or now > r.stop_deadline:
+                    st.replicas.remove(r)
+                    self._kill(r)
+        target = 0 if st.deleting else st.target_replicas
+        live = [r for r in st.replicas if r.state in ("STARTING", "RUNNING")]
+        if len(live) < target and not (st.error and len(live) == 0 and st.counter > 3 * max(1, target)):
+            for _ in range(target - len(live)):
+                self._start_replica(st)
+        elif len(live) > target:
+            # drain the least loaded / newest replicas first
+            order = sorted(live, key=lambda r: (r.state == "RUNNING", -r.started))
+            for r in order[: len(live) - target]:
+                if r.state == "STARTING":
+                    st.replicas.remove(r)
+                    self._kill(r)
+                else:
+                    self._stop_replica(st, r)
+        # health checks + metrics
+        for r in st.running():
+            if r.health_ref is not None:
+                ready, _ = core.wait([r.health_ref], timeout=0)
+                if ready:
+                    try:
+                        core.get(r.health_ref)
+                        r.health_ref = None
+                    except RayError:
+                        r.state = "DEAD"
+                elif now - r.health_sent > st.config.health_check_timeout_s:
+                    r.state = "DEAD"
+            elif now - r.health_sent > st.config.health_check_period_s:
+                r.health_ref = r.handle.check_health.remote()
+                r.health_sent = now
+            if r.state == "DEAD":
+                st.replicas.remove(r)
+                st.version += 1
+                self._kill(r)
+                continue
+            if r.metrics_ref is not None:
+                ready, _ = core.wait([r.metrics_ref], timeout=0)
+                if ready:
+                    try:
+                        m = core.get(r.metrics_ref)
+                        models_changed = m.get("models") != r.metrics.get("models")
+                        r.metrics = m
+                        if models_changed:
+                            st.version += 1
+                    except RayError:
+                        pass
+                    r.metrics_ref = None
+            else:
+                interval = st.config.autoscaling_config.metrics_interval_s if st.config.autoscaling_config else 0.5
+                if now - r.metrics.get("_sent", 0) > interval:
+                    r.metrics["_sent"] = now
+                    r.metrics_ref = r.handle.get_metrics.remote()
+        if st.config.autoscaling_config is not None and not st.deleting:
+            self._autoscale(st, now)
+
+    def _autoscale(self, st: _DeploymentState, now: float):
+        cfg = st.config.autoscaling_config
+        run = st.running()
+        total = sum(r.metrics.get("ongoing", 0) for r in run) + getattr(st, "handle_queued", 0)
+        st.metric_hist.append((now, total))
+        st.metric_hist = [(t, v) for t, v in st.metric_hist if now - t <= cfg.look_back_period_s]
+        avg = sum(v for _, v in st.metric_hist) / max(1, len(st.metric_hist))
+        desired = cfg.desired(avg, max(1, len(run)) if run else st.target_replicas)
+        if desired == st.target_replicas:
+            st.scale_since, st.scale_dir = None, 0
+            return
+        d = 1 if desired > st.target_replicas else -1
+        if st.scale_dir != d:
+            st.scale_dir, st.scale_since = d, now
+            return
+        delay = cfg.upscale_delay_s if d > 0 else cfg.downscale_delay_s
+        if now - st.scale_since >= delay:
+            st.target_replicas = desired
+            st.scale_since, st.scale_dir = None, 0
+
+    def _kill(self, r: _ReplicaState):
+        try:
+            core.kill(r.handle)
+        except Exception:
+            pass

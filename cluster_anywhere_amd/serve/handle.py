@@ -1,0 +1,255 @@
+"""Deployment handles and the client-side router (reference:
+python/ray/serve/handle.py, _private/router.py,
+_private/replica_scheduler/pow_2_scheduler.py).
+
+Routing is power-of-two-choices over the replicas' in-flight counts tracked
+locally by this process's router (incremented at send, decremented when the
+response future completes). Requests carrying a multiplexed model id prefer
+replicas that already hold the model. Replica membership is cached and
+refreshed from the controller when its version changes (polled at most every
+``_REFRESH_S``) or when a replica dies."""
+from __future__ import annotations
+
+import asyncio
+import concurrent.futures
+import random
+import threading
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+from ..core import api as core
+
+_REFRESH_S = 0.5
+
+
+def _controller():
+    from .controller import CONTROLLER_NAME, NAMESPACE
+
+    return core.get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
+
+
+class _Router:
+    def __init__(self, app: str, deployment: str):
+        self.app, self.deployment = app, deployment
+        self.replicas: List[tuple] = []  # (tag, handle, models)
+        self.version = -1
+        self.inflight: Dict[str, int] = {}
+        self.max_ongoing = 5
+        self.last_refresh = 0.0
+        self.lock = threading.Lock()
+        self.rng = random.Random()
+
+    def _refresh(self, force=False):
+        now = time.time()
+        if not force and now - self.last_refresh < _REFRESH_S and self.replicas:
+            return
+        self.last_refresh = now
+        snap = core.get(_controller().get_replicas.remote(self.app, self.deployment))
+        if snap is None:
+            raise KeyError(f"deployment {self.deployment!r} of application {self.app!r} does not exist")
+        version, reps, self.max_ongoing = snap
+        if version != self.version:
+            self.version = version
+            self.replicas = reps
+            for tag, _, _ in reps:
+                self.inflight.setdefault(tag, 0)
+
+    def choose(self, model_id: str = "", timeout_s: float = 60.0):
+        deadline = time.time() + timeout_s
+        while True:
+            self._refresh(force=not self.replicas)
+            if self.replicas:
+                break
+            if time.time() > deadline:
+                raise TimeoutError(f"no running replica of {self.app}/{self.deployment}")
+            time.sleep(0.05)
+        cands = self.replicas
+        if model_id:
+            having = [r for r in cands if model_id in r[2]]
+            if having:
+                cands = having
+            else:
+                # deterministic placement for a new model: same replica for same id
+                cands = [cands[hash(model_id) % len(cands)]] if len(cands) > 1 else cands
+        with self.lock:
+            if len(cands) == 1:
+                pick = cands[0]
+            else:
+                a, b = self.rng.sample(cands, 2)
+                pick = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
+            self.inflight[pick[0]] = self.inflight.get(pick[0], 0) + 1
+        return pick
+
+    def done(self, tag):
+        with self.lock:
+            self.inflight[tag] = max(0, self.inflight.get(tag, 0) - 1)
+
+    def invalidate(self):
+        self.last_refresh = 0.0
+        self.version = -1
+        self.replicas = []
+
+
+_routers: Dict[tuple, _Router] = {}
+_routers_lock = threading.Lock()
+
+
+def _router(app, dep) -> _Router:
+    with _routers_lock:
+        r = _routers.get((app, dep))
+        if r is None:
+            r = _routers[(app, dep)] = _Router(app, dep)
+        return r
+
+
+def _unwrap(x):
+    if isinstance(x, DeploymentResponse):
+        return x._to_object_ref()
+    return x
+
+
+class DeploymentResponse:
+    def __init__(self, router: _Router, tag: str, ref, resend):
+        self._router = router
+        self._tag = tag
+        self._ref = ref
+        self._resend = resend
+        self._fut = None
+        self._lock = threading.Lock()
+
+    def _future(self) -> concurrent.futures.Future:
+        with self._lock:
+            if self._fut is None:
+                self._fut = self._ref.future()
+                self._fut.add_done_callback(lambda f, t=self._tag, r=self._router: r.done(t))
+            return self._fut
+
+    def result(self, timeout_s: Optional[float] = None, _retries: int = 1):
+        from ..exceptions import RayActorError
+
+        try:
+            return self._future().result(timeout_s)
+        except concurrent.futures.TimeoutError:
+            from ..exceptions import GetTimeoutError
+
+            raise GetTimeoutError(f"response not ready after {timeout_s}s")
+        except RayActorError:
+            if _retries <= 0:
+                raise
+            self._router.invalidate()
+            again = self._resend()
+            return again.result(timeout_s, _retries - 1)
+
+    def __await__(self):
+        return asyncio.wrap_future(self._future()).__await__()
+
+    def _to_object_ref(self):
+        return self._ref
+
+    async def _to_object_ref_async(self):
+        return self._ref
+
+    def _to_object_ref_sync(self):
+        return self._ref
+
+    def cancel(self):
+        try:
+            core.cancel(self._ref)
+        except Exception:
+            pass
+
+    @property
+    def request_id(self):
+        return self._ref.hex()
+
+
+class DeploymentResponseGenerator:
+    def __init__(self, router: _Router, tag: str, gen):
+        self._router = router
+        self._tag = tag
+        self._gen = gen
+        self._done = False
+
+    def _finish(self):
+        if not self._done:
+            self._done = True
+            self._router.done(self._tag)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        try:
+            ref = next(self._gen)
+        except StopIteration:
+            self._finish()
+            raise
+        return core.get(ref)
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self):
+        try:
+            ref = await self._gen.__anext__()
+        except StopAsyncIteration:
+            self._finish()
+            raise
+        return await ref
+
+    def cancel(self):
+        self._finish()
+
+
+class DeploymentHandle:
+    def __init__(self, deployment_name: str, app_name: str = "default", *, method_name: str = "__call__",
+                 multiplexed_model_id: str = "", stream: bool = False):
+        self.deployment_name = deployment_name
+        self.app_name = app_name
+        self._method = method_name
+        self._model_id = multiplexed_model_id
+        self._stream = stream
+
+    def options(self, *, method_name: Optional[str] = None, multiplexed_model_id: Optional[str] = None,
+                stream: Optional[bool] = None, use_new_handle_api: bool = True, **_ignored) -> "DeploymentHandle":
+        return DeploymentHandle(self.deployment_name, self.app_name,
+                                method_name=method_name if method_name is not None else self._method,
+                                multiplexed_model_id=multiplexed_model_id if multiplexed_model_id is not None
+                                else self._model_id,
+                                stream=self._stream if stream is None else stream)
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        return self.options(method_name=name)
+
+    def remote(self, *args, **kwargs):
+        router = _router(self.app_name, self.deployment_name)
+        args = tuple(_unwrap(a) for a in args)
+        kwargs = {k: _unwrap(v) for k, v in kwargs.items()}
+        meta = {"method": self._method, "model_id": self._model_id, "request_id": uuid.uuid4().hex[:12]}
+
+        if self._stream:
+            tag, h, _ = router.choose(self._model_id)
+            gen = h.handle_request_streaming.options(num_returns="streaming").remote(meta, *args, **kwargs)
+            return DeploymentResponseGenerator(router, tag, gen)
+
+        def send():
+            tag, h, _ = router.choose(self._model_id)
+            ref = h.handle_request.remote(meta, *args, **kwargs)
+            return DeploymentResponse(router, tag, ref, send)
+
+        resp = send()
+        resp._future()  # start tracking completion now (in-flight accounting)
+        return resp
+
+    def __reduce__(self):
+        return (DeploymentHandle, (self.deployment_name, self.app_name),
+                {"_method": self._method, "_model_id": self._model_id, "_stream": self._stream})
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+
+    def __repr__(self):
+        return f"DeploymentHandle(deployment={self.deployment_name!r}, app={self.app_name!r})"

@@ -1,0 +1,255 @@
+"""Serve: deployments, handles + composition, HTTP proxy, FastAPI ingress,
+@serve.batch, streaming, multiplexing, user_config, autoscaling, replica
+failure recovery (reference: python/ray/serve/tests/test_api.py,
+test_handle_api.py, test_batching.py, test_multiplex.py,
+test_autoscaling_policy.py, test_streaming_response.py)."""
+import asyncio
+import json
+import os
+import time
+import urllib.request
+
+import pytest
+
+import cluster_anywhere_amd as ray
+from cluster_anywhere_amd import serve
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=8)
+    serve.start(http_options={"port": 0})
+    yield
+    serve.shutdown()
+    ray.shutdown()
+
+
+def _http(path, data=None, headers=None):
+    port = serve.http_port()
+    req = urllib.request.Request(f"http://127.0.0.1:{port}{path}", data=data, headers=headers or {})
+    with urllib.request.urlopen(req, timeout=30) as r:
+        return r.status, r.read()
+
+
+@serve.deployment
+def hello(request):
+    return "hello " + request.query_params.get("name", "world")
+
+
+def test_function_deployment_http(cluster):
+    h = serve.run(hello.bind(), name="hello", route_prefix="/hello")
+    assert _http("/hello?name=mi355x") == (200, b"hello mi355x")
+    assert _http("/-/healthz") == (200, b"success")
+    st = serve.status()
+    assert st.applications["hello"].status == "RUNNING"
+    serve.delete("hello")
+    assert "hello" not in serve.status().applications
+
+
+@serve.deployment(num_replicas=2)
+class Adder:
+    def __init__(self, inc):
+        self.inc = inc
+
+    def __call__(self, x):
+        return x + self.inc
+
+    def pid(self):
+        return os.getpid()
+
+
+@serve.deployment
+class Pipeline:
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+    async def __call__(self, x):
+        y = await self.a.remote(x)
+        return await self.b.remote(y)
+
+
+def test_composition_and_routing(cluster):
+    app = Pipeline.bind(Adder.bind(1), Adder.options(name="Adder2").bind(10))
+    h = serve.run(app, name="pipe", route_prefix=None)
+    assert h.remote(5).result() == 16
+    assert [r.result() for r in [h.remote(i) for i in range(20)]] == [i + 11 for i in range(20)]
+    # both replicas of a deployment receive traffic
+    ah = serve.get_deployment_handle("Adder", "pipe")
+    pids = {ah.pid.remote().result() for _ in range(30)}
+    assert len(pids) == 2
+    # responses can be passed into other calls unresolved
+    assert ah.remote(ah.remote(1)).result() == 3
+    serve.delete("pipe")
+
+
+@serve.deployment(max_ongoing_requests=32)
+class Batcher:
+    def __init__(self):
+        self.sizes = []
+
+    @serve.batch(max_batch_size=8, batch_wait_timeout_s=0.05)
+    async def __call__(self, xs):
+        self.sizes.append(len(xs))
+        return [x * 2 for x in xs]
+
+    def sizes_seen(self):
+        return self.sizes
+
+
+def test_batching(cluster):
+    h = serve.run(Batcher.bind(), name="batch", route_prefix=None)
+    rs = [h.remote(i) for i in range(16)]
+    assert [r.result() for r in rs] == [2 * i for i in range(16)]
+    sizes = h.sizes_seen.remote().result()
+    assert max(sizes) > 1 and sum(sizes) == 16
+    serve.delete("batch")
+
+
+@serve.deployment
+class Streamer:
+    def __call__(self, n):
+        for i in range(n):
+            yield i
+
+    async def agen(self, n):
+        for i in range(n):
+            await asyncio.sleep(0.001)
+            yield f"tok{i}"
+
+
+def test_streaming(cluster):
+    h = serve.run(Streamer.bind(), name="stream", route_prefix=None)
+    assert list(h.options(stream=True).remote(5)) == [0, 1, 2, 3, 4]
+    assert list(h.options(stream=True, method_name="agen").remote(3)) == ["tok0", "tok1", "tok2"]
+    serve.delete("stream")
+
+
+@serve.deployment(num_replicas=2)
+class Multi:
+    @serve.multiplexed(max_num_models_per_replica=2)
+    async def get_model(self, model_id):
+        return {"id": model_id, "pid": os.getpid()}
+
+    async def __call__(self, x):
+        m = await self.get_model(serve.get_multiplexed_model_id())
+        return m["id"], m["pid"], x
+
+
+def test_multiplexing(cluster):
+    h = serve.run(Multi.bind(), name="mux", route_prefix=None)
+    r = h.options(multiplexed_model_id="m1").remote(1).result()
+    assert r[0] == "m1"
+    time.sleep(1.2)  # replica reports its loaded models to the controller
+    pids = {h.options(multiplexed_model_id="m1").remote(i).result()[1] for i in range(10)}
+    assert pids == {r[1]}
+    serve.delete("mux")
+
+
+@serve.deployment(user_config={"threshold": 1})
+class Configurable:
+    def __init__(self):
+        self.t = None
+
+    def reconfigure(self, cfg):
+        self.t = cfg["threshold"]
+
+    def __call__(self, _):
+        return self.t
+
+
+def test_user_config_update(cluster):
+    h = serve.run(Configurable.options(version="v1").bind(), name="cfg", route_prefix=None)
+    assert h.remote(0).result() == 1
+    h = serve.run(Configurable.options(version="v1", user_config={"threshold": 7}).bind(), name="cfg",
+                  route_prefix=None)
+    deadline = time.time() + 10
+    while h.remote(0).result() != 7 and time.time() < deadline:
+        time.sleep(0.05)
+    assert h.remote(0).result() == 7
+    serve.delete("cfg")
+
+
+def test_fastapi_ingress(cluster):
+    from fastapi import FastAPI
+
+    api = FastAPI()
+
+    @serve.deployment
+    @serve.ingress(api)
+    class Api:
+        def __init__(self, greeting):
+            self.greeting = greeting
+
+        @api.get("/hi/{name}")
+        def hi(self, name: str):
+            return {"msg": f"{self.greeting} {name}"}
+
+        @api.post("/sum")
+        async def sum_(self, body: dict):
+            return {"sum": sum(body["xs"])}
+
+    serve.run(Api.bind("hey"), name="api", route_prefix="/api")
+    st, body = _http("/api/hi/amd")
+    assert st == 200 and json.loads(body) == {"msg": "hey amd"}
+    st, body = _http("/api/sum", data=json.dumps({"xs": [1, 2, 3]}).encode(),
+                     headers={"content-type": "application/json"})
+    assert json.loads(body) == {"sum": 6}
+    serve.delete("api")
+
+
+@serve.deployment(autoscaling_config={"min_replicas": 1, "max_replicas": 3, "target_ongoing_requests": 1,
+                                      "upscale_delay_s": 0.2, "downscale_delay_s": 0.5,
+                                      "metrics_interval_s": 0.1, "look_back_period_s": 0.5},
+                  max_ongoing_requests=10)
+class Slow:
+    async def __call__(self, t):
+        await asyncio.sleep(t)
+        return os.getpid()
+
+
+def test_autoscaling(cluster):
+    h = serve.run(Slow.bind(), name="auto", route_prefix=None)
+    assert serve.status().applications["auto"].deployments["Slow"].running_replicas == 1
+    rs = [h.remote(3.0) for _ in range(8)]
+    deadline = time.time() + 20
+    peak = 1
+    while time.time() < deadline:
+        peak = max(peak, serve.status().applications["auto"].deployments["Slow"].target_replicas)
+        if peak >= 2:
+            break
+        time.sleep(0.1)
+    assert peak >= 2
+    [r.result() for r in rs]
+    deadline = time.time() + 20
+    while time.time() < deadline:
+        if serve.status().applications["auto"].deployments["Slow"].target_replicas == 1:
+            break
+        time.sleep(0.2)
+    assert serve.status().applications["auto"].deployments["Slow"].target_replicas == 1
+    serve.delete("auto")
+
+
+@serve.deployment(health_check_period_s=0.2, health_check_timeout_s=2)
+class Fragile:
+    def __call__(self, die=False):
+        if die:
+            os._exit(1)
+        return os.getpid()
+
+
+def test_replica_failure_recovery(cluster):
+    h = serve.run(Fragile.bind(), name="frag", route_prefix=None)
+    pid = h.remote().result()
+    with pytest.raises(Exception):
+        h.remote(True).result(_retries=0)
+    deadline = time.time() + 30
+    new = None
+    while time.time() < deadline:
+        try:
+            new = h.remote().result(timeout_s=5)
+            if new != pid:
+                break
+        except Exception:
+            time.sleep(0.2)
+    assert new is not None and new != pid
+    serve.delete("frag")
