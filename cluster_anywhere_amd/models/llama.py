@@ -1,0 +1,196 @@
+"""Llama-family decoder (Llama-3 architecture: RMSNorm, RoPE with llama3
+frequency scaling, grouped-query attention, SwiGLU) laid out for serving on
+MI355X: one fused ``w_qkv`` and one fused ``w_gate_up`` GEMM per layer, the
+paged KV cache in ``[num_blocks, KVH, block_size, D]`` bf16, and every
+non-GEMM op a gfx950 kernel (``ops/llm.py``).
+
+This is the model of the Serve LLM path (BASELINE.json config
+"Ray Serve Llama-3-8B bf16, one replica per MI355X, continuous batching");
+the reference serves it through vLLM (python/ray/llm/_internal/serve/...),
+here the engine is ``cluster_anywhere_amd/llm/engine.py``.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import llm as L
+
+
+@dataclass
+class LlamaConfig:
+    vocab_size: int = 128256
+    d_model: int = 4096
+    n_layer: int = 32
+    n_head: int = 32
+    n_kv_head: int = 8
+    ffn_dim: int = 14336
+    rope_theta: float = 500000.0
+    rope_scaling: Optional[dict] = field(default_factory=lambda: {
+        "rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0, "high_freq_factor": 4.0,
+        "original_max_position_embeddings": 8192})
+    norm_eps: float = 1e-5
+    max_position: int = 8192
+    tie_embeddings: bool = False
+
+    @property
+    def head_dim(self):
+        return self.d_model // self.n_head
+
+    @classmethod
+    def named(cls, name: str) -> "LlamaConfig":
+        if name in ("llama3-8b", "llama-3-8b", "Llama-3-8B"):
+            return cls()
+        if name in ("llama3-70b",):
+            return cls(d_model=8192, n_layer=80, n_head=64, n_kv_head=8, ffn_dim=28672)
+        if name in ("llama3.2-1b",):
+            return cls(d_model=2048, n_layer=16, n_head=32, n_kv_head=8, ffn_dim=8192, tie_embeddings=True,
+                       rope_scaling={"rope_type": "llama3", "factor": 32.0, "low_freq_factor": 1.0,
+                                     "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+        if name == "llama-tiny":
+            return cls(vocab_size=512, d_model=256, n_layer=2, n_head=4, n_kv_head=2, ffn_dim=512,
+                       rope_theta=10000.0, rope_scaling=None, max_position=1024)
+        if name == "llama-small":
+            return cls(vocab_size=4096, d_model=1024, n_layer=4, n_head=8, n_kv_head=2, ffn_dim=2816,
+                       max_position=4096)
+        raise ValueError(f"unknown Llama config {name!r}")
+
+    def num_params(self):
+        d, f, hd = self.d_model, self.ffn_dim, self.head_dim
+        per = d * (self.n_head + 2 * self.n_kv_head) * hd + self.n_head * hd * d + 3 * d * f + 2 * d
+        emb = self.vocab_size * d * (1 if self.tie_embeddings else 2)
+        return self.n_layer * per + emb + d
+
+
+class LlamaLayer(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        d, hd = cfg.d_model, cfg.head_dim
+        self.cfg = cfg
+        self.attn_norm = nn.Parameter(torch.ones(d))
+        self.w_qkv = nn.Parameter(torch.empty((cfg.n_head + 2 * cfg.n_kv_head) * hd, d))
+        self.w_o = nn.Parameter(torch.empty(d, cfg.n_head * hd))
+        self.mlp_norm = nn.Parameter(torch.ones(d))
+        self.w_gate_up = nn.Parameter(torch.empty(2 * cfg.ffn_dim, d))
+        self.w_down = nn.Parameter(torch.empty(d, cfg.ffn_dim))
+
+
+class Llama(nn.Module):
+    def __init__(self, cfg: LlamaConfig):
+        super().__init__()
+        self.cfg = cfg
+        self.embed = nn.Parameter(torch.empty(cfg.vocab_size, cfg.d_model))
+        self.layers = nn.ModuleList([LlamaLayer(cfg) for _ in range(cfg.n_layer)])
+        self.final_norm = nn.Parameter(torch.ones(cfg.d_model))
+        self.lm_head = None if cfg.tie_embeddings else nn.Parameter(torch.empty(cfg.vocab_size, cfg.d_model))
+        self._cos_sin = None
+
+    @torch.no_grad()
+    def init_weights(self, std: float = 0.02, seed: int = 0):
+        g = torch.Generator(device="cpu").manual_seed(seed)
+        for name, p in self.named_parameters():
+            if p.dim() >= 2:
+                if p.is_cuda:
+                    p.normal_(0.0, std)
+                else:
+                    p.copy_(torch.randn(p.shape, generator=g) * std)
+            else:
+                p.fill_(1.0)
+        return self
+
+    def cos_sin(self, device):
+        if self._cos_sin is None or self._cos_sin.device != torch.device(device):
+            self._cos_sin = L.rope_cos_sin(self.cfg.head_dim, self.cfg.max_position, self.cfg.rope_theta,
+                                           self.cfg.rope_scaling, device)
+        return self._cos_sin
+
+    def _head(self, x):
+        w = self.embed if self.lm_head is None else self.lm_head
+        return F.linear(x, w)
+
+    # -------------------------------------------------------------- prefill
+    @torch.no_grad()
+    def prefill(self, tokens: torch.Tensor, positions: torch.Tensor, slots: Optional[torch.Tensor],
+                k_caches, v_caches, last_idx: torch.Tensor) -> torch.Tensor:
+        """``tokens/positions [B, T]`` (right-padded), ``slots [B*T]`` cache slots
+        (-1 = padding), ``last_idx [B]`` index of each sequence's last prompt
+        token -> logits ``[B, vocab]`` of those positions."""
+        cfg = self.cfg
+        B, T = tokens.shape
+        H, KVH, hd = cfg.n_head, cfg.n_kv_head, cfg.head_dim
+        cs = self.cos_sin(tokens.device)
+        x = F.embedding(tokens, self.embed)  # [B, T, d]
+        res = None
+        pos = positions.reshape(-1).to(torch.int32)
+        for i, layer in enumerate(self.layers):
+            h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
+            if res is None:
+                res = x
+            qkv = F.linear(h, layer.w_qkv)  # [B, T, (H+2KVH)*hd]
+            L.rope_cache_(qkv, cs, pos, slots, k_caches[i] if k_caches is not None else None,
+                          v_caches[i] if v_caches is not None else None, H, KVH)
+            q = qkv[..., : H * hd]
+            k = qkv[..., H * hd: (H + KVH) * hd]
+            v = qkv[..., (H + KVH) * hd:]
+            o = L.prefill_attention(q, k, v, H, KVH, causal=True)
+            x = F.linear(o, layer.w_o)
+            h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
+            x = F.linear(L.silu_mul(F.linear(h, layer.w_gate_up)), layer.w_down)
+        h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
+        last = h[torch.arange(B, device=h.device), last_idx.long()]
+        return self._head(last)
+
+    # --------------------------------------------------------------- decode
+    @torch.no_grad()
+    def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, k_caches, v_caches,
+               block_tables: torch.Tensor, ctx_lens: torch.Tensor, max_ctx: int) -> torch.Tensor:
+        """One new token per sequence: ``tokens/positions/slots/ctx_lens [B]``
+        (ctx_lens include the new token), ``block_tables [B, max_blocks]``."""
+        cfg = self.cfg
+        H, KVH, hd = cfg.n_head, cfg.n_kv_head, cfg.head_dim
+        cs = self.cos_sin(tokens.device)
+        x = F.embedding(tokens, self.embed)  # [B, d]
+        res = None
+        pos = positions.to(torch.int32)
+        for i, layer in enumerate(self.layers):
+            h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
+            if res is None:
+                res = x
+            qkv = F.linear(h, layer.w_qkv)  # [B, (H+2KVH)*hd]
+            L.rope_cache_(qkv, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
+            o = L.paged_decode_attention(qkv, k_caches[i], v_caches[i], block_tables, ctx_lens, max_ctx, H)
+            x = F.linear(o, layer.w_o)
+            h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
+            x = F.linear(L.silu_mul(F.linear(h, layer.w_gate_up)), layer.w_down)
+        h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
+        return self._head(h)
+
+    # ------------------------------------------------ reference full forward
+    @torch.no_grad()
+    def forward(self, tokens: torch.Tensor) -> torch.Tensor:
+        """Dense causal forward over ``tokens [B, T]`` (no cache) -> logits."""
+        B, T = tokens.shape
+        pos = torch.arange(T, device=tokens.device).expand(B, T)
+        cfg = self.cfg
+        H, KVH, hd = cfg.n_head, cfg.n_kv_head, cfg.head_dim
+        cs = self.cos_sin(tokens.device)
+        x = F.embedding(tokens, self.embed)
+        res = None
+        for layer in self.layers:
+            h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
+            if res is None:
+                res = x
+            qkv = F.linear(h, layer.w_qkv)
+            L.rope_cache_(qkv, cs, pos.reshape(-1).to(torch.int32), None, None, None, H, KVH)
+            o = L.prefill_attention(qkv[..., : H * hd], qkv[..., H * hd: (H + KVH) * hd],
+                                    qkv[..., (H + KVH) * hd:], H, KVH, causal=True)
+            x = F.linear(o, layer.w_o)
+            h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
+            x = F.linear(L.silu_mul(F.linear(h, layer.w_gate_up)), layer.w_down)
+        h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
+        return self._head(h)

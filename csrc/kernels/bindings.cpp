@@ -376,6 +376,155 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, 
   return dqkv;
 }
 
+// ---- LLM serving kernels (llm.hip) -------------------------------------------------
+namespace caamd {
+void rmsnorm_launch(const bf16*, const bf16*, bf16*, const bf16*, bf16*, int, int, float, hipStream_t);
+void silu_mul_launch(const bf16*, bf16*, int, int, hipStream_t);
+void rope_cache_launch(bf16*, const float*, const int*, const int*, bf16*, bf16*, int, int, int, int, int,
+                       hipStream_t);
+bool paged_decode_launch(const bf16*, int, const bf16*, const bf16*, const int*, int, const int*, bf16*, float*,
+                         float*, int, int, int, int, int, int, float, hipStream_t);
+int paged_max_parts(int);
+void fa_fwd_gqa_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
+                       int, hipStream_t);
+}
+
+std::vector<Tensor> rmsnorm(const Tensor& x, const Tensor& w, double eps, const c10::optional<Tensor>& residual) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  const int D = (int)x.size(-1);
+  TORCH_CHECK(D % 8 == 0 && D <= 16 * 512, "rmsnorm: D must be a multiple of 8 and <= 8192");
+  TORCH_CHECK(w.numel() == D, "rmsnorm: weight size");
+  const int rows = (int)(x.numel() / D);
+  auto y = at::empty_like(x);
+  Tensor s_out;
+  const caamd::bf16* r = nullptr;
+  if (residual.has_value()) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->sizes() == x.sizes(), "rmsnorm: residual shape");
+    s_out = at::empty_like(x);
+    r = bp(*residual);
+  }
+  if (rows > 0) {
+    caamd::rmsnorm_launch(bp(x), r, r ? bp(s_out) : nullptr, bp(w), bp(y), rows, D, (float)eps, cur_stream());
+    LAUNCH_CHECK();
+  }
+  return {y, s_out};
+}
+
+Tensor silu_mul(const Tensor& gu) {
+  CHECK_BF16(gu);
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "silu_mul: last dim must be 2*F with F % 8 == 0");
+  const int F = (int)(F2 / 2);
+  const int rows = (int)(gu.numel() / F2);
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F;
+  auto out = at::empty(sizes, gu.options());
+  if (rows > 0) {
+    caamd::silu_mul_launch(bp(gu), bp(out), rows, F, cur_stream());
+    LAUNCH_CHECK();
+  }
+  return out;
+}
+
+void rope_cache_(Tensor& qkv, const Tensor& cos_sin, const Tensor& positions, const c10::optional<Tensor>& slots,
+                 const c10::optional<Tensor>& k_cache, const c10::optional<Tensor>& v_cache, int64_t H,
+                 int64_t KVH) {
+  CHECK_BF16(qkv);
+  CHECK_F32(cos_sin);
+  CHECK_GPU(positions);
+  CHECK_CONTIG(positions);
+  CHECK_DT(positions, at::kInt);
+  const int N = (int)positions.numel();
+  TORCH_CHECK(qkv.numel() % ((int64_t)N * (H + 2 * KVH)) == 0, "rope_cache: qkv shape");
+  const int D = (int)(qkv.numel() / ((int64_t)N * (H + 2 * KVH)));
+  TORCH_CHECK(D % 2 == 0 && cos_sin.size(-2) == D / 2 && cos_sin.size(-1) == 2, "rope_cache: cos_sin must be [P, D/2, 2]");
+  caamd::bf16 *kc = nullptr, *vc = nullptr;
+  const int* sl = nullptr;
+  int BS = 1;
+  if (k_cache.has_value()) {
+    TORCH_CHECK(slots.has_value() && v_cache.has_value(), "rope_cache: slots and v_cache required with k_cache");
+    CHECK_BF16(*k_cache);
+    CHECK_BF16(*v_cache);
+    CHECK_DT(*slots, at::kInt);
+    TORCH_CHECK(slots->numel() == N, "rope_cache: slots shape");
+    TORCH_CHECK(k_cache->dim() == 4 && k_cache->size(1) == KVH && k_cache->size(3) == D,
+                "rope_cache: cache must be [num_blocks, KVH, BS, D]");
+    BS = (int)k_cache->size(2);
+    kc = bp(*k_cache);
+    vc = bp(*v_cache);
+    sl = slots->data_ptr<int>();
+  }
+  if (N > 0) {
+    caamd::rope_cache_launch(bp(qkv), cos_sin.data_ptr<float>(), positions.data_ptr<int>(), sl, kc, vc, N, (int)H,
+                             (int)KVH, D, BS, cur_stream());
+    LAUNCH_CHECK();
+  }
+}
+
+Tensor paged_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
+                    const Tensor& ctx_lens, int64_t max_ctx, int64_t H, double scale) {
+  CHECK_GPU(q);
+  CHECK_DT(q, at::kBFloat16);
+  TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "paged_decode: q must be [B, >=H*D] with unit inner stride");
+  CHECK_BF16(k_cache);
+  CHECK_BF16(v_cache);
+  TORCH_CHECK(k_cache.dim() == 4, "paged_decode: cache must be [num_blocks, KVH, BS, D]");
+  const int KVH = (int)k_cache.size(1), BS = (int)k_cache.size(2), D = (int)k_cache.size(3);
+  const int B = (int)q.size(0);
+  TORCH_CHECK(q.size(1) >= H * D, "paged_decode: q width");
+  TORCH_CHECK(H % KVH == 0, "paged_decode: H must be a multiple of KVH");
+  CHECK_GPU(block_tables);
+  CHECK_CONTIG(block_tables);
+  CHECK_DT(block_tables, at::kInt);
+  CHECK_GPU(ctx_lens);
+  CHECK_DT(ctx_lens, at::kInt);
+  TORCH_CHECK(block_tables.size(0) == B && ctx_lens.numel() == B, "paged_decode: batch mismatch");
+  TORCH_CHECK(max_ctx <= block_tables.size(1) * BS, "paged_decode: max_ctx exceeds block table capacity");
+  auto out = at::empty({B, H * D}, q.options());
+  const int mp = caamd::paged_max_parts((int)max_ctx);
+  Tensor pacc, pml;
+  if (mp > 1) {
+    pacc = at::empty({B, H, mp, D}, q.options().dtype(at::kFloat));
+    pml = at::empty({B, H, mp, 2}, q.options().dtype(at::kFloat));
+  }
+  if (B > 0) {
+    const bool ok = caamd::paged_decode_launch(
+        bp(q), (int)q.stride(0), bp(k_cache), bp(v_cache), block_tables.data_ptr<int>(), (int)block_tables.size(1),
+        ctx_lens.data_ptr<int>(), bp(out), mp > 1 ? pacc.data_ptr<float>() : nullptr,
+        mp > 1 ? pml.data_ptr<float>() : nullptr, B, (int)H, KVH, D, BS, (int)max_ctx, (float)scale, cur_stream());
+    TORCH_CHECK(ok, "paged_decode: unsupported head_dim/group (D in {64,128}, H/KVH in {1,2,4,8})");
+    LAUNCH_CHECK();
+  }
+  return out;
+}
+
+// q/k/v: [B, T, width] views (e.g. slices of one fused qkv projection) with unit inner stride
+std::vector<Tensor> flash_attn_gqa(const Tensor& q, const Tensor& k, const Tensor& v, int64_t H, int64_t KVH,
+                                   bool causal) {
+  for (const Tensor* t : {&q, &k, &v}) {
+    CHECK_GPU(*t);
+    CHECK_DT(*t, at::kBFloat16);
+    TORCH_CHECK(t->dim() == 3 && t->stride(2) == 1 && t->stride(0) == t->size(1) * t->stride(1),
+                "flash_attn_gqa: q/k/v must be [B, T, width] with dense rows");
+  }
+  const int B = (int)q.size(0), T = (int)q.size(1);
+  TORCH_CHECK(q.size(2) % H == 0, "flash_attn_gqa: q width");
+  const int D = (int)(q.size(2) / H);
+  TORCH_CHECK(D == 64 || D == 128, "flash_attn_gqa: head dim must be 64 or 128");
+  TORCH_CHECK(k.size(2) == KVH * D && v.size(2) == KVH * D && H % KVH == 0, "flash_attn_gqa: kv width");
+  TORCH_CHECK(k.stride(1) == v.stride(1), "flash_attn_gqa: k/v row strides differ");
+  auto out = at::empty({B, T, H * D}, q.options());
+  auto lse = at::empty({B, H, T}, q.options().dtype(at::kFloat));
+  if (B > 0 && T > 0) {
+    caamd::fa_fwd_gqa_launch(bp(q), bp(k), bp(v), (int)q.stride(1), (int)k.stride(1), (int)(H / KVH), bp(out),
+                             lse.data_ptr<float>(), B, T, (int)H, D, causal ? 1 : 0, cur_stream());
+    LAUNCH_CHECK();
+  }
+  return {out, lse};
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cluster_anywhere_amd gfx950 HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -391,4 +540,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("vtrace", &vtrace);
   m.def("flash_attn_fwd", &flash_attn_fwd);
   m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("rmsnorm", &rmsnorm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("eps"),
+        pybind11::arg("residual") = pybind11::none());
+  m.def("silu_mul", &silu_mul);
+  m.def("rope_cache_", &rope_cache_);
+  m.def("paged_decode", &paged_decode);
+  m.def("flash_attn_gqa", &flash_attn_gqa);
 }

@@ -142,7 +142,10 @@ template <int D>
 constexpr int qblk_for() { return 4 * 32 * qs_for<D>(); }  // queries per block (fwd, dq)
 
 template <int D>
-__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16* __restrict__ qp,
+                                                        const bf16* __restrict__ kp,
+                                                        const bf16* __restrict__ vp, int q_rs,
+                                                        int kv_rs, int group,
                                                         bf16* __restrict__ out,
                                                         float* __restrict__ lse, int T, int H,
                                                         int nqb, float scale_log2, int causal) {
@@ -157,10 +160,11 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16* __restrict__
   const int b = bh / H, hh = bh % H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
-  const size_t rs = (size_t)3 * H * D;
-  const bf16* qbase = qkv + (size_t)b * T * rs + (size_t)hh * D;
-  const bf16* kbase = qbase + (size_t)H * D;
-  const bf16* vbase = kbase + (size_t)H * D;
+  // q rows of stride q_rs; k/v rows of stride kv_rs, kv head = hh / group (GQA)
+  const size_t rs = (size_t)q_rs, krs = (size_t)kv_rs;
+  const bf16* qbase = qp + (size_t)b * T * rs + (size_t)hh * D;
+  const bf16* kbase = kp + (size_t)b * T * krs + (size_t)(hh / group) * D;
+  const bf16* vbase = vp + (size_t)b * T * krs + (size_t)(hh / group) * D;
   const int q0w = qb * kQBlk + wave * 32 * kQS;
 
   bf16x8 qf[kQS][NS];
@@ -186,8 +190,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16* __restrict__
   const int qend = min(T, qb * kQBlk + kQBlk);
   const int nkt = causal ? (qend + 63) / 64 : (T + 63) / 64;
   TileRegs<D> kr, vr;
-  tile_load<D>(kr, kbase, rs, 0, T);
-  tile_load<D>(vr, vbase, rs, 0, T);
+  tile_load<D>(kr, kbase, krs, 0, T);
+  tile_load<D>(vr, vbase, krs, 0, T);
   tile_store_rows<D>(kr, smem);
   tile_store_trans<D>(vr, smem + rows_img<D>());
   __syncthreads();
@@ -197,8 +201,8 @@ __global__ __launch_bounds__(256, 2) void fa_fwd_kernel(const bf16* __restrict__
     const bf16* vt_lds = k_lds + rows_img<D>();
     const bool more = kt + 1 < nkt;
     if (more) {
-      tile_load<D>(kr, kbase, rs, k0 + 64, T);
-      tile_load<D>(vr, vbase, rs, k0 + 64, T);
+      tile_load<D>(kr, kbase, krs, k0 + 64, T);
+      tile_load<D>(vr, vbase, krs, k0 + 64, T);
     }
     // wave-uniform: skip tiles entirely above this wave's causal diagonal
     const bool active = !(causal && k0 > q0w + 32 * kQS - 1) && q0w < T;
@@ -621,19 +625,26 @@ static void fa_set_attrs() {
   g_fa_attr_done = true;
 }
 
-void fa_fwd_launch(const bf16* qkv, bf16* out, float* lse, int B, int T, int H, int D, int causal,
-                   hipStream_t st) {
+void fa_fwd_gqa_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int kv_rs, int group,
+                       bf16* out, float* lse, int B, int T, int H, int D, int causal, hipStream_t st) {
   const int qblk = D == 64 ? qblk_for<64>() : qblk_for<128>();
   const int nqb = (T + qblk - 1) / qblk;
   const float scale_log2 = 1.44269504089f / sqrtf((float)D);
   fa_set_attrs();
   dim3 grid(B * H * nqb), block(256);
   if (D == 64)
-    hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, block, fwd_lds<64>(), st, qkv, out, lse, T, H, nqb,
-                       scale_log2, causal);
+    hipLaunchKernelGGL(fa_fwd_kernel<64>, grid, block, fwd_lds<64>(), st, q, k, v, q_rs, kv_rs, group,
+                       out, lse, T, H, nqb, scale_log2, causal);
   else
-    hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, block, fwd_lds<128>(), st, qkv, out, lse, T, H,
-                       nqb, scale_log2, causal);
+    hipLaunchKernelGGL(fa_fwd_kernel<128>, grid, block, fwd_lds<128>(), st, q, k, v, q_rs, kv_rs, group,
+                       out, lse, T, H, nqb, scale_log2, causal);
+}
+
+void fa_fwd_launch(const bf16* qkv, bf16* out, float* lse, int B, int T, int H, int D, int causal,
+                   hipStream_t st) {
+  // packed [B, T, 3, H, D]: q/k/v share the row stride 3*H*D, no grouping
+  fa_fwd_gqa_launch(qkv, qkv + (size_t)H * D, qkv + (size_t)2 * H * D, 3 * H * D, 3 * H * D, 1, out, lse,
+                    B, T, H, D, causal, st);
 }
 
 void fa_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse,
