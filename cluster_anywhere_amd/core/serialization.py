@@ -151,7 +151,17 @@ class _CloudPickler(cloudpickle.CloudPickler):
         if type(obj).__name__ == "State" and type(obj).__module__ == "starlette.datastructures":
             # starlette's State.__getattr__ recurses when unpickled attribute-by-attribute
             return (type(obj), (dict(obj._state),))
+        if type(obj).__name__ == "MockValSer" and type(obj).__module__ == "pydantic._internal._mock_val_ser":
+            # same __getattr__ recursion for pydantic's lazy validator placeholders (FastAPI apps)
+            kind = "validator" if obj._val_or_ser.__name__ == "SchemaValidator" else "serializer"
+            return (_rebuild_mock_val_ser, (obj._error_message, obj._code, kind, obj._attempt_rebuild))
         return super().reducer_override(obj)
+
+
+def _rebuild_mock_val_ser(msg, code, kind, attempt):
+    from pydantic._internal._mock_val_ser import MockValSer
+
+    return MockValSer(msg, code=code, val_or_ser=kind, attempt_rebuild=attempt)
 
 
 def serialize(value: Any) -> SerializedObject:

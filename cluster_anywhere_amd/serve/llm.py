@@ -1,0 +1,191 @@
+"""Serve LLM: an OpenAI-compatible LLM deployment over the native engine
+(reference: python/ray/serve/llm.py, python/ray/llm/_internal/serve/
+deployments/llm/llm_server.py, routers/router.py).
+
+``LLMServer`` (one replica per GPU, ``num_gpus=1``) owns an ``AsyncLLMEngine``;
+``build_openai_app`` wires ``/v1/completions``, ``/v1/chat/completions`` and
+``/v1/models`` through a FastAPI ingress (``LLMRouter``) that load-balances to
+the LLMServer replicas via handles (streaming with ``stream=True``)."""
+
+import json
+import time
+import uuid
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Union
+
+from .deployment import Application, deployment, ingress
+
+
+@dataclass
+class LLMConfig:
+    model_id: str = "llama-tiny"
+    model_source: Optional[str] = None  # local HF checkpoint dir; None -> random init of model_id preset
+    tokenizer_source: Optional[str] = None
+    dtype: str = "bfloat16"
+    engine_kwargs: Dict[str, Any] = field(default_factory=dict)
+    deployment_config: Dict[str, Any] = field(default_factory=dict)
+    accelerator_type: Optional[str] = None
+    seed: int = 0
+
+
+def _build_engine(cfg: LLMConfig):
+    import torch
+
+    from ..llm import LLMEngine
+    from ..llm.async_engine import AsyncLLMEngine
+    from ..llm.tokenizer import get_tokenizer
+    from ..models.llama import Llama, LlamaConfig
+
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    dtype = getattr(torch, cfg.dtype) if dev == "cuda" else torch.float32
+    if cfg.model_source:
+        from ..llm.weights import load_hf_llama
+
+        model = load_hf_llama(cfg.model_source, dev, dtype)
+    else:
+        lc = LlamaConfig.named(cfg.model_id)
+        with torch.device(dev):
+            model = Llama(lc).to(dtype)
+        torch.manual_seed(cfg.seed)
+        model.init_weights(std=0.02, seed=cfg.seed)
+    tok = get_tokenizer(cfg.tokenizer_source or (cfg.model_source if cfg.tokenizer_source is None and
+                                                 cfg.model_source else None), model.cfg.vocab_size)
+    kw = dict(cfg.engine_kwargs)
+    kw.setdefault("eos_token_id", getattr(tok, "eos_token_id", None))
+    if dev == "cpu":
+        kw.setdefault("num_blocks", 256)
+        kw.setdefault("use_graphs", False)
+    eng = LLMEngine(model, **kw)
+    return AsyncLLMEngine(eng), tok
+
+
+def _sampling(body: Dict):
+    from ..llm import SamplingParams
+
+    stop = body.get("stop_token_ids") or []
+    return SamplingParams(max_tokens=int(body.get("max_tokens", 16)), temperature=float(body.get("temperature", 0.0)),
+                          top_p=float(body.get("top_p", 1.0)), top_k=int(body.get("top_k", -1)),
+                          stop_token_ids=list(stop), ignore_eos=bool(body.get("ignore_eos", False)),
+                          seed=body.get("seed"))
+
+
+class LLMServer:
+    """One engine replica. ``generate`` returns a completion dict;
+    ``stream`` yields text deltas."""
+
+    def __init__(self, llm_config: Union[LLMConfig, Dict]):
+        if isinstance(llm_config, dict):
+            llm_config = LLMConfig(**llm_config)
+        self.config = llm_config
+        self.engine, self.tokenizer = _build_engine(llm_config)
+        self.model_id = llm_config.model_id
+
+    def _prompt_ids(self, body: Dict) -> List[int]:
+        if "prompt_token_ids" in body:
+            return list(body["prompt_token_ids"])
+        if "messages" in body:
+            text = "".join(f"<|{m['role']}|>{m['content']}\n" for m in body["messages"]) + "<|assistant|>"
+        else:
+            text = body.get("prompt", "")
+        return self.tokenizer.encode(text)
+
+    async def generate(self, body: Dict) -> Dict:
+        ids = self._prompt_ids(body)
+        final = None
+        async for o in self.engine.generate(ids, _sampling(body)):
+            final = o
+        text = self.tokenizer.decode(final.output_token_ids)
+        return {"id": f"cmpl-{uuid.uuid4().hex[:12]}", "object": "text_completion", "created": int(time.time()),
+                "model": self.model_id,
+                "choices": [{"index": 0, "text": text, "token_ids": final.output_token_ids,
+                             "finish_reason": final.finish_reason}],
+                "usage": {"prompt_tokens": len(ids), "completion_tokens": len(final.output_token_ids),
+                          "total_tokens": len(ids) + len(final.output_token_ids)}}
+
+    async def stream(self, body: Dict):
+        ids = self._prompt_ids(body)
+        sent = 0
+        async for o in self.engine.generate(ids, _sampling(body)):
+            new = o.output_token_ids[sent:]
+            sent = len(o.output_token_ids)
+            yield {"token_ids": new, "text": self.tokenizer.decode(new), "finish_reason": o.finish_reason}
+
+    def stats(self):
+        return dict(self.engine.engine.stats)
+
+    def check_health(self):
+        if self.engine.error is not None:
+            raise RuntimeError(f"engine failed: {self.engine.error}")
+
+
+def _router_cls():
+    from fastapi import FastAPI, Request
+    from fastapi.responses import JSONResponse, StreamingResponse
+
+    api = FastAPI()
+
+    @ingress(api)
+    class LLMRouter:
+        def __init__(self, servers: Dict[str, Any]):
+            self.servers = servers
+
+        def _server(self, body):
+            mid = body.get("model") or next(iter(self.servers))
+            if mid not in self.servers:
+                return None
+            return self.servers[mid]
+
+        @api.get("/v1/models")
+        async def models(self):
+            return {"object": "list", "data": [{"id": m, "object": "model", "owned_by": "cluster_anywhere_amd"}
+                                                for m in self.servers]}
+
+        @api.post("/v1/completions")
+        async def completions(self, request: Request):
+            body = await request.json()
+            h = self._server(body)
+            if h is None:
+                return JSONResponse({"error": f"unknown model {body.get('model')}"}, status_code=404)
+            if body.get("stream"):
+                chunks = []
+                async for d in h.options(stream=True, method_name="stream").remote(body):
+                    chunks.append("data: " + json.dumps({"choices": [{"text": d["text"],
+                                                                      "finish_reason": d["finish_reason"]}]}) + "\n\n")
+                chunks.append("data: [DONE]\n\n")
+                return StreamingResponse(iter(chunks), media_type="text/event-stream")
+            return await h.generate.remote(body)
+
+        @api.post("/v1/chat/completions")
+        async def chat(self, request: Request):
+            body = await request.json()
+            h = self._server(body)
+            if h is None:
+                return JSONResponse({"error": f"unknown model {body.get('model')}"}, status_code=404)
+            r = await h.generate.remote(body)
+            c = r["choices"][0]
+            return {"id": r["id"].replace("cmpl", "chatcmpl"), "object": "chat.completion", "created": r["created"],
+                    "model": r["model"], "usage": r["usage"],
+                    "choices": [{"index": 0, "message": {"role": "assistant", "content": c["text"]},
+                                 "finish_reason": c["finish_reason"]}]}
+
+    return LLMRouter
+
+
+def build_llm_deployment(llm_config: LLMConfig, *, name_prefix: str = "LLMServer:") -> Application:
+    import torch
+
+    dc = {"max_ongoing_requests": 256}
+    dc.update(llm_config.deployment_config or {})
+    opts = dict(dc.pop("ray_actor_options", {}))
+    if torch.cuda.is_available() or opts.get("num_gpus"):
+        opts.setdefault("num_gpus", 1)
+    d = deployment(LLMServer, name=f"{name_prefix}{llm_config.model_id}")
+    return d.options(ray_actor_options=opts, **dc).bind(llm_config)
+
+
+def build_openai_app(llm_serving_args: Union[Dict, List[LLMConfig]]) -> Application:
+    configs = llm_serving_args.get("llm_configs") if isinstance(llm_serving_args, dict) else llm_serving_args
+    configs = [c if isinstance(c, LLMConfig) else LLMConfig(**c) for c in configs]
+    servers = {c.model_id: build_llm_deployment(c) for c in configs}
+    Router = deployment(_router_cls(), name="LLMRouter")
+    return Router.bind(servers)

@@ -99,3 +99,15 @@ def test_sampling_params():
     assert len(c.output_token_ids) <= 3
     with pytest.raises(ValueError):
         eng.add_request([1] * 120, SamplingParams(max_tokens=20))
+
+
+def test_hf_checkpoint_roundtrip(tmp_path):
+    from cluster_anywhere_amd.llm.weights import load_hf_llama, save_hf_llama
+
+    m = _model()
+    save_hf_llama(m, str(tmp_path))
+    m2 = load_hf_llama(str(tmp_path), device="cpu", dtype=torch.float32)
+    for (n1, p1), (n2, p2) in zip(m.named_parameters(), m2.named_parameters()):
+        assert n1 == n2 and torch.equal(p1, p2)
+    x = torch.tensor([[3, 1, 4, 1, 5]])
+    assert torch.equal(m(x), m2(x))

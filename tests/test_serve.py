@@ -253,3 +253,31 @@ def test_replica_failure_recovery(cluster):
             time.sleep(0.2)
     assert new is not None and new != pid
     serve.delete("frag")
+
+
+def test_llm_openai_app(cluster, tmp_path):
+    from cluster_anywhere_amd.serve.llm import LLMConfig, build_openai_app
+
+    app = build_openai_app({"llm_configs": [LLMConfig(model_id="llama-tiny",
+                                                      engine_kwargs={"max_model_len": 256})]})
+    serve.run(app, name="llm", route_prefix="/llm")
+    st, body = _http("/llm/v1/models")
+    assert json.loads(body)["data"][0]["id"] == "llama-tiny"
+    req = {"model": "llama-tiny", "prompt": "hello", "max_tokens": 7}
+    st, body = _http("/llm/v1/completions", data=json.dumps(req).encode(),
+                     headers={"content-type": "application/json"})
+    r = json.loads(body)
+    assert st == 200 and r["usage"]["completion_tokens"] == 7 and r["usage"]["prompt_tokens"] == 6
+    # concurrent requests share the engine (continuous batching) and stay deterministic (greedy)
+    h = serve.get_deployment_handle("LLMServer:llama-tiny", "llm")
+    outs = [h.generate.remote(dict(req)) for _ in range(6)]
+    ids = [o.result()["choices"][0]["token_ids"] for o in outs]
+    assert all(i == r["choices"][0]["token_ids"] for i in ids)
+    # streaming deltas concatenate to the full completion
+    deltas = list(h.options(stream=True, method_name="stream").remote(dict(req)))
+    assert sum((d["token_ids"] for d in deltas), []) == ids[0]
+    st, body = _http("/llm/v1/chat/completions", data=json.dumps(
+        {"model": "llama-tiny", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 3}).encode(),
+        headers={"content-type": "application/json"})
+    assert json.loads(body)["usage"]["completion_tokens"] == 3
+    serve.delete("llm")
