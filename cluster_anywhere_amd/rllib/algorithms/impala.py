@@ -1,0 +1,168 @@
+"""IMPALA and APPO (reference: rllib/algorithms/impala/impala.py,
+impala_learner.py, torch/vtrace_torch_v2.py; rllib/algorithms/appo/appo.py,
+appo_learner.py).
+
+EnvRunners sample asynchronously: every runner always has one ``sample``
+call in flight; each training step consumes the fragments that are ready,
+refreshes only those runners' weights and re-launches them. Off-policy
+correction is V-trace on the learner device (``rl_returns.hip`` kernel, one
+thread per env column, reverse scan over T). APPO replaces the IMPALA policy
+gradient by PPO's clipped surrogate on the V-trace advantages, with a target
+network providing the KL anchor."""
+from __future__ import annotations
+
+import copy
+from typing import Any, Dict, List
+
+import numpy as np
+import torch
+
+from ...ops.rl import vtrace
+from ..core.learner import Learner, _to_tensor
+from .algorithm import Algorithm, AlgorithmConfig, concat_fragments
+
+
+class IMPALAConfig(AlgorithmConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or IMPALA)
+        self.lr = 5e-4
+        self.vtrace_clip_rho_threshold = 1.0
+        self.vtrace_clip_pg_rho_threshold = 1.0
+        self.vf_loss_coeff = 0.5
+        self.entropy_coeff = 0.01
+        self.rollout_fragment_length = 50
+        self.train_batch_size = 500
+        self.minibatch_size = None
+        self.num_epochs = 1
+        self.grad_clip = 40.0
+        self.max_requests_in_flight_per_env_runner = 1
+        # APPO
+        self.clip_param = 0.4
+        self.use_kl_loss = False
+        self.kl_coeff = 1.0
+        self.target_network_update_freq = 1
+
+
+class IMPALALearner(Learner):
+    appo = False
+
+    def build(self):
+        if self.appo:
+            self.target = copy.deepcopy(self.module)
+            for p in self.target.parameters():
+                p.requires_grad_(False)
+            self.updates_since_target = 0
+
+    def compute_loss(self, b):
+        c = self.config
+        T, N = b["rewards"].shape
+        flat = lambda x: x.reshape((T * N,) + tuple(x.shape[2:]))
+        out = self.module.forward_train({"obs": flat(b["obs"])})
+        dist = self.module.dist_cls(out["action_dist_inputs"])
+        logp = dist.logp(flat(b["actions"])).view(T, N)
+        values = out["vf_preds"].view(T, N)
+        with torch.no_grad():
+            boot = self.module.compute_values({"obs": b["last_obs"]})
+            disc = c["gamma"] * (1.0 - b["terminateds"].float())
+            vs, pg_adv = vtrace(logp.detach() - b["action_logp"], disc, b["rewards"], values.detach(), boot,
+                                c["vtrace_clip_rho_threshold"], c["vtrace_clip_pg_rho_threshold"])
+        if self.appo:
+            ratio = torch.exp(logp - b["action_logp"])
+            adv = (pg_adv - pg_adv.mean()) / (pg_adv.std() + 1e-8)
+            cp = c["clip_param"]
+            pi_loss = -torch.min(ratio * adv, ratio.clamp(1 - cp, 1 + cp) * adv).mean()
+        else:
+            pi_loss = -(logp * pg_adv).mean()
+        vf_loss = 0.5 * ((values - vs) ** 2).mean()
+        ent = dist.entropy().mean()
+        loss = pi_loss + c["vf_loss_coeff"] * vf_loss - c["entropy_coeff"] * ent
+        stats = {"total_loss": loss.detach(), "policy_loss": pi_loss.detach(), "vf_loss": vf_loss.detach(),
+                 "entropy": ent.detach()}
+        if self.appo and c.get("use_kl_loss"):
+            with torch.no_grad():
+                old = self.target.forward_train({"obs": flat(b["obs"])})["action_dist_inputs"]
+            kl = self.module.dist_cls(old).kl(dist).mean()
+            loss = loss + c["kl_coeff"] * kl
+            stats["mean_kl_loss"] = kl.detach()
+        return {"default": loss}, stats
+
+    def after_update(self):
+        if self.appo:
+            self.updates_since_target += 1
+            if self.updates_since_target >= self.config.get("target_network_update_freq", 1):
+                self.target.load_state_dict(self.module.state_dict())
+                self.updates_since_target = 0
+
+    def learn_fragments(self, frag: Dict[str, Any]):
+        keys = ["obs", "actions", "rewards", "terminateds", "action_logp"]
+        b = {k: _to_tensor(frag[k], self.device) for k in keys}
+        b["rewards"] = b["rewards"].float()
+        b["last_obs"] = _to_tensor(frag["last_obs"], self.device)
+        return {k: float(v) for k, v in self.update_once(b).items()}
+
+
+class APPOLearner(IMPALALearner):
+    appo = True
+
+
+class IMPALA(Algorithm):
+    config_class = IMPALAConfig
+    learner_class = IMPALALearner
+
+    def setup_algo(self):
+        self._inflight: Dict[int, Any] = {}
+
+    def _collect(self) -> List[Dict]:
+        g = self.env_runner_group
+        if g.local is not None:
+            return g.sample()
+        from ...core import api as core
+
+        for i, r in enumerate(g.remote):
+            if i not in self._inflight:
+                self._inflight[i] = r.sample.remote()
+        refs = list(self._inflight.values())
+        ready, _ = core.wait(refs, num_returns=1)
+        ready_set = set(ready)
+        frags, done = [], []
+        for i, ref in list(self._inflight.items()):
+            if ref in ready_set:
+                frags.append(core.get(ref))
+                done.append(i)
+                del self._inflight[i]
+        # only the runners that returned get fresh weights (others keep sampling)
+        st = core.put(self.learner_group.get_module_state())
+        core.get([g.remote[i].set_weights.remote(st) for i in done])
+        for i in done:
+            self._inflight[i] = g.remote[i].sample.remote()
+        return frags
+
+    def _sync_weights(self, extra=None):
+        if self.env_runner_group.local is not None or not getattr(self, "_inflight", None):
+            super()._sync_weights(extra)
+
+    def training_step(self):
+        c = self.algo_config
+        frags = self._collect()
+        frag = concat_fragments(frags)
+        steps = int(frag["rewards"].size)
+        self.env_steps_sampled += steps
+        lg = self.learner_group
+        stats = lg.local.learn_fragments(frag) if lg.local is not None else lg.call("learn_fragments", frag)
+        self.env_steps_trained += steps
+        if self.env_runner_group.local is not None:
+            self._sync_weights()
+        return stats
+
+
+class APPOConfig(IMPALAConfig):
+    def __init__(self, algo_class=None):
+        super().__init__(algo_class or APPO)
+        self.use_kl_loss = True
+        self.kl_coeff = 0.1
+        self.lr = 5e-4
+
+
+class APPO(IMPALA):
+    config_class = APPOConfig
+    learner_class = APPOLearner

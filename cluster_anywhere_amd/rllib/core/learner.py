@@ -1,0 +1,247 @@
+"""Learner / LearnerGroup (reference: rllib/core/learner/learner.py,
+learner_group.py, torch/torch_learner.py).
+
+A Learner keeps its RLModule's parameters in ONE flat fp32 buffer
+(``FlatParamSpace``), so the optimizer is one fused AdamW launch
+(``adamw.hip``, with device-side global-norm clipping) and data-parallel
+learners all-reduce one contiguous gradient buffer over RCCL (gloo on CPU).
+``LearnerGroup`` runs either a local learner or ``num_learners`` learner actors
+(one GPU each), sharding every train batch across them."""
+from __future__ import annotations
+
+import os
+import socket
+from typing import Any, Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ...ops.optim import FusedAdamW
+from ...parallel.flat import FlatParamSpace
+
+
+def _to_tensor(x, device):
+    if isinstance(x, torch.Tensor):
+        return x.to(device, non_blocking=True)
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    if device.type == "cuda":
+        t = t.pin_memory().to(device, non_blocking=True)
+    return t
+
+
+class Learner:
+    def __init__(self, config: Dict[str, Any], module_factory: Callable, obs_space, act_space,
+                 device: Optional[str] = None, rank: int = 0, world: int = 1):
+        self.config = config
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() and config.get("num_gpus_per_learner", 1) > 0 else "cpu"
+        self.device = torch.device(device)
+        self.rank, self.world = rank, world
+        if config.get("seed") is not None:
+            torch.manual_seed(config["seed"])
+        self.module = module_factory(obs_space, act_space).to(self.device)
+        if world > 1:  # data-parallel replicas start from rank 0's weights
+            import torch.distributed as dist
+
+            with torch.no_grad():
+                for t in list(self.module.parameters()) + list(self.module.buffers()):
+                    dist.broadcast(t.data, 0)
+        self.obs_space, self.act_space = obs_space, act_space
+        self.build()
+        self.optimizers: Dict[str, FusedAdamW] = {}
+        self.flats: Dict[str, FlatParamSpace] = {}
+        for name, params_module in self.param_groups().items():
+            flat = FlatParamSpace(params_module, dtype=torch.float32, master_fp32=False,
+                                  decay_rule=lambda n, p: False)
+            flat.master = flat.param_buffer  # fp32 params are the master weights
+            self.flats[name] = flat
+            self.optimizers[name] = FusedAdamW(flat, lr=self.lr_for(name), betas=(0.9, 0.999),
+                                               eps=config.get("adam_eps", 1e-7), weight_decay=0.0,
+                                               max_grad_norm=config.get("grad_clip") or 0.0)
+        self.num_updates = 0
+
+    # ---------------------------------------------------------------- hooks
+    def build(self):
+        pass
+
+    def param_groups(self) -> Dict[str, torch.nn.Module]:
+        return {"default": self.module}
+
+    def lr_for(self, name: str) -> float:
+        return self.config.get("lr", 5e-5)
+
+    def compute_loss(self, batch: Dict[str, torch.Tensor]) -> (Dict[str, torch.Tensor], Dict[str, float]):
+        """Returns ({param_group: loss}, stats)."""
+        raise NotImplementedError
+
+    def after_update(self):
+        pass
+
+    # --------------------------------------------------------------- update
+    def _allreduce(self, flat: FlatParamSpace):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_reduce(flat.grad_buffer)
+
+    def update_once(self, batch: Dict[str, torch.Tensor]) -> Dict[str, float]:
+        losses, stats = self.compute_loss(batch)
+        names = list(losses)
+        if len(names) == 1:  # .grad of every parameter is a view of the flat grad buffer
+            flat = self.flats[names[0]]
+            flat.zero_grad()
+            losses[names[0]].backward()
+            self._allreduce(flat)
+            self.optimizers[names[0]].step(inv_world=1.0 / self.world)
+            self.num_updates += 1
+            self.after_update()
+            return stats
+        for i, name in enumerate(names):
+            flat = self.flats[name]
+            flat.zero_grad()
+            # each group's loss only differentiates w.r.t. its own parameters
+            params = [s.param for s in flat.slots]
+            grads = torch.autograd.grad(losses[name], params, retain_graph=i < len(names) - 1, allow_unused=True)
+            with torch.no_grad():
+                for s, g in zip(flat.slots, grads):
+                    if g is not None:
+                        flat.grad_buffer[s.offset: s.offset + s.numel].copy_(g.reshape(-1))
+            self._allreduce(flat)
+            self.optimizers[name].step(inv_world=1.0 / self.world)
+        self.num_updates += 1
+        self.after_update()
+        return stats
+
+    def update(self, batch: Dict[str, Any], minibatch_size: Optional[int] = None,
+               num_epochs: int = 1, shuffle: bool = True) -> Dict[str, float]:
+        b = {k: _to_tensor(v, self.device) for k, v in batch.items()}
+        n = next(iter(b.values())).shape[0]
+        mbs = min(minibatch_size or n, n)
+        agg: Dict[str, List[float]] = {}
+        for _ in range(num_epochs):
+            perm = torch.randperm(n, device=self.device) if shuffle else torch.arange(n, device=self.device)
+            for s in range(0, n - mbs + 1, mbs):
+                idx = perm[s: s + mbs]
+                mb = {k: v[idx] for k, v in b.items()}
+                st = self.update_once(mb)
+                for k, v in st.items():
+                    agg.setdefault(k, []).append(float(v))
+        return {k: float(np.mean(v)) for k, v in agg.items()}
+
+    # ---------------------------------------------------------------- state
+    def get_module_state(self):
+        return self.module.get_state()
+
+    def get_state(self):
+        return {"module": self.module.get_state(),
+                "optim": {k: {kk: (vv.cpu() if isinstance(vv, torch.Tensor) else vv)
+                              for kk, vv in o.state_dict().items()} for k, o in self.optimizers.items()},
+                "num_updates": self.num_updates}
+
+    def set_state(self, st):
+        self.module.set_state(st["module"])
+        for k, o in self.optimizers.items():
+            if k in st.get("optim", {}):
+                sd = {kk: (vv.to(self.device) if isinstance(vv, torch.Tensor) else vv)
+                      for kk, vv in st["optim"][k].items()}
+                sd["master"] = self.flats[k].param_buffer.clone()
+                o.load_state_dict(sd)
+        self.num_updates = st.get("num_updates", 0)
+        return True
+
+
+class _LearnerActor:
+    def __init__(self, learner_cls, config, module_factory, obs_space, act_space, rank, world, addr, port):
+        if world > 1:
+            import torch.distributed as dist
+
+            os.environ.update({"MASTER_ADDR": addr, "MASTER_PORT": str(port), "RANK": str(rank),
+                               "WORLD_SIZE": str(world)})
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if torch.cuda.is_available():
+                gpus = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
+                torch.cuda.set_device(gpus[0] if gpus else 0)
+            dist.init_process_group(backend, rank=rank, world_size=world)
+        dev = None
+        if torch.cuda.is_available():
+            gpus = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
+            dev = f"cuda:{gpus[0]}" if gpus and os.environ.get("CAAMD_NOSET_ROCR_VISIBLE_DEVICES") else "cuda"
+        self.learner = learner_cls(config, module_factory, obs_space, act_space, dev, rank, world)
+
+    def call(self, method, *args, **kwargs):
+        return getattr(self.learner, method)(*args, **kwargs)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class LearnerGroup:
+    def __init__(self, learner_cls, config: Dict[str, Any], module_factory, obs_space, act_space):
+        self.n = config.get("num_learners", 0)
+        self.local = None
+        self.actors = []
+        if self.n == 0:
+            self.local = learner_cls(config, module_factory, obs_space, act_space)
+        else:
+            from ...core import api as core
+            from ...core.actor import ActorClass
+
+            A = ActorClass(_LearnerActor, {})
+            port = _free_port()
+            gpus = config.get("num_gpus_per_learner", 1) if core.cluster_resources().get("GPU", 0) > 0 else 0
+            self.actors = [A.options(num_cpus=config.get("num_cpus_per_learner", 1), num_gpus=gpus,
+                                     runtime_env={"env_vars": {"CAAMD_NOSET_ROCR_VISIBLE_DEVICES": "1",
+                                                               "HSA_ENABLE_IPC_MODE_LEGACY": "0"}})
+                           .remote(learner_cls, config, module_factory, obs_space, act_space, i, self.n,
+                                   "127.0.0.1", port) for i in range(self.n)]
+            core.get([a.call.remote("get_module_state") for a in self.actors])
+
+    def _shard(self, batch, i):
+        n = next(iter(batch.values())).shape[0]
+        per = n // self.n
+        return {k: v[i * per:(i + 1) * per] for k, v in batch.items()}
+
+    def update(self, batch, minibatch_size=None, num_epochs=1, shuffle=True):
+        if self.local is not None:
+            return self.local.update(batch, minibatch_size, num_epochs, shuffle)
+        from ...core import api as core
+
+        mbs = None if minibatch_size is None else max(1, minibatch_size // self.n)
+        res = core.get([a.call.remote("update", self._shard(batch, i), mbs, num_epochs, shuffle)
+                        for i, a in enumerate(self.actors)])
+        return {k: float(np.mean([r[k] for r in res])) for k in res[0]}
+
+    def call(self, method, *args, **kwargs):
+        """Run a learner method on the local learner / all learner actors (rank 0's result)."""
+        if self.local is not None:
+            return getattr(self.local, method)(*args, **kwargs)
+        from ...core import api as core
+
+        return core.get([a.call.remote(method, *args, **kwargs) for a in self.actors])[0]
+
+    def get_module_state(self):
+        return self.call("get_module_state")
+
+    def get_state(self):
+        return self.call("get_state")
+
+    def set_state(self, st):
+        if self.local is not None:
+            return self.local.set_state(st)
+        from ...core import api as core
+
+        core.get([a.call.remote("set_state", st) for a in self.actors])
+
+    def stop(self):
+        from ...core import api as core
+
+        for a in self.actors:
+            try:
+                core.kill(a)
+            except Exception:
+                pass

@@ -1,0 +1,207 @@
+"""RLModules (reference: rllib/core/rl_module/rl_module.py,
+rllib/core/models/catalog.py — default MLP / Nature-CNN encoders,
+rllib/models/torch/torch_distributions.py).
+
+``RLModule`` wraps a torch module with three forward modes:
+  forward_inference  — greedy actions (evaluation / serving)
+  forward_exploration— sampled actions + logp + value (EnvRunners)
+  forward_train      — distribution inputs + values for the loss (Learner)
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..env import Box, Discrete, Space
+
+
+# ---------------------------------------------------------- distributions
+class Categorical:
+    def __init__(self, logits):
+        self.logits = logits - logits.logsumexp(-1, keepdim=True)
+
+    def sample(self):
+        return torch.multinomial(self.logits.exp(), 1).squeeze(-1)
+
+    def deterministic(self):
+        return self.logits.argmax(-1)
+
+    def logp(self, a):
+        return self.logits.gather(-1, a.long().unsqueeze(-1)).squeeze(-1)
+
+    def entropy(self):
+        return -(self.logits.exp() * self.logits).sum(-1)
+
+    def kl(self, other: "Categorical"):
+        p = self.logits.exp()
+        return (p * (self.logits - other.logits)).sum(-1)
+
+
+class DiagGaussian:
+    def __init__(self, inputs):
+        self.mean, log_std = inputs.chunk(2, dim=-1)
+        self.log_std = log_std.clamp(-20, 2)
+        self.std = self.log_std.exp()
+
+    def sample(self):
+        return self.mean + self.std * torch.randn_like(self.mean)
+
+    def deterministic(self):
+        return self.mean
+
+    def logp(self, a):
+        z = (a - self.mean) / self.std
+        return (-0.5 * z * z - self.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+
+    def entropy(self):
+        return (self.log_std + 0.5 * math.log(2 * math.pi * math.e)).sum(-1)
+
+    def kl(self, other: "DiagGaussian"):
+        return (other.log_std - self.log_std + (self.std ** 2 + (self.mean - other.mean) ** 2)
+                / (2 * other.std ** 2) - 0.5).sum(-1)
+
+
+def dist_class(action_space: Space):
+    return Categorical if isinstance(action_space, Discrete) else DiagGaussian
+
+
+def dist_input_dim(action_space: Space) -> int:
+    if isinstance(action_space, Discrete):
+        return action_space.n
+    return 2 * int(np.prod(action_space.shape))
+
+
+# --------------------------------------------------------------- encoders
+def mlp(sizes: Sequence[int], act=nn.Tanh, out_act=False):
+    layers = []
+    for i in range(len(sizes) - 1):
+        layers.append(nn.Linear(sizes[i], sizes[i + 1]))
+        if i < len(sizes) - 2 or out_act:
+            layers.append(act())
+    return nn.Sequential(*layers)
+
+
+class NatureCNN(nn.Module):
+    """84x84xC uint8 -> 512 (Mnih et al. 2015), channels-last input."""
+
+    def __init__(self, in_ch: int = 4, out: int = 512):
+        super().__init__()
+        self.conv = nn.Sequential(nn.Conv2d(in_ch, 32, 8, 4), nn.ReLU(), nn.Conv2d(32, 64, 4, 2), nn.ReLU(),
+                                  nn.Conv2d(64, 64, 3, 1), nn.ReLU(), nn.Flatten())
+        self.fc = nn.Sequential(nn.Linear(64 * 7 * 7, out), nn.ReLU())
+        self.out_dim = out
+
+    def forward(self, x):
+        x = x.permute(0, 3, 1, 2).float() * (1.0 / 255.0)
+        return self.fc(self.conv(x.contiguous(memory_format=torch.channels_last)))
+
+
+def _act(name):
+    return {"tanh": nn.Tanh, "relu": nn.ReLU, "silu": nn.SiLU, "elu": nn.ELU}[name]
+
+
+@dataclass
+class RLModuleSpec:
+    module_class: Optional[type] = None
+    model_config: Dict = field(default_factory=dict)
+
+
+class RLModule(nn.Module):
+    def __init__(self, observation_space: Space, action_space: Space, model_config: Optional[Dict] = None):
+        super().__init__()
+        self.observation_space, self.action_space = observation_space, action_space
+        self.model_config = dict(model_config or {})
+        self.setup()
+
+    def setup(self):
+        pass
+
+    def forward_inference(self, batch: Dict) -> Dict:
+        raise NotImplementedError
+
+    def forward_exploration(self, batch: Dict) -> Dict:
+        raise NotImplementedError
+
+    def forward_train(self, batch: Dict) -> Dict:
+        raise NotImplementedError
+
+    def get_state(self):
+        return {k: v.detach().cpu() for k, v in self.state_dict().items()}
+
+    def set_state(self, state):
+        self.load_state_dict(state)
+
+
+class DefaultActorCriticModule(RLModule):
+    """Encoder (MLP or Nature-CNN for image obs) + pi head + value head; the
+    encoder is shared unless ``vf_share_layers`` is False."""
+
+    def setup(self):
+        mc = self.model_config
+        obs = self.observation_space
+        hiddens = list(mc.get("fcnet_hiddens", [256, 256]))
+        act = _act(mc.get("fcnet_activation", "tanh"))
+        self.image = len(obs.shape) == 3
+        self.share = mc.get("vf_share_layers", self.image)
+        if self.image:
+            self.encoder = NatureCNN(obs.shape[-1])
+            feat = self.encoder.out_dim
+            self.vf_encoder = None
+        else:
+            d = int(np.prod(obs.shape))
+            self.encoder = mlp([d] + hiddens, act, out_act=True)
+            feat = hiddens[-1]
+            self.vf_encoder = None if self.share else mlp([d] + hiddens, act, out_act=True)
+        self.pi = nn.Linear(feat, dist_input_dim(self.action_space))
+        self.vf = nn.Linear(feat, 1)
+        nn.init.normal_(self.pi.weight, std=0.01)
+        nn.init.zeros_(self.pi.bias)
+        self.dist_cls = dist_class(self.action_space)
+        if not isinstance(self.action_space, Discrete) and mc.get("free_log_std", True):
+            # state-independent log std (as RLlib's free_log_std)
+            self.log_std = nn.Parameter(torch.zeros(int(np.prod(self.action_space.shape))))
+            with torch.no_grad():
+                self.pi = nn.Linear(feat, int(np.prod(self.action_space.shape)))
+                nn.init.normal_(self.pi.weight, std=0.01)
+                nn.init.zeros_(self.pi.bias)
+        else:
+            self.log_std = None
+
+    def _obs(self, batch):
+        o = batch["obs"]
+        return o if self.image else o.reshape(o.shape[0], -1).float()
+
+    def _heads(self, obs):
+        z = self.encoder(obs)
+        logits = self.pi(z)
+        if self.log_std is not None:
+            logits = torch.cat([logits, self.log_std.expand_as(logits)], -1)
+        zv = z if self.vf_encoder is None else self.vf_encoder(obs)
+        return logits, self.vf(zv).squeeze(-1)
+
+    def forward_train(self, batch):
+        logits, v = self._heads(self._obs(batch))
+        return {"action_dist_inputs": logits, "vf_preds": v}
+
+    @torch.no_grad()
+    def forward_exploration(self, batch):
+        logits, v = self._heads(self._obs(batch))
+        d = self.dist_cls(logits)
+        a = d.sample()
+        return {"actions": a, "action_logp": d.logp(a), "vf_preds": v, "action_dist_inputs": logits}
+
+    @torch.no_grad()
+    def forward_inference(self, batch):
+        logits, _ = self._heads(self._obs(batch))
+        return {"actions": self.dist_cls(logits).deterministic()}
+
+    def compute_values(self, batch):
+        obs = self._obs(batch)
+        z = self.encoder(obs) if self.vf_encoder is None else self.vf_encoder(obs)
+        return self.vf(z).squeeze(-1)

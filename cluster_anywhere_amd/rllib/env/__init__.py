@@ -1,0 +1,261 @@
+"""Environments (gymnasium is not installed, so the env API, spaces, registry and
+the classic-control / Atari-shaped envs used by RLlib's examples and tuned
+benchmarks are built in; a gymnasium env is used when gymnasium is importable).
+
+reference: rllib/env/ (env_context.py, vector_env.py, utils/), gymnasium
+CartPole-v1 / Pendulum-v1 dynamics, rllib/env/wrappers/atari_wrappers.py
+(84x84x4 uint8 frame stacks)."""
+from __future__ import annotations
+
+import math
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import numpy as np
+
+
+# ----------------------------------------------------------------- spaces
+class Space:
+    shape: Tuple[int, ...] = ()
+    dtype = np.float32
+
+    def sample(self, rng: Optional[np.random.Generator] = None):
+        raise NotImplementedError
+
+    def contains(self, x) -> bool:
+        raise NotImplementedError
+
+
+class Discrete(Space):
+    def __init__(self, n: int):
+        self.n = int(n)
+        self.shape = ()
+        self.dtype = np.int64
+
+    def sample(self, rng=None):
+        return int((rng or np.random.default_rng()).integers(self.n))
+
+    def contains(self, x):
+        return 0 <= int(x) < self.n
+
+    def __repr__(self):
+        return f"Discrete({self.n})"
+
+
+class Box(Space):
+    def __init__(self, low, high, shape=None, dtype=np.float32):
+        shape = tuple(shape) if shape is not None else np.shape(low)
+        self.low = np.broadcast_to(np.asarray(low, dtype=dtype), shape).copy()
+        self.high = np.broadcast_to(np.asarray(high, dtype=dtype), shape).copy()
+        self.shape = shape
+        self.dtype = dtype
+
+    def sample(self, rng=None):
+        rng = rng or np.random.default_rng()
+        lo = np.where(np.isfinite(self.low), self.low, -1.0)
+        hi = np.where(np.isfinite(self.high), self.high, 1.0)
+        if np.issubdtype(self.dtype, np.integer):
+            return rng.integers(lo, hi + 1, size=self.shape).astype(self.dtype)
+        return rng.uniform(lo, hi, size=self.shape).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and np.all(x >= self.low) and np.all(x <= self.high)
+
+    def __repr__(self):
+        return f"Box({self.shape}, {np.dtype(self.dtype).name})"
+
+
+# -------------------------------------------------------------------- envs
+class Env:
+    observation_space: Space
+    action_space: Space
+    spec_max_episode_steps: Optional[int] = None
+
+    def reset(self, *, seed: Optional[int] = None, options=None):
+        raise NotImplementedError
+
+    def step(self, action):
+        raise NotImplementedError
+
+    def close(self):
+        pass
+
+
+class CartPoleEnv(Env):
+    """Classic cart-pole (gymnasium CartPole-v1 dynamics: Euler integration,
+    reward 1 per step, terminate at |x| > 2.4 or |theta| > 12 deg, truncate at 500)."""
+
+    gravity, masscart, masspole, length, force_mag, tau = 9.8, 1.0, 0.1, 0.5, 10.0, 0.02
+
+    def __init__(self, config: Optional[Dict] = None):
+        config = config or {}
+        self.max_steps = config.get("max_episode_steps", 500)
+        high = np.array([4.8, np.inf, 0.418, np.inf], dtype=np.float32)
+        self.observation_space = Box(-high, high)
+        self.action_space = Discrete(2)
+        self.rng = np.random.default_rng()
+        self.state = None
+        self.t = 0
+
+    def reset(self, *, seed=None, options=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.state = self.rng.uniform(-0.05, 0.05, size=4)
+        self.t = 0
+        return self.state.astype(np.float32), {}
+
+    def step(self, action):
+        x, xd, th, thd = self.state
+        force = self.force_mag if int(action) == 1 else -self.force_mag
+        ct, st = math.cos(th), math.sin(th)
+        total = self.masspole + self.masscart
+        pml = self.masspole * self.length
+        temp = (force + pml * thd * thd * st) / total
+        thacc = (self.gravity * st - ct * temp) / (self.length * (4.0 / 3.0 - self.masspole * ct * ct / total))
+        xacc = temp - pml * thacc * ct / total
+        x, xd = x + self.tau * xd, xd + self.tau * xacc
+        th, thd = th + self.tau * thd, thd + self.tau * thacc
+        self.state = np.array([x, xd, th, thd])
+        self.t += 1
+        terminated = bool(x < -2.4 or x > 2.4 or th < -0.2095 or th > 0.2095)
+        truncated = self.t >= self.max_steps
+        return self.state.astype(np.float32), 1.0, terminated, truncated, {}
+
+
+class PendulumEnv(Env):
+    """Inverted pendulum swing-up (gymnasium Pendulum-v1 dynamics, 200-step episodes)."""
+
+    max_speed, max_torque, dt, g, m, l = 8.0, 2.0, 0.05, 10.0, 1.0, 1.0
+
+    def __init__(self, config: Optional[Dict] = None):
+        config = config or {}
+        self.max_steps = config.get("max_episode_steps", 200)
+        high = np.array([1.0, 1.0, self.max_speed], dtype=np.float32)
+        self.observation_space = Box(-high, high)
+        self.action_space = Box(-self.max_torque, self.max_torque, shape=(1,))
+        self.rng = np.random.default_rng()
+
+    def _obs(self):
+        th, thd = self.state
+        return np.array([math.cos(th), math.sin(th), thd], dtype=np.float32)
+
+    def reset(self, *, seed=None, options=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.state = np.array([self.rng.uniform(-math.pi, math.pi), self.rng.uniform(-1, 1)])
+        self.t = 0
+        return self._obs(), {}
+
+    def step(self, action):
+        th, thd = self.state
+        u = float(np.clip(np.asarray(action).reshape(-1)[0], -self.max_torque, self.max_torque))
+        ang = ((th + math.pi) % (2 * math.pi)) - math.pi
+        cost = ang ** 2 + 0.1 * thd ** 2 + 0.001 * u ** 2
+        thd = thd + (3 * self.g / (2 * self.l) * math.sin(th) + 3.0 / (self.m * self.l ** 2) * u) * self.dt
+        thd = float(np.clip(thd, -self.max_speed, self.max_speed))
+        th = th + thd * self.dt
+        self.state = np.array([th, thd])
+        self.t += 1
+        return self._obs(), -cost, False, self.t >= self.max_steps, {}
+
+
+class FakeAtariEnv(Env):
+    """Atari-shaped env for throughput benchmarks: 84x84x4 uint8 frame stacks,
+    6 discrete actions, reward for matching a hidden target action that is
+    encoded in the frame (so a conv policy can actually learn it)."""
+
+    def __init__(self, config: Optional[Dict] = None):
+        config = config or {}
+        self.max_steps = config.get("max_episode_steps", 1000)
+        self.observation_space = Box(0, 255, shape=(84, 84, 4), dtype=np.uint8)
+        self.action_space = Discrete(6)
+        self.rng = np.random.default_rng()
+        self.frame = np.zeros((84, 84, 4), dtype=np.uint8)
+
+    def _new_target(self):
+        self.target = int(self.rng.integers(6))
+        self.frame = np.roll(self.frame, -1, axis=2)
+        f = self.rng.integers(0, 32, size=(84, 84), dtype=np.uint8)
+        f[self.target * 14:(self.target + 1) * 14, :] = 200
+        self.frame[..., -1] = f
+
+    def reset(self, *, seed=None, options=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        self.t = 0
+        self.frame[:] = 0
+        self._new_target()
+        return self.frame.copy(), {}
+
+    def step(self, action):
+        r = 1.0 if int(action) == self.target else 0.0
+        self.t += 1
+        self._new_target()
+        return self.frame.copy(), r, False, self.t >= self.max_steps, {}
+
+
+_REGISTRY: Dict[str, Callable[[Dict], Env]] = {
+    "CartPole-v1": lambda cfg: CartPoleEnv(cfg),
+    "CartPole-v0": lambda cfg: CartPoleEnv(dict({"max_episode_steps": 200}, **(cfg or {}))),
+    "Pendulum-v1": lambda cfg: PendulumEnv(cfg),
+    "FakeAtari-v0": lambda cfg: FakeAtariEnv(cfg),
+    "ale_py:ALE/Pong-v5": lambda cfg: FakeAtariEnv(cfg),
+}
+
+
+def register_env(name: str, creator: Callable[[Dict], Env]):
+    _REGISTRY[name] = creator
+
+
+def make_env(env, config: Optional[Dict] = None) -> Env:
+    config = config or {}
+    if isinstance(env, str):
+        if env in _REGISTRY:
+            return _REGISTRY[env](config)
+        try:  # optional gymnasium
+            import gymnasium as gym
+
+            return gym.make(env, **config)
+        except ImportError:
+            raise ValueError(f"unknown env {env!r} (registered: {sorted(_REGISTRY)})")
+    if isinstance(env, type):
+        return env(config)
+    if callable(env):
+        return env(config)
+    raise TypeError(f"cannot build env from {env!r}")
+
+
+class VectorEnv:
+    """``num_envs`` copies stepped in lock-step with auto-reset (numpy batched)."""
+
+    def __init__(self, env, num_envs: int, config: Optional[Dict] = None, seed: Optional[int] = None):
+        self.envs = [make_env(env, config) for _ in range(num_envs)]
+        self.num_envs = num_envs
+        self.observation_space = self.envs[0].observation_space
+        self.action_space = self.envs[0].action_space
+        self.seed = seed
+
+    def reset(self):
+        obs = []
+        for i, e in enumerate(self.envs):
+            o, _ = e.reset(seed=None if self.seed is None else self.seed + i)
+            obs.append(o)
+        return np.stack(obs)
+
+    def step(self, actions):
+        """Returns obs (after auto-reset), rewards, terminated, truncated, final_obs."""
+        obs, rew, term, trunc, final = [], [], [], [], []
+        for e, a in zip(self.envs, actions):
+            o, r, te, tr, _ = e.step(a)
+            final.append(o)
+            if te or tr:
+                o, _ = e.reset()
+            obs.append(o)
+            rew.append(r)
+            term.append(te)
+            trunc.append(tr)
+        return (np.stack(obs), np.asarray(rew, np.float32), np.asarray(term), np.asarray(trunc), np.stack(final))
+
+
+__all__ = ["Space", "Discrete", "Box", "Env", "CartPoleEnv", "PendulumEnv", "FakeAtariEnv", "register_env",
+           "make_env", "VectorEnv"]
