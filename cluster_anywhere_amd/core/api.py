@@ -178,13 +178,15 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
         _session.update({"address": address, "node_id": cw.node_hex, "session_dir": cw.session_dir,
                          "namespace": cw.namespace, "job_id": job_id.hex(),
                          "object_store_address": getattr(cw.store, "name", ""),
-                         "webui_url": None, "gcs_address": address})
+                         "webui_url": None, "gcs_address": (_head.tcp_address if _head is not None and
+                                                             _head.tcp_address else address)})
         if runtime_env:
             _session["runtime_env"] = runtime_env
         if include_dashboard:
             from ..dashboard import start_dashboard
 
-            _session["webui_url"] = start_dashboard(dashboard_host, dashboard_port or 8265)
+            _session["webui_url"] = start_dashboard(dashboard_host, 8265 if dashboard_port is None else dashboard_port,
+                                                    head=_head, control_address=address)
         return RayContext(dict(_session))
 
 
@@ -226,6 +228,10 @@ def shutdown(_exiting_interpreter: bool = False):
                 w.close()
             except Exception:
                 pass
+        if _session.get("webui_url"):
+            from ..dashboard import stop_dashboard
+
+            stop_dashboard()
         if _head is not None:
             _head.shutdown()
             _head = None
@@ -363,9 +369,7 @@ def get_gpu_ids():
     return [int(x) for x in env.split(",") if x]
 
 
-def timeline(filename: Optional[str] = None):
-    """Chrome-trace events of task execution (reference: state.py:965)."""
-    ev = _state("events")
+def _timeline_events(ev):
     starts = {}
     out = []
     for e in ev:
@@ -376,6 +380,12 @@ def timeline(filename: Optional[str] = None):
             out.append({"cat": "task", "name": s[2], "ph": "X", "ts": s[3] * 1e6,
                         "dur": (e[3] - s[3]) * 1e6, "pid": "node", "tid": s[4] or 0,
                         "args": {"task_id": e[1].hex()}})
+    return out
+
+
+def timeline(filename: Optional[str] = None):
+    """Chrome-trace events of task execution (reference: state.py:965)."""
+    out = _timeline_events(_state("events"))
     if filename:
         with open(filename, "w") as f:
             json.dump(out, f)

@@ -62,7 +62,7 @@ class TaskSpec:
 
 class ObjEntry:
     __slots__ = ("state", "inline", "size", "node", "refcount", "pins", "waiters", "contained",
-                 "is_error", "owner_task", "spilled_path", "gen_end")
+                 "is_error", "owner_task", "spilled_path", "gen_end", "lost")
 
     def __init__(self):
         self.state = PENDING
@@ -77,6 +77,7 @@ class ObjEntry:
         self.owner_task = None
         self.spilled_path = None
         self.gen_end = None
+        self.lost = False
 
 
 class WorkerInfo:
@@ -127,6 +128,10 @@ class Head:
         self.worker_env = worker_env or {}
         self.spill_dir = spill_dir or os.path.join(session_dir, "spill")
         self.sock_path = os.path.join(session_dir, "head.sock")
+        if len(self.sock_path) > 100:  # AF_UNIX path limit (108 bytes)
+            import tempfile
+
+            self.sock_path = os.path.join(tempfile.gettempdir(), f"caamd-{node_id.hex()[:12]}.sock")
         self.sel = selectors.DefaultSelector()
         self.lsock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         try:
@@ -147,6 +152,20 @@ class Head:
             self.tsock.setblocking(False)
             self.tcp_address = f"{host}:{self.tsock.getsockname()[1]}"
             self.sel.register(self.tsock, selectors.EVENT_READ, ("listen", None))
+        # multi-node: per-node store names, object-server addresses, agent connections
+        self.head_hex = node_id.hex()
+        self.node_store = {self.head_hex: store_name}
+        self.node_obj_addr: Dict[str, str] = {}
+        self.node_conns: Dict[str, Conn] = {}
+        self.obj_server = None
+        if listen_tcp:
+            from .object_server import ObjectServer
+
+            bind_host = listen_tcp.rsplit(":", 1)[0]
+            adv = "127.0.0.1" if bind_host in ("0.0.0.0", "") else bind_host
+            self.obj_server = ObjectServer(self.store, bind_host or "0.0.0.0")
+            self.node_obj_addr[self.head_hex] = self.obj_server.address(adv)
+            self.node_info[self.head_hex]["NodeManagerAddress"] = adv
         # wakeup pipe for cross-thread calls
         self._wr, self._ww = socket.socketpair()
         self._wr.setblocking(False)
@@ -177,6 +196,7 @@ class Head:
         self.handle_objs: Dict[bytes, bytes] = {}  # handle object id -> actor id
         self.events: collections.deque = collections.deque(maxlen=200000)
         self.jobs: Dict[bytes, dict] = {}
+        self.metrics: Dict[str, dict] = {}
         self.max_workers = int(max(4, resources.get("CPU", 1) * 4))
         self.running = True
         self.thread = None
@@ -295,9 +315,13 @@ class Head:
         self._send(c, ("reply", req, value))
 
     def _h_register(self, c, kind, worker_id, pid, node_hex, extra):
-        self.clients[c] = {"id": worker_id, "kind": kind, "pid": pid, "node": node_hex}
-        self._send(c, ("registered", {"store_name": self.store_name,
-                                      "node_id": node_hex or self.node_id.hex(),
+        node = node_hex or self.head_hex
+        self.clients[c] = {"id": worker_id, "kind": kind, "pid": pid, "node": node}
+        if kind == "node":
+            self._register_node(c, node_hex, extra)
+            return
+        self._send(c, ("registered", {"store_name": self.node_store.get(node, self.store_name),
+                                      "node_id": node,
                                       "namespace": self.namespace,
                                       "session_dir": self.session_dir}))
         if kind == "worker":
@@ -407,10 +431,15 @@ class Head:
             self._on_handles_gone(aid)
             return
         if e.inline is None and e.spilled_path is None:
-            try:
-                self.store.remove(oid)
-            except Exception:
-                pass
+            if e.node and e.node != self.head_hex:
+                nc = self.node_conns.get(e.node)
+                if nc is not None:
+                    self._send(nc, ("free", [oid]))
+            else:
+                try:
+                    self.store.remove(oid)
+                except Exception:
+                    pass
         if e.spilled_path:
             try:
                 os.unlink(e.spilled_path)
@@ -422,14 +451,22 @@ class Head:
                 ce.pins -= 1
                 self._maybe_free(r)
 
-    def _obj_payload(self, oid):
+    def _obj_payload(self, oid, node=None):
         e = self.objects.get(oid)
-        if e is None:
+        if e is None or getattr(e, "lost", False):
             return ("lost", None)
         if e.inline is not None:
             return ("err" if e.is_error else "inline", e.inline)
         if e.spilled_path is not None:
             self._restore(oid, e)
+            e.node = self.head_hex
+        src = e.node or self.head_hex
+        if node is not None and src != node:
+            addr = self.node_obj_addr.get(src)
+            if addr is None:
+                return ("lost", None)
+            # the reader pulls straight from the owning node's object server
+            return ("err_remote" if e.is_error else "remote", (addr, e.size))
         return ("err_store" if e.is_error else "store", e.size)
 
     def _restore(self, oid, e):
@@ -471,7 +508,8 @@ class Head:
         return freed
 
     def _h_evict(self, c, req, need):
-        self._reply(c, req, self._evict(need))
+        node = self.clients.get(c, {}).get("node") or self.head_hex
+        self._reply(c, req, self._evict(need) if node == self.head_hex else 0)
 
     def _h_get(self, c, req, oids, timeout):
         """Reply when every object is ready (or on timeout with what is ready)."""
@@ -480,8 +518,9 @@ class Head:
             e = self._obj(o)
             if e.state != READY:
                 missing.add(o)
+        rnode = self.clients.get(c, {}).get("node") or self.head_hex
         if not missing:
-            self._reply(c, req, [(o, *self._obj_payload(o)) for o in oids])
+            self._reply(c, req, [(o, *self._obj_payload(o, rnode)) for o in oids])
             return
         state = {"missing": missing, "done": False}
 
@@ -489,7 +528,7 @@ class Head:
             state["missing"].discard(oid)
             if not state["missing"] and not state["done"]:
                 state["done"] = True
-                self._reply(c, req, [(o, *self._obj_payload(o)) for o in oids])
+                self._reply(c, req, [(o, *self._obj_payload(o, rnode)) for o in oids])
 
         for o in missing:
             self._obj(o).waiters.append(on_ready)
@@ -721,6 +760,8 @@ class Head:
         worker_id = worker_id or os.urandom(16)
         key = (node, tuple(gpu_ids))
         self.starting[key] += 1
+        if node != self.head_hex:
+            return self._spawn_remote(node, gpu_ids, worker_id, env)
         e = dict(os.environ)
         e.update(self.worker_env)
         e["CAAMD_HEAD"] = self.sock_path if node == self.node_id.hex() else (self.tcp_address or "")
@@ -755,6 +796,27 @@ class Head:
         self.workers[worker_id] = w
         return w
 
+    def _spawn_remote(self, node, gpu_ids, worker_id, env):
+        """Ask the node's agent to start a worker (reference: raylet worker pool)."""
+        extra = dict(self.worker_env)
+        renv = env or {}
+        noset = (renv.get("env_vars") or {}).get("CAAMD_NOSET_ROCR_VISIBLE_DEVICES")
+        if gpu_ids and not noset:
+            extra["ROCR_VISIBLE_DEVICES"] = ",".join(str(g) for g in gpu_ids)
+        for k, v in (renv.get("env_vars") or {}).items():
+            extra[k] = str(v)
+        if renv:
+            import json
+
+            extra["CAAMD_RUNTIME_ENV"] = json.dumps(renv)
+        extra["CAAMD_GPU_IDS"] = ",".join(str(g) for g in gpu_ids)
+        extra["CAAMD_SYS_PATH"] = os.pathsep.join(p for p in sys.path if p and os.path.isdir(p))
+        self._send(self.node_conns.get(node), ("spawn", worker_id.hex(), list(gpu_ids), extra))
+        w = WorkerInfo(worker_id=worker_id, pid=None, node=node, gpu_key=tuple(gpu_ids),
+                       kind="worker", proc=None, alive=False)
+        self.workers[worker_id] = w
+        return w
+
     def _dispatch_to(self, w: WorkerInfo, spec: TaskSpec):
         w.idle = False
         w.task = spec.task_id
@@ -773,7 +835,7 @@ class Head:
             w.fns.add(spec.fn_id)
         resolved = {}
         for r in spec.arg_refs:
-            resolved[r] = self._obj_payload(r)
+            resolved[r] = self._obj_payload(r, w.node)
         return (spec, fn_blob, resolved)
 
     def _h_fetch_fn(self, c, req, fn_id):
@@ -1089,6 +1151,9 @@ class Head:
         c.close()
         info = self.clients.pop(c, {})
         w = self.conn_worker.pop(c, None)
+        if info.get("kind") == "node":
+            self._on_node_death(info.get("node"))
+            return
         if w is None:
             if info.get("kind") == "driver":
                 self._on_driver_exit(info.get("id"))
@@ -1259,7 +1324,34 @@ class Head:
     def _h_state(self, c, req, what, arg):
         self._reply(c, req, self.state(what, arg))
 
+    def _h_metric(self, c, name, kind, desc, tag_keys, tags, value, boundaries):
+        """Application metrics (reference: python/ray/util/metrics.py -> per-node
+        metrics agent); aggregated here and exported by the dashboard's /metrics."""
+        m = self.metrics.get(name)
+        if m is None:
+            m = self.metrics[name] = {"kind": kind, "desc": desc, "tag_keys": tuple(tag_keys),
+                                      "boundaries": list(boundaries or []), "series": {}}
+        key = tuple(tags)
+        if kind == "counter":
+            m["series"][key] = m["series"].get(key, 0.0) + value
+        elif kind == "gauge":
+            m["series"][key] = value
+        else:  # histogram: (bucket counts, sum, count)
+            b = m["boundaries"]
+            cur = m["series"].get(key) or [[0] * (len(b) + 1), 0.0, 0]
+            i = 0
+            while i < len(b) and value > b[i]:
+                i += 1
+            cur[0][i] += 1
+            cur[1] += value
+            cur[2] += 1
+            m["series"][key] = cur
+
     def state(self, what, arg=None):
+        if what == "metrics":
+            import copy
+
+            return copy.deepcopy(self.metrics)
         if what == "cluster_resources":
             return self.sched.cluster_total()
         if what == "available_resources":
@@ -1320,6 +1412,43 @@ class Head:
         self._retry_pending_pgs()
         self._retry_infeasible()
         self._schedule()
+
+    def _register_node(self, c, node_hex, extra):
+        """A node agent joined (reference: raylet registering with the GCS node manager)."""
+        res = {k: float(v) for k, v in extra["resources"].items()}
+        addr = extra.get("address", "127.0.0.1")
+        res.setdefault(f"node:{addr}", 1.0)
+        self.sched.add_node(node_hex, res)
+        self.free_gpus[node_hex] = list(extra.get("gpu_ids", ()))
+        self.node_store[node_hex] = extra["store_name"]
+        self.node_obj_addr[node_hex] = extra["obj_addr"]
+        self.node_conns[node_hex] = c
+        self.node_resources[node_hex] = dict(res)
+        self.node_info[node_hex] = {"NodeID": node_hex, "Alive": True, "NodeManagerAddress": addr,
+                                    "Resources": dict(res), "local": False, "pid": extra.get("pid")}
+        self._send(c, ("registered", {"store_name": extra["store_name"], "node_id": node_hex,
+                                      "namespace": self.namespace, "session_dir": self.session_dir,
+                                      "head_tcp": self.tcp_address}))
+        self.events.append(("node_added", node_hex, time.time()))
+        self._retry_pending_pgs()
+        self._retry_infeasible()
+        self._schedule()
+
+    def _on_node_death(self, node_hex):
+        self.node_conns.pop(node_hex, None)
+        self.sched.set_alive(node_hex, False)
+        if node_hex in self.node_info:
+            self.node_info[node_hex]["Alive"] = False
+        self.events.append(("node_removed", node_hex, time.time()))
+        # objects whose only copy lived there are lost
+        for oid, e in list(self.objects.items()):
+            if e.node == node_hex and e.inline is None and e.state == READY:
+                e.lost = True
+        # workers of that node: their control connections drop on their own; fail
+        # anything still attributed to them (e.g. they never connected)
+        for w in list(self.workers.values()):
+            if w.node == node_hex and w.conn is None:
+                self.workers.pop(w.worker_id, None)
 
     def _h_remove_node(self, c, node_hex):
         self.sched.set_alive(node_hex, False)

@@ -1,0 +1,88 @@
+"""Standalone head process (reference: ``ray start --head`` -> gcs_server +
+raylet + dashboard processes; here one process: the Head event loop (GCS +
+head-node raylet), the head node's object server, and the dashboard thread).
+
+Writes ``<temp>/caamd/latest_address`` (TCP control address for node agents
+and remote drivers) and ``<temp>/caamd/head.json`` (pid, addresses, dashboard
+URL) so ``init(address="auto")`` and the CLI can find it."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import signal
+import tempfile
+import threading
+import time
+import uuid
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--port", type=int, default=6380)
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--num-cpus", type=float, default=None)
+    ap.add_argument("--num-gpus", type=int, default=None)
+    ap.add_argument("--resources", default="{}")
+    ap.add_argument("--object-store-memory", type=int, default=None)
+    ap.add_argument("--dashboard-host", default="127.0.0.1")
+    ap.add_argument("--dashboard-port", type=int, default=8265)
+    ap.add_argument("--include-dashboard", default="true")
+    ap.add_argument("--temp-dir", default=None)
+    a = ap.parse_args(argv)
+
+    from .api import _default_cpus, _default_store_bytes, _mem_bytes, detect_gpus
+    from .head import Head
+
+    root = a.temp_dir or os.path.join(tempfile.gettempdir(), "caamd")
+    sess = f"session_{time.strftime('%Y%m%d-%H%M%S')}_{os.getpid()}_{uuid.uuid4().hex[:6]}"
+    session_dir = os.path.join(root, sess)
+    gpus = list(range(a.num_gpus)) if a.num_gpus is not None else detect_gpus()
+    res = {"CPU": float(a.num_cpus if a.num_cpus is not None else _default_cpus()), "memory": float(_mem_bytes())}
+    if gpus:
+        res["GPU"] = float(len(gpus))
+    store_bytes = int(a.object_store_memory or _default_store_bytes())
+    res["object_store_memory"] = float(store_bytes)
+    res[f"node:{a.host}"] = 1.0
+    res["node:__internal_head__"] = 1.0
+    res.update({k: float(v) for k, v in json.loads(a.resources).items()})
+    store_name = f"/caamd_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    head = Head(session_dir, os.urandom(16), res, store_name, store_bytes, gpus,
+                listen_tcp=f"{a.host}:{a.port}")
+    head.start()
+    url = None
+    if a.include_dashboard.lower() in ("1", "true", "yes"):
+        from ..dashboard import start_dashboard
+
+        url = start_dashboard(a.dashboard_host, a.dashboard_port, head=head, control_address=head.sock_path)
+    os.makedirs(root, exist_ok=True)
+    info = {"pid": os.getpid(), "address": head.tcp_address, "unix": head.sock_path, "dashboard": url,
+            "session_dir": session_dir, "node_id": head.head_hex}
+    with open(os.path.join(root, "head.json"), "w") as f:
+        json.dump(info, f)
+    with open(os.path.join(root, "latest_address"), "w") as f:
+        f.write(head.sock_path)
+    print(json.dumps(info), flush=True)
+    stop = threading.Event()
+
+    def on_sig(*_):
+        stop.set()
+
+    signal.signal(signal.SIGTERM, on_sig)
+    signal.signal(signal.SIGINT, on_sig)
+    while not stop.is_set():
+        stop.wait(0.5)
+    try:
+        from ..dashboard import stop_dashboard
+
+        stop_dashboard()
+    finally:
+        head.shutdown()
+        try:
+            os.unlink(os.path.join(root, "head.json"))
+        except OSError:
+            pass
+
+
+if __name__ == "__main__":
+    main()

@@ -226,6 +226,15 @@ class CoreWorker:
             if pb is None:
                 raise ObjectLostError(oid.hex(), "object is not in the local object store")
             return serialization.deserialize(memoryview(pb))
+        if kind in ("remote", "err_remote"):
+            from .object_server import pull
+
+            data = pull(payload[0], oid)
+            if data is None:
+                raise ObjectLostError(oid.hex(), f"object is gone from its node ({payload[0]})")
+            if kind == "remote":
+                return serialization.deserialize(memoryview(data))
+            raise _as_raisable(serialization.deserialize(memoryview(data)))
         if kind in ("err", "err_store"):
             if kind == "err":
                 err = serialization.deserialize(payload)
