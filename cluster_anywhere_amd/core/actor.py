@@ -15,13 +15,19 @@ from .ids import ActorID
 
 
 def method(*args, **kwargs):
-    """``@method(num_returns=2, concurrency_group=...)`` for actor methods."""
+    """``@method(num_returns=2, concurrency_group=..., tensor_transport="ipc")`` for
+    actor methods. ``tensor_transport="ipc"`` returns GPU tensors as HIP IPC
+    handles (zero-copy for same-node readers, experimental/gpu_objects.py)."""
 
     def deco(fn):
         if "num_returns" in kwargs:
             fn.__ray_num_returns__ = kwargs["num_returns"]
         if "concurrency_group" in kwargs:
             fn.__ray_concurrency_group__ = kwargs["concurrency_group"]
+        if kwargs.get("tensor_transport") not in (None, "object_store", "ipc"):
+            raise ValueError("tensor_transport must be 'object_store' (host copy) or 'ipc'")
+        if kwargs.get("tensor_transport") == "ipc":
+            fn.__ray_tensor_transport__ = "ipc"
         return fn
 
     if len(args) == 1 and callable(args[0]) and not kwargs:

@@ -246,12 +246,15 @@ def _w():
     return context.worker
 
 
-def put(value, *, _owner=None) -> ObjectRef:
+def put(value, *, _owner=None, _tensor_transport: Optional[str] = None) -> ObjectRef:
+    """``_tensor_transport="ipc"``: GPU tensors in ``value`` are shared with
+    same-node readers through HIP IPC handles (zero copy) instead of host copies
+    (see experimental/gpu_objects.py)."""
     if context.local_mode:
         from .local_mode import local_put
 
         return local_put(value)
-    return _w().put(value)
+    return _w().put(value, tensor_transport=_tensor_transport)
 
 
 def get(object_refs, *, timeout: Optional[float] = None):

@@ -82,7 +82,8 @@ class ObjEntry:
 
 class WorkerInfo:
     __slots__ = ("worker_id", "conn", "pid", "node", "gpu_key", "idle", "actor_id", "task",
-                 "proc", "fns", "alive", "kind", "started", "tasks_inflight", "env_key", "client_id")
+                 "proc", "fns", "alive", "kind", "started", "tasks_inflight", "env_key", "client_id",
+                 "oom_killed")
 
     def __init__(self, **kw):
         for s in self.__slots__:
@@ -203,6 +204,11 @@ class Head:
         self._prestart = prestart
         self.cpu_count = resources.get("CPU", 1)
         self._last_health = time.time()
+        from .memory_monitor import MemoryMonitor
+
+        self.mem_monitor = MemoryMonitor()
+        self._last_mem = 0.0
+        self._oom_quiet_until = 0.0
 
     # ------------------------------------------------------------------ loop
     def start(self):
@@ -272,6 +278,9 @@ class Head:
             if now - self._last_health > 1.0:
                 self._last_health = now
                 self._health_check()
+            if self.mem_monitor.enabled and now - self._last_mem >= self.mem_monitor.refresh_s:
+                self._last_mem = now
+                self._check_memory(now)
 
     def _on_readable(self, c: Conn):
         try:
@@ -926,12 +935,12 @@ class Head:
         self.infeasible = still
 
     def _fail_task(self, spec, err):
-        from ..exceptions import (ActorDiedError, TaskCancelledError, TaskPlacementGroupRemoved,
-                                  WorkerCrashedError, RayError)
+        from ..exceptions import (ActorDiedError, OutOfMemoryError, RayError, TaskCancelledError,
+                                  TaskPlacementGroupRemoved, WorkerCrashedError)
 
         kind, msg = err
         cls = {"ActorDiedError": ActorDiedError, "TaskCancelledError": TaskCancelledError,
-               "WorkerCrashedError": WorkerCrashedError,
+               "WorkerCrashedError": WorkerCrashedError, "OutOfMemoryError": OutOfMemoryError,
                "TaskPlacementGroupRemoved": TaskPlacementGroupRemoved}.get(kind, RayError)
         exc = cls(msg) if cls is not TaskCancelledError else TaskCancelledError(spec.task_id.hex(), msg)
         blob = serialization.serialize(exc).to_bytes()
@@ -1173,12 +1182,17 @@ class Head:
             if spec.kind != NORMAL:
                 continue
             self._release(spec)
+            mr = spec.max_retries if spec.max_retries is not None else 3
             if spec.cancelled:
                 self._fail_task(spec, ("TaskCancelledError", "task was cancelled"))
-            elif spec.attempt < (spec.max_retries if spec.max_retries is not None else 3):
+            elif mr < 0 or spec.attempt < mr:
                 spec.attempt += 1
                 spec.state = "pending"
                 self._enqueue_ready(spec)
+            elif w.oom_killed:
+                self._fail_task(spec, ("OutOfMemoryError", (
+                    "Task was killed due to the node running low on memory (memory monitor "
+                    f"threshold {self.mem_monitor.threshold:.2f}); retries exhausted.")))
             else:
                 self._fail_task(spec, ("WorkerCrashedError", "the worker died while running the task"))
         w.tasks_inflight.clear()
@@ -1192,6 +1206,46 @@ class Head:
                 a.restarts_left = 0
                 a.death_cause = "owner exited"
                 self._kill_worker(a.worker)
+
+    # ------------------------------------------------------------ OOM killer
+    def _check_memory(self, now):
+        """Kill one worker when the node is over the memory threshold (see
+        core/memory_monitor.py; reference: raylet MemoryMonitor + worker killing policy)."""
+        if now < self._oom_quiet_until:
+            return
+        frac = self.mem_monitor.over_threshold()
+        if frac is None:
+            return
+        from .memory_monitor import pick_victim
+
+        cands = []
+        for w in self.workers.values():
+            if not w.alive or w.node != self.head_hex or w.oom_killed:
+                continue
+            if w.actor_id is not None:
+                a = self.actors.get(w.actor_id)
+                if a is None or a.state == "DEAD":
+                    continue
+                start = a.spec.start_time if a.spec is not None and a.spec.start_time else 0.0
+                cands.append((w, bool(a.restarts_left), start))
+            elif w.tasks_inflight:
+                spec = next(iter(w.tasks_inflight.values()))
+                mr = spec.max_retries if spec.max_retries is not None else 3
+                cands.append((w, mr < 0 or spec.attempt < mr, spec.start_time or 0.0))
+        w = pick_victim(cands)
+        if w is None:
+            return
+        w.oom_killed = True
+        self.mem_monitor.kills += 1
+        self.events.append(("oom_kill", w.worker_id.hex(), time.time(), frac))
+        if w.actor_id is not None:
+            a = self.actors.get(w.actor_id)
+            if a is not None:
+                a.death_cause = (f"the actor's worker was killed by the memory monitor: node memory "
+                                 f"usage {frac:.2f} >= threshold {self.mem_monitor.threshold:.2f}")
+        self._kill_worker(w.worker_id)
+        # let the kernel reclaim the victim's memory before judging again
+        self._oom_quiet_until = now + max(1.0, 4 * self.mem_monitor.refresh_s)
 
     def _health_check(self):
         for w in list(self.workers.values()):
@@ -1397,6 +1451,30 @@ class Head:
             a = self.actors.get(arg)
             return None if a is None else {"state": a.state, "name": a.name, "pid": a.pid,
                                            "num_restarts": a.num_restarts}
+        if what == "autoscaler":
+            # resource demand the cluster cannot place right now (reference: GCS
+            # autoscaler state: pending tasks/actors by shape + pending PG bundles)
+            demand = []
+            for q in self.ready_queues.values():
+                for spec in q:
+                    if not spec.cancelled and not (spec.strategy and spec.strategy[0] == "pg"):
+                        demand.append(dict(spec.resources))
+            for spec in self.infeasible:
+                if not spec.cancelled:
+                    demand.append(dict(spec.resources))
+            pg_bundles = []
+            for pid in self.pending_pgs:
+                g = self.pgs.get(pid)
+                if g is not None:
+                    pg_bundles.append({"strategy": g["strategy"], "bundles": [dict(b) for b in g["bundles"]]})
+            busy = {}
+            for w in self.workers.values():
+                if w.alive and (w.tasks_inflight or w.actor_id is not None):
+                    busy[w.node] = busy.get(w.node, 0) + 1
+            nodes = {n: {"total": self.sched.total(n), "available": self.sched.available(n),
+                         "alive": info.get("Alive", False), "busy_workers": busy.get(n, 0),
+                         "head": n == self.head_hex} for n, info in self.node_info.items()}
+            return {"demand": demand, "pending_placement_groups": pg_bundles, "nodes": nodes}
         if what == "named_actors":
             return [(ns, n) for (ns, n), aid in self.named_actors.items()
                     if self.actors.get(aid) and self.actors[aid].state != "DEAD"]

@@ -12,8 +12,9 @@ Wire/arena format::
 ``ObjectRef`` / ``ActorHandle`` values found while pickling are recorded as
 contained references (the object store keeps them alive while the outer object
 lives).  torch GPU tensors are copied to host on serialisation and restored onto
-the same device index when the reader has a GPU (same-node GPU->GPU zero-copy
-hand-off uses :mod:`cluster_anywhere_amd.core.gpu_objects` instead).
+the same device index when the reader has a GPU; with ``tensor_transport="ipc"``
+they travel as HIP IPC handles instead (same-node GPU->GPU zero-copy hand-off,
+:mod:`cluster_anywhere_amd.experimental.gpu_objects`).
 """
 from __future__ import annotations
 
@@ -21,6 +22,7 @@ import io
 import pickle
 import struct
 import sys
+import threading
 from typing import Any, List, Tuple
 
 import cloudpickle
@@ -28,6 +30,15 @@ import cloudpickle
 MAGIC = 0xCA5E0001
 ALIGN = 64
 _HDR = struct.Struct("<IIQ")
+_tls = threading.local()  # .transport: None (host copy) | "ipc" (see experimental/gpu_objects.py)
+
+
+def _gpu_reduce(t):
+    if t.is_cuda and getattr(_tls, "transport", None) == "ipc":
+        from ..experimental.gpu_objects import reduce_ipc
+
+        return reduce_ipc(t)
+    return _reduce_torch(t)
 
 
 def _pad(n: int) -> int:
@@ -78,7 +89,11 @@ class SerializedObject:
 def _rebuild_torch(arr, dtype_name, shape, device_index):
     import torch
 
-    t = torch.from_numpy(arr)
+    import warnings
+
+    with warnings.catch_warnings():  # read-only arena views: torch warns, the data is never written
+        warnings.simplefilter("ignore", UserWarning)
+        t = torch.from_numpy(arr)
     dt = getattr(torch, dtype_name)
     if dt in (torch.bfloat16,) or t.dtype != dt:
         t = t.view(dt)
@@ -126,7 +141,7 @@ class _Pickler(pickle.Pickler):
             import torch
 
             if isinstance(obj, torch.Tensor) and not isinstance(obj, torch.nn.Parameter):
-                return _reduce_torch(obj)
+                return _gpu_reduce(obj)
         if type(obj).__name__ == "State" and mod == "starlette.datastructures":
             return (type(obj), (dict(obj._state),))
         return NotImplemented
@@ -147,7 +162,7 @@ class _CloudPickler(cloudpickle.CloudPickler):
             import torch
 
             if isinstance(obj, torch.Tensor) and not isinstance(obj, torch.nn.Parameter):
-                return _reduce_torch(obj)
+                return _gpu_reduce(obj)
         if type(obj).__name__ == "State" and type(obj).__module__ == "starlette.datastructures":
             # starlette's State.__getattr__ recurses when unpickled attribute-by-attribute
             return (type(obj), (dict(obj._state),))
@@ -164,17 +179,24 @@ def _rebuild_mock_val_ser(msg, code, kind, attempt):
     return MockValSer(msg, code=code, val_or_ser=kind, attempt_rebuild=attempt)
 
 
-def serialize(value: Any) -> SerializedObject:
+def serialize(value: Any, tensor_transport: Any = None) -> SerializedObject:
+    """``tensor_transport="ipc"``: GPU tensors travel as HIP IPC handles (zero
+    copy for readers on the same node) instead of host copies."""
     buffers: List[pickle.PickleBuffer] = []
     refs: List[bytes] = []
     f = io.BytesIO()
+    prev = getattr(_tls, "transport", None)
+    _tls.transport = tensor_transport
     try:
-        _Pickler(f, buffers.append, refs).dump(value)
-    except Exception:
-        buffers.clear()
-        refs.clear()
-        f = io.BytesIO()
-        _CloudPickler(f, buffers.append, refs).dump(value)
+        try:
+            _Pickler(f, buffers.append, refs).dump(value)
+        except Exception:
+            buffers.clear()
+            refs.clear()
+            f = io.BytesIO()
+            _CloudPickler(f, buffers.append, refs).dump(value)
+    finally:
+        _tls.transport = prev
     return SerializedObject(f.getvalue(), buffers, refs)
 
 

@@ -207,10 +207,10 @@ class CoreWorker:
         self.store.seal(oid)
         return None, size, self.node_hex
 
-    def put(self, value, _owner_ref=True) -> ObjectRef:
+    def put(self, value, _owner_ref=True, tensor_transport=None) -> ObjectRef:
         if isinstance(value, ObjectRef):
             raise TypeError("Calling put() on an ObjectRef is not allowed")
-        so = serialization.serialize(value)
+        so = serialization.serialize(value, tensor_transport)
         oid = ObjectID.for_put(self.worker_id)
         inline, size, node = self._store(oid, so)
         self.send(("put", oid, inline, size, node, so.contained_refs, False))
@@ -587,14 +587,17 @@ class CoreWorker:
             result = DynamicObjectRefGenerator(refs)
             return [self._result_entry(spec.return_ids[0], result)]
         n = spec.num_returns
+        tt = None
+        if spec.kind == ACTOR_METHOD and self.actor_instance is not None:
+            tt = getattr(getattr(type(self.actor_instance), spec.method, None), "__ray_tensor_transport__", None)
         if n == 1:
-            return [self._result_entry(spec.return_ids[0], result)]
+            return [self._result_entry(spec.return_ids[0], result, tt)]
         if n == 0:
             return []
         vals = tuple(result) if result is not None else None
         if vals is None or len(vals) != n:
             raise ValueError(f"task declared num_returns={n} but returned {result!r}")
-        return [self._result_entry(o, v) for o, v in zip(spec.return_ids, vals)]
+        return [self._result_entry(o, v, tt) for o, v in zip(spec.return_ids, vals)]
 
     def _stream_item(self, spec, i, item):
         oid = ObjectID.for_task_return(spec.task_id, i)
@@ -620,11 +623,8 @@ class CoreWorker:
             self._stream_error(spec, i, e)
         return []
 
-    def _result_entry(self, oid, value):
-        if isinstance(value, ObjectRef):
-            # returning a ref: the result object holds the ref (nested)
-            pass
-        so = serialization.serialize(value)
+    def _result_entry(self, oid, value, tensor_transport=None):
+        so = serialization.serialize(value, tensor_transport)
         inline, size, node = self._store(oid, so)
         return (oid, inline, size, node, so.contained_refs, False)
 

@@ -1,0 +1,6 @@
+"""Experimental APIs (reference: python/ray/experimental/): the internal KV
+table and zero-copy GPU tensor hand-off between processes of one node
+(``tensor_transport="ipc"``, see :mod:`.gpu_objects`)."""
+from . import internal_kv  # noqa: F401
+
+__all__ = ["internal_kv"]

@@ -38,6 +38,10 @@ class DataParallelStep:
         self.world = world
         self.zero = bool(zero and world > 1)
         p0 = next(model.parameters())
+        if p0.is_cuda:
+            from ..ops.gemm_tuning import use_tuned_gemms
+
+            use_tuned_gemms()  # shipped per-shape hipBLASLt/rocBLAS selections (lookup only)
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if p0.is_cuda else torch.float32
         align = 64
