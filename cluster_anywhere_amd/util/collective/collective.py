@@ -87,8 +87,12 @@ class CollectiveGroup:
 
             opts = dist.ProcessGroupNCCL.Options()
             opts._timeout = timeout
+            opts.group_name = group_name
             self.pg = dist.ProcessGroupNCCL(self._store, rank, world_size, opts)
             self.device = f"cuda:{torch.cuda.current_device()}"
+            # build the RCCL communicator now (what init_process_group(device_id=..)
+            # does), not lazily inside the first collective
+            self.pg.eager_connect_single_device(torch.device(self.device))
 
     # -- collectives (every call blocks until the result is in place) ----------
     def allreduce(self, t, op=ReduceOp.SUM):
