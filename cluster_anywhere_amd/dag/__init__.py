@@ -2,8 +2,9 @@
 ``actor.method.bind(...)``, ``InputNode``, ``MultiOutputNode``; ``dag.execute(x)``
 submits the graph as ordinary tasks (ObjectRefs flow between nodes, so the
 scheduler overlaps independent branches); ``dag.experimental_compile()`` builds a
-:class:`~cluster_anywhere_amd.dag.compiled.CompiledDAG` that re-executes the same
-actor pipeline with pre-resolved handles and no per-call graph walk."""
+:class:`~cluster_anywhere_amd.dag.compiled.CompiledDAG`: resident per-actor
+execution loops connected by native shared-memory channels (and RCCL for
+tensor-transport edges)."""
 from __future__ import annotations
 
 from typing import Any, Dict, List
@@ -36,6 +37,12 @@ class DAGNode:
     def execute(self, *args, **kwargs):
         inp = InputValue(args, kwargs)
         return self._exec({}, inp)
+
+    def with_tensor_transport(self, transport: str = "auto", **_kw):
+        """Mark this node's output for out-of-band tensor transfer in a compiled
+        graph: ``"nccl"``/``"rccl"`` (GPU→GPU over xGMI) or ``"gloo"`` (CPU)."""
+        self._transport = transport
+        return self
 
     def experimental_compile(self, **kw):
         from .compiled import CompiledDAG

@@ -1,58 +1,488 @@
-"""Compiled DAGs (reference: python/ray/dag/compiled_dag_node.py).
+"""Compiled graphs (reference: python/ray/dag/compiled_dag_node.py,
+python/ray/experimental/channel/{shared_memory_channel,torch_tensor_nccl_channel}.py).
 
-``dag.experimental_compile()`` freezes the graph: actor handles are created once,
-the topological order is computed once, and every ``execute()`` replays the
-pre-planned submissions (no per-call graph walk, no re-binding). Results are
-returned as :class:`CompiledDAGRef` (``ray.get``-able)."""
+``dag.experimental_compile()`` turns a DAG of actor-method nodes into a
+standing pipeline:
+
+* every participating actor runs ONE resident execution loop (a thread started
+  through ``__ray_call__``) over its slice of the graph in topological order —
+  no task submission, scheduling or object-store round trip per call;
+* edges are native shared-memory rings (:mod:`experimental.channel`,
+  ``csrc/runtime/channel.cc``): the driver writes the input into one ring,
+  every producer writes its result into one ring that all its consumers read,
+  and results consumed on the same actor are passed in-process;
+* an edge marked ``node.with_tensor_transport("nccl")`` (alias ``"rccl"``;
+  ``"gloo"`` for CPU) sends only tensor metadata through the ring and the tensor
+  payload point-to-point over an RCCL communicator spanning the graph's actors
+  — on MI355X that is a direct xGMI GPU→GPU copy, never a host bounce;
+* up to ``_max_inflight_executions`` executions are pipelined (the ring depth);
+  ``execute()`` returns a :class:`CompiledDAGRef`; ``ray.get`` on it reads the
+  outputs in submission order. An exception inside a node is forwarded through
+  the graph and re-raised by ``get`` as a ``RayTaskError``.
+
+Graphs that contain plain task nodes (``f.bind``) fall back to a pre-planned
+replay through ordinary task submission (:class:`_ReplayDAG`).
+"""
 from __future__ import annotations
 
-from typing import Any, List
+import asyncio
+import inspect
+import os
+import threading
+import traceback
+from typing import Any, Dict, List, Optional
+
+from ..experimental.channel import DEFAULT_SLOT_BYTES, Channel, ChannelClosedError
+
+COLLECTIVE_TRANSPORTS = ("nccl", "rccl", "gloo")
 
 
+class _Stop:
+    """Teardown sentinel flowing through the graph."""
+
+
+class _DagError:
+    def __init__(self, err):
+        self.err = err
+
+
+class _TensorSlot:
+    """Placeholder for a tensor sent out-of-band over the collective group."""
+
+    def __init__(self, i, shape, dtype):
+        self.i, self.shape, self.dtype = i, tuple(shape), dtype
+
+
+# --------------------------------------------------------------------- refs
 class CompiledDAGRef:
-    def __init__(self, refs, multi):
-        self._refs = refs
-        self._multi = multi
+    def __init__(self, dag, seq, multi):
+        self._dag, self._seq, self._multi = dag, seq, multi
+        self._refs = None  # replay mode
+        self._done = False
 
     def get(self, timeout=None):
-        from ..core.api import get
+        if self._done:
+            raise ValueError("a CompiledDAGRef can be fetched only once")
+        self._done = True
+        if self._refs is not None:
+            from ..core.api import get
 
-        vals = get(self._refs, timeout=timeout)
-        return vals if self._multi else vals[0]
+            vals = get(self._refs, timeout=timeout)
+            return vals if self._multi else vals[0]
+        return self._dag._fetch(self._seq, timeout)
+
+    def __repr__(self):
+        return f"CompiledDAGRef(seq={self._seq})"
+
+
+# --------------------------------------------------------------------- actor side
+def _split_tensors(value):
+    """Replace torch tensors at the top level of value (or in a list/tuple/dict)
+    by _TensorSlot placeholders; returns (skeleton, tensors)."""
+    import torch
+
+    tensors = []
+
+    def sub(v):
+        if isinstance(v, torch.Tensor):
+            tensors.append(v.contiguous())
+            return _TensorSlot(len(tensors) - 1, v.shape, v.dtype)
+        return v
+
+    if isinstance(value, (list, tuple)):
+        sk = type(value)(sub(v) for v in value)
+    elif isinstance(value, dict):
+        sk = {k: sub(v) for k, v in value.items()}
+    else:
+        sk = sub(value)
+    return sk, tensors
+
+
+def _fill_tensors(skel, tensors):
+    def sub(v):
+        return tensors[v.i] if isinstance(v, _TensorSlot) else v
+
+    if isinstance(skel, (list, tuple)):
+        return type(skel)(sub(v) for v in skel)
+    if isinstance(skel, dict):
+        return {k: sub(v) for k, v in skel.items()}
+    return sub(skel)
+
+
+def _slots(skel):
+    vals = list(skel) if isinstance(skel, (list, tuple)) else (
+        list(skel.values()) if isinstance(skel, dict) else [skel])
+    return [v for v in vals if isinstance(v, _TensorSlot)]
+
+
+class _ActorLoop:
+    def __init__(self, instance, plan):
+        self.inst = instance
+        self.plan = plan
+        self.group = None
+
+    def _setup_group(self):
+        g = self.plan.get("group")
+        if not g:
+            return
+        from ..util.collective import collective as col
+
+        col.init_collective_group(g["world"], g["rank"], backend=g["backend"], group_name=g["name"])
+        self.group = col._check_and_get_group(g["name"])
+        import torch
+
+        self.device = (torch.device("cuda", torch.cuda.current_device()) if g["backend"] != "gloo"
+                       else torch.device("cpu"))
+
+    def _read(self, ch, reader, producer_rank):
+        v = ch.read(reader)
+        if producer_rank is not None and not isinstance(v, (_Stop, _DagError)):
+            import torch
+
+            slots = _slots(v)
+            bufs = [torch.empty(s.shape, dtype=s.dtype, device=self.device) for s in slots]
+            works = [self.group.pg.recv([b], producer_rank, 0) for b in bufs]
+            for w in works:
+                w.wait()
+            v = _fill_tensors(v, {s.i: b for s, b in zip(slots, bufs)})
+        return v
+
+    def _write(self, out, value):
+        ch, dst_ranks = out["chan"], out.get("dst_ranks")
+        if dst_ranks and not isinstance(value, (_Stop, _DagError)):
+            skel, tensors = _split_tensors(value)
+            ch.write(skel)
+            works = [self.group.pg.send([t], r, 0) for r in dst_ranks for t in tensors]
+            for w in works:
+                w.wait()
+        else:
+            ch.write(value)
+
+    def _call(self, method, a, k):
+        fn = getattr(self.inst, method)
+        r = fn(*a, **k)
+        if inspect.iscoroutine(r):
+            from ..core import context
+
+            loop = getattr(context.worker, "async_loop", None) if context.worker else None
+            if loop is not None and loop.is_running():
+                r = asyncio.run_coroutine_threadsafe(r, loop).result()
+            else:
+                r = asyncio.run(r)
+        return r
+
+    def run(self):
+        from ..exceptions import RayTaskError
+
+        try:
+            self._setup_group()
+        except Exception:  # pragma: no cover - surfaced through the graph outputs
+            err = _DagError(RayTaskError("compiled-graph setup", traceback.format_exc()))
+            for t in self.plan["tasks"]:
+                if t["out"]:
+                    t["out"]["chan"].write(err)
+            return
+        tasks = self.plan["tasks"]
+        while True:
+            cache: Dict[Any, Any] = {}
+            local: Dict[int, Any] = {}
+            stop = False
+
+            def resolve(spec):
+                kind = spec[0]
+                if kind == "const":
+                    return spec[1]
+                if kind == "loc":
+                    return local[spec[1]]
+                key = (spec[1].name, spec[2])
+                if key not in cache:
+                    cache[key] = self._read(spec[1], spec[2], spec[4] if len(spec) > 4 else None)
+                v = cache[key]
+                if kind == "in" and not isinstance(v, (_Stop, _DagError)):
+                    return _input_select(v, spec[3])
+                return v
+
+            for t in tasks:
+                try:
+                    a = [resolve(s) for s in t["args"]]
+                    k = {n: resolve(s) for n, s in t["kwargs"].items()}
+                except ChannelClosedError:
+                    return
+                vals = a + list(k.values())
+                if any(isinstance(v, _Stop) for v in vals):
+                    stop = True
+                    res = _Stop()
+                else:
+                    err = next((v for v in vals if isinstance(v, _DagError)), None)
+                    if err is not None:
+                        res = err
+                    else:
+                        try:
+                            res = self._call(t["method"], a, k)
+                        except Exception as e:
+                            res = _DagError(RayTaskError(t["method"], traceback.format_exc(), e))
+                local[t["idx"]] = res
+                if t["out"] is not None:
+                    try:
+                        self._write(t["out"], res)
+                    except ChannelClosedError:
+                        return
+            if stop:
+                if self.group is not None:
+                    from ..util import collective as col
+
+                    try:
+                        col.destroy_collective_group(self.plan["group"]["name"])
+                    except Exception:
+                        pass
+                return
+
+
+def _input_select(inp, key):
+    args, kwargs = inp
+    if key is None:
+        if len(args) == 1 and not kwargs:
+            return args[0]
+        return args if args else kwargs
+    if isinstance(key, int):
+        return args[key]
+    return kwargs[key] if key in kwargs else getattr(args[0], key)
+
+
+def _start_loop(instance, plan):
+    loop = _ActorLoop(instance, plan)
+    th = threading.Thread(target=loop.run, name="caamd-compiled-dag", daemon=True)
+    th.start()
+    return os.getpid()
+
+
+# --------------------------------------------------------------------- driver side
+def _topo(root):
+    order, seen = [], set()
+
+    def visit(n):
+        if id(n) in seen:
+            return
+        seen.add(id(n))
+        for c in n._children():
+            visit(c)
+        tgt = getattr(n, "_target", None)
+        if tgt is not None and hasattr(tgt, "_children"):
+            visit(tgt)
+        order.append(n)
+
+    visit(root)
+    return order
 
 
 class CompiledDAG:
-    def __init__(self, root, **kw):
+    def __new__(cls, root, **kw):
+        from . import FunctionNode
+
+        if any(isinstance(n, FunctionNode) for n in _topo(root)):
+            return _ReplayDAG(root)
+        return super().__new__(cls)
+
+    def __init__(self, root, _max_inflight_executions: Optional[int] = None,
+                 _buffer_size_bytes: Optional[int] = None, **_kw):
+        from . import (ClassMethodNode, ClassNode, InputAttributeNode, InputNode,
+                       MultiOutputNode)
+        from ..core.api import get
+
+        self._multi = isinstance(root, MultiOutputNode)
+        self._slots = int(_max_inflight_executions or 8)
+        slot_bytes = int(_buffer_size_bytes or DEFAULT_SLOT_BYTES)
+        order = _topo(root)
+        tasks = [n for n in order if isinstance(n, ClassMethodNode)]
+        if not tasks:
+            raise ValueError("a compiled graph needs at least one actor method node")
+        outputs = list(root._args) if self._multi else [root]
+        for o in outputs:
+            if not isinstance(o, ClassMethodNode):
+                raise ValueError("compiled graph outputs must be actor method nodes")
+        # actor handle per task (ClassNode targets are instantiated once, here)
+        handles = {}
+        for t in tasks:
+            tgt = t._target
+            h = tgt._exec({}, None) if isinstance(tgt, ClassNode) else tgt
+            handles[id(t)] = h
+        actors: List[Any] = []
+        for t in tasks:
+            if handles[id(t)] not in actors:
+                actors.append(handles[id(t)])
+        akey = {id(t): actors.index(handles[id(t)]) for t in tasks}
+        tidx = {id(t): i for i, t in enumerate(tasks)}
+
+        def deps(n):
+            return list(n._args) + list(n._kwargs.values())
+
+        # consumers of each producer (other actors) and of the input
+        input_readers: List[int] = []
+        consumers: Dict[int, List[Any]] = {id(t): [] for t in tasks}
+        for t in tasks:
+            a = akey[id(t)]
+            for d in deps(t):
+                if isinstance(d, (InputNode, InputAttributeNode)):
+                    if a not in input_readers:
+                        input_readers.append(a)
+                elif isinstance(d, ClassMethodNode):
+                    if akey[id(d)] != a and a not in consumers[id(d)]:
+                        consumers[id(d)].append(a)
+                elif hasattr(d, "_children"):
+                    raise ValueError(f"unsupported node in a compiled graph: {type(d).__name__}")
+        for o in outputs:
+            if "driver" not in consumers[id(o)]:
+                consumers[id(o)].append("driver")
+        if not input_readers:
+            raise ValueError("a compiled graph must consume its InputNode")
+
+        # collective group for tensor-transport edges (ranks = actor order)
+        transports = {getattr(t, "_transport", None) for t in tasks} - {None, "auto", "shm"}
+        bad = transports - set(COLLECTIVE_TRANSPORTS)
+        if bad:
+            raise ValueError(f"unknown tensor transport(s) {sorted(bad)}")
+        if len(transports) > 1:
+            raise ValueError("one compiled graph uses one collective transport")
+        backend = None
+        if transports:
+            backend = transports.pop()
+            backend = "nccl" if backend == "rccl" else backend
+        self._group = f"cdag-{os.getpid()}-{os.urandom(4).hex()}" if backend else None
+
+        self._input = Channel(len(input_readers), self._slots, slot_bytes)
+        chans: Dict[int, Channel] = {}
+        for t in tasks:
+            if consumers[id(t)]:
+                chans[id(t)] = Channel(len(consumers[id(t)]), self._slots, slot_bytes)
+        self._channels = [self._input] + list(chans.values())
+        self._out_specs = []  # (channel, reader) per output position
+        for o in outputs:
+            self._out_specs.append((chans[id(o)], consumers[id(o)].index("driver")))
+
+        plans = {a: {"tasks": [], "group": None} for a in range(len(actors))}
+        if backend:
+            for a in plans:
+                plans[a]["group"] = {"world": len(actors), "rank": a, "backend": backend,
+                                     "name": self._group}
+
+        def spec(d, a):
+            if isinstance(d, InputNode):
+                return ("in", self._input, input_readers.index(a), None)
+            if isinstance(d, InputAttributeNode):
+                return ("in", self._input, input_readers.index(a), d._key)
+            if isinstance(d, ClassMethodNode):
+                if akey[id(d)] == a:
+                    return ("loc", tidx[id(d)])
+                tr = getattr(d, "_transport", None) if backend else None
+                src = akey[id(d)] if tr in COLLECTIVE_TRANSPORTS else None
+                return ("ch", chans[id(d)], consumers[id(d)].index(a), None, src)
+            return ("const", d)
+
+        for t in tasks:
+            a = akey[id(t)]
+            out = None
+            if id(t) in chans:
+                out = {"chan": chans[id(t)]}
+                tr = getattr(t, "_transport", None)
+                if backend and tr in COLLECTIVE_TRANSPORTS:
+                    if "driver" in consumers[id(t)]:
+                        raise ValueError("a tensor-transport node cannot be a graph output "
+                                         "(the driver is not in the collective group)")
+                    out["dst_ranks"] = list(consumers[id(t)])
+            plans[a]["tasks"].append({
+                "idx": tidx[id(t)], "method": t._method, "out": out,
+                "args": [spec(d, a) for d in t._args],
+                "kwargs": {k: spec(d, a) for k, d in t._kwargs.items()},
+            })
+        self._actors = actors
+        get([h.__ray_call__.remote(_start_loop, plans[i]) for i, h in enumerate(actors)])
+        self._submitted = 0
+        self._fetched = 0
+        self._results: Dict[int, Any] = {}
+        self._lock = threading.Lock()
+        self._torn_down = False
+
+    # -- execution ---------------------------------------------------------------
+    def execute(self, *args, **kwargs) -> CompiledDAGRef:
+        if self._torn_down:
+            raise RuntimeError("compiled graph was torn down")
+        with self._lock:
+            # keep at most `slots` executions in flight: drain the oldest first
+            while self._submitted - self._fetched >= self._slots:
+                self._read_one(None)
+            self._input.write((args, kwargs))
+            seq = self._submitted
+            self._submitted += 1
+        return CompiledDAGRef(self, seq, self._multi)
+
+    def _read_one(self, timeout):
+        vals = [ch.read(r, timeout) for ch, r in self._out_specs]
+        self._results[self._fetched] = vals
+        self._fetched += 1
+
+    def _fetch(self, seq, timeout):
+        with self._lock:
+            while seq not in self._results:
+                if seq < self._fetched:
+                    raise ValueError("result already fetched")
+                self._read_one(timeout)
+            vals = self._results.pop(seq)
+        for v in vals:
+            if isinstance(v, _DagError):
+                e = v.err
+                raise e.as_instanceof_cause() if hasattr(e, "as_instanceof_cause") else e
+        return vals if self._multi else vals[0]
+
+    def teardown(self, timeout: float = 30.0):
+        if self._torn_down:
+            return
+        self._torn_down = True
+        try:
+            self._input.write(_Stop(), timeout=timeout)
+            # drain until every output ring delivered the stop sentinel
+            for ch, r in self._out_specs:
+                while True:
+                    v = ch.read(r, timeout)
+                    if isinstance(v, _Stop):
+                        break
+        except (TimeoutError, ChannelClosedError):
+            pass
+        finally:
+            for c in self._channels:
+                try:
+                    c.destroy()
+                except Exception:
+                    pass
+
+    def __del__(self):
+        try:
+            if not self._torn_down:
+                for c in self._channels:
+                    c.destroy()
+        except Exception:
+            pass
+
+
+class _ReplayDAG:
+    """Graphs with plain task nodes: actors are created once and the topological
+    order is computed once; every ``execute()`` replays the submissions."""
+
+    def __init__(self, root):
         from . import ClassNode, MultiOutputNode
 
         self._root = root
         self._multi = isinstance(root, MultiOutputNode)
-        # instantiate actors once
-        order, seen = [], set()
-
-        def visit(n):
-            if id(n) in seen:
-                return
-            seen.add(id(n))
-            for c in n._children():
-                visit(c)
-            tgt = getattr(n, "_target", None)
-            if tgt is not None and hasattr(tgt, "_children"):
-                visit(tgt)
-            order.append(n)
-
-        visit(root)
-        self._order = order
-        for n in order:
+        for n in _topo(root):
             if isinstance(n, ClassNode):
                 n._exec({}, None)
 
     def execute(self, *args, **kwargs):
         from . import InputValue
 
-        cache = {}
-        out = self._root._exec(cache, InputValue(args, kwargs))
-        return CompiledDAGRef(out if self._multi else [out], self._multi)
+        out = self._root._exec({}, InputValue(args, kwargs))
+        ref = CompiledDAGRef(None, 0, self._multi)
+        ref._refs = out if self._multi else [out]
+        return ref
 
     def teardown(self):
         pass

@@ -1,7 +1,9 @@
-// pybind11 bindings of the native runtime: object store + cluster scheduler.
+// pybind11 bindings of the native runtime: object store, cluster scheduler,
+// compiled-graph shm channels.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "channel.h"
 #include "object_store.h"
 #include "scheduler.h"
 
@@ -103,4 +105,49 @@ PYBIND11_MODULE(_native, m) {
       .def("reserve_pg", &ClusterScheduler::reserve_pg)
       .def("remove_pg", &ClusterScheduler::remove_pg)
       .def("pg_feasible", &ClusterScheduler::pg_feasible);
+
+  // Channel: timeouts in seconds (< 0 = wait forever); waits release the GIL.
+  py::class_<Channel, std::shared_ptr<Channel>>(m, "Channel")
+      .def(py::init<const std::string&, bool, uint32_t, uint32_t, uint64_t>(), py::arg("name"),
+           py::arg("create") = false, py::arg("num_readers") = 1, py::arg("num_slots") = 2,
+           py::arg("slot_bytes") = 1 << 20)
+      .def("write",
+           [](Channel& c, py::buffer b, uint64_t flags, double timeout) {
+             py::buffer_info info = b.request();
+             int rc;
+             {
+               py::gil_scoped_release g;
+               rc = c.write(info.ptr, (uint64_t)(info.size * info.itemsize), flags, timeout);
+             }
+             if (rc == -1) throw py::value_error("timeout");  // mapped to TimeoutError in Python
+             if (rc == -2) throw py::stop_iteration("channel closed");
+             if (rc == -3) throw py::buffer_error("message larger than the channel slot");
+           },
+           py::arg("data"), py::arg("flags") = 0, py::arg("timeout") = -1.0)
+      .def("read",
+           [](Channel& c, uint32_t reader, double timeout) -> py::tuple {
+             const uint8_t* data;
+             uint64_t len, flags;
+             int rc;
+             {
+               py::gil_scoped_release g;
+               rc = c.begin_read(reader, &data, &len, &flags, timeout);
+             }
+             if (rc == -1) throw py::value_error("timeout");
+             if (rc == -2) throw py::stop_iteration("channel closed");
+             if (rc != 0) throw py::index_error("bad reader index");
+             py::bytes out((const char*)data, (size_t)len);
+             c.end_read(reader);
+             return py::make_tuple(out, flags);
+           },
+           py::arg("reader") = 0, py::arg("timeout") = -1.0)
+      .def("close", &Channel::close)
+      .def("unlink", &Channel::unlink)
+      .def_property_readonly("closed", &Channel::closed)
+      .def_property_readonly("num_readers", &Channel::num_readers)
+      .def_property_readonly("num_slots", &Channel::num_slots)
+      .def_property_readonly("slot_bytes", &Channel::slot_bytes)
+      .def_property_readonly("write_seq", &Channel::write_seq)
+      .def("read_seq", &Channel::read_seq)
+      .def_property_readonly("name", &Channel::name);
 }
