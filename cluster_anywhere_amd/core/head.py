@@ -118,6 +118,7 @@ class Head:
         self.node_id = node_id
         self.store_name = store_name
         self.store = _native.ObjectStore(store_name, store_capacity, 1 << 18, True)
+        self.store.prefault_async(int(os.environ.get("CAAMD_OBJECT_STORE_PREFAULT_BYTES", str(2 << 30))))
         self.sched = _native.ClusterScheduler(0.5)
         self.sched.add_node(node_id.hex(), resources)
         self.node_resources = {node_id.hex(): dict(resources)}

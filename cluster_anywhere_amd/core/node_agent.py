@@ -45,6 +45,7 @@ def main(argv=None):
     res.update({k: float(v) for k, v in json.loads(a.resources).items()})
     store_name = f"/caamd_node_{os.getpid()}_{uuid.uuid4().hex[:8]}"
     store = _native.ObjectStore(store_name, store_bytes, 1 << 18, True)
+    store.prefault_async(int(os.environ.get("CAAMD_OBJECT_STORE_PREFAULT_BYTES", str(2 << 30))))
     osrv = ObjectServer(store, a.node_ip_address)
     conn = connect(a.address)
     conn.send(("register", "node", os.urandom(16), os.getpid(), node_hex,

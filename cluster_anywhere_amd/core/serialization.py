@@ -63,7 +63,9 @@ class SerializedObject:
     def total_bytes(self) -> int:
         return self._size
 
-    def write_into(self, mv: memoryview) -> None:
+    def write_into(self, mv: memoryview, big_copy=None) -> None:
+        """``big_copy(offset, buffer)``, if given, copies buffers >= 8 MiB (the
+        native multi-threaded arena copy)."""
         nb = len(self.buffers)
         _HDR.pack_into(mv, 0, MAGIC, nb, len(self.pickled))
         off = _HDR.size
@@ -75,7 +77,11 @@ class SerializedObject:
         off += _pad(len(self.pickled))
         for b, n in zip(self.buffers, self._lens):
             if n:
-                mv[off : off + n] = b.cast("B") if b.format != "B" or b.ndim != 1 else b
+                src = b.cast("B") if b.format != "B" or b.ndim != 1 else b
+                if big_copy is not None and n >= (8 << 20):
+                    big_copy(off, src)
+                else:
+                    mv[off : off + n] = src
             off += _pad(n)
 
     def to_bytes(self) -> bytes:

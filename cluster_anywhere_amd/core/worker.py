@@ -30,6 +30,9 @@ from .object_ref import DynamicObjectRefGenerator, ObjectRef, ObjectRefGenerator
 from .protocol import ConnectionClosed, connect
 
 
+_COPY_THREADS = max(1, min(8, (os.cpu_count() or 1) // 2))
+
+
 class RefCounter:
     """Process-local counts; 0->1 borrow announcements and 1->0 releases are
     queued IN ORDER and flushed ahead of the next control message."""
@@ -38,6 +41,10 @@ class RefCounter:
         self.counts: Dict[bytes, int] = {}
         self.lock = threading.Lock()
         self.ops: List[tuple] = []
+        # resolved (kind, payload) of immutable objects this process holds refs
+        # to: ray.get of them needs no round trip to the head (the reference's
+        # in-process memory store for owned/inlined objects)
+        self.cache: Dict[bytes, tuple] = {}
 
     def add(self, oid: bytes, announce: bool):
         with self.lock:
@@ -53,6 +60,7 @@ class RefCounter:
                 return
             if c <= 1:
                 del self.counts[oid]
+                self.cache.pop(oid, None)
                 self.ops.append(("d", oid))
             else:
                 self.counts[oid] = c - 1
@@ -203,7 +211,8 @@ class CoreWorker:
             raise ObjectStoreFullError(
                 f"object of {size} bytes does not fit in the object store "
                 f"(capacity {self.store.capacity}, used {self.store.used})")
-        so.write_into(self.store.buffer(off, size, False))
+        so.write_into(self.store.buffer(off, size, False),
+                      lambda o, b: self.store.copy_in(off + o, b, _COPY_THREADS))
         self.store.seal(oid)
         return None, size, self.node_hex
 
@@ -214,7 +223,9 @@ class CoreWorker:
         oid = ObjectID.for_put(self.worker_id)
         inline, size, node = self._store(oid, so)
         self.send(("put", oid, inline, size, node, so.contained_refs, False))
-        return ObjectRef(oid, _owned=True)
+        ref = ObjectRef(oid, _owned=True)
+        self.refs.cache[bytes(oid)] = ("inline", inline) if inline is not None else ("store", None)
+        return ref
 
     def _materialize(self, oid, kind, payload):
         from ..exceptions import ObjectLostError
@@ -255,6 +266,9 @@ class CoreWorker:
             if not isinstance(r, ObjectRef):
                 raise TypeError(f"get() expects ObjectRefs, got {type(r).__name__}")
         ids = [r.binary() for r in refs]
+        out = self._get_cached(ids)
+        if out is not None:
+            return out[0] if single else out
         blocked = self._maybe_blocked(True)
         try:
             res = self.request(lambda req: ("get", req, ids, timeout))
@@ -263,8 +277,29 @@ class CoreWorker:
                 self._maybe_blocked(False)
         if res is None:
             raise GetTimeoutError(f"get() timed out after {timeout}s")
+        cache, counts = self.refs.cache, self.refs.counts
+        for (o, k, p) in res:
+            if k in ("inline", "store") and o in counts:
+                cache[o] = (k, p)
         out = [self._materialize(o, k, p) for (o, k, p) in res]
         return out[0] if single else out
+
+    def _get_cached(self, ids):
+        cache = self.refs.cache
+        ent = [cache.get(i) for i in ids]
+        if any(e is None for e in ent):
+            return None
+        out = []
+        for i, (k, p) in zip(ids, ent):
+            if k == "store":
+                pb = self.store.get_pinned(i)
+                if pb is None:  # spilled / evicted since: ask the head
+                    cache.pop(i, None)
+                    return None
+                out.append(serialization.deserialize(memoryview(pb)))
+            else:
+                out.append(serialization.deserialize(p))
+        return out
 
     def get_future(self, ref: ObjectRef) -> concurrent.futures.Future:
         out = concurrent.futures.Future()

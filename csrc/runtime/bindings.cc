@@ -81,6 +81,16 @@ PYBIND11_MODULE(_native, m) {
              for (auto& x : s.list_ids()) out.emplace_back(x);
              return out;
            })
+      .def("copy_in",
+           [](ObjectStore& s, uint64_t off, py::buffer b, int threads) {
+             py::buffer_info info = b.request();
+             const uint64_t n = (uint64_t)(info.size * info.itemsize);
+             if (off + n > s.map_size()) throw py::index_error("copy_in past the end of the arena");
+             py::gil_scoped_release g;
+             s.copy_in(off, info.ptr, n, threads);
+           },
+           py::arg("offset"), py::arg("data"), py::arg("threads") = 8)
+      .def("prefault_async", &ObjectStore::prefault_async)
       .def("largest_free", &ObjectStore::largest_free)
       .def("unlink", &ObjectStore::unlink)
       .def_property_readonly("capacity", &ObjectStore::capacity)

@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <stdexcept>
+#include <thread>
+#include <vector>
 
 namespace caamd_rt {
 
@@ -86,6 +88,8 @@ ObjectStore::ObjectStore(const std::string& name, uint64_t capacity, uint64_t ta
 }
 
 ObjectStore::~ObjectStore() {
+  stop_prefault_.store(true);
+  if (prefault_.joinable()) prefault_.join();  // never unmap under the prefault thread
   if (base_ && base_ != MAP_FAILED) munmap(base_, map_size_);
   if (fd_ >= 0) close(fd_);
 }
@@ -328,6 +332,47 @@ uint64_t ObjectStore::largest_free() {
   for (uint64_t f = hdr_->free_head; f; f = B(f)->next_free) m = std::max(m, B(f)->size);
   unlock();
   return m > sizeof(BlockHdr) ? m - sizeof(BlockHdr) : 0;
+}
+
+void ObjectStore::copy_in(uint64_t off, const void* src, uint64_t n, int threads) {
+  uint8_t* dst = base_ + off;
+  const uint8_t* s = (const uint8_t*)src;
+  const uint64_t kMinChunk = 16ull << 20;
+  int nt = (int)std::min<uint64_t>((uint64_t)std::max(threads, 1), (n + kMinChunk - 1) / kMinChunk);
+  if (nt <= 1) {
+    memcpy(dst, s, n);
+    return;
+  }
+  const uint64_t chunk = ((n + nt - 1) / nt + 4095) & ~4095ull;
+  std::vector<std::thread> ts;
+  for (int i = 0; i < nt; ++i) {
+    const uint64_t b = (uint64_t)i * chunk;
+    if (b >= n) break;
+    const uint64_t e = std::min(n, b + chunk);
+    ts.emplace_back([=] { memcpy(dst + b, s + b, e - b); });
+  }
+  for (auto& t : ts) t.join();
+}
+
+void ObjectStore::prefault_async(uint64_t max_bytes) {
+  uint8_t* lo = base_ + (map_size_ - std::min<uint64_t>(map_size_, capacity()));
+  const uint64_t n = std::min<uint64_t>(max_bytes, (uint64_t)(base_ + map_size_ - lo));
+  if (prefault_.joinable()) return;
+  prefault_ = std::thread([this, lo, n] {
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23
+#endif
+    const uint64_t step = 64ull << 20;
+    for (uint64_t o = 0; o < n && !stop_prefault_.load(std::memory_order_relaxed); o += step) {
+      const uint64_t len = std::min(step, n - o);
+      if (madvise(lo + o, len, MADV_POPULATE_WRITE) != 0 && errno == EINVAL) {
+        // older kernels: fault pages in by touching them (a read-modify-write of
+        // one byte per page keeps any data a concurrent put already wrote)
+        volatile uint8_t* p = lo + o;
+        for (uint64_t q = 0; q < len; q += 4096) __atomic_fetch_add(&p[q], 0, __ATOMIC_RELAXED);
+      }
+    }
+  });
 }
 
 }  // namespace caamd_rt

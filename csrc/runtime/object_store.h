@@ -14,7 +14,9 @@
 #include <pthread.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace caamd_rt {
@@ -74,6 +76,7 @@ class ObjectStore {
   bool abort(const std::string& id);   // remove an unsealed object
 
   uint64_t capacity() const { return hdr_->data_size; }
+  uint64_t map_size() const { return map_size_; }
   uint64_t used() const { return hdr_->used_bytes; }
   uint64_t num_objects() const { return hdr_->num_objects; }
   uint8_t* base() const { return base_; }
@@ -83,6 +86,13 @@ class ObjectStore {
   std::vector<std::string> list_ids();
   uint64_t largest_free();
   void unlink();
+  // Copy n bytes into the arena at `off` with up to `threads` threads (large
+  // puts: first-touch page faults of fresh shm pages cost ~1 GB/s on one core;
+  // spread over cores they scale, and faulted pages copy at memcpy speed).
+  void copy_in(uint64_t off, const void* src, uint64_t n, int threads);
+  // Touch (fault in) the first `max_bytes` of the data region in a detached
+  // background thread, so the first large puts do not pay page faults.
+  void prefault_async(uint64_t max_bytes);
 
  private:
   void lock();
@@ -100,6 +110,8 @@ class ObjectStore {
   uint64_t map_size_ = 0;
   Header* hdr_ = nullptr;
   ObjectEntry* table_ = nullptr;
+  std::thread prefault_;
+  std::atomic<bool> stop_prefault_{false};
 };
 
 }  // namespace caamd_rt
