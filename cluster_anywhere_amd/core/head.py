@@ -881,9 +881,17 @@ class Head:
             a = self.actors.get(spec.actor_id)
             if a is not None:
                 if error_kind:
+                    detail = ""
+                    for (_o, inline, _s, _n, _c, is_err) in results:
+                        if is_err and inline is not None:
+                            try:
+                                detail = str(serialization.deserialize(inline))
+                            except Exception:
+                                pass
                     a.state = "DEAD"
-                    a.death_cause = "creation task failed"
-                    self._fail_actor_queue(a, "ActorDiedError", "actor constructor raised")
+                    a.death_cause = "creation task failed" + (f": {detail}" if detail else "")
+                    self._fail_actor_queue(a, "ActorDiedError",
+                                           "actor constructor raised" + (f":\n{detail}" if detail else ""))
                     self._kill_worker(a.worker)
                 else:
                     a.state = "ALIVE"

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import io
 import pickle
+import types
 import struct
 import sys
 import threading
@@ -142,6 +143,11 @@ class _Pickler(pickle.Pickler):
         if isinstance(obj, ObjectRef):
             self._refs.append(obj.binary())
             return obj.__reduce__()
+        if isinstance(obj, (type, types.FunctionType)) and getattr(obj, "__module__", None) in (
+                "__main__", "__mp_main__"):
+            # by-reference pickling of a driver-script class/function cannot be
+            # resolved in a worker: fall back to cloudpickle (by value)
+            raise pickle.PicklingError("__main__ object")
         mod = type(obj).__module__
         if mod == "torch" and "torch" in sys.modules:
             import torch

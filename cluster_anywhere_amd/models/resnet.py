@@ -1,0 +1,276 @@
+"""ResNet family (18/34/50/101/152; v1.5: stride on the 3x3 conv of a bottleneck)
+for the Data GPU ``map_batches`` inference benchmark (BASELINE.json: "Ray Data
+streaming map_batches ResNet-50 inference, 8 GPU actors").
+
+Training form is an ordinary ``nn.Module`` (BatchNorm, fp32 or bf16).
+:meth:`ResNet.fuse_for_inference` produces the MI355X serving form:
+
+* every BatchNorm folded into the preceding convolution (weight scaled per output
+  channel, bias added) — one MIOpen conv kernel per conv, no BN kernels;
+* bf16 weights and activations in channels_last (NHWC), the layout MIOpen's
+  gfx950 convolution kernels consume natively — no layout transposes;
+* the bottleneck join ``relu(conv3(x) + identity)`` is one HIP kernel
+  (``ops.add_relu_``), in place;
+* input is uint8 NHWC straight from the object-store block, normalised by one
+  HIP kernel (``ops.image_normalize``) into bf16 channels_last.
+
+:class:`ResNetPredictor` wraps that in a fixed-batch HIP-graph replay (the whole
+forward is one graph launch; partial batches are padded), which is what the
+Data GPU actors run.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.vision import IMAGENET_MEAN, IMAGENET_STD, add_relu_, image_normalize
+
+
+def _conv(cin, cout, k, stride=1):
+    return nn.Conv2d(cin, cout, k, stride=stride, padding=k // 2, bias=False)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, width, stride=1):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1, self.bn1 = _conv(cin, width, 3, stride), nn.BatchNorm2d(width)
+        self.conv2, self.bn2 = _conv(width, cout, 3), nn.BatchNorm2d(cout)
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = nn.Sequential(_conv(cin, cout, 1, stride), nn.BatchNorm2d(cout))
+
+    def convs(self):
+        return [(self.conv1, self.bn1, True), (self.conv2, self.bn2, False)]
+
+    def forward(self, x):
+        idt = x if self.down is None else self.down(x)
+        y = F.relu(self.bn1(self.conv1(x)))
+        return F.relu(self.bn2(self.conv2(y)) + idt)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1, self.bn1 = _conv(cin, width, 1), nn.BatchNorm2d(width)
+        self.conv2, self.bn2 = _conv(width, width, 3, stride), nn.BatchNorm2d(width)
+        self.conv3, self.bn3 = _conv(width, cout, 1), nn.BatchNorm2d(cout)
+        self.down = None
+        if stride != 1 or cin != cout:
+            self.down = nn.Sequential(_conv(cin, cout, 1, stride), nn.BatchNorm2d(cout))
+
+    def convs(self):
+        return [(self.conv1, self.bn1, True), (self.conv2, self.bn2, True), (self.conv3, self.bn3, False)]
+
+    def forward(self, x):
+        idt = x if self.down is None else self.down(x)
+        y = F.relu(self.bn1(self.conv1(x)))
+        y = F.relu(self.bn2(self.conv2(y)))
+        return F.relu(self.bn3(self.conv3(y)) + idt)
+
+
+_CFG = {
+    "resnet18": (BasicBlock, [2, 2, 2, 2]),
+    "resnet34": (BasicBlock, [3, 4, 6, 3]),
+    "resnet50": (Bottleneck, [3, 4, 6, 3]),
+    "resnet101": (Bottleneck, [3, 4, 23, 3]),
+    "resnet152": (Bottleneck, [3, 8, 36, 3]),
+}
+
+
+class ResNet(nn.Module):
+    def __init__(self, name: str = "resnet50", num_classes: int = 1000):
+        super().__init__()
+        block, counts = _CFG[name]
+        self.name = name
+        self.conv1, self.bn1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False), nn.BatchNorm2d(64)
+        layers, cin = [], 64
+        for i, (n, w) in enumerate(zip(counts, (64, 128, 256, 512))):
+            for j in range(n):
+                blk = block(cin, w, stride=2 if (j == 0 and i > 0) else 1)
+                layers.append(blk)
+                cin = w * block.expansion
+        self.blocks = nn.ModuleList(layers)
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x):
+        x = F.max_pool2d(F.relu(self.bn1(self.conv1(x))), 3, 2, 1)
+        for b in self.blocks:
+            x = b(x)
+        return self.fc(torch.flatten(F.adaptive_avg_pool2d(x, 1), 1))
+
+    def flops_per_image(self, hw: int = 224) -> float:
+        """Forward FLOPs (2 x MACs) of the convolutions + fc at hw x hw input."""
+        return _analytic_flops(self, hw)
+
+    @torch.no_grad()
+    def fuse_for_inference(self, dtype=torch.bfloat16, device=None) -> "FusedResNet":
+        return FusedResNet(self, dtype, device)
+
+
+def _analytic_flops(net: ResNet, hw: int) -> float:
+    def conv_flops(c: nn.Conv2d, h_in: int):
+        h_out = (h_in + 2 * c.padding[0] - c.kernel_size[0]) // c.stride[0] + 1
+        return 2.0 * h_out * h_out * c.out_channels * c.in_channels * c.kernel_size[0] * c.kernel_size[1], h_out
+
+    tot, h = conv_flops(net.conv1, hw)
+    h = (h + 2 - 3) // 2 + 1  # maxpool 3x3 / 2
+    for b in net.blocks:
+        h_in = h
+        for conv, _, _ in b.convs():
+            f, h = conv_flops(conv, h)
+            tot += f
+        if b.down is not None:
+            tot += conv_flops(b.down[0], h_in)[0]
+    return tot + 2.0 * net.fc.in_features * net.fc.out_features
+
+
+def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, dtype, device):
+    w = conv.weight.detach().float()
+    scale = bn.weight.detach().float() / torch.sqrt(bn.running_var.detach().float() + bn.eps)
+    b = bn.bias.detach().float() - bn.running_mean.detach().float() * scale
+    w = w * scale.view(-1, 1, 1, 1)
+    w = w.to(device=device, dtype=dtype).contiguous(memory_format=torch.channels_last)
+    return w, b.to(device=device, dtype=dtype)
+
+
+class _FConv:
+    __slots__ = ("w", "b", "stride", "pad", "relu")
+
+    def __init__(self, conv, bn, relu, dtype, device):
+        self.w, self.b = _fold(conv, bn, dtype, device)
+        self.stride, self.pad, self.relu = conv.stride, conv.padding, relu
+
+    def __call__(self, x):
+        y = F.conv2d(x, self.w, self.b, self.stride, self.pad)
+        return F.relu_(y) if self.relu else y
+
+
+class FusedResNet(nn.Module):
+    """BN-folded bf16 channels_last inference form of a :class:`ResNet`."""
+
+    def __init__(self, net: ResNet, dtype, device):
+        super().__init__()
+        device = device or next(net.parameters()).device
+        self.dtype, self.device = dtype, torch.device(device)
+        self.stem = _FConv(net.conv1, net.bn1, True, dtype, device)
+        self.blocks: List[tuple] = []
+        for b in net.blocks:
+            convs = [_FConv(c, bn, r, dtype, device) for c, bn, r in b.convs()]
+            down = _FConv(b.down[0], b.down[1], False, dtype, device) if b.down is not None else None
+            self.blocks.append((convs, down))
+        self.fc_w = net.fc.weight.detach().to(device=device, dtype=dtype)
+        self.fc_b = net.fc.bias.detach().to(device=device, dtype=dtype)
+
+    @torch.no_grad()
+    def forward(self, x):
+        """x: normalised [N, 3, H, W] (channels_last, model dtype) -> logits [N, classes]."""
+        x = F.max_pool2d(self.stem(x), 3, 2, 1)
+        for convs, down in self.blocks:
+            idt = x if down is None else down(x)
+            y = x
+            for c in convs:
+                y = c(y)
+            x = add_relu_(y, idt)
+        x = x.mean(dim=(2, 3))
+        return F.linear(x, self.fc_w, self.fc_b)
+
+    @torch.no_grad()
+    def predict_uint8(self, images: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD):
+        """uint8 NHWC on this device -> logits."""
+        x = image_normalize(images, mean, std)
+        if x.dtype != self.dtype:
+            x = x.to(self.dtype)
+        return self.forward(x)
+
+
+def resnet(name: str = "resnet50", num_classes: int = 1000) -> ResNet:
+    return ResNet(name, num_classes)
+
+
+def resnet50(num_classes: int = 1000) -> ResNet:
+    return ResNet("resnet50", num_classes)
+
+
+class ResNetPredictor:
+    """Fixed-batch inference engine: uint8 NHWC host batch -> top-1 class ids.
+
+    On GPU the whole normalise + forward + argmax is captured once in a HIP
+    graph at ``batch_size`` and replayed per batch (partial batches are padded);
+    host→HBM copies go through a pinned staging buffer on a side stream so the
+    copy of batch i+1 overlaps the compute of batch i.
+    """
+
+    def __init__(self, name: str = "resnet50", batch_size: int = 256, hw: int = 224,
+                 device: Optional[str] = None, use_graph: bool = True, seed: int = 0):
+        torch.manual_seed(seed)
+        dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        self.device, self.bs, self.hw = dev, batch_size, hw
+        net = resnet(name).eval()
+        self.model = net.fuse_for_inference(torch.bfloat16 if dev.type == "cuda" else torch.float32, dev)
+        self.graph = None
+        if dev.type == "cuda":
+            self.copy_stream = torch.cuda.Stream(dev)
+            self.staging = [torch.empty((batch_size, hw, hw, 3), dtype=torch.uint8, pin_memory=True)
+                            for _ in range(2)]
+            self.static_in = torch.zeros((batch_size, hw, hw, 3), dtype=torch.uint8, device=dev)
+            self._flip = 0
+            if use_graph:
+                self._capture()
+
+    def _run(self, x_u8):
+        return self.model.predict_uint8(x_u8).argmax(dim=1)
+
+    def _capture(self):
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up MIOpen algorithm selection outside the graph
+                self._run(self.static_in)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.static_out = self._run(self.static_in)
+        torch.cuda.synchronize(self.device)
+
+    def __call__(self, images) -> "np.ndarray":  # noqa: F821
+        import numpy as np
+
+        arr = np.asarray(images)
+        n = arr.shape[0]
+        if self.device.type != "cuda":
+            x = torch.from_numpy(np.ascontiguousarray(arr))
+            return self._run(x).numpy()
+        out = []
+        for i in range(0, n, self.bs):
+            chunk = arr[i:i + self.bs]
+            m = chunk.shape[0]
+            st = self.staging[self._flip]
+            self._flip ^= 1
+            st[:m].copy_(torch.from_numpy(np.ascontiguousarray(chunk)))
+            with torch.cuda.stream(self.copy_stream):
+                self.copy_stream.wait_stream(torch.cuda.current_stream(self.device))
+                self.static_in[:m].copy_(st[:m], non_blocking=True)
+            torch.cuda.current_stream(self.device).wait_stream(self.copy_stream)
+            if self.graph is not None:
+                self.graph.replay()
+                res = self.static_out
+            else:
+                res = self._run(self.static_in)
+            out.append(res[:m].to("cpu", non_blocking=False).numpy())
+        return np.concatenate(out) if out else np.zeros((0,), dtype=np.int64)

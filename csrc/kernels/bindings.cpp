@@ -525,6 +525,47 @@ std::vector<Tensor> flash_attn_gqa(const Tensor& q, const Tensor& k, const Tenso
   return {out, lse};
 }
 
+// ---- vision (Data GPU map_batches / ResNet-50) ------------------------------
+namespace caamd {
+void image_normalize_launch(const uint8_t*, bf16*, int64_t, const float*, const float*, hipStream_t);
+void add_relu_launch(bf16*, const bf16*, int64_t, hipStream_t);
+}
+
+Tensor image_normalize(const Tensor& x, std::vector<double> mean, std::vector<double> std) {
+  CHECK_GPU(x);
+  CHECK_CONTIG(x);
+  CHECK_DT(x, at::kByte);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 3, "image_normalize: expects uint8 [N, H, W, 3]");
+  TORCH_CHECK(mean.size() == 3 && std.size() == 3, "image_normalize: 3 means / stds");
+  TORCH_CHECK(((uintptr_t)x.data_ptr()) % 16 == 0, "image_normalize: input must be 16-byte aligned");
+  // bf16 [N, 3, H, W] in channels_last = physically NHWC, the same element order as x
+  auto out = at::empty({x.size(0), 3, x.size(1), x.size(2)},
+                       x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+  float sc[3], bi[3];
+  for (int c = 0; c < 3; ++c) {
+    sc[c] = (float)(1.0 / (255.0 * std[c]));
+    bi[c] = (float)(-mean[c] / std[c]);
+  }
+  if (x.numel())
+    caamd::image_normalize_launch(x.data_ptr<uint8_t>(), bp(out), x.numel(), sc, bi, cur_stream());
+  LAUNCH_CHECK();
+  return out;
+}
+
+void add_relu_(Tensor& y, const Tensor& r) {
+  CHECK_GPU(y);
+  CHECK_GPU(r);
+  CHECK_DT(y, at::kBFloat16);
+  CHECK_DT(r, at::kBFloat16);
+  TORCH_CHECK(y.sizes() == r.sizes() && y.strides() == r.strides(), "add_relu_: shape/stride mismatch");
+  TORCH_CHECK(y.is_non_overlapping_and_dense(), "add_relu_: y must be dense");
+  TORCH_CHECK(y.numel() % 8 == 0, "add_relu_: numel must be a multiple of 8");
+  TORCH_CHECK(((uintptr_t)y.data_ptr()) % 16 == 0 && ((uintptr_t)r.data_ptr()) % 16 == 0,
+              "add_relu_: 16-byte alignment");
+  if (y.numel()) caamd::add_relu_launch(bp(y), bp(r), y.numel(), cur_stream());
+  LAUNCH_CHECK();
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cluster_anywhere_amd gfx950 HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
@@ -546,4 +587,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_cache_", &rope_cache_);
   m.def("paged_decode", &paged_decode);
   m.def("flash_attn_gqa", &flash_attn_gqa);
+  m.def("image_normalize", &image_normalize);
+  m.def("add_relu_", &add_relu_);
 }

@@ -1,0 +1,95 @@
+"""ResNet family + vision kernels (Data GPU map_batches path). CPU tests check the
+BN folding and the predictor; GPU tests compare the HIP kernels and the bf16
+channels_last HIP-graph forward against plain fp32 PyTorch references."""
+import numpy as np
+import pytest
+import torch
+
+from cluster_anywhere_amd.models.resnet import ResNetPredictor, resnet
+from cluster_anywhere_amd.ops.vision import add_relu_, image_normalize, image_normalize_ref
+
+
+def test_resnet50_shape_params_flops():
+    n = resnet("resnet50")
+    assert sum(p.numel() for p in n.parameters()) == 25_557_032
+    assert abs(n.flops_per_image(224) / 1e9 - 8.18) < 0.05
+    x = torch.randn(2, 3, 64, 64)
+    assert n.eval()(x).shape == (2, 1000)
+
+
+def test_bn_folding_matches_reference():
+    torch.manual_seed(0)
+    n = resnet("resnet18").eval()
+    # non-trivial running stats so the fold is exercised
+    for m in n.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.5, 0.5)
+            m.running_var.uniform_(0.5, 2.0)
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x = torch.randint(0, 256, (3, 64, 64, 3), dtype=torch.uint8)
+    f = n.fuse_for_inference(torch.float32, "cpu")
+    with torch.no_grad():
+        ref = n(image_normalize_ref(x).contiguous())
+        out = f.predict_uint8(x)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+
+
+def test_predictor_cpu_batches():
+    p = ResNetPredictor("resnet18", batch_size=4, hw=32, device="cpu")
+    imgs = np.random.randint(0, 256, (10, 32, 32, 3), dtype=np.uint8)
+    out = p(imgs)
+    assert out.shape == (10,) and out.dtype == np.int64
+    assert np.array_equal(out[:4], p(imgs[:4]))
+
+
+C = pytest.mark.gpu
+
+
+@C
+@pytest.mark.parametrize("n", [1, 7, 64])
+def test_image_normalize_gpu(n):
+    x = torch.randint(0, 256, (n, 224, 224, 3), dtype=torch.uint8, device="cuda")
+    out = image_normalize(x)
+    ref = image_normalize_ref(x.cpu(), dtype=torch.float32)
+    assert out.dtype == torch.bfloat16 and out.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(out.float().cpu(), ref, rtol=8e-3, atol=8e-3)
+
+
+@C
+def test_image_normalize_tail_gpu():
+    x = torch.randint(0, 256, (1, 5, 3, 3), dtype=torch.uint8, device="cuda")  # 45 bytes: tail only
+    torch.testing.assert_close(image_normalize(x).float().cpu(), image_normalize_ref(x.cpu()), rtol=8e-3, atol=8e-3)
+
+
+@C
+def test_add_relu_gpu():
+    y = torch.randn(4, 256, 14, 14, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    r = torch.randn_like(y)
+    ref = torch.relu(y.float() + r.float())
+    add_relu_(y, r)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+@C
+def test_fused_resnet50_gpu_matches_fp32():
+    torch.manual_seed(0)
+    n = resnet("resnet50").eval()
+    x = torch.randint(0, 256, (8, 224, 224, 3), dtype=torch.uint8)
+    with torch.no_grad():
+        ref = n(image_normalize_ref(x).contiguous())
+    f = n.fuse_for_inference(torch.bfloat16, "cuda")
+    out = f.predict_uint8(x.cuda()).float().cpu()
+    # bf16 through 53 layers: compare relative to the logit scale
+    err = (out - ref).abs().max() / ref.abs().max()
+    assert err < 0.05, float(err)
+
+
+@C
+def test_predictor_hip_graph_matches_eager():
+    imgs = np.random.randint(0, 256, (300, 224, 224, 3), dtype=np.uint8)
+    g = ResNetPredictor("resnet50", batch_size=128, use_graph=True)
+    e = ResNetPredictor("resnet50", batch_size=128, use_graph=False)
+    a, b = g(imgs), e(imgs)
+    assert a.shape == (300,)
+    assert (a == b).mean() > 0.98
