@@ -11,7 +11,7 @@ class DataContext:
     target_max_block_size: int = 128 * 1024 * 1024
     target_min_block_size: int = 1 * 1024 * 1024
     max_tasks_in_flight_per_op: int = int(os.environ.get("CAAMD_DATA_MAX_INFLIGHT", "0"))
-    actor_max_tasks_in_flight: int = 2
+    actor_max_tasks_in_flight: int = 4
     execution_preserve_order: bool = True
     enable_progress_bars: bool = False
     read_op_min_num_blocks: int = 8

@@ -36,3 +36,16 @@ def add_relu_(y: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
         kernels().add_relu_(y, r)
         return y
     return y.add_(r).relu_()
+
+
+def bias_act_(y: torch.Tensor, b: torch.Tensor, residual=None, relu: bool = True) -> torch.Tensor:
+    """In place: y = act(y + b[channel] (+ residual)), y channels_last [N, C, H, W]."""
+    if (y.is_cuda and y.dtype == torch.bfloat16 and y.dim() == 4 and y.size(1) % 8 == 0
+            and y.is_contiguous(memory_format=torch.channels_last)
+            and (residual is None or residual.stride() == y.stride())):
+        kernels().bias_act_(y, b, residual, relu)
+        return y
+    y.add_(b.view(1, -1, 1, 1))
+    if residual is not None:
+        y.add_(residual)
+    return y.relu_() if relu else y

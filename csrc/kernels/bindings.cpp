@@ -529,6 +529,27 @@ std::vector<Tensor> flash_attn_gqa(const Tensor& q, const Tensor& k, const Tenso
 namespace caamd {
 void image_normalize_launch(const uint8_t*, bf16*, int64_t, const float*, const float*, hipStream_t);
 void add_relu_launch(bf16*, const bf16*, int64_t, hipStream_t);
+void bias_act_launch(bf16*, const bf16*, const bf16*, int64_t, int, bool, hipStream_t);
+}
+
+// y: [N, C, H, W] bf16 in channels_last (physically NHWC), b: [C]; in place.
+void bias_act_(Tensor& y, const Tensor& b, const c10::optional<Tensor>& r, bool relu) {
+  CHECK_GPU(y);
+  CHECK_DT(y, at::kBFloat16);
+  CHECK_BF16(b);
+  TORCH_CHECK(y.dim() == 4 && y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bias_act_: y must be 4-D channels_last");
+  const int C = (int)y.size(1);
+  TORCH_CHECK(C % 8 == 0 && b.numel() == C, "bias_act_: C % 8 == 0 and bias of size C");
+  const caamd::bf16* rp = nullptr;
+  if (r.has_value()) {
+    CHECK_GPU(*r);
+    CHECK_DT(*r, at::kBFloat16);
+    TORCH_CHECK(r->sizes() == y.sizes() && r->strides() == y.strides(), "bias_act_: residual layout");
+    rp = bp(*r);
+  }
+  if (y.numel()) caamd::bias_act_launch(bp(y), bp(b), rp, y.numel(), C, relu, cur_stream());
+  LAUNCH_CHECK();
 }
 
 Tensor image_normalize(const Tensor& x, std::vector<double> mean, std::vector<double> std) {
@@ -589,4 +610,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("flash_attn_gqa", &flash_attn_gqa);
   m.def("image_normalize", &image_normalize);
   m.def("add_relu_", &add_relu_);
+  m.def("bias_act_", &bias_act_);
 }

@@ -78,11 +78,15 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(
   }
 }
 
-// Backward in ONE HBM pass: a wave owns TWO rows at a time (two independent
-// load -> cross-lane-reduction -> store chains hide each other's latency), keeps
-// both rows' x and dy as packed bf16 in VGPRs between the statistics and the dx
-// pass, and accumulates dgamma/dbeta of its columns in fp32 registers across
-// the rows it visits (merged per block with LDS atomics at the end).
+// Backward in ONE HBM pass. A wave owns one row per iteration (x / dy chunks
+// as packed bf16 in VGPRs between the statistics and the dx pass; dres loaded
+// after pass 1, its latency overlapping the cross-lane reduction) and
+// accumulates dgamma / dbeta of its columns in fp32 registers across all rows
+// it visits; the 4 waves of a block merge them with LDS float atomics ONCE at
+// the end (per-row LDS atomics from 4 waves on the same addresses serialize in
+// the LDS and cost ~0.5 ms per call at 32k x 1600). One fp32 partial row per
+// block, summed by colsum_bf16_kernel. ~170 VGPRs -> 2-3 waves per SIMD (the
+// earlier two-rows-per-wave variant needed 314 = 1 wave per SIMD).
 template <int NV, bool HAS_DRES>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ g,
@@ -93,84 +97,69 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nchunk = D >> 3;
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) red[i] = 0.f;
-  bf16x8 gv[NV];
   float dg[NV][8], db[NV][8];
 #pragma unroll
-  for (int c = 0; c < NV; ++c) {
-    const int ch = lane + c * 64;
-    if (ch < nchunk) gv[c] = *reinterpret_cast<const bf16x8*>(g + ch * 8);
+  for (int c = 0; c < NV; ++c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (ch >= nchunk) gv[c][j] = (bf16)0.f;
-      dg[c][j] = db[c][j] = 0.f;
-    }
-  }
+    for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
   const float inv_d = 1.f / (float)D;
   const int stride = gridDim.x * 4;
-  for (int r0 = blockIdx.x * 4 + wave; r0 < rows; r0 += 2 * stride) {
-    const int r1 = r0 + stride;
-    const bool v1 = r1 < rows;
-    const size_t b0 = (size_t)r0 * D, b1 = (size_t)(v1 ? r1 : r0) * D;
-    bf16x8 xa[NV], da[NV], xb[NV], dbb[NV];
+  for (int r = blockIdx.x * 4 + wave; r < rows; r += stride) {
+    const size_t base = (size_t)r * D;
+    bf16x8 xv[NV], dv[NV], rv[NV];
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int ch = lane + c * 64;
       if (ch < nchunk) {
-        xa[c] = *reinterpret_cast<const bf16x8*>(x + b0 + ch * 8);
-        da[c] = *reinterpret_cast<const bf16x8*>(dy + b0 + ch * 8);
-        xb[c] = *reinterpret_cast<const bf16x8*>(x + b1 + ch * 8);
-        dbb[c] = *reinterpret_cast<const bf16x8*>(dy + b1 + ch * 8);
+        xv[c] = *reinterpret_cast<const bf16x8*>(x + base + ch * 8);
+        dv[c] = *reinterpret_cast<const bf16x8*>(dy + base + ch * 8);
       }
     }
-    const float mua = mean[r0], rsa = rstd[r0];
-    const float mub = mean[v1 ? r1 : r0], rsb = rstd[v1 ? r1 : r0];
-    float s1a = 0.f, s2a = 0.f, s1b = 0.f, s2b = 0.f;
+    const float mu = mean[r], rs = rstd[r];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int ch = lane + c * 64;
       if (ch < nchunk) {
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + ch * 8);  // L1/L2-resident
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float gj = (float)gv[c][j];
-          const float dva = (float)da[c][j], xha = ((float)xa[c][j] - mua) * rsa;
-          const float dvb = v1 ? (float)dbb[c][j] : 0.f, xhb = ((float)xb[c][j] - mub) * rsb;
-          s1a += dva * gj;
-          s2a += dva * gj * xha;
-          s1b += dvb * gj;
-          s2b += dvb * gj * xhb;
-          dg[c][j] += dva * xha + dvb * xhb;
-          db[c][j] += dva + dvb;
+          const float d = (float)dv[c][j], xh = ((float)xv[c][j] - mu) * rs;
+          const float gd = d * (float)gv[j];
+          s1 += gd;
+          s2 += gd * xh;
+          dg[c][j] += d * xh;
+          db[c][j] += d;
         }
       }
     }
-    s1a = wave_sum(s1a);
-    s2a = wave_sum(s2a);
-    s1b = wave_sum(s1b);
-    s2b = wave_sum(s2b);
-    const float m1a = s1a * inv_d, m2a = s2a * inv_d, m1b = s1b * inv_d, m2b = s2b * inv_d;
+    if (HAS_DRES) {
+#pragma unroll
+      for (int c = 0; c < NV; ++c) {
+        const int ch = lane + c * 64;
+        if (ch < nchunk) rv[c] = *reinterpret_cast<const bf16x8*>(dres + base + ch * 8);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    const float m1 = s1 * inv_d, m2 = s2 * inv_d;
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
       const int ch = lane + c * 64;
       if (ch < nchunk) {
-        float oa[8], ob[8];
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + ch * 8);
+        bf16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float gj = (float)gv[c][j];
-          oa[j] = rsa * ((float)da[c][j] * gj - m1a - ((float)xa[c][j] - mua) * rsa * m2a);
-          ob[j] = rsb * ((float)dbb[c][j] * gj - m1b - ((float)xb[c][j] - mub) * rsb * m2b);
+          const float xh = ((float)xv[c][j] - mu) * rs;
+          float v = rs * ((float)dv[c][j] * (float)gv[j] - m1 - xh * m2);
+          if (HAS_DRES) v += (float)rv[c][j];
+          o[j] = (bf16)v;
         }
-        if (HAS_DRES) {
-          float ta[8], tb[8];
-          load8(dres + b0 + ch * 8, ta);
-          if (v1) load8(dres + b1 + ch * 8, tb);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            oa[j] += ta[j];
-            if (v1) ob[j] += tb[j];
-          }
-        }
-        store8(dx + b0 + ch * 8, oa);
-        if (v1) store8(dx + b1 + ch * 8, ob);
+        *reinterpret_cast<bf16x8*>(dx + base + ch * 8) = o;
       }
     }
   }
@@ -268,8 +257,9 @@ int ln_nv_for(int D) {
 }
 
 int ln_bwd_num_blocks(int rows) {
+  // 768 blocks = 3 per CU (the VGPR-limited residency), >= 8 rows per block
   int nb = (rows + 7) / 8;
-  return nb < 512 ? nb : 512;
+  return nb < 768 ? nb : 768;
 }
 
 void ln_fwd_launch(const bf16* x, const bf16* r, bf16* s, const bf16* g, const bf16* b, bf16* y,

@@ -74,4 +74,41 @@ void add_relu_launch(bf16* y, const bf16* r, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(add_relu_kernel, dim3(ew_grid(n8, 256)), dim3(256), 0, st, y, r, n8);
 }
 
+// Epilogue of a bias-free MIOpen convolution in NHWC: y = act(y + b[c] (+ r)).
+// Replaces MIOpen's separate bias kernel + torch's ReLU (+ the residual add):
+// one read-modify-write pass instead of three. C % 8 == 0, so every 8-element
+// chunk lies inside one pixel and its channels are c0 .. c0 + 7.
+template <bool RES, bool RELU>
+__global__ __launch_bounds__(256) void bias_act_kernel(bf16* __restrict__ y, const bf16* __restrict__ b,
+                                                       const bf16* __restrict__ r, int64_t n8, int C) {
+  const int c8 = C >> 3;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    bf16x8 a = reinterpret_cast<const bf16x8*>(y)[i];
+    const bf16x8 bb = reinterpret_cast<const bf16x8*>(b)[i % c8];
+    bf16x8 rr;
+    if (RES) rr = reinterpret_cast<const bf16x8*>(r)[i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = (float)a[j] + (float)bb[j];
+      if (RES) v += (float)rr[j];
+      if (RELU) v = fmaxf(v, 0.f);
+      a[j] = (bf16)v;
+    }
+    reinterpret_cast<bf16x8*>(y)[i] = a;
+  }
+}
+
+void bias_act_launch(bf16* y, const bf16* b, const bf16* r, int64_t n, int C, bool relu, hipStream_t st) {
+  const int64_t n8 = n / 8;
+  dim3 g(ew_grid(n8, 256)), blk(256);
+  if (r) {
+    if (relu) hipLaunchKernelGGL((bias_act_kernel<true, true>), g, blk, 0, st, y, b, r, n8, C);
+    else hipLaunchKernelGGL((bias_act_kernel<true, false>), g, blk, 0, st, y, b, r, n8, C);
+  } else {
+    if (relu) hipLaunchKernelGGL((bias_act_kernel<false, true>), g, blk, 0, st, y, b, r, n8, C);
+    else hipLaunchKernelGGL((bias_act_kernel<false, false>), g, blk, 0, st, y, b, r, n8, C);
+  }
+}
+
 }  // namespace caamd

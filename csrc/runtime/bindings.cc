@@ -94,6 +94,7 @@ PYBIND11_MODULE(_native, m) {
       .def("largest_free", &ObjectStore::largest_free)
       .def("unlink", &ObjectStore::unlink)
       .def_property_readonly("capacity", &ObjectStore::capacity)
+      .def_property_readonly("map_size", &ObjectStore::map_size)
       .def_property_readonly("used", &ObjectStore::used)
       .def_property_readonly("num_objects", &ObjectStore::num_objects)
       .def_property_readonly("name", &ObjectStore::name);

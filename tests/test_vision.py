@@ -93,3 +93,17 @@ def test_predictor_hip_graph_matches_eager():
     a, b = g(imgs), e(imgs)
     assert a.shape == (300,)
     assert (a == b).mean() > 0.98
+
+
+@C
+@pytest.mark.parametrize("res,relu", [(False, True), (False, False), (True, True)])
+def test_bias_act_gpu(res, relu):
+    from cluster_anywhere_amd.ops.vision import bias_act_
+
+    y = torch.randn(3, 64, 7, 9, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    b = torch.randn(64, device="cuda").to(torch.bfloat16)
+    r = torch.randn_like(y) if res else None
+    ref = y.float() + b.float().view(1, -1, 1, 1) + (r.float() if res else 0)
+    ref = ref.relu() if relu else ref
+    bias_act_(y, b, r, relu)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)

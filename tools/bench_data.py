@@ -70,7 +70,7 @@ def main():
         ds = data.range(n, override_num_blocks=max(1, min(blocks, n // args.batch_size or 1)))
         ds = ds.map_batches(make_images, batch_size=args.batch_size, fn_kwargs={"hw": args.hw})
         ds = ds.map_batches(ResNet50Actor, batch_size=args.batch_size, num_gpus=1 if gpu else 0,
-                            concurrency=max(1, args.gpus),
+                            concurrency=max(1, args.gpus), zero_copy_batch=True,
                             fn_constructor_kwargs={"model": args.model, "batch_size": args.batch_size,
                                                    "hw": args.hw})
         return ds
