@@ -31,6 +31,9 @@ from . import serialization
 from .ids import ObjectID
 from .protocol import Conn, ConnectionClosed
 
+# cap on retained lineage (reference: RAY_max_lineage_bytes); beyond it objects
+# created by further tasks are simply not recoverable
+LINEAGE_MAX_TASKS = int(os.environ.get("CAAMD_LINEAGE_MAX_TASKS", "200000"))
 INLINE_MAX = int(os.environ.get("CAAMD_INLINE_MAX", str(100 * 1024)))
 
 # task kinds
@@ -62,10 +65,11 @@ class TaskSpec:
 
 class ObjEntry:
     __slots__ = ("state", "inline", "size", "node", "refcount", "pins", "waiters", "contained",
-                 "is_error", "owner_task", "spilled_path", "gen_end", "lost")
+                 "is_error", "owner_task", "spilled_path", "gen_end", "lost", "lineage_refs")
 
     def __init__(self):
         self.state = PENDING
+        self.lineage_refs = 0
         self.inline = None
         self.size = 0
         self.node = None
@@ -177,6 +181,8 @@ class Head:
         self.objects: Dict[bytes, ObjEntry] = {}
         self.tasks: Dict[bytes, TaskSpec] = {}
         self.waiting_deps: Dict[bytes, Set[bytes]] = {}  # task -> unresolved object ids
+        self.lineage: Dict[bytes, TaskSpec] = {}  # finished tasks kept for object recovery
+        self.num_reconstructions = 0
         self.dep_index: Dict[bytes, List[bytes]] = collections.defaultdict(list)
         # ready tasks grouped by scheduling class (demand + strategy), like the
         # reference's per-SchedulingClass queues: a blocked class costs O(1) per pass
@@ -435,7 +441,12 @@ class Head:
             t = self.tasks.get(e.owner_task)
             if t is not None and t.state in ("pending", "running"):
                 return
-        del self.objects[oid]
+        if e.lineage_refs > 0:
+            # data goes, metadata stays: a retained downstream lineage may need to
+            # re-create this object (reference: lineage pinning, reference_count.cc)
+            e.state = FREED
+        else:
+            del self.objects[oid]
         aid = self.handle_objs.pop(oid, None)
         if aid is not None:
             self._on_handles_gone(aid)
@@ -460,6 +471,115 @@ class Head:
             if ce is not None:
                 ce.pins -= 1
                 self._maybe_free(r)
+        e.contained = ()
+        if e.state != FREED:
+            self._lineage_release_if_unused(e.owner_task)
+
+    # ------------------------------------------------- lineage reconstruction
+    # Reference: src/ray/core_worker/object_recovery_manager.cc (re-execute the task
+    # that created a lost object, recursively recovering lost arguments) and
+    # task_manager.cc:ResubmitTask (re-executions count against max_retries).
+    # Lineage of a finished NORMAL task is retained while any of its return objects
+    # still has an entry; arguments keep metadata-only entries (``lineage_refs``)
+    # so their own lineage survives even after their data was freed.
+    def _lineage_retain(self, spec):
+        if spec.kind != NORMAL or spec.generator is not None or spec.state != "finished":
+            return False
+        mr = spec.max_retries if spec.max_retries is not None else 3
+        if mr == 0 or (0 <= mr <= spec.attempt) or len(self.lineage) >= LINEAGE_MAX_TASKS:
+            return False
+        self.lineage[spec.task_id] = spec
+        for r in spec.arg_refs:
+            self._obj(r).lineage_refs += 1
+        return True
+
+    def _lineage_release_if_unused(self, tid):
+        spec = self.lineage.get(tid) if tid is not None else None
+        if spec is None or any(r in self.objects for r in spec.return_ids or ()):
+            return
+        del self.lineage[tid]
+        for r in spec.arg_refs:
+            e = self.objects.get(r)
+            if e is None:
+                continue
+            e.lineage_refs -= 1
+            if e.lineage_refs <= 0 and e.state == FREED:
+                del self.objects[r]
+                self._lineage_release_if_unused(e.owner_task)
+
+    def _reconstruct(self, oid, _seen=None) -> bool:
+        """Re-execute the task that created ``oid``; False if it cannot be recovered."""
+        e = self.objects.get(oid)
+        if e is None:
+            return False
+        tid = e.owner_task
+        live = self.tasks.get(tid) if tid is not None else None
+        if live is not None and live.state in ("pending", "running"):
+            return True  # already being (re)computed
+        spec = self.lineage.get(tid) if tid is not None else None
+        if spec is None:
+            return False
+        mr = spec.max_retries if spec.max_retries is not None else 3
+        if 0 <= mr <= spec.attempt:
+            return False
+        seen = _seen if _seen is not None else set()
+        if tid in seen:
+            return True
+        seen.add(tid)
+        # arguments whose data is gone are recovered first (recursively)
+        for r in spec.arg_refs:
+            ae = self.objects.get(r)
+            if ae is None:
+                return False
+            if ae.state == FREED or ae.lost:
+                if not self._reconstruct(r, seen):
+                    return False
+        del self.lineage[tid]
+        spec.attempt += 1
+        spec.state = "pending"
+        spec.node = spec.worker = spec.acquired = spec.gpu_ids = None
+        spec.cancelled = False
+        self.tasks[tid] = spec
+        for r in spec.arg_refs:
+            ae = self.objects[r]
+            ae.pins += 1
+            ae.lineage_refs -= 1
+        for r in spec.return_ids or ():
+            re_ = self.objects.get(r)
+            if re_ is None:
+                continue
+            if re_.state == READY and not re_.lost and (re_.inline is not None or re_.spilled_path):
+                continue  # this copy survived (inlined / spilled on the head)
+            for cr in re_.contained:
+                ce = self.objects.get(cr)
+                if ce is not None:
+                    ce.pins -= 1
+            re_.contained = ()
+            re_.state = PENDING
+            re_.lost = False
+            re_.inline = None
+            re_.node = None
+        self.events.append(("reconstruct", tid, spec.fn_name, time.time()))
+        self.num_reconstructions += 1
+        self._enqueue_when_ready(spec)
+        return True
+
+    def _h_report_lost(self, c, req, oid):
+        """A reader could not pull ``oid`` from its node (it died before the head noticed)."""
+        e = self.objects.get(oid)
+        if e is None:
+            self._reply(c, req, False)
+            return
+        if e.state == PENDING:
+            self._reply(c, req, True)
+            return
+        if e.inline is not None:
+            self._reply(c, req, True)
+            return
+        ok = self._reconstruct(oid)
+        if not ok:
+            e.lost = True
+        self._reply(c, req, ok)
 
     def _obj_payload(self, oid, node=None):
         e = self.objects.get(oid)
@@ -904,6 +1024,7 @@ class Head:
     def _task_cleanup(self, spec):
         if spec.kind == ACTOR_CREATE:
             return  # creation args stay pinned for restarts; released when the actor dies
+        retained = self._lineage_retain(spec)
         for r in list(spec.arg_refs) + list(spec.pinned_refs or ()):
             e = self.objects.get(r)
             if e is not None:
@@ -913,6 +1034,8 @@ class Head:
             self._maybe_free(oid)
         if spec.kind != ACTOR_CREATE:
             self.tasks.pop(spec.task_id, None)
+        if retained:
+            self._lineage_release_if_unused(spec.task_id)
 
     def _finish_worker(self, w, spec):
         if w is None or not w.alive or w.actor_id is not None:
@@ -1527,10 +1650,14 @@ class Head:
         if node_hex in self.node_info:
             self.node_info[node_hex]["Alive"] = False
         self.events.append(("node_removed", node_hex, time.time()))
-        # objects whose only copy lived there are lost
+        # objects whose only copy lived there are lost: re-execute their lineage
+        # where possible (reference: object_recovery_manager.cc RecoverObject)
         for oid, e in list(self.objects.items()):
-            if e.node == node_hex and e.inline is None and e.state == READY:
+            if e.node == node_hex and e.inline is None and e.state == READY and not e.spilled_path:
                 e.lost = True
+        for oid, e in list(self.objects.items()):
+            if e.lost and e.state == READY and e.refcount > 0:
+                self._reconstruct(oid)
         # workers of that node: their control connections drop on their own; fail
         # anything still attributed to them (e.g. they never connected)
         for w in list(self.workers.values()):

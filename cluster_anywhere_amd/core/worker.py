@@ -281,8 +281,30 @@ class CoreWorker:
         for (o, k, p) in res:
             if k in ("inline", "store") and o in counts:
                 cache[o] = (k, p)
-        out = [self._materialize(o, k, p) for (o, k, p) in res]
+        out = [self._materialize_or_recover(o, k, p, timeout) for (o, k, p) in res]
         return out[0] if single else out
+
+    def _materialize_or_recover(self, oid, kind, payload, timeout, attempts=3):
+        """Materialize; when the copy's node vanished, ask the head to re-execute the
+        object's lineage and wait for the new copy (reference: object recovery)."""
+        from ..exceptions import ObjectLostError
+
+        while True:
+            try:
+                return self._materialize(oid, kind, payload)
+            except ObjectLostError:
+                if kind not in ("remote", "err_remote", "lost") or attempts <= 0:
+                    raise
+                attempts -= 1
+                if not self.request(lambda req: ("report_lost", req, oid)):
+                    raise
+                self.refs.cache.pop(oid, None)
+                res = self.request(lambda req: ("get", req, [oid], timeout))
+                if res is None:
+                    from ..exceptions import GetTimeoutError
+
+                    raise GetTimeoutError(f"get() timed out after {timeout}s")
+                _o, kind, payload = res[0]
 
     def _get_cached(self, ids):
         cache = self.refs.cache

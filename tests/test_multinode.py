@@ -97,3 +97,42 @@ def test_node_death_detected(two_nodes):
     r = where.remote()
     ready, _ = ray.wait([r], timeout=1.0)
     assert not ready
+
+
+def _start_agent(addr):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    return subprocess.Popen([sys.executable, "-m", "cluster_anywhere_amd.core.node_agent", "--address", addr,
+                             "--num-cpus", "2", "--num-gpus", "0", "--resources", '{"remote": 4}',
+                             "--object-store-memory", str(256 << 20)], env=env)
+
+
+@ray.remote(resources={"remote": 1})
+def plus_one(arr):
+    return arr + 1
+
+
+def test_lineage_reconstruction_after_node_death(two_nodes):
+    """Objects whose only copy lived on a dead node are re-created by re-executing
+    their lineage, including a lost intermediate argument whose own ref was dropped
+    (reference: object_recovery_manager.cc, test_reconstruction*.py)."""
+    me = ray.get_runtime_context().get_node_id()
+    a = make_big.remote(1_000_000)            # 8 MB, lives in the remote node's store
+    b = plus_one.remote(a)
+    c = make_big.options(max_retries=0).remote(1_000_000)  # not recoverable
+    ray.wait([b, c], num_returns=2, timeout=60)
+    del a                                      # only b's lineage references a now
+    assert ray.get(where.remote())[0] != me
+    two_nodes.kill()
+    two_nodes.wait()
+    deadline = time.time() + 30
+    while time.time() < deadline and sum(n["Alive"] for n in ray.nodes()) > 1:
+        time.sleep(0.1)
+    agent2 = _start_agent(ray.get_runtime_context().gcs_address)
+    try:
+        out = ray.get(b, timeout=90)
+        assert out.shape == (1_000_000,) and out[0] == 1 and out[-1] == 1_000_000
+        with pytest.raises(ray.exceptions.ObjectLostError):
+            ray.get(c, timeout=30)
+    finally:
+        agent2.kill()
+        agent2.wait()
