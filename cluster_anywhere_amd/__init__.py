@@ -51,7 +51,7 @@ from .runtime_context import get_runtime_context  # noqa: E402
 
 _LAZY = {"train", "data", "tune", "serve", "rllib", "dag", "ops", "models", "parallel", "util",
          "air", "autoscaler", "dashboard", "job_submission", "workflow", "experimental", "llm",
-         "cluster_utils", "scripts"}
+         "cluster_utils", "scripts", "runtime_env", "job_config", "client_builder"}
 
 
 def __getattr__(name):
@@ -59,6 +59,14 @@ def __getattr__(name):
         mod = _importlib.import_module(f".{name}", __name__)
         globals()[name] = mod
         return mod
+    if name == "JobConfig":
+        from .job_config import JobConfig
+
+        return JobConfig
+    if name == "client":
+        from .client_builder import client
+
+        return client
     raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
 
 

@@ -127,7 +127,16 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
             _session.clear()
             _session.update({"node_id": "local", "address": "local"})
             return RayContext(dict(_session))
+        if job_config is not None:
+            runtime_env = runtime_env or (job_config.runtime_env or None)
+            namespace = namespace or job_config.ray_namespace
+        if runtime_env:
+            _check_runtime_env(runtime_env)
         address = address or os.environ.get("CAAMD_ADDRESS") or os.environ.get("RAY_ADDRESS")
+        if address and address.startswith("ray://"):
+            from ..client_builder import connect
+
+            return RayContext(connect(address, namespace=namespace, runtime_env=runtime_env))
         if address == "local":
             address = None
         from .worker import CoreWorker
@@ -197,6 +206,27 @@ def _mem_bytes():
         return psutil.virtual_memory().total
     except Exception:
         return 16 << 30
+
+
+def _check_runtime_env(renv):
+    """Validate a runtime_env; ``pip``/``conda``/``uv`` packages must already be
+    importable (no package index on the pods — see runtime_env/__init__.py)."""
+    from ..exceptions import RuntimeEnvSetupError
+    from ..runtime_env import RuntimeEnv, missing_packages
+
+    RuntimeEnv(**dict(renv))
+    for key in ("pip", "uv", "conda"):
+        spec = renv.get(key)
+        if spec is None:
+            continue
+        if key == "conda":
+            spec = [d for d in (spec.get("dependencies", []) if isinstance(spec, dict) else [])
+                    if isinstance(d, str) and not d.startswith("python")]
+        miss = missing_packages(spec)
+        if miss:
+            raise RuntimeEnvSetupError(
+                f"runtime_env {key} packages {miss} are not installed in this image and "
+                "cannot be fetched (no package index available)")
 
 
 def _worker_env_from(renv):

@@ -58,6 +58,10 @@ def validate(opts: Dict[str, Any], defaults: Dict[str, Any], what: str) -> Dict[
         v = out.get(k)
         if v is not None and (not isinstance(v, (int, float)) or v < 0):
             raise ValueError(f"{k} must be a non-negative number, got {v!r}")
+    if out.get("runtime_env"):
+        from .api import _check_runtime_env
+
+        _check_runtime_env(out["runtime_env"])
     nr = out.get("num_returns")
     if nr is not None and not (nr in ("streaming", "dynamic") or (isinstance(nr, int) and nr >= 0)):
         raise ValueError(f"num_returns must be a non-negative int, 'streaming' or 'dynamic', got {nr!r}")

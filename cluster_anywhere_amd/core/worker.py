@@ -109,13 +109,16 @@ class CoreWorker:
         self.node_hex = info["node_id"]
         self.namespace = info["namespace"]
         self.session_dir = info["session_dir"]
-        from .. import _native
-
-        self.store = _native.ObjectStore(info["store_name"], 0, 0, False)
+        self.store = self._attach_store(info["store_name"])
         self._reader = threading.Thread(target=self._read_loop, name="caamd-reader", daemon=True)
         self._reader.start()
         self._flusher = threading.Thread(target=self._flush_loop, name="caamd-flush", daemon=True)
         self._flusher.start()
+
+    def _attach_store(self, store_name):
+        from .. import _native
+
+        return _native.ObjectStore(store_name, 0, 0, False)
 
     # ------------------------------------------------------------- transport
     def send(self, msg):
