@@ -34,6 +34,9 @@ class RemoteFunction:
     def options(self, **kw) -> "RemoteFunction":
         rf = RemoteFunction.__new__(RemoteFunction)
         rf.__dict__.update(self.__dict__)
+        wf = kw.pop("_workflow_options", None)  # workflow.options(...) (workflow/api.py)
+        if wf is not None:
+            rf._workflow_opts = dict(getattr(self, "_workflow_opts", {}) or {}, **wf)
         merged = dict(self._options)
         merged.update(kw)
         rf._options = opt_utils.validate(merged, opt_utils.TASK_DEFAULTS, "remote function")

@@ -39,3 +39,9 @@ __all__ = [
     "NodeAffinitySchedulingStrategy", "NodeLabelSchedulingStrategy", "get_node_ip_address",
     "list_named_actors",
 ]
+
+
+def inspect_serializability(*a, **k):
+    from .check_serialize import inspect_serializability as _i
+
+    return _i(*a, **k)
