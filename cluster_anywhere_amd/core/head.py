@@ -127,6 +127,7 @@ class Head:
         self.sched.add_node(node_id.hex(), resources)
         self.node_resources = {node_id.hex(): dict(resources)}
         self.free_gpus = {node_id.hex(): list(gpu_ids)}
+        self.gpu_partial: Dict[str, Dict[int, float]] = {}  # node -> gpu id -> fraction in use
         self.node_info = {node_id.hex(): {"NodeID": node_id.hex(), "Alive": True,
                                           "NodeManagerAddress": "127.0.0.1",
                                           "Resources": dict(resources), "local": True}}
@@ -837,19 +838,14 @@ class Head:
             return True  # parked
         if node == "":
             return False
-        ngpu = int(round(spec.resources.get("GPU", 0)))
-        gpu_ids = ()
-        if ngpu > 0:
-            free = self.free_gpus.get(node, [])
-            if len(free) < ngpu:
-                return False
-            gpu_ids = tuple(free[:ngpu])
+        gamt = float(spec.resources.get("GPU", 0) or 0)
+        gpu_ids = self._pick_gpus(node, gamt)
+        if gpu_ids is None:
+            return False
         if spec.kind == ACTOR_CREATE:
             if not self.sched.acquire(node, demand):
                 return False
-            if gpu_ids:
-                for g in gpu_ids:
-                    self.free_gpus[node].remove(g)
+            self._take_gpus(node, gpu_ids, gamt)
             spec.acquired = (node, demand)
             spec.gpu_ids = gpu_ids
             a = self.actors[spec.actor_id]
@@ -874,13 +870,57 @@ class Head:
             w.idle = True
             self.idle[key].append(w)
             return False
-        if gpu_ids:
-            for g in gpu_ids:
-                self.free_gpus[node].remove(g)
+        self._take_gpus(node, gpu_ids, gamt)
         spec.acquired = (node, demand)
         spec.gpu_ids = gpu_ids
         self._dispatch_to(w, spec)
         return True
+
+    # GPU ids: whole GPUs for num_gpus >= 1; fractions pack onto one GPU (the
+    # fullest one that still fits), so e.g. two num_gpus=0.5 actors share a device
+    def _pick_gpus(self, node, amount):
+        if amount <= 0:
+            return ()
+        free = self.free_gpus.get(node, [])
+        if amount >= 1 - 1e-9:
+            n = int(round(amount))
+            return tuple(free[:n]) if len(free) >= n else None
+        part = self.gpu_partial.setdefault(node, {})
+        best = None
+        for g, used in part.items():
+            if used + amount <= 1 + 1e-9 and (best is None or used > part[best]):
+                best = g
+        if best is not None:
+            return (best,)
+        return (free[0],) if free else None
+
+    def _take_gpus(self, node, gids, amount):
+        if not gids:
+            return
+        if amount >= 1 - 1e-9:
+            for g in gids:
+                self.free_gpus[node].remove(g)
+            return
+        g = gids[0]
+        part = self.gpu_partial.setdefault(node, {})
+        if g not in part:
+            self.free_gpus[node].remove(g)
+            part[g] = 0.0
+        part[g] += amount
+
+    def _give_gpus(self, node, gids, amount):
+        if not gids:
+            return
+        if amount >= 1 - 1e-9:
+            self.free_gpus.setdefault(node, []).extend(gids)
+            return
+        part = self.gpu_partial.get(node, {})
+        g = gids[0]
+        if g in part:
+            part[g] -= amount
+            if part[g] <= 1e-9:
+                del part[g]
+                self.free_gpus.setdefault(node, []).append(g)
 
     def _num_workers(self, node):
         return sum(1 for w in self.workers.values() if w.node == node and w.alive) + sum(
@@ -1048,8 +1088,7 @@ class Head:
         if spec.acquired and spec.kind != ACTOR_CREATE:
             node, demand = spec.acquired
             self.sched.release(node, demand)
-            for g in spec.gpu_ids or ():
-                self.free_gpus[node].append(g)
+            self._give_gpus(node, spec.gpu_ids or (), float(spec.resources.get("GPU", 0) or 0))
             spec.acquired = None
             self._retry_pending_pgs()
             self._retry_infeasible()
@@ -1249,8 +1288,7 @@ class Head:
             node, demand = a.acquired
             if a.restarts_left == 0 or a.restarts_left is None:
                 self.sched.release(node, demand)
-                for g in a.gpu_ids or ():
-                    self.free_gpus[node].append(g)
+                self._give_gpus(node, a.gpu_ids or (), float(a.spec.resources.get("GPU", 0) or 0))
                 a.acquired = None
         if a.restarts_left and a.restarts_left != 0 and a.state != "DEAD":
             if a.restarts_left > 0:

@@ -23,6 +23,10 @@ from typing import Any, Callable, Dict, Iterator, List, Optional, Tuple
 from . import block as B
 from .context import DataContext
 
+import os as _os
+
+_PROFILE = _os.environ.get("CAAMD_DATA_PROFILE") == "1"
+
 
 # ------------------------------------------------------------------ remote work
 def _apply_chain(block, chain):
@@ -71,6 +75,28 @@ class _MapWorker:
         self.fn = make_fn(self.udf)
 
     def process(self, block):
+        if _PROFILE:
+            return self._process_profiled(block)
+        return self._process(block)
+
+    def _process_profiled(self, block):
+        import sys
+
+        t0 = time.perf_counter()
+        st = self.__dict__.setdefault("_st", {"gap": 0.0, "body": 0.0, "n": 0, "last": None})
+        if st["last"] is not None:
+            st["gap"] += t0 - st["last"]
+        r = self._process(block)
+        t1 = time.perf_counter()
+        st["body"] += t1 - t0
+        st["n"] += 1
+        st["last"] = t1
+        if st["n"] % 20 == 0:
+            print(f"[MapWorker] {st['n']} blocks: {st['body'] / st['n'] * 1e3:.1f} ms in process, "
+                  f"{st['gap'] / (st['n'] - 1) * 1e3:.1f} ms between calls", file=sys.stderr, flush=True)
+        return r
+
+    def _process(self, block):
         out = []
         for b in _apply_chain(block, self.chain_before):
             for r in self.fn(b):

@@ -21,6 +21,10 @@ Data GPU actors run.
 """
 from __future__ import annotations
 
+import os
+import sys
+import time
+
 from typing import List, Optional, Sequence
 
 import torch
@@ -222,6 +226,8 @@ class ResNetPredictor:
         torch.manual_seed(seed)
         dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         self.device, self.bs, self.hw = dev, batch_size, hw
+        self._stats = ({"calls": 0, "ms": 0.0, "pinned": 0, "staged": 0}
+                       if os.environ.get("CAAMD_PREDICTOR_STATS") == "1" else None)
         net = resnet(name).eval()
         self.model = net.fuse_for_inference(torch.bfloat16 if dev.type == "cuda" else torch.float32, dev)
         self.graph = None
@@ -264,12 +270,17 @@ class ResNetPredictor:
             x = torch.from_numpy(np.ascontiguousarray(arr))
             return self._run(x).numpy()
         out = []
+        st = self._stats
+        t0 = time.perf_counter()
         for i in range(0, n, self.bs):
             chunk = arr[i:i + self.bs]
             m = chunk.shape[0]
             from ..core.hip_pinning import arena_contains
 
-            if chunk.flags["C_CONTIGUOUS"] and arena_contains(chunk):
+            pinned = chunk.flags["C_CONTIGUOUS"] and arena_contains(chunk)
+            if st is not None:
+                st["pinned" if pinned else "staged"] += 1
+            if pinned:
                 import warnings
 
                 with warnings.catch_warnings():  # read-only shm view; only ever read
@@ -289,4 +300,10 @@ class ResNetPredictor:
             else:
                 res = self._run(self.static_in)
             out.append(res[:m].to("cpu", non_blocking=False).numpy())
+        if st is not None:
+            st["calls"] += 1
+            st["ms"] += (time.perf_counter() - t0) * 1e3
+            if st["calls"] % 32 == 0:
+                print(f"[ResNetPredictor] {st['calls']} calls, {st['ms'] / st['calls']:.2f} ms/call, "
+                      f"pinned {st['pinned']} staged {st['staged']}", file=sys.stderr, flush=True)
         return np.concatenate(out) if out else np.zeros((0,), dtype=np.int64)

@@ -438,3 +438,38 @@ def test_local_mode():
         assert ray.get(A.remote().f.remote()) == 7
     finally:
         ray.shutdown()
+
+
+def test_fractional_gpu_packing():
+    """num_gpus=0.5 actors pack two per device; whole-GPU work waits for a free one
+    (reference: fractional GPU resources, accelerators/amd_gpu.py)."""
+    import cluster_anywhere_amd as ray
+
+    ray.init(num_cpus=8, num_gpus=2)
+    try:
+        @ray.remote(num_gpus=0.5, num_cpus=0)
+        class Half:
+            def ids(self):
+                import os
+
+                return tuple(int(x) for x in os.environ["CAAMD_GPU_IDS"].split(","))  # physical ids
+
+        @ray.remote(num_gpus=1, num_cpus=0)
+        def whole():
+            import os
+
+            return tuple(int(x) for x in os.environ["CAAMD_GPU_IDS"].split(","))
+
+        hs = [Half.remote() for _ in range(2)]
+        ids = ray.get([h.ids.remote() for h in hs])
+        assert all(len(i) == 1 for i in ids)
+        from collections import Counter
+
+        c = Counter(i[0] for i in ids)
+        assert max(c.values()) == 2                      # packed, not spread
+        w = ray.get(whole.remote(), timeout=30)          # the other GPU is still whole
+        assert len(w) == 1 and w[0] not in c
+        ready, _ = ray.wait([Half.remote().ids.remote()], timeout=30)
+        assert ready
+    finally:
+        ray.shutdown()

@@ -50,12 +50,16 @@ class ResNet50Actor:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--rows", type=int, default=200000)
+    ap.add_argument("--rows", type=int, default=204800)
     ap.add_argument("--batch-size", type=int, default=512)
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--hw", type=int, default=224)
     ap.add_argument("--read-blocks", type=int, default=0)
     ap.add_argument("--cpus", type=int, default=0)
+    ap.add_argument("--actors-per-gpu", type=int, default=2,
+                    help=">1 shares each GPU between actors (fractional num_gpus) so one's H2D "
+                         "copy / host work overlaps another's graph replay")
+    ap.add_argument("--timeline", default="", help="write a chrome trace + per-function summary here")
     args = ap.parse_args()
     import torch
 
@@ -66,13 +70,18 @@ def main():
     ncpu = args.cpus or min(os.cpu_count() or 8, 16 * max(1, args.gpus))
     ray.init(num_cpus=ncpu, num_gpus=args.gpus if gpu else 0,
              object_store_memory=min(64 << 30, max(4 << 30, args.batch_size * args.hw * args.hw * 3 * 64)))
-    blocks = args.read_blocks or max(8, args.rows // args.batch_size)
+    # whole batches per block: a block of batch_size+1 rows would cost the actor a
+    # second (padded) graph replay for its 1-row remainder
+    per = args.batch_size * max(1, args.gpus)
+    args.rows = max(per, (args.rows // per) * per)
+    blocks = args.read_blocks or max(1, args.rows // args.batch_size)
 
     def pipeline(n):
         ds = data.range(n, override_num_blocks=max(1, min(blocks, n // args.batch_size or 1)))
         ds = ds.map_batches(make_images, batch_size=args.batch_size, fn_kwargs={"hw": args.hw})
-        ds = ds.map_batches(ResNet50Actor, batch_size=args.batch_size, num_gpus=1 if gpu else 0,
-                            concurrency=max(1, args.gpus), zero_copy_batch=True,
+        apg = max(1, args.actors_per_gpu)
+        ds = ds.map_batches(ResNet50Actor, batch_size=args.batch_size, num_gpus=(1.0 / apg) if gpu else 0,
+                            concurrency=max(1, args.gpus) * apg, zero_copy_batch=True,
                             fn_constructor_kwargs={"model": args.model, "batch_size": args.batch_size,
                                                    "hw": args.hw})
         return ds
@@ -100,11 +109,23 @@ def main():
         "seconds": round(dt, 3), "higher_is_better": True, "scaling": "strong",
         "dtype": "bf16" if gpu else "fp32", "data": "synthetic uint8 224x224x3 images, random-init weights",
         "config": {"model": args.model, "batch_size": args.batch_size, "hw": args.hw, "read_blocks": blocks,
-                   "actors": args.gpus, "cpus": ncpu},
+                   "actors": args.gpus * max(1, args.actors_per_gpu), "cpus": ncpu},
         "model_tflops_per_gpu": round(rps * gflop / 1e3 / max(1, args.gpus), 1),
         "time_to_first_batch_s": round(t_first - t0, 3),
         "steady_state_rows_per_s": round((n - n_first) / max(1e-9, t_end - t_first), 1),
     }), flush=True)
+    if args.timeline:
+        ev = ray.timeline()
+        with open(args.timeline, "w") as f:
+            json.dump(ev, f)
+        agg = {}
+        for e in ev:
+            if e.get("ph") == "X":
+                a = agg.setdefault(e.get("name", "?"), [0, 0.0])
+                a[0] += 1
+                a[1] += e.get("dur", 0) / 1e3
+        for k, (c, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+            print(f"timeline {k}: {c} calls, {ms:.0f} ms total, {ms / max(c, 1):.1f} ms avg", flush=True)
     ray.shutdown()
 
 
