@@ -191,12 +191,21 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                                                              _head.tcp_address else address)})
         if runtime_env:
             _session["runtime_env"] = runtime_env
+        global _log_monitor
+        if log_to_driver and cw.session_dir and os.path.isdir(cw.session_dir) and \
+                os.environ.get("CAAMD_LOG_TO_DRIVER", "1") != "0":
+            from .log_monitor import LogMonitor
+
+            _log_monitor = LogMonitor(cw.session_dir).start()
         if include_dashboard:
             from ..dashboard import start_dashboard
 
             _session["webui_url"] = start_dashboard(dashboard_host, 8265 if dashboard_port is None else dashboard_port,
                                                     head=_head, control_address=address)
         return RayContext(dict(_session))
+
+
+_log_monitor = None
 
 
 def _mem_bytes():
@@ -251,6 +260,13 @@ def shutdown(_exiting_interpreter: bool = False):
             from .local_mode import reset_local
 
             reset_local()
+        global _log_monitor
+        if _log_monitor is not None:
+            try:
+                _log_monitor.stop()
+            except Exception:
+                pass
+            _log_monitor = None
         w = context.worker
         context.worker = None
         if w is not None:

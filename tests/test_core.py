@@ -473,3 +473,30 @@ def test_fractional_gpu_packing():
         assert ready
     finally:
         ray.shutdown()
+
+
+def test_worker_output_streams_to_driver(capsys):
+    """print() inside tasks shows up on the driver (reference: log_to_driver)."""
+    import time
+
+    import cluster_anywhere_amd as ray
+
+    ray.init(num_cpus=2)
+    try:
+        @ray.remote
+        def chatty(i):
+            print(f"hello-from-task-{i}", flush=True)
+            return i
+
+        assert ray.get([chatty.remote(i) for i in range(3)]) == [0, 1, 2]
+        deadline = time.time() + 10
+        seen = ""
+        while time.time() < deadline:
+            seen += capsys.readouterr().out
+            if all(f"hello-from-task-{i}" in seen for i in range(3)):
+                break
+            time.sleep(0.1)
+        assert all(f"hello-from-task-{i}" in seen for i in range(3)), seen
+        assert "(pid=" in seen
+    finally:
+        ray.shutdown()
