@@ -1,12 +1,13 @@
 """RL algorithms (reference: rllib/algorithms/)."""
 from .algorithm import Algorithm, AlgorithmConfig
+from .cql import CQL, CQLConfig
 from .dqn import DQN, DQNConfig
 from .impala import APPO, APPOConfig, IMPALA, IMPALAConfig
 from .marwil import BC, BCConfig, MARWIL, MARWILConfig
 from .ppo import PPO, PPOConfig
 from .sac import SAC, SACConfig
 
-ALGORITHMS = {"PPO": PPO, "APPO": APPO, "IMPALA": IMPALA, "DQN": DQN, "SAC": SAC, "BC": BC, "MARWIL": MARWIL}
+ALGORITHMS = {"PPO": PPO, "APPO": APPO, "IMPALA": IMPALA, "DQN": DQN, "SAC": SAC, "BC": BC, "MARWIL": MARWIL, "CQL": CQL}
 
 
 def get_algorithm_class(name: str):

@@ -182,3 +182,39 @@ def test_tune_over_ppo(tmp_path):
         assert all(r.metrics["training_iteration"] == 2 for r in grid)
     finally:
         ray.shutdown()
+
+
+def test_cql_offline_pendulum(tmp_path):
+    """CQL on a fixed Pendulum dataset (reference: rllib/algorithms/cql/tests)."""
+    from cluster_anywhere_amd.rllib.env import make_env
+
+    env = make_env("Pendulum-v1")
+    rng = np.random.default_rng(0)
+    cols = {k: [] for k in ("obs", "actions", "rewards", "next_obs", "terminateds")}
+    o, _ = env.reset(seed=0)
+    for t in range(2000):
+        a = np.clip(-2.0 * o[2:3] + 0.3 * rng.standard_normal(1), -2, 2).astype(np.float32)
+        o2, r, te, tr, _ = env.step(a)
+        for k, v in zip(cols, (o, a, r, o2, te)):
+            cols[k].append(v)
+        o = o2
+        if te or tr:
+            o, _ = env.reset()
+    data = {k: np.asarray(v) for k, v in cols.items()}
+    cfg = (rllib.CQLConfig().environment("Pendulum-v1").offline_data(input_=data)
+           .training(train_batch_size=128, bc_iters=20, num_actions=4,
+                     model={"policy_hiddens": [32, 32], "q_hiddens": [32, 32]}).debugging(seed=0))
+    algo = cfg.build()
+    for _ in range(40):
+        r = algo.train()
+    st = r["learners"]["default_policy"]
+    assert math.isfinite(st["qf_loss"]) and math.isfinite(st["cql_loss"])
+    path = algo.save_to_path(str(tmp_path / "cql"))
+    algo2 = rllib.Algorithm.from_checkpoint(path)
+    obs = np.array([1.0, 0.0, 0.0], dtype=np.float32)
+    assert np.allclose(algo.compute_single_action(obs), algo2.compute_single_action(obs), atol=1e-6)
+    cfg_l = cfg.copy() if hasattr(cfg, "copy") else cfg
+    cfg_l.lagrangian = True
+    algo3 = cfg_l.build()
+    r3 = algo3.train()
+    assert "alpha_prime_value" in r3["learners"]["default_policy"]
