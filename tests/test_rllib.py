@@ -218,3 +218,27 @@ def test_cql_offline_pendulum(tmp_path):
     algo3 = cfg_l.build()
     r3 = algo3.train()
     assert "alpha_prime_value" in r3["learners"]["default_policy"]
+
+
+def test_dreamerv3_cartpole_and_pendulum(tmp_path):
+    """DreamerV3 nano model learns a world model + actor-critic in imagination
+    (reference: rllib/algorithms/dreamerv3/tests/test_dreamerv3.py compilation test)."""
+    for env in ("CartPole-v1", "Pendulum-v1"):
+        cfg = (rllib.DreamerV3Config().environment(env)
+               .training(model_size="nano", batch_size_B=4, batch_length_T=16, horizon_H=5,
+                         training_ratio=64, env_steps_per_iteration=32)
+               .learners(num_gpus_per_learner=0).debugging(seed=0))
+        algo = cfg.build()
+        first = None
+        for _ in range(12):
+            r = algo.train()
+            st = r["learners"]["default_policy"]
+            if st and first is None:
+                first = st["WORLD_MODEL_L_total"]
+        assert st and all(math.isfinite(v) for v in st.values())
+        assert st["WORLD_MODEL_L_total"] < first      # the world model is learning
+        obs = algo.envs[0].reset(seed=1)[0]
+        path = algo.save_to_path(str(tmp_path / env))
+        algo2 = rllib.Algorithm.from_checkpoint(path)
+        a1, a2 = algo.compute_single_action(obs), algo2.compute_single_action(obs)
+        assert np.allclose(a1, a2, atol=1e-5)
