@@ -26,6 +26,28 @@ from .read_api import (
     read_parquet,
     read_text,
 )
+from .read_api import (  # noqa: E402  (formats without extra deps + honest stubs)
+    read_parquet_bulk,
+    read_tfrecords,
+    read_webdataset,
+    read_sql,
+    from_dask,
+    from_spark,
+    from_modin,
+    from_mars,
+    from_tf,
+    read_bigquery,
+    read_mongo,
+    read_lance,
+    read_iceberg,
+    read_hudi,
+    read_delta_sharing_tables,
+    read_databricks_tables,
+    read_clickhouse,
+    read_avro,
+    read_audio,
+    read_videos,
+)
 
 __all__ = [
     "Dataset", "MaterializedDataset", "GroupedData", "DataIterator", "DataContext", "Schema",
@@ -34,4 +56,4 @@ __all__ = [
     "from_pandas", "from_arrow", "from_numpy_refs", "from_pandas_refs", "from_arrow_refs",
     "from_torch", "from_huggingface", "read_parquet", "read_csv", "read_json", "read_text",
     "read_numpy", "read_binary_files", "read_images", "read_datasource", "preprocessors",
-]
+] + ['read_parquet_bulk', 'read_tfrecords', 'read_webdataset', 'read_sql', 'from_dask', 'from_spark', 'from_modin', 'from_mars', 'from_tf', 'read_bigquery', 'read_mongo', 'read_lance', 'read_iceberg', 'read_hudi', 'read_delta_sharing_tables', 'read_databricks_tables', 'read_clickhouse', 'read_avro', 'read_audio', 'read_videos']

@@ -223,7 +223,8 @@ def _slice_concat(specs):
 
 
 def _write_block(block, path, fmt, idx, kw):
-    os.makedirs(path, exist_ok=True)
+    if path:
+        os.makedirs(path, exist_ok=True)
     fn = os.path.join(path, f"{idx:06d}.{ 'npy' if fmt == 'numpy' else fmt}")
     if fmt == "parquet":
         import pyarrow as pa
@@ -237,6 +238,31 @@ def _write_block(block, path, fmt, idx, kw):
     elif fmt == "numpy":
         col = kw.get("column") or next(iter(block))
         np.save(fn, block[col])
+    elif fmt in ("tfrecords", "webdataset"):
+        from . import formats
+
+        fn = fn[: -len(fmt)] + ("tfrecords" if fmt == "tfrecords" else "tar")
+        if fmt == "tfrecords":
+            formats.write_tfrecords(B.iter_rows(block), fn)
+        else:
+            formats.write_webdataset(B.iter_rows(block), fn, start_key=idx * 1_000_000)
+    elif fmt == "images":
+        from PIL import Image
+
+        col, ext = kw["column"], kw.get("file_format", "png")
+        fn = []
+        for j, row in enumerate(B.iter_rows(block)):
+            f = os.path.join(path, f"{idx:06d}_{j:06d}.{ext}")
+            Image.fromarray(np.asarray(row[col])).save(f)
+            fn.append(f)
+    elif fmt == "sql":
+        conn = kw["connection_factory"]()
+        try:
+            cur = conn.cursor()
+            cur.executemany(kw["sql"], [tuple(B._scalar(v) for v in r.values()) for r in B.iter_rows(block)])
+            conn.commit()
+        finally:
+            conn.close()
     return fn
 
 
@@ -737,6 +763,75 @@ class Dataset:
 
     def write_numpy(self, path: str, *, column: Optional[str] = None, **kw):
         self._write(path, "numpy", column=column)
+
+    def write_tfrecords(self, path: str, **kw):
+        self._write(path, "tfrecords")
+
+    def write_webdataset(self, path: str, **kw):
+        self._write(path, "webdataset")
+
+    def write_images(self, path: str, column: str, file_format: str = "png", **kw):
+        self._write(path, "images", column=column, file_format=file_format)
+
+    def write_sql(self, sql: str, connection_factory, **kw):
+        """``INSERT ... VALUES (?, ...)`` per row through DB-API ``executemany``."""
+        self._write("", "sql", sql=sql, connection_factory=connection_factory)
+
+    # ------------------------------------------------ misc reference surface
+    @property
+    def context(self):
+        from .context import DataContext
+
+        return DataContext.get_current()
+
+    def copy(self) -> "Dataset":
+        ds = Dataset(self._source, list(self._ops))
+        ds._materialized = self._materialized
+        return ds
+
+    def has_serializable_lineage(self) -> bool:
+        return self._source[0] == "read"
+
+    def serialize_lineage(self) -> bytes:
+        """The logical plan (read tasks + ops), re-executable in another job."""
+        if not self.has_serializable_lineage():
+            raise ValueError("lineage of datasets created from in-memory refs cannot be serialized")
+        import cloudpickle
+
+        return cloudpickle.dumps((self._source, self._ops))
+
+    @staticmethod
+    def deserialize_lineage(serialized: bytes) -> "Dataset":
+        import cloudpickle  # our own serialize_lineage() output
+
+        src, ops = cloudpickle.loads(serialized)
+        return Dataset(src, ops)
+
+    def iter_internal_ref_bundles(self):
+        for r, meta in self._execute():
+            yield [(r, meta)]
+
+    def to_random_access_dataset(self, key: str, num_workers: Optional[int] = None):
+        from .random_access import RandomAccessDataset
+
+        return RandomAccessDataset(self, key, num_workers or 2)
+
+    def iter_tf_batches(self, *a, **k):
+        raise ImportError("iter_tf_batches needs tensorflow, which is not installed in this image")
+
+    to_tf = iter_tf_batches
+
+    def to_dask(self, *a, **k):
+        raise ImportError("to_dask needs dask, which is not installed in this image")
+
+    def to_spark(self, *a, **k):
+        raise ImportError("to_spark needs pyspark, which is not installed in this image")
+
+    def to_modin(self, *a, **k):
+        raise ImportError("to_modin needs modin, which is not installed in this image")
+
+    def to_mars(self, *a, **k):
+        raise ImportError("to_mars needs mars, which is not installed in this image")
 
     def write_datasink(self, datasink, **kw):
         from ..core.api import get

@@ -239,6 +239,62 @@ def read_images(paths, *, size=None, mode=None, include_paths: bool = False, **k
     return _file_ds(files, rd)
 
 
+def read_parquet_bulk(paths, *, columns: Optional[List[str]] = None, **kw) -> Dataset:
+    """Many small parquet files, no metadata pre-pass (reference: read_parquet_bulk)."""
+    return read_parquet(paths, columns=columns, **kw)
+
+
+def read_tfrecords(paths, *, verify_crc: bool = True, **kw) -> Dataset:
+    """TFRecord files of ``tf.train.Example`` (decoded without TensorFlow, see formats.py)."""
+    from . import formats
+
+    files = _expand(paths, [".tfrecords", ".tfrecord"])
+    return _file_ds(files, lambda f: B.from_rows(formats.read_tfrecords(f, verify_crc)))
+
+
+def read_webdataset(paths, *, decode: bool = True, **kw) -> Dataset:
+    """WebDataset tar shards; one row per sample key, one column per member suffix."""
+    from . import formats
+
+    files = _expand(paths, [".tar"])
+    return _file_ds(files, lambda f: B.from_rows(formats.read_webdataset(f, decode)))
+
+
+def read_sql(sql: str, connection_factory, *, parallelism: int = -1, **kw) -> Dataset:
+    """Run ``sql`` on a DB-API 2 connection from ``connection_factory()`` (reference: read_sql)."""
+
+    def rd():
+        conn = connection_factory()
+        try:
+            cur = conn.cursor()
+            cur.execute(sql)
+            names = [d[0] for d in cur.description]
+            rows = cur.fetchall()
+        finally:
+            conn.close()
+        return {n: B._to_array([r[i] for r in rows]) for i, n in enumerate(names)}
+
+    return Dataset(("read", [rd]))
+
+
+def _unavailable(name: str, lib: str):
+    def fn(*a, **k):
+        raise ImportError(f"{name} needs {lib}, which is not installed in this image "
+                          "(no package index on MI355X pods)")
+
+    fn.__name__ = name
+    return fn
+
+
+for _n, _lib in (("from_dask", "dask"), ("from_spark", "pyspark"), ("from_modin", "modin"),
+                 ("from_mars", "mars"), ("from_tf", "tensorflow"), ("read_bigquery", "google-cloud-bigquery"),
+                 ("read_mongo", "pymongo"), ("read_lance", "lance"), ("read_iceberg", "pyiceberg"),
+                 ("read_hudi", "hudi"), ("read_delta_sharing_tables", "delta-sharing"),
+                 ("read_databricks_tables", "databricks-sql-connector"), ("read_clickhouse", "clickhouse-connect"),
+                 ("read_avro", "fastavro"), ("read_audio", "soundfile"), ("read_videos", "decord")):
+    globals()[_n] = _unavailable(_n, _lib)
+
+
 def read_datasource(datasource, *, parallelism: int = -1, **kw) -> Dataset:
     tasks = datasource.get_read_tasks(parallelism if parallelism > 0 else 8)
     return Dataset(("read", [(lambda t=t: B.concat([B.from_batch(x) for x in t()])) for t in tasks]))

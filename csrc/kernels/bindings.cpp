@@ -14,6 +14,7 @@ void ln_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, const fl
                    bf16*, float*, bf16*, bf16*, int, int, hipStream_t);
 int ln_nv_for(int D);
 int ln_bwd_num_blocks(int rows);
+void ln_bwd_config(int variant, int max_blocks);
 void bias_gelu_fwd_launch(const bf16*, const bf16*, bf16*, int64_t, int, hipStream_t);
 void bias_gelu_bwd_launch(const bf16*, const bf16*, const bf16*, bf16*, float*, bf16*, int, int,
                           hipStream_t);
@@ -591,6 +592,11 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "cluster_anywhere_amd gfx950 HIP kernels";
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("ln_bwd_config", [](int variant, int max_blocks) {
+    TORCH_CHECK(variant == 0 || variant == 1, "ln_bwd_config: variant must be 0 or 1");
+    TORCH_CHECK(max_blocks >= 0 && max_blocks <= 65536, "ln_bwd_config: bad max_blocks");
+    caamd::ln_bwd_config(variant, max_blocks);
+  });
   m.def("bias_gelu_fwd", &bias_gelu_fwd);
   m.def("bias_gelu_bwd", &bias_gelu_bwd);
   m.def("bias_grad_", &bias_grad_);

@@ -14,6 +14,10 @@
 
 namespace caamd {
 
+// backward kernel selection (ln_bwd_config): 0 = one row at a time, 1 = prefetching
+static int g_ln_bwd_variant = 0;
+static int g_ln_bwd_blocks = 0;  // 0 = default grid cap
+
 template <int NV, bool HAS_RES>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(
     const bf16* __restrict__ x, const bf16* __restrict__ r, bf16* __restrict__ s_out,
@@ -180,6 +184,116 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) out[i] = red[i];
 }
 
+// Software-pipelined variant: the next row's x / dy / dres loads are issued
+// before the current row is reduced and written, so every wave keeps two rows
+// of HBM traffic in flight (the one-row loop above exposes the full load
+// latency once per row).
+template <int NV, bool HAS_DRES>
+__global__ __launch_bounds__(256) void ln_bwd_pf_kernel(
+    const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ g,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const bf16* __restrict__ dres, bf16* __restrict__ dx, float* __restrict__ partial,
+    int rows, int D) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [2D] dgamma | dbeta
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nchunk = D >> 3;
+  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) red[i] = 0.f;
+  float dg[NV][8], db[NV][8];
+#pragma unroll
+  for (int c = 0; c < NV; ++c)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dg[c][j] = db[c][j] = 0.f;
+  const float inv_d = 1.f / (float)D;
+  const int stride = gridDim.x * 4;
+  bf16x8 xv[NV], dv[NV], rv[NV];
+  float mu = 0.f, rs = 0.f;
+  int r = blockIdx.x * 4 + wave;
+  auto load_row = [&](int rr, bf16x8* X, bf16x8* Dv, bf16x8* R, float& m, float& s) {
+    const size_t base = (size_t)rr * D;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nchunk) {
+        X[c] = *reinterpret_cast<const bf16x8*>(x + base + ch * 8);
+        Dv[c] = *reinterpret_cast<const bf16x8*>(dy + base + ch * 8);
+        if (HAS_DRES) R[c] = *reinterpret_cast<const bf16x8*>(dres + base + ch * 8);
+      }
+    }
+    m = mean[rr];
+    s = rstd[rr];
+  };
+  if (r < rows) load_row(r, xv, dv, rv, mu, rs);
+  for (; r < rows; r += stride) {
+    bf16x8 xn[NV], dn[NV], rn[NV];
+    float mun = 0.f, rsn = 0.f;
+    const int nxt = r + stride;
+    if (nxt < rows) load_row(nxt, xn, dn, rn, mun, rsn);
+    const size_t base = (size_t)r * D;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nchunk) {
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + ch * 8);  // L1/L2-resident
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = (float)dv[c][j], xh = ((float)xv[c][j] - mu) * rs;
+          const float gd = d * (float)gv[j];
+          s1 += gd;
+          s2 += gd * xh;
+          dg[c][j] += d * xh;
+          db[c][j] += d;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    const float m1 = s1 * inv_d, m2 = s2 * inv_d;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      const int ch = lane + c * 64;
+      if (ch < nchunk) {
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + ch * 8);
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = ((float)xv[c][j] - mu) * rs;
+          float v = rs * ((float)dv[c][j] * (float)gv[j] - m1 - xh * m2);
+          if (HAS_DRES) v += (float)rv[c][j];
+          o[j] = (bf16)v;
+        }
+        *reinterpret_cast<bf16x8*>(dx + base + ch * 8) = o;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+      xv[c] = xn[c];
+      dv[c] = dn[c];
+      if (HAS_DRES) rv[c] = rn[c];
+    }
+    mu = mun;
+    rs = rsn;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int ch = lane + c * 64;
+    if (ch < nchunk) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        atomicAdd(&red[ch * 8 + j], dg[c][j]);
+        atomicAdd(&red[D + ch * 8 + j], db[c][j]);
+      }
+    }
+  }
+  __syncthreads();
+  float* out = partial + (size_t)blockIdx.x * 2 * D;
+  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) out[i] = red[i];
+}
+
 // Column sum of an fp32 [nrow, ncol] slab -> bf16, split at column `split`
 // (columns < split -> o0[c], the rest -> o1[c - split]). One block = 64 columns
 // x 16 waves; wave w sums rows w, w+16, ... with 8 loads in flight; LDS merge.
@@ -239,6 +353,15 @@ static void ln_bwd_dispatch(const bf16* dy, const bf16* x, const bf16* g, const 
                             int nblk, int rows, int D, hipStream_t st) {
   dim3 grid(nblk), block(256);
   size_t lds = (size_t)2 * D * sizeof(float);
+  if (g_ln_bwd_variant == 1) {
+    if (dres)
+      hipLaunchKernelGGL((ln_bwd_pf_kernel<NV, true>), grid, block, lds, st, dy, x, g, mean, rstd,
+                         dres, dx, partial, rows, D);
+    else
+      hipLaunchKernelGGL((ln_bwd_pf_kernel<NV, false>), grid, block, lds, st, dy, x, g, mean, rstd,
+                         dres, dx, partial, rows, D);
+    return;
+  }
   if (dres)
     hipLaunchKernelGGL((ln_bwd_kernel<NV, true>), grid, block, lds, st, dy, x, g, mean, rstd, dres,
                        dx, partial, rows, D);
@@ -258,8 +381,14 @@ int ln_nv_for(int D) {
 
 int ln_bwd_num_blocks(int rows) {
   // 768 blocks = 3 per CU (the VGPR-limited residency), >= 8 rows per block
+  const int cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : 768;
   int nb = (rows + 7) / 8;
-  return nb < 768 ? nb : 768;
+  return nb < cap ? nb : cap;
+}
+
+void ln_bwd_config(int variant, int max_blocks) {
+  g_ln_bwd_variant = variant;
+  g_ln_bwd_blocks = max_blocks;
 }
 
 void ln_fwd_launch(const bf16* x, const bf16* r, bf16* s, const bf16* g, const bf16* b, bf16* y,

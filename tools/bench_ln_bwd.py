@@ -1,0 +1,52 @@
+#!/usr/bin/env python
+"""LayerNorm backward variants on the GPT-2-XL shape [32768, 1600] (+ residual
+grad): correctness vs an fp32 torch reference and time per call / effective
+HBM bandwidth for each (variant, grid cap)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cluster_anywhere_amd.ops import kernels  # noqa: E402
+
+
+def main():
+    C = kernels()
+    R, D = 32768, 1600
+    torch.manual_seed(0)
+    x = torch.randn(R, D, device="cuda", dtype=torch.bfloat16)
+    dy = torch.randn(R, D, device="cuda", dtype=torch.bfloat16)
+    dres = torch.randn(R, D, device="cuda", dtype=torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(D, device="cuda")).bfloat16()
+    b = (0.1 * torch.randn(D, device="cuda")).bfloat16()
+    y, mean, rstd, _ = C.layernorm_fwd(x, None, g, b, 1e-5)
+    xr = x.float().requires_grad_(True)
+    gr, br = g.float().requires_grad_(True), b.float().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), gr, br, 1e-5)
+    yr.backward(dy.float())
+    ref_dx = xr.grad + dres.float()
+    for variant, blocks in ((0, 0), (1, 0), (1, 512), (1, 1024), (0, 1024), (1, 2048)):
+        C.ln_bwd_config(variant, blocks)
+        dx, dg, db = C.layernorm_bwd(dy, x, g, mean, rstd, dres)
+        err = float((dx.float() - ref_dx).abs().max())
+        gerr = float((dg.float() - gr.grad).abs().max() / gr.grad.abs().max())
+        for _ in range(3):
+            C.layernorm_bwd(dy, x, g, mean, rstd, dres)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(50):
+            C.layernorm_bwd(dy, x, g, mean, rstd, dres)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / 50 * 1e3
+        print(json.dumps({"variant": variant, "max_blocks": blocks, "us": round(us, 1),
+                          "TB_s": round(4 * R * D * 2 / us / 1e6, 2), "dx_maxerr": err, "dgamma_relerr": gerr}),
+              flush=True)
+    C.ln_bwd_config(0, 0)
+
+
+if __name__ == "__main__":
+    main()
