@@ -67,6 +67,14 @@ def __getattr__(name):
         from .client_builder import client
 
         return client
+    if name == "ClientBuilder":
+        from .client_builder import ClientBuilder
+
+        return ClientBuilder
+    if name in ("Language", "LoggingConfig", "cpp_function", "java_function", "java_actor_class"):
+        from . import _compat
+
+        return getattr(_compat, name)
     raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
 
 

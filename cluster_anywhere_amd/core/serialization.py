@@ -132,6 +132,23 @@ def _reduce_torch(t):
     return _rebuild_torch, (arr, dtype_name, tuple(src.shape), dev)
 
 
+# user-registered serializers (util.register_serializer; reference:
+# util/serialization.py): type -> (serializer, deserializer)
+_CUSTOM: dict = {}
+
+
+def _custom_rebuild(deserializer, payload):
+    return deserializer(payload)
+
+
+def _custom_reduce(obj):
+    ent = _CUSTOM.get(type(obj))
+    if ent is None:
+        return None
+    ser, de = ent
+    return (_custom_rebuild, (de, ser(obj)))
+
+
 class _Pickler(pickle.Pickler):
     def __init__(self, file, buffer_callback, refs):
         super().__init__(file, protocol=5, buffer_callback=buffer_callback)
@@ -143,6 +160,8 @@ class _Pickler(pickle.Pickler):
         if isinstance(obj, ObjectRef):
             self._refs.append(obj.binary())
             return obj.__reduce__()
+        if _CUSTOM and type(obj) in _CUSTOM:
+            raise pickle.PicklingError("custom serializer")  # by-value path below
         if isinstance(obj, (type, types.FunctionType)) and getattr(obj, "__module__", None) in (
                 "__main__", "__mp_main__"):
             # by-reference pickling of a driver-script class/function cannot be
@@ -170,6 +189,10 @@ class _CloudPickler(cloudpickle.CloudPickler):
         if isinstance(obj, ObjectRef):
             self._refs.append(obj.binary())
             return obj.__reduce__()
+        if _CUSTOM:
+            red = _custom_reduce(obj)
+            if red is not None:
+                return red
         if type(obj).__module__ == "torch" and "torch" in sys.modules:
             import torch
 

@@ -220,3 +220,108 @@ def enable_reproducibility(seed: int = 0):
 __all__ = ["TorchTrainer", "TorchConfig", "get_device", "get_devices", "prepare_model",
            "prepare_data_loader", "prepare_optimizer", "prepare_data_parallel_step", "backward",
            "accelerate", "enable_reproducibility"]
+
+
+# ----------------------------------------------------------- checkpoint / predict
+class TorchCheckpoint(Checkpoint):
+    """Directory checkpoint holding a model state dict (reference:
+    train/torch/torch_checkpoint.py). The state dict is stored with
+    ``torch.save`` and read back with ``weights_only=True``; the module class is
+    supplied by the caller on load (no pickled code in the checkpoint)."""
+
+    MODEL_FILENAME = "model.pt"
+
+    @classmethod
+    def from_state_dict(cls, state_dict, *, preprocessor=None) -> "TorchCheckpoint":
+        import tempfile
+
+        import torch
+
+        d = tempfile.mkdtemp(prefix="torch_ckpt_")
+        torch.save({k: v.detach().cpu() for k, v in state_dict.items()}, os.path.join(d, cls.MODEL_FILENAME))
+        return cls(d)
+
+    @classmethod
+    def from_model(cls, model, *, preprocessor=None) -> "TorchCheckpoint":
+        return cls.from_state_dict(model.state_dict())
+
+    def get_state_dict(self):
+        import torch
+
+        return torch.load(os.path.join(self.path, self.MODEL_FILENAME), weights_only=True, map_location="cpu")
+
+    def get_model(self, model=None):
+        if model is None:
+            raise ValueError("pass the (uninitialised) nn.Module to load the state dict into")
+        model.load_state_dict(self.get_state_dict())
+        return model
+
+
+class TorchPredictor:
+    """Batch inference with a torch module (reference: train/torch/torch_predictor.py);
+    bf16 autocast on the GPU when ``use_gpu``."""
+
+    def __init__(self, model, preprocessor=None, use_gpu: bool = False):
+        import torch
+
+        self.use_gpu = use_gpu and torch.cuda.is_available()
+        self.device = torch.device("cuda" if self.use_gpu else "cpu")
+        self.model = model.to(self.device).eval()
+        self.preprocessor = preprocessor
+
+    @classmethod
+    def from_checkpoint(cls, checkpoint: "TorchCheckpoint", model=None, use_gpu: bool = False):
+        ck = checkpoint if isinstance(checkpoint, TorchCheckpoint) else TorchCheckpoint(checkpoint.path)
+        return cls(ck.get_model(model), use_gpu=use_gpu)
+
+    def _to_tensor(self, x):
+        import numpy as np
+        import torch
+
+        return torch.as_tensor(np.asarray(x)).to(self.device)
+
+    def call_model(self, inputs):
+        return self.model(inputs)
+
+    def predict(self, data, dtype=None):
+        import torch
+
+        if self.preprocessor is not None:
+            data = self.preprocessor.transform_batch(data)
+        if isinstance(data, dict):
+            cols = list(data)
+            x = self._to_tensor(data[cols[0]]) if len(cols) == 1 else {k: self._to_tensor(v) for k, v in data.items()}
+        else:
+            x = self._to_tensor(data)
+        if dtype is not None and not isinstance(x, dict):
+            x = x.to(dtype)
+        with torch.no_grad(), torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_gpu):
+            out = self.call_model(x)
+        if isinstance(out, dict):
+            return {k: v.float().cpu().numpy() for k, v in out.items()}
+        return {"predictions": out.float().cpu().numpy()}
+
+
+class TorchDetectionPredictor(TorchPredictor):
+    """Detection models take a list of CHW images and return a list of dicts."""
+
+    def call_model(self, inputs):
+        imgs = [im for im in (inputs if isinstance(inputs, (list, tuple)) else inputs.unbind(0))]
+        outs = self.model(imgs)
+        keys = outs[0].keys() if outs else []
+        return {k: [o[k] for o in outs] for k in keys}
+
+    def predict(self, data, dtype=None):
+        import numpy as np
+        import torch
+
+        x = data["image"] if isinstance(data, dict) else data
+        x = self._to_tensor(x)
+        if dtype is not None:
+            x = x.to(dtype)
+        with torch.no_grad():
+            outs = self.call_model(x)
+        return {k: np.array([v.cpu().numpy() for v in vs], dtype=object) for k, vs in outs.items()}
+
+
+__all__ += ["TorchCheckpoint", "TorchPredictor", "TorchDetectionPredictor"]

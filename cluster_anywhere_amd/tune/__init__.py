@@ -14,6 +14,12 @@ from .stopper import (CombinedStopper, ExperimentPlateauStopper, FunctionStopper
 from .trainable import PlacementGroupFactory, Trainable, with_parameters, with_resources
 from .tuner import ExperimentAnalysis, ResultGrid, TuneConfig, Tuner, run
 
+from .registry import (Experiment, ResumeConfig, create_scheduler, create_searcher, register_env,
+                       register_trainable, run_experiments)
+from ..train.trainer import Result
+from ..train.session import TrainContext as TuneContext
+
+JupyterNotebookReporter = CLIReporter
 TuneError = RuntimeError
 
 __all__ = [n for n in dir() if not n.startswith("_")]

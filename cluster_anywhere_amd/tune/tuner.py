@@ -141,7 +141,9 @@ class Tuner:
     def __init__(self, trainable=None, *, param_space: Optional[Dict] = None,
                  tune_config: Optional[TuneConfig] = None, run_config: Optional[RunConfig] = None,
                  _restored_trials: Optional[List[Trial]] = None, _exp_dir: Optional[str] = None):
-        self.trainable = trainable
+        from .registry import resolve
+
+        self.trainable = resolve(trainable)
         self.param_space = param_space or {}
         self.tune_config = tune_config or TuneConfig()
         if run_config is None:
@@ -284,7 +286,9 @@ def run(run_or_experiment, *, config: Optional[Dict] = None, name: Optional[str]
         callbacks=None, verbose: int = 1, fail_fast: bool = False, **_ignored) -> ExperimentAnalysis:
     from .trainable import with_resources
 
-    trainable = run_or_experiment
+    from .registry import resolve
+
+    trainable = resolve(run_or_experiment)
     if resources_per_trial is not None:
         trainable = with_resources(trainable, resources_per_trial)
     rc = RunConfig(name=name, storage_path=storage_path, stop=stop, callbacks=callbacks,

@@ -45,3 +45,36 @@ def inspect_serializability(*a, **k):
     from .check_serialize import inspect_serializability as _i
 
     return _i(*a, **k)
+
+
+from .debug import disable_log_once_globally, enable_periodic_logging, log_once  # noqa: E402
+from .serialization import deregister_serializer, register_serializer  # noqa: E402
+from . import accelerators, iter  # noqa: E402
+from . import rpdb as pdb  # noqa: E402
+
+
+def connect(conn_str, secure=False, metadata=None, connection_retries=3, job_config=None,
+            namespace=None, ignore_version=False, _credentials=None, ray_init_kwargs=None):
+    """Client-mode connect (reference: util/client_connect.py)."""
+    from ..core.api import init
+
+    addr = conn_str if conn_str.startswith("ray://") else "ray://" + conn_str
+    return init(addr, namespace=namespace, job_config=job_config, **(ray_init_kwargs or {}))
+
+
+def disconnect():
+    from ..core.api import shutdown
+
+    shutdown()
+
+
+def ray_debugpy(*a, **k):
+    raise ImportError("debugpy is not installed in this image; use util.pdb.set_trace()")
+
+
+def __getattr__(name):
+    if name == "collective":
+        import importlib
+
+        return importlib.import_module(".collective", __name__)
+    raise AttributeError(name)
