@@ -1520,7 +1520,9 @@ class Head:
                 a.restarts_left = 0
                 a.death_cause = "placement group removed"
                 if a.acquired:
-                    a.acquired = None  # group resources vanish with the group
+                    # group resources vanish with the group; device ids go back to the node
+                    self._give_gpus(a.acquired[0], a.gpu_ids or (), float(a.spec.resources.get("GPU", 0) or 0))
+                    a.acquired = None
                 self._kill_worker(a.worker)
         self.sched.remove_pg(pg_id.hex())
         self._retry_pending_pgs()

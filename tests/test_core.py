@@ -500,3 +500,34 @@ def test_worker_output_streams_to_driver(capsys):
         assert "(pid=" in seen
     finally:
         ray.shutdown()
+
+
+def test_gpu_ids_return_when_placement_group_removed():
+    """Removing a PG whose GPU actor is alive hands the device id back (a later
+    fractional actor must still be placeable)."""
+    import cluster_anywhere_amd as ray
+    from cluster_anywhere_amd.util import placement_group, remove_placement_group
+    from cluster_anywhere_amd.util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+    ray.init(num_cpus=4, num_gpus=1)
+    try:
+        @ray.remote(num_gpus=1, num_cpus=0)
+        class G:
+            def f(self):
+                return 1
+
+        pg = placement_group([{"CPU": 1, "GPU": 1}])
+        ray.get(pg.ready())
+        a = G.options(scheduling_strategy=PlacementGroupSchedulingStrategy(pg, 0)).remote()
+        assert ray.get(a.f.remote()) == 1
+        ray.kill(a)
+        remove_placement_group(pg)
+
+        @ray.remote(num_gpus=0.4, num_cpus=0)
+        class H:
+            def f(self):
+                return 3
+
+        assert ray.get(H.remote().f.remote(), timeout=30) == 3
+    finally:
+        ray.shutdown()
