@@ -1228,8 +1228,8 @@ class Head:
             try:
                 w.conn.sock.setblocking(True)
                 w.conn.send_many(batch)
-            except ConnectionClosed:
-                pass
+            except (ConnectionClosed, OSError):
+                pass  # the actor's connection is going away; its death handling fails the calls
             finally:
                 try:
                     w.conn.sock.setblocking(False)

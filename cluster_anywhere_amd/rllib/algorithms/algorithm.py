@@ -264,7 +264,7 @@ class Algorithm(Trainable):
                "num_env_steps_sampled_lifetime": self.env_steps_sampled,
                "num_env_steps_trained_lifetime": self.env_steps_trained,
                "episode_return_mean": m["episode_return_mean"],
-               "timers": {"training_step_s": time.time() - t0}}
+               "timers": dict(getattr(self, "_timers", {}), training_step_s=time.time() - t0)}
         c = self.algo_config
         if c.evaluation_interval and (self.iteration + 1) % c.evaluation_interval == 0:
             out["evaluation"] = self.evaluate()

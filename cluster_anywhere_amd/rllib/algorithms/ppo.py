@@ -91,9 +91,13 @@ class PPO(Algorithm):
     learner_class = PPOLearner
 
     def training_step(self):
+        import time
+
         c = self.algo_config
+        t0 = time.perf_counter()
         frags = self.env_runner_group.sample()
         frag = concat_fragments(frags)
+        t1 = time.perf_counter()
         steps = int(frag["rewards"].size)
         self.env_steps_sampled += steps
         lg = self.learner_group
@@ -107,5 +111,7 @@ class PPO(Algorithm):
             stats = lg.update(batch, c.minibatch_size, c.num_epochs)
             stats["curr_kl_coeff"] = lg.call("update_kl", stats.get("mean_kl_loss", 0.0))
         self.env_steps_trained += steps
+        t2 = time.perf_counter()
         self._sync_weights()
+        self._timers = {"sample_s": t1 - t0, "learn_s": t2 - t1, "sync_weights_s": time.perf_counter() - t2}
         return stats
