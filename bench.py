@@ -84,6 +84,10 @@ def train_loop_per_worker(cfg):
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
+    if rank == 0 and os.environ.get("CAAMD_TUNE_GEMMS"):
+        from cluster_anywhere_amd.ops.gemm_tuning import dump_tuned
+
+        dump_tuned()  # online-tuned table for this shape set (see ops/gemm_tuning.py)
     train.report({
         "dt": dt, "loss": float(last.item()), "world": world, "params": model.num_params(),
         "flops_per_token": model.flops_per_token(T), "zero": step.zero,

@@ -39,16 +39,51 @@ def use_tuned_gemms() -> bool:
     import torch.cuda.tunable as tn
 
     tn.enable(True)
-    tn.tuning_enable(False)
-    try:
-        tn.write_file_on_exit(False)
-    except Exception:
-        pass
+    # CAAMD_TUNE_GEMMS=<csv>: online-tune every shape the run issues that the
+    # shipped tables miss (exact shapes/layouts/bias epilogues of the real step),
+    # then write shipped + new winners to <csv> at exit (merge it into tuning/).
+    out = os.environ.get("CAAMD_TUNE_GEMMS", "")
+    tn.tuning_enable(bool(out))
+    if out:
+        tn.set_max_tuning_duration(60)
+        tn.set_max_tuning_iterations(20)
     ok = False
     for t in tables():
         try:
             ok = bool(tn.read_file(t)) or ok
         except Exception:
             pass
+    if out:
+        tn.set_filename(out, False)
+
+        def _beat():  # tuning a shape can take a minute: keep the run visibly alive
+            import sys
+            import time
+
+            t0 = time.time()
+            while True:
+                time.sleep(30)
+                print(f"# gemm tuning ... {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+        import threading
+
+        threading.Thread(target=_beat, daemon=True).start()
     _DONE = True
     return ok
+
+
+def dump_tuned() -> None:
+    """Write shipped + newly tuned winners to ``$CAAMD_TUNE_GEMMS`` (no-op otherwise)."""
+    out = os.environ.get("CAAMD_TUNE_GEMMS", "")
+    if not out or not _DONE:
+        return
+    import importlib.util
+
+    import torch.cuda.tunable as tn
+
+    path = os.path.join(os.path.dirname(os.path.dirname(TUNING_DIR)), "tools", "bench_gemm.py")
+    spec = importlib.util.spec_from_file_location("_caamd_bench_gemm", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    mod.write_results(tn, out)

@@ -49,13 +49,15 @@ def run(tokens, d, vocab, only=None):
         print(f"# {name} N={n} K={k}", flush=True)
         x = torch.randn(tokens, k, device=dev, dtype=torch.bfloat16)
         w = torch.randn(n, k, device=dev, dtype=torch.bfloat16) * 0.02
-        b = torch.randn(n, device=dev, dtype=torch.bfloat16) if name != "lm" else None
+        # the step's fc GEMM has no bias (bias + GELU run fused in bias_gelu.hip)
+        b = torch.randn(n, device=dev, dtype=torch.bfloat16) if name not in ("lm", "fc") else None
         dy = torch.randn(tokens, n, device=dev, dtype=torch.bfloat16)
         g = torch.zeros(n, k, device=dev, dtype=torch.bfloat16)
         fl = 2.0 * tokens * n * k
         for role, fn in (("fwd", lambda: F.linear(x, w, b)),
                          ("dgrad", lambda: dy @ w),
-                         ("wgrad", lambda: g.addmm_(dy.t(), x))):
+                         # lm head (tied wte, plain autograd): dW = dY^T X without accumulate
+                         ("wgrad", (lambda: dy.t() @ x) if name == "lm" else (lambda: g.addmm_(dy.t(), x)))):
             ms = bench(fn)
             tot_ms += ms
             rows.append({"gemm": name, "role": role, "M": tokens, "N": n, "K": k,
