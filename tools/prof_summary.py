@@ -24,8 +24,20 @@ def family(name: str) -> str:
 
 
 def main(d, out):
-    f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)[0]
-    rows = list(csv.DictReader(open(f)))
+    fs = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+    if fs:
+        rows = list(csv.DictReader(open(fs[0])))
+    else:  # rocprofv3 7.x default output: rocpd SQLite database
+        import sqlite3
+
+        db = sqlite3.connect(glob.glob(os.path.join(d, "**", "*.db"), recursive=True)[0])
+        q = ("select name, count(*), sum(duration) from kernels group by name "
+             "order by sum(duration) desc")
+        rows = [{"Name": n, "Calls": c, "TotalDurationNs": t, "AverageNs": t / c, "Percentage": 0.0}
+                for n, c, t in db.execute(q)]
+        tot_ = sum(r["TotalDurationNs"] for r in rows)
+        for r in rows:
+            r["Percentage"] = 100.0 * r["TotalDurationNs"] / tot_
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     fam = {}
     for r in rows:
