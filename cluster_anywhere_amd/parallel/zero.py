@@ -10,6 +10,15 @@ fused AdamW launch updates all of it. Reduce-scatters are launched from the
 post-accumulate-grad hooks (overlapping backward); all-gathers write straight
 into the model's flat bf16 weight buffer.
 
+All-gather overlap: ``step()`` only *issues* the bucket all-gathers (async, on
+RCCL's stream) in the order the next forward first touches the buckets, and
+returns. A forward pre-hook on every module that owns parameters makes the
+compute stream wait (``work.wait()`` — a stream dependency, not a host sync) on
+exactly the buckets holding that module's parameters, so layer *l*'s forward
+runs while the gathers of layers *l+1..L* are still on the xGMI links. The
+first-use order is recorded on the first forward after a step and reused.
+Anything that reads the weights outside a forward calls ``wait_params()``.
+
 Reference parity: the ZeRO/FSDP path Ray Train exposes through its DeepSpeed /
 FSDP integrations (``python/ray/train/torch/train_loop_utils.py:162``,
 ``parallel_strategy="fsdp"``).
@@ -48,6 +57,7 @@ class Zero1Reducer:
         weight_decay: float = 0.1,
         max_grad_norm: float = 1.0,
         broadcast_init: bool = True,
+        module=None,
     ):
         self.flat = flat
         self.pg = process_group
@@ -57,8 +67,8 @@ class Zero1Reducer:
         assert flat.align % (8 * W) == 0, "FlatParamSpace align must be a multiple of 8*world"
         assert flat.master is not None
         if broadcast_init:
-            dist.broadcast(flat.master, src=0, group=process_group)
-            dist.broadcast(flat.param_buffer, src=0, group=process_group)
+            dist.broadcast(flat.master, src=self._global_src(), group=process_group)
+            dist.broadcast(flat.param_buffer, src=self._global_src(), group=process_group)
         cap = int(bucket_cap_mb * (1 << 20)) // flat.grad_buffer.element_size()
         self.buckets: List[_Bucket] = []
         owner = {}
@@ -101,6 +111,34 @@ class Zero1Reducer:
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._on_grad) for s in slots]
         for s in slots:
             s.param._ca_grad_ready = self._on_grad
+        # all-gather overlap with the next forward
+        self._ag = {}            # bucket index -> pending all-gather work
+        self._ag_order = None    # first-use order of buckets in a forward (recorded)
+        self._ag_seen = []
+        self._fwd_hooks = []
+        if module is not None:
+            for mod in module.modules():
+                own = [id(p) for p in mod.parameters(recurse=False)]
+                bis = sorted({owner[i] for i in own if i in owner}, reverse=True)
+                if bis:
+                    self._fwd_hooks.append(mod.register_forward_pre_hook(self._make_pre_hook(bis)))
+
+    def _global_src(self):
+        return 0 if self.pg is None else dist.get_global_rank(self.pg, 0)
+
+    def _make_pre_hook(self, bucket_ids):
+        def hook(_mod, _args):
+            if self._ag:
+                for bi in bucket_ids:
+                    self._wait_bucket(bi)
+        return hook
+
+    def _wait_bucket(self, bi):
+        h = self._ag.pop(bi, None)
+        if h is not None:
+            if self._ag_order is None:
+                self._ag_seen.append(bi)
+            h.wait()
 
     # -- backward-side -------------------------------------------------------------
     def start(self):
@@ -149,19 +187,29 @@ class Zero1Reducer:
             dist.all_reduce(opt.sumsq, op=dist.ReduceOp.SUM, group=self.pg)
             sumsq = opt.sumsq
         opt.step(inv_world=1.0 / self.world, sumsq=sumsq)
-        handles = []
-        for b in self.buckets:
-            off, ss, _ = self.shard_offsets[b.index]
-            handles.append(
-                dist.all_gather_into_tensor(
-                    self.flat.param_buffer[b.start : b.end], self.param_shard[off : off + ss],
-                    group=self.pg, async_op=True,
-                )
+        self.wait_params()  # (no-op unless a forward skipped some module)
+        if self._ag_order is None and self._ag_seen:
+            seen = list(dict.fromkeys(self._ag_seen))
+            self._ag_order = seen + [b.index for b in reversed(self.buckets) if b.index not in seen]
+        order = self._ag_order or [b.index for b in reversed(self.buckets)]
+        self._ag_seen = []
+        for bi in order:
+            b = self.buckets[bi]
+            off, ss, _ = self.shard_offsets[bi]
+            self._ag[bi] = dist.all_gather_into_tensor(
+                self.flat.param_buffer[b.start : b.end], self.param_shard[off : off + ss],
+                group=self.pg, async_op=True,
             )
-        for h in handles:
-            h.wait()
+        if not self._fwd_hooks:
+            self.wait_params()
+
+    def wait_params(self):
+        """Make the current stream wait for every outstanding weight all-gather."""
+        for bi in list(self._ag):
+            self._wait_bucket(bi)
 
     def remove_hooks(self):
-        for h in self._hooks:
+        self.wait_params()
+        for h in self._hooks + self._fwd_hooks:
             h.remove()
-        self._hooks = []
+        self._hooks, self._fwd_hooks = [], []

@@ -56,7 +56,7 @@ class DataParallelStep:
 
             self.reducer = Zero1Reducer(
                 self.flat, process_group, bucket_cap_mb, lr=lr, betas=betas, eps=eps,
-                weight_decay=weight_decay, max_grad_norm=max_grad_norm or 0.0,
+                weight_decay=weight_decay, max_grad_norm=max_grad_norm or 0.0, module=model,
             )
             self.optimizer = self.reducer.optimizer
         else:
@@ -65,6 +65,12 @@ class DataParallelStep:
                 self.flat, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                 max_grad_norm=max_grad_norm,
             )
+
+    def wait_params(self):
+        """Weights are up to date on the current stream after this (ZeRO-1 defers
+        the all-gather into the next forward)."""
+        if self.zero:
+            self.reducer.wait_params()
 
     def set_lr(self, lr: float):
         self.optimizer.lr = lr

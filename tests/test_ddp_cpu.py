@@ -50,6 +50,7 @@ def _worker(rank, world, port, zero, bucket_mb, q):
                 grads = full / world
             else:
                 grads = st.flat.grad_buffer.clone() / world
+    st.wait_params()  # ZeRO-1 defers the weight all-gather into the next forward
     if rank == 0:
         q.put((st.flat.param_buffer.clone(), grads))
     dist.barrier()
