@@ -4,8 +4,10 @@ Pre-LN transformer. The residual stream is carried as (h, pending_delta) so ever
 ``h = h + delta; a = LN(h)`` pair is ONE fused ``add_layer_norm`` kernel. MLP
 bias+GELU is one fused kernel (dbias fused in backward); the LM head is tied to
 the token embedding, the vocab is padded to a multiple of 64 for the GEMMs and
-the fused cross-entropy masks the padding. GEMMs are plain hipBLASLt
-(``F.linear``); attention goes through :func:`ops.attention`.
+the fused cross-entropy masks the padding. The projection GEMMs (forward and
+input-gradient) are the hand-written MFMA kernels of ``ops/gemm.py`` with bias /
+bias+GELU / GELU' fused into their epilogues (weight gradients and the LM head on
+hipBLASLt); attention goes through :func:`ops.attention`.
 
 This is the model behind the headline benchmark (Ray Train
 TorchTrainer DDP GPT-2-XL tokens/s).
@@ -20,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import add_layer_norm, attention, bias_gelu, cross_entropy, layer_norm
-from ..ops.linear import linear
+from ..ops.linear import linear, mlp
 
 
 @dataclass
@@ -83,8 +85,7 @@ class Block(nn.Module):
         y = attention(qkv, self.n_head, causal=True)
         attn_out = linear(y, self.proj_w, self.proj_b)
         h, m = add_layer_norm(h, attn_out, self.ln2_w, self.ln2_b, self.eps)
-        u = bias_gelu(linear(m, self.fc_w), self.fc_b)
-        return h, linear(u, self.fc2_w, self.fc2_b)
+        return h, mlp(m, self.fc_w, self.fc_b, self.fc2_w, self.fc2_b)
 
 
 class GPT2(nn.Module):

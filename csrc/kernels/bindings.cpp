@@ -29,6 +29,12 @@ void gae_launch(const float*, const float*, const float*, float*, float*, int, i
                 hipStream_t);
 void vtrace_launch(const float*, const float*, const float*, const float*, const float*, float*,
                    float*, int, int, float, float, hipStream_t);
+hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
+                       const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
+                       int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st);
+void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
+                        bool accumulate, hipStream_t st);
+void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
 }  // namespace caamd
 
 using at::Tensor;
@@ -588,8 +594,97 @@ void add_relu_(Tensor& y, const Tensor& r) {
   LAUNCH_CHECK();
 }
 
+// ---- hand-written MFMA GEMM (gemm.hip) ------------------------------------------
+// layout 0: a[M,K] b[N,K] (y = x W^T) · 1: a[M,K] b[K,N] (dx = dy W) · 2: a[K,M] b[K,N] (dW = dy^T x)
+// epi 0: c = acc(+bias) · 1: c += acc(+bias) · 2: ws[s] = partial (split-K; then reduced into c)
+//     3: zout = acc+bias, c = gelu(zout) (layout 0) · 4: c = acc*gelu'(z), dbias += colsum(c) (layout 0)
+static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi, int64_t bm,
+                      int64_t bn, c10::optional<Tensor> bias, c10::optional<Tensor> z,
+                      c10::optional<Tensor> zout, c10::optional<Tensor> dbias, int64_t splitk,
+                      c10::optional<Tensor> ws, bool accumulate, int64_t algo) {
+  CHECK_BF16(a);
+  CHECK_BF16(b);
+  CHECK_BF16(c);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm: 2-D operands");
+  TORCH_CHECK(layout >= 0 && layout <= 2, "gemm: bad layout");
+  const int64_t M = layout == 2 ? a.size(1) : a.size(0);
+  const int64_t K = layout == 2 ? a.size(0) : a.size(1);
+  const int64_t N = layout == 0 ? b.size(0) : b.size(1);
+  const int64_t Kb = layout == 0 ? b.size(1) : b.size(0);
+  TORCH_CHECK(Kb == K, "gemm: K mismatch");
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: output shape mismatch");
+  TORCH_CHECK((bm == 256 && (bn == 256 || bn == 320)) || (bm == 128 && bn == 320), "gemm: tile");
+  TORCH_CHECK(M % bm == 0 && N % bn == 0 && K % 64 == 0, "gemm: M%BM, N%BN, K%64 must be 0");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm: size");
+  TORCH_CHECK(splitk >= 1 && splitk <= K / 64, "gemm: splitk");
+  using caamd::bf16;
+  const bf16* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == N, "gemm: bias size");
+    bp = (const bf16*)bias->data_ptr();
+  }
+  const bf16* zp = nullptr;
+  bf16* zop = nullptr;
+  float* dbp = nullptr;
+  void* cp = c.data_ptr();
+  int ek = (int)epi;
+  if (epi == 3) {
+    TORCH_CHECK(layout == 0 && zout.has_value(), "gemm: bias_gelu needs layout 0 and zout");
+    CHECK_BF16(*zout);
+    TORCH_CHECK(zout->sizes() == c.sizes(), "gemm: zout shape");
+    zop = (bf16*)zout->data_ptr();
+  } else if (epi == 4) {
+    TORCH_CHECK(layout == 0 && z.has_value() && dbias.has_value(), "gemm: dgelu needs layout 0 (B = W^T), z, dbias");
+    CHECK_BF16(*z);
+    CHECK_F32(*dbias);
+    TORCH_CHECK(z->sizes() == c.sizes() && dbias->numel() == N, "gemm: z / dbias shape");
+    zp = (const bf16*)z->data_ptr();
+    dbp = dbias->data_ptr<float>();
+  } else if (epi == 2 || splitk > 1) {
+    TORCH_CHECK(ws.has_value(), "gemm: split-K needs a workspace");
+    CHECK_F32(*ws);
+    TORCH_CHECK(ws->numel() >= splitk * M * N, "gemm: workspace too small");
+    TORCH_CHECK(bp == nullptr, "gemm: split-K has no bias epilogue");
+    cp = ws->data_ptr();
+    ek = 2;
+  } else {
+    TORCH_CHECK(epi == 0 || epi == 1, "gemm: bad epilogue");
+    ek = accumulate ? 1 : 0;
+  }
+  TORCH_CHECK(splitk == 1 || ek == 2, "gemm: split-K only with the f32 partial epilogue");
+  const int lda = (int)a.size(1), ldb = (int)b.size(1), ldc = (int)N;
+  hipError_t e = caamd::gemm_launch((int)layout, ek, (int)bm, (int)bn, (const bf16*)a.data_ptr(),
+                                    (const bf16*)b.data_ptr(), cp, bp, zp, zop, dbp, (int)M, (int)N,
+                                    (int)K, lda, ldb, ldc, (int)splitk, (int)algo, cur_stream());
+  TORCH_CHECK(e == hipSuccess, "gemm launch failed: ", hipGetErrorString(e));
+  if (ek == 2) {
+    caamd::gemm_splitk_reduce(ws->data_ptr<float>(), (int)splitk, M * N, (bf16*)c.data_ptr(),
+                              (int)M, (int)N, ldc, accumulate, cur_stream());
+    LAUNCH_CHECK();
+  }
+}
+
+static Tensor transpose_bf16(const Tensor& x) {
+  CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 2 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose: [R,C] with R,C % 64 == 0");
+  auto y = at::empty({x.size(1), x.size(0)}, x.options());
+  if (x.numel() > 0) {
+    caamd::transpose_bf16((const caamd::bf16*)x.data_ptr(), (caamd::bf16*)y.data_ptr(), (int)x.size(0),
+                          (int)x.size(1), cur_stream());
+    LAUNCH_CHECK();
+  }
+  return y;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cluster_anywhere_amd gfx950 HIP kernels";
+  m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
+        pybind11::arg("layout"), pybind11::arg("epi"), pybind11::arg("bm"), pybind11::arg("bn"),
+        pybind11::arg("bias"), pybind11::arg("z"), pybind11::arg("zout"), pybind11::arg("dbias"),
+        pybind11::arg("splitk"), pybind11::arg("ws"), pybind11::arg("accumulate"),
+        pybind11::arg("algo") = 1);
+  m.def("transpose_bf16", &transpose_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("ln_bwd_config", [](int variant, int max_blocks) {

@@ -1,0 +1,985 @@
+// Hand-written CDNA4 (gfx950) bf16 GEMM on MFMA for the training hot path.
+//
+//   C[M,N] (+)= sum_k A(m,k) * B(k,n)   (fp32 accumulate, epilogue below)
+//
+// Operand layouts (template flags):
+//   A_KMAJ: A(m,k) = A[m*lda + k]   (activations X, dY)      else A[k*lda + m] (dY for wgrad)
+//   B_KMAJ: B(k,n) = B[n*ldb + k]   (nn.Linear weight W[N,K]) else B[k*ldb + n] (W in dgrad, X in wgrad)
+// so  forward  y  = x W^T      -> <A_KMAJ, B_KMAJ>
+//     dgrad    dx = dy W       -> <A_KMAJ, !B_KMAJ>
+//     wgrad    dW = dy^T x     -> <!A_KMAJ, !B_KMAJ>
+//
+// Design (MI355X-first; see /opt/skills/guides/cdna_hip_programming.md §5):
+//  * 512-thread workgroup = 8 waves (2 x 4 over the BM x BN tile), 2 waves per
+//    SIMD, tile BM x BN x BK=64 with BM = 256 and BN = 256 or 320 (320 divides
+//    GPT-2-XL's 1600 / 4800 / 6400 widths exactly; 256 does not).
+//  * Global -> LDS by LDS-DMA (`global_load_lds_dwordx4`, 16 B per lane, no VGPR
+//    staging), two LDS stages, the next K-tile's DMA issued before the current
+//    tile's MFMAs.
+//  * LDS images are XOR-swizzled on the DMA *source* address (the DMA writes
+//    lane-linear), read with the same XOR: K-major tiles (128-B rows) are read
+//    with ds_read_b128, MN-major tiles ([k][BM] rows) with the gfx950 hardware
+//    transpose read ds_read_b64_tr_b16. Both swizzles are bank-conflict free
+//    (checked by tools/gemm_swizzle_check.py).
+//  * v_mfma_f32_16x16x32_bf16 with the operands swapped (D = B_frag * A_frag):
+//    each lane then owns 4 consecutive output COLUMNS of one row, so the
+//    epilogue stores 8-byte bf16x4 (or 16-byte f32x4) vectors.
+//  * XCD-aware block order: the 8 XCDs each get a contiguous range of tiles in
+//    GROUP_M-grouped order, so neighbouring tiles share A/B panels in one L2.
+//  * Epilogues: bf16 store (+bias), bf16 read-add-store (gradient accumulation),
+//    fp32 partial slabs for split-K, bias+GELU(tanh) (stores pre-activation and
+//    activation), and dGELU (dz = acc * gelu'(z)) with fused bias-grad column sums.
+#include "common.h"
+
+#include <mutex>
+#include <unordered_set>
+
+namespace caamd {
+namespace gemm {
+
+typedef __attribute__((address_space(3))) char lds_char;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+constexpr int BKT = 64;  // K-tile depth
+constexpr int NTHR = 512;
+
+enum Epi : int {
+  EPI_BF16 = 0,       // C = acc (+ bias[n])
+  EPI_BF16_ACC = 1,   // C = C + acc (+ bias[n])
+  EPI_F32 = 2,        // Cf32[slice] = acc          (split-K partial slab)
+  EPI_BIAS_GELU = 3,  // Z = acc + bias ; C = gelu(Z)
+  EPI_DGELU = 4,      // C = acc * gelu'(Z[m,n]) ; dbias[n] += colsum(C) (f32 atomics)
+};
+
+__device__ __forceinline__ float gelu_tanh(float z) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float t = tanhf(k0 * (z + k1 * z * z * z));
+  return 0.5f * z * (1.f + t);
+}
+__device__ __forceinline__ float gelu_tanh_grad(float z) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float z2 = z * z;
+  float t = tanhf(k0 * (z + k1 * z2 * z));
+  return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k0 * (1.f + 3.f * k1 * z2);
+}
+
+// K-major swizzle: 16-B chunk c of row r lives at chunk position c ^ ((r >> 1) & 7).
+__device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }
+// MN-major swizzle for [k][R] images (R = 256: 32 chunks/row, R = 320: 40 chunks/row).
+template <int R>
+__device__ __forceinline__ int mswz(int k) {
+  if constexpr ((R % 128) == 0) return 2 * ((k & 3) | (((k >> 3) & 1) << 2));
+  else return 2 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+}
+
+template <int BM, int BN, bool AK, bool BK_>
+struct Cfg {
+  static constexpr int WM = 2, WN = 4;
+  static constexpr int TM = BM / WM / 16;
+  static constexpr int TN = BN / WN / 16;
+  static constexpr int A_BYTES = BM * BKT * 2;
+  static constexpr int B_BYTES = BN * BKT * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_DMA = A_BYTES / (NTHR * 16);
+  static constexpr int B_DMA = B_BYTES / (NTHR * 16);
+  static constexpr int LDS = 2 * STAGE;
+  static_assert(A_BYTES % (NTHR * 16) == 0 && B_BYTES % (NTHR * 16) == 0, "tile/DMA mismatch");
+  static_assert(TM * 16 * WM == BM && TN * 16 * WN == BN, "tile/wave mismatch");
+};
+
+// ---- global -> LDS (one operand, one K-tile) ------------------------------------
+// K-major operand: rows [r0, r0+R) x k [k0, k0+64) of X[r*ld + k].
+template <int R>
+__device__ __forceinline__ void dma_kmaj(const bf16* __restrict__ X, int ld, int r0, int k0,
+                                         lds_char* dst, int wid, int lane) {
+  constexpr int N = R * BKT * 2 / (NTHR * 16);
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const int lin = j * NTHR + wid * 64 + lane;  // 16-B chunk index in LDS order
+    const int row = lin >> 3, pos = lin & 7;
+    const int c = pos ^ kswz(row);
+    const bf16* src = X + (size_t)(r0 + row) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (void __attribute__((address_space(3)))*)(dst + (j * NTHR + wid * 64) * 16),
+                                     16, 0, 0);
+  }
+}
+// MN-major operand: k [k0, k0+64) x rows [r0, r0+R) of X[k*ld + r].
+template <int R>
+__device__ __forceinline__ void dma_mmaj(const bf16* __restrict__ X, int ld, int r0, int k0,
+                                         lds_char* dst, int wid, int lane) {
+  constexpr int N = R * BKT * 2 / (NTHR * 16);
+  constexpr int CPR = R / 8;  // chunks per k-row
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const int lin = j * NTHR + wid * 64 + lane;
+    const int k = lin / CPR, pos = lin - k * CPR;
+    const int c = pos ^ mswz<R>(k);
+    const bf16* src = X + (size_t)(k0 + k) * ld + r0 + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src, (void __attribute__((address_space(3)))*)(dst + (j * NTHR + wid * 64) * 16),
+                                     16, 0, 0);
+  }
+}
+
+// ---- LDS -> MFMA fragments ------------------------------------------------------
+// Fragment of 16 rows [rr, rr+16) x k-sub ks (32 deep): lane l gets row rr+(l&15),
+// k = ks*32 + 8*(l>>4) + j, j = 0..7.
+__device__ __forceinline__ bf16x8_t frag_kmaj(const lds_char* img, int rr, int ks, int lane) {
+  const int row = rr + (lane & 15);
+  const int c = ks * 4 + (lane >> 4);
+  const int pos = c ^ kswz(row);
+  typedef __attribute__((address_space(3))) const bf16x8_t lds_bf16x8;
+  return *(lds_bf16x8*)(img + row * 128 + pos * 16);
+}
+template <int R>
+__device__ __forceinline__ bf16x8_t frag_mmaj(const lds_char* img, int rr, int ks, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int m = rr + 4 * p;
+  const int chunk = m >> 3;
+  const int within = (p & 1) * 8;
+  s16x4 lo, hi;
+  {
+    const int k = ks * 32 + 8 * g + q;
+    const int pos = chunk ^ mswz<R>(k);
+    lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + k * (R * 2) + pos * 16 + within));
+  }
+  {
+    const int k = ks * 32 + 8 * g + 4 + q;
+    const int pos = chunk ^ mswz<R>(k);
+    hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + k * (R * 2) + pos * 16 + within));
+  }
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+struct Args {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  const bf16* bias;   // [N] or null
+  const bf16* Z;      // dGELU: pre-activation [M,N] (ldc); BIAS_GELU: out pre-activation
+  bf16* Zout;
+  float* dbias;       // dGELU: [N] fp32 accumulated
+  int M, N, K;
+  int lda, ldb, ldc;
+  int splitk;         // K slices (EPI_F32 only)
+  int tiles_m, tiles_n;
+  long long slab;     // elements between split-K slabs
+  int algo;           // 0: 2-stage BK=64 kernel, 1: ping-pong BK=32 4-stage kernel
+};
+
+// Output tile staged through LDS: the MFMA fragments (each lane: 4 columns of one
+// row) are rounded to bf16 and written into a padded [BM/2][BN] image, one m-half
+// of every wave at a time, then the whole workgroup streams the image out row by
+// row with 16-byte vectors (a 320-wide row = 40 lanes = 5 full 128-B lines),
+// applying the elementwise epilogue on the way. Direct per-fragment stores touch
+// 16 rows x 32 B per instruction and ran the store path at ~1.6 TB/s.
+template <int BM, int BN, int TM, int TN, int EPI, int ABL>
+__device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][TN], int m0, int n0,
+                                                int wr, int wc, int lane, lds_char* smem, int tid) {
+  constexpr int ROWB = BN * 2 + 16;       // padded image row (bytes)
+  constexpr int HR = BM / 2;              // image rows per pass
+  constexpr int CPR = BN / 8;             // 16-B chunks per row
+  constexpr int TMH = TM / 2;
+  constexpr int ITERS = (HR * CPR + NTHR - 1) / NTHR;
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  typedef __attribute__((address_space(3))) const bf16x8_t lds_bf16x8;
+  const int mrow = lane & 15, ncol = 4 * (lane >> 4);
+  // row pass: thread t owns column chunk t % CPR and rows t / CPR + RG * it, so a
+  // thread's bias-gradient partial sums stay in one column chunk for the whole tile
+  constexpr int RG = NTHR / CPR;          // row groups per iteration
+  constexpr int ACTIVE = RG * CPR;
+  constexpr int RITERS = (HR + RG - 1) / RG;
+  const int c = tid % CPR, rg = tid / CPR;
+  const int n = n0 + c * 8;
+  float dsum[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) dsum[r] = 0.f;
+  float bv[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) bv[r] = 0.f;
+  if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BIAS_GELU) {
+    if (p.bias && tid < ACTIVE) {
+      bf16x8_t b8 = *reinterpret_cast<const bf16x8_t*>(p.bias + n);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) bv[r] = (float)b8[r];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();  // image free
+#pragma unroll
+    for (int i = 0; i < TMH; ++i) {
+      const int ir = wr * (TMH * 16) + i * 16 + mrow;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nc = wc * (TN * 16) + j * 16 + ncol;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[h * TMH + i][j][r];
+        *(lds_bf16x4*)(smem + ir * ROWB + nc * 2) = o;
+      }
+    }
+    __syncthreads();
+    if constexpr (ABL & 8) continue;
+    if (tid >= ACTIVE) continue;
+    for (int it = 0; it < RITERS; ++it) {
+      const int ir = it * RG + rg;
+      if (ir >= HR) break;
+      const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
+      const int m = m0 + wr_ * (TM * 16) + h * (TMH * 16) + rem;
+      bf16x8_t v = *(lds_bf16x8*)(smem + ir * ROWB + c * 16);
+      const size_t off = (size_t)m * p.ldc + n;
+      float f[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) f[r] = (float)v[r] + bv[r];
+      bf16x8_t o;
+      if constexpr (EPI == EPI_BF16) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) o[r] = (bf16)f[r];
+      } else if constexpr (EPI == EPI_BF16_ACC) {
+        bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>((bf16*)p.C + off);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) o[r] = (bf16)(f[r] + (float)prev[r]);
+      } else if constexpr (EPI == EPI_BIAS_GELU) {
+        bf16x8_t z;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          z[r] = (bf16)f[r];
+          o[r] = (bf16)gelu_tanh((float)z[r]);
+        }
+        *reinterpret_cast<bf16x8_t*>(p.Zout + off) = z;
+      } else if constexpr (EPI == EPI_DGELU) {
+        bf16x8_t z = *reinterpret_cast<const bf16x8_t*>(p.Z + off);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          o[r] = (bf16)(f[r] * gelu_tanh_grad((float)z[r]));
+          dsum[r] += (float)o[r];
+        }
+      }
+      *reinterpret_cast<bf16x8_t*>((bf16*)p.C + off) = o;
+    }
+  }
+  if constexpr (EPI == EPI_DGELU) {
+    // reduce the RG row-group partials of each column chunk in LDS, then one fp32
+    // atomic per output column per tile
+    typedef __attribute__((address_space(3))) float lds_float;
+    lds_float* red = (lds_float*)smem;
+    __syncthreads();  // image reads done
+    if (tid < ACTIVE) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) red[rg * (CPR * 8) + c * 8 + r] = dsum[r];
+    }
+    __syncthreads();
+    for (int col = tid; col < CPR * 8; col += NTHR) {
+      float t = 0.f;
+#pragma unroll
+      for (int g = 0; g < RG; ++g) t += red[g * (CPR * 8) + col];
+      atomicAdd(p.dbias + n0 + col, t);
+    }
+  }
+}
+
+template <int BM, int BN, int TM, int TN, int EPI>
+__device__ __forceinline__ void epilogue(const Args& p, f32x4 (&acc)[TM][TN], int m0, int n0, int wr,
+                                         int wc, int lane, int slice) {
+  // lane owns C[m][n..n+3] for every (i, j)
+  const int mrow = lane & 15;
+  const int ncol = 4 * (lane >> 4);
+  if constexpr (EPI == EPI_DGELU) {
+    // column sums of the output tile for the bias gradient: reduce over this
+    // lane's rows, then across the 16 lanes of the same column group.
+    float csum[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) csum[j][r] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wr * (TM * 16) + i * 16 + mrow;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wc * (TN * 16) + j * 16 + ncol;
+        const size_t off = (size_t)m * p.ldc + n;
+        bf16x4 z = *reinterpret_cast<const bf16x4*>(p.Z + off);
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = acc[i][j][r] * gelu_tanh_grad((float)z[r]);
+          o[r] = (bf16)v;
+          csum[j][r] += (float)o[r];
+        }
+        *reinterpret_cast<bf16x4*>((bf16*)p.C + off) = o;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = csum[j][r];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        csum[j][r] = v;
+      }
+    if (mrow == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wc * (TN * 16) + j * 16 + ncol;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(p.dbias + n + r, csum[j][r]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wc * (TN * 16) + j * 16 + ncol;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BIAS_GELU) {
+        if (p.bias) {
+          bf16x4 b4 = *reinterpret_cast<const bf16x4*>(p.bias + n);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[r] = (float)b4[r];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wr * (TM * 16) + i * 16 + mrow;
+        const size_t off = (size_t)m * p.ldc + n;
+        if constexpr (EPI == EPI_F32) {
+          float* Cf = (float*)p.C + (size_t)slice * p.slab;
+          *reinterpret_cast<f32x4*>(Cf + off) = acc[i][j];
+        } else if constexpr (EPI == EPI_BF16) {
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] + bv[r]);
+          *reinterpret_cast<bf16x4*>((bf16*)p.C + off) = o;
+        } else if constexpr (EPI == EPI_BF16_ACC) {
+          bf16x4 prev = *reinterpret_cast<const bf16x4*>((bf16*)p.C + off);
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] + bv[r] + (float)prev[r]);
+          *reinterpret_cast<bf16x4*>((bf16*)p.C + off) = o;
+        } else if constexpr (EPI == EPI_BIAS_GELU) {
+          bf16x4 z, o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            z[r] = (bf16)(acc[i][j][r] + bv[r]);
+            o[r] = (bf16)gelu_tanh((float)z[r]);
+          }
+          *reinterpret_cast<bf16x4*>(p.Zout + off) = z;
+          *reinterpret_cast<bf16x4*>((bf16*)p.C + off) = o;
+        }
+      }
+    }
+  }
+}
+
+// ABL (development ablations, tools/gemm_dev.py --ablate): bit 0 = no DMA in the
+// loop, bit 1 = no LDS fragment reads, bit 2 = no MFMA. Production uses ABL = 0.
+template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL = 0>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(Args p) {
+  using C_ = Cfg<BM, BN, AK, BK_>;
+  constexpr int TM = C_::TM, TN = C_::TN;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  // ---- XCD-aware tile order ----------------------------------------------------
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  int sid;
+  {
+    const int xcd = bid & 7, loc = bid >> 3;
+    const int q = nwg >> 3, r = nwg & 7;
+    sid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int slice = sid % p.splitk;
+  const int tile = sid / p.splitk;
+  constexpr int GROUP_M = 8;
+  const int group_sz = GROUP_M * p.tiles_n;
+  const int g = tile / group_sz;
+  const int first_m = g * GROUP_M;
+  const int gm = min(p.tiles_m - first_m, GROUP_M);
+  const int tin = tile - g * group_sz;
+  const int tm = first_m + tin % gm;
+  const int tn = tin / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int nk_total = p.K / BKT;
+  const int per = (nk_total + p.splitk - 1) / p.splitk;
+  const int kt0 = slice * per;
+  const int kt1 = min(nk_total, kt0 + per);
+  const int nk = kt1 - kt0;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int s, int kt) {
+    lds_char* base = smem + s * C_::STAGE;
+    const int k0 = kt * BKT;
+    if constexpr (AK) dma_kmaj<BM>(p.A, p.lda, m0, k0, base, wid, lane);
+    else dma_mmaj<BM>(p.A, p.lda, m0, k0, base, wid, lane);
+    if constexpr (BK_) dma_kmaj<BN>(p.B, p.ldb, n0, k0, base + C_::A_BYTES, wid, lane);
+    else dma_mmaj<BN>(p.B, p.ldb, n0, k0, base + C_::A_BYTES, wid, lane);
+  };
+
+  if (nk > 0) {
+    stage(0, kt0);
+    __syncthreads();  // vmcnt(0) + barrier: tile kt0 landed
+    for (int it = 0; it < nk; ++it) {
+      const int cur = it & 1;
+      if (!(ABL & 1) && it + 1 < nk) stage(cur ^ 1, kt0 + it + 1);
+      const lds_char* As = smem + cur * C_::STAGE;
+      const lds_char* Bs = As + C_::A_BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t bf[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int rr = wc * (TN * 16) + j * 16;
+          if constexpr (ABL & 2) { bf[j] = bf16x8_t{}; asm volatile("" : "+v"(bf[j])); }
+          else if constexpr (BK_) bf[j] = frag_kmaj(Bs, rr, ks, lane);
+          else bf[j] = frag_mmaj<BN>(Bs, rr, ks, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int rr = wr * (TM * 16) + i * 16;
+          bf16x8_t af;
+          if constexpr (ABL & 2) { af = bf16x8_t{}; asm volatile("" : "+v"(af)); }
+          else if constexpr (AK) af = frag_kmaj(As, rr, ks, lane);
+          else af = frag_mmaj<BM>(As, rr, ks, lane);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if constexpr (ABL & 4) asm volatile("" :: "v"(bf[j]), "v"(af));
+            else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
+        }
+      }
+      __syncthreads();  // next tile landed (vmcnt(0)); everyone done with `cur`
+    }
+  }
+
+  if constexpr (EPI == EPI_F32) epilogue<BM, BN, TM, TN, EPI>(p, acc, m0, n0, wr, wc, lane, slice);
+  else epilogue_staged<BM, BN, TM, TN, EPI, ABL>(p, acc, m0, n0, wr, wc, lane, smem, tid);
+}
+
+// ================================================================================
+// Ping-pong kernel ("pp"): BK = 32 K-steps through a 4-deep LDS ring, LDS-DMA two
+// steps ahead with COUNTED vmcnt waits (never vmcnt(0) in the steady state), and
+// the two waves of every SIMD (wave w and w+4 = the two wave-rows) staggered by
+// one barrier so that one of them is in its MFMA segment while the other issues
+// its LDS reads and DMA. Per K-step a wave runs two phases (m-half 0/1):
+//   R(mh): [DMA step t+2 (mh=0)] ds_read A frags (4 m-tiles) [+ B frags (mh=0)]
+//   barrier | M(mh): (TM/2) x TN MFMAs | barrier
+// Intervals between barriers alternate (g0 R / g1 M), (g0 M / g1 R): the MFMA
+// pipe of each SIMD is always fed by one of its two waves.
+// RAW: step t+1 is read first by g0 after barrier 4t+4; every wave retires its
+// step-t+1 DMA with vmcnt(#DMA of step t+2) at the end of R(t,1), before it.
+// WAR: step t+2 reuses the stage of step t-2, whose last reads (g1, R(t-2,1))
+// were consumed 4 intervals before the DMA issue at R(t,0).
+// ================================================================================
+__device__ __forceinline__ int kswz64(int row) { return ((row >> 3) & 1) * 2; }
+
+template <int R>
+__device__ __forceinline__ void dma_kmaj32_one(const bf16* __restrict__ X, int ld, int r0, int k0,
+                                               lds_char* dst, int j, int wid, int lane) {
+  const int lin = j * NTHR + wid * 64 + lane;
+  const int row = lin >> 2, pos = lin & 3;
+  const int c = pos ^ kswz64(row);
+  const bf16* src = X + (size_t)(r0 + row) * ld + k0 + c * 8;
+  __builtin_amdgcn_global_load_lds((const void*)src,
+                                   (void __attribute__((address_space(3)))*)(dst + (j * NTHR + wid * 64) * 16),
+                                   16, 0, 0);
+}
+template <int R>
+__device__ __forceinline__ void dma_mmaj32_one(const bf16* __restrict__ X, int ld, int r0, int k0,
+                                               lds_char* dst, int j, int wid, int lane) {
+  constexpr int CPR = R / 8;
+  const int lin = j * NTHR + wid * 64 + lane;
+  const int k = lin / CPR, pos = lin - k * CPR;
+  const int c = pos ^ mswz<R>(k);
+  const bf16* src = X + (size_t)(k0 + k) * ld + r0 + c * 8;
+  __builtin_amdgcn_global_load_lds((const void*)src,
+                                   (void __attribute__((address_space(3)))*)(dst + (j * NTHR + wid * 64) * 16),
+                                   16, 0, 0);
+}
+// One K-step (32 deep) of an R-row operand: FULL whole 8-KiB rounds, then a
+// partial round issued by the first REM/1KiB waves only (wave-uniform branch).
+template <int R, bool KMAJ>
+__device__ __forceinline__ void dma_step32(const bf16* __restrict__ X, int ld, int r0, int k0,
+                                           lds_char* dst, int wid, int lane) {
+  constexpr int BYTES = R * 32 * 2;
+  constexpr int FULL = BYTES / (NTHR * 16);
+  constexpr int REM = BYTES - FULL * NTHR * 16;
+#pragma unroll
+  for (int j = 0; j < FULL; ++j) {
+    if constexpr (KMAJ) dma_kmaj32_one<R>(X, ld, r0, k0, dst, j, wid, lane);
+    else dma_mmaj32_one<R>(X, ld, r0, k0, dst, j, wid, lane);
+  }
+  if constexpr (REM > 0) {
+    if (wid * 1024 < REM) {
+      if constexpr (KMAJ) dma_kmaj32_one<R>(X, ld, r0, k0, dst, FULL, wid, lane);
+      else dma_mmaj32_one<R>(X, ld, r0, k0, dst, FULL, wid, lane);
+    }
+  }
+}
+// DMA instructions one wave issues per K-step for an R-row operand (wave-uniform).
+template <int R>
+__device__ __forceinline__ constexpr int dma_count32(int wid) {
+  constexpr int BYTES = R * 32 * 2;
+  constexpr int FULL = BYTES / (NTHR * 16);
+  constexpr int REM = BYTES - FULL * NTHR * 16;  // multiple of 1 KiB
+  return FULL + (wid * 1024 < REM ? 1 : 0);
+}
+__device__ __forceinline__ bf16x8_t frag_kmaj64(const lds_char* img, int rr, int lane) {
+  const int row = rr + (lane & 15);
+  const int c = lane >> 4;
+  const int pos = c ^ kswz64(row);
+  typedef __attribute__((address_space(3))) const bf16x8_t lds_bf16x8;
+  return *(lds_bf16x8*)(img + row * 64 + pos * 16);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL = 0, int PH = 2, int DIST = 2>
+__global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
+  static_assert(DIST == 2 || (DIST == 3 && PH == 1), "prefetch distance 3 is WAR-safe only with one phase");
+  constexpr int WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int TMH = TM / PH;  // m-tiles per phase (PH phases per K-step)
+  static_assert(TM % PH == 0, "pp kernel splits the wave's m-tiles evenly over the phases");
+  constexpr int KS = 32, NST = 4;
+  constexpr int A_ST = BM * KS * 2, B_ST = BN * KS * 2, ST = A_ST + B_ST;
+  static_assert(A_ST % 1024 == 0 && B_ST % 1024 == 0, "stage must be whole KiB");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  int sid;
+  {
+    const int xcd = bid & 7, loc = bid >> 3;
+    const int q = nwg >> 3, r = nwg & 7;
+    sid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int slice = sid % p.splitk;
+  const int tile = sid / p.splitk;
+  constexpr int GROUP_M = 8;
+  const int group_sz = GROUP_M * p.tiles_n;
+  const int g = tile / group_sz;
+  const int first_m = g * GROUP_M;
+  const int gm = min(p.tiles_m - first_m, GROUP_M);
+  const int tin = tile - g * group_sz;
+  const int tm = first_m + tin % gm;
+  const int tn = tin / gm;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int ns_total = p.K / KS;
+  const int per = (ns_total + p.splitk - 1) / p.splitk;
+  const int s0 = slice * per;
+  const int nk = min(ns_total, s0 + per) - s0;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto dma = [&](int t) {
+    lds_char* base = smem + (t & (NST - 1)) * ST;
+    const int k0 = (ABL & 16) ? s0 * KS : (s0 + t) * KS;  // ABL 16: L2-hot re-reads (timing only)
+    dma_step32<BM, AK>(p.A, p.lda, m0, k0, base, wid, lane);
+    dma_step32<BN, BK_>(p.B, p.ldb, n0, k0, base + A_ST, wid, lane);
+  };
+  // per-step DMA count of this wave: the two wave rows differ when a stage is not a
+  // whole number of 8 KiB rounds (BN = 320)
+  const bool lo_grp = wr == 0;
+  constexpr int CNT_LO = dma_count32<BM>(0) + dma_count32<BN>(0);
+  constexpr int CNT_HI = dma_count32<BM>(4) + dma_count32<BN>(4);
+  // (count of waves 0..3 equals count of wave 0, waves 4..7 that of wave 4)
+  static_assert(dma_count32<BM>(3) == dma_count32<BM>(0) && dma_count32<BN>(3) == dma_count32<BN>(0),
+                "DMA count must be uniform per wave row");
+  static_assert(dma_count32<BM>(7) == dma_count32<BM>(4) && dma_count32<BN>(7) == dma_count32<BN>(4),
+                "DMA count must be uniform per wave row");
+  // retire step t+1's DMA: leave the DMAs of the (up to DIST-1) newer steps in flight
+  auto wait_ahead = [&](int newer) {
+    if (newer >= 2 && DIST >= 3) {
+      if (lo_grp) wait_vm<2 * CNT_LO>(); else wait_vm<2 * CNT_HI>();
+    } else if (newer >= 1) {
+      if (lo_grp) wait_vm<CNT_LO>(); else wait_vm<CNT_HI>();
+    } else {
+      wait_vm<0>();
+    }
+  };
+
+  if (nk > 0) {
+#pragma unroll
+    for (int d = 0; d < DIST; ++d)
+      if (d < nk) dma(d);
+    wait_ahead(min(nk, DIST) - 1);
+    __builtin_amdgcn_s_barrier();
+    if (!lo_grp) __builtin_amdgcn_s_barrier();  // stagger the second wave row by one barrier
+    bf16x8_t bf[TN];
+    bf16x8_t af[TMH];
+    for (int t = 0; t < nk; ++t) {
+      const lds_char* As = smem + (t & (NST - 1)) * ST;
+      const lds_char* Bs = As + A_ST;
+#pragma unroll
+      for (int mh = 0; mh < PH; ++mh) {
+        // ---- R segment
+        if (mh == 0) {
+          if (!(ABL & 1) && t + DIST < nk) dma(t + DIST);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int rr = wc * (TN * 16) + j * 16;
+            if constexpr (ABL & 2) { bf[j] = bf16x8_t{}; asm volatile("" : "+v"(bf[j])); }
+            else if constexpr (BK_) bf[j] = frag_kmaj64(Bs, rr, lane);
+            else bf[j] = frag_mmaj<BN>(Bs, rr, 0, lane);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TMH; ++i) {
+          const int rr = wr * (TM * 16) + (mh * TMH + i) * 16;
+          if constexpr (ABL & 2) { af[i] = bf16x8_t{}; asm volatile("" : "+v"(af[i])); }
+          else if constexpr (AK) af[i] = frag_kmaj64(As, rr, lane);
+          else af[i] = frag_mmaj<BM>(As, rr, 0, lane);
+        }
+        if (mh == PH - 1 && !(ABL & 32)) wait_ahead(min(nk - 1, t + DIST) - (t + 1));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- M segment
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TMH; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if constexpr (ABL & 4) asm volatile("" :: "v"(bf[j]), "v"(af[i]));
+            else acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[mh * TMH + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (lo_grp) __builtin_amdgcn_s_barrier();  // equal barrier counts for both rows
+  }
+  if constexpr (EPI == EPI_F32) epilogue<BM, BN, TM, TN, EPI>(p, acc, m0, n0, wr, wc, lane, slice);
+  else epilogue_staged<BM, BN, TM, TN, EPI, ABL>(p, acc, m0, n0, wr, wc, lane, smem, tid);
+}
+
+// ================================================================================
+// Persistent ping-pong kernel (algo 4): one workgroup per CU walks a fixed list of
+// output tiles (each XCD owns a contiguous, GROUP_M-grouped range of tiles; its
+// workgroups stride through it), and the LDS ring of K-steps runs continuously
+// ACROSS tiles: the first two K-steps of tile i+1 are already in flight while the
+// last steps of tile i compute and while tile i's epilogue stores directly from
+// the accumulators (no LDS staging, no barrier). That hides the per-tile pipeline
+// fill and spreads the output stores over the next tile's main loop instead of
+// bunching every CU's stores into one chip-wide burst. Same R / M segments,
+// counted vmcnt and wave-row stagger as gemm_pp_kernel (one phase per K-step).
+// ================================================================================
+template <int BM, int BN, bool AK, bool BK_, int EPI>
+__global__ __launch_bounds__(NTHR, 2) void gemm_persist_kernel(Args p) {
+  constexpr int WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int KS = 32, NST = 4, DIST = 2;
+  constexpr int A_ST = BM * KS * 2, B_ST = BN * KS * 2, ST = A_ST + B_ST;
+  static_assert(A_ST % 1024 == 0 && B_ST % 1024 == 0, "stage must be whole KiB");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const bool lo_grp = wr == 0;
+
+  const int T = p.tiles_m * p.tiles_n;
+  const int bid = blockIdx.x, G = gridDim.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q = T >> 3, r = T & 7;
+  const int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int size = q + (xcd < r ? 1 : 0);
+  const int nbx = (G >> 3) + (xcd < (G & 7) ? 1 : 0);
+  const int my_tiles = loc < size ? (size - loc + nbx - 1) / nbx : 0;
+  constexpr int GROUP_M = 8;
+  auto tile_origin = [&](int i, int& m0, int& n0) {
+    const int tile = start + loc + i * nbx;
+    const int group_sz = GROUP_M * p.tiles_n;
+    const int g = tile / group_sz;
+    const int first_m = g * GROUP_M;
+    const int gm = min(p.tiles_m - first_m, GROUP_M);
+    const int tin = tile - g * group_sz;
+    m0 = (first_m + tin % gm) * BM;
+    n0 = (tin / gm) * BN;
+  };
+  const int nk = p.K / KS;
+  const int total = my_tiles * nk;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto dma = [&](int gs) {
+    const int ti = gs / nk, ks = gs - ti * nk;
+    int m0, n0;
+    tile_origin(ti, m0, n0);
+    lds_char* base = smem + (gs & (NST - 1)) * ST;
+    const int k0 = ks * KS;
+    dma_step32<BM, AK>(p.A, p.lda, m0, k0, base, wid, lane);
+    dma_step32<BN, BK_>(p.B, p.ldb, n0, k0, base + A_ST, wid, lane);
+  };
+  constexpr int CNT_LO = dma_count32<BM>(0) + dma_count32<BN>(0);
+  constexpr int CNT_HI = dma_count32<BM>(4) + dma_count32<BN>(4);
+  auto wait_ahead = [&](int newer) {
+    if (newer >= 1) {
+      if (lo_grp) wait_vm<CNT_LO>(); else wait_vm<CNT_HI>();
+    } else {
+      wait_vm<0>();
+    }
+  };
+
+  if (total > 0) {
+    dma(0);
+    if (total > 1) dma(1);
+    wait_ahead(min(total, DIST) - 1);
+    __builtin_amdgcn_s_barrier();
+    if (!lo_grp) __builtin_amdgcn_s_barrier();
+    int m0c, n0c;
+    tile_origin(0, m0c, n0c);
+    int ti = 0, ks = 0;
+    bf16x8_t bf[TN];
+    bf16x8_t af[TM];
+    for (int gs = 0; gs < total; ++gs) {
+      const lds_char* As = smem + (gs & (NST - 1)) * ST;
+      const lds_char* Bs = As + A_ST;
+      if (gs + DIST < total) dma(gs + DIST);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int rr = wc * (TN * 16) + j * 16;
+        if constexpr (BK_) bf[j] = frag_kmaj64(Bs, rr, lane);
+        else bf[j] = frag_mmaj<BN>(Bs, rr, 0, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int rr = wr * (TM * 16) + i * 16;
+        if constexpr (AK) af[i] = frag_kmaj64(As, rr, lane);
+        else af[i] = frag_mmaj<BM>(As, rr, 0, lane);
+      }
+      wait_ahead(min(total - 1, gs + DIST) - (gs + 1));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (++ks == nk) {
+        epilogue<BM, BN, TM, TN, EPI>(p, acc, m0c, n0c, wr, wc, lane, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ks = 0;
+        if (++ti < my_tiles) tile_origin(ti, m0c, n0c);
+      }
+    }
+    if (lo_grp) __builtin_amdgcn_s_barrier();
+  }
+}
+
+// Split-K combine: out(bf16) [+]= sum_s slab_s (+ bias); f32 partials [S][M][ldc].
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S,
+                                                            long long slab, bf16* __restrict__ out,
+                                                            int M, int N, int ldc, bool accumulate) {
+  const long long total4 = (long long)M * (N / 4);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long m = i / (N / 4);
+    const int n = (int)(i - m * (N / 4)) * 4;
+    const size_t off = (size_t)m * ldc + n;
+    f32x4 s = *reinterpret_cast<const f32x4*>(part + off);
+    for (int k = 1; k < S; ++k) s += *reinterpret_cast<const f32x4*>(part + (size_t)k * slab + off);
+    bf16x4 o;
+    if (accumulate) {
+      bf16x4 prev = *reinterpret_cast<const bf16x4*>(out + off);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)(s[r] + (float)prev[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)s[r];
+    }
+    *reinterpret_cast<bf16x4*>(out + off) = o;
+  }
+}
+
+template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL>
+static hipError_t launch_abl(const Args& a, hipStream_t st);
+
+// Raise the dynamic-LDS limit once per kernel (above 64 KiB needs the attribute).
+static void ensure_lds(const void* k, int bytes) {
+  static std::mutex mu;
+  static std::unordered_set<const void*> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.insert(k).second)
+    (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+template <int BM, int BN, bool AK, bool BK_, int EPI>
+static hipError_t launch_t(const Args& a, hipStream_t st) {
+  if constexpr (BM == 256 && BN == 320 && AK && BK_ && EPI == 0) {
+    if (a.algo >= 10) {
+      switch (a.algo / 10) {
+        case 1: return launch_abl<BM, BN, AK, BK_, EPI, 1>(a, st);
+        case 2: return launch_abl<BM, BN, AK, BK_, EPI, 2>(a, st);
+        case 3: return launch_abl<BM, BN, AK, BK_, EPI, 3>(a, st);
+        case 4: return launch_abl<BM, BN, AK, BK_, EPI, 4>(a, st);
+        case 5: return launch_abl<BM, BN, AK, BK_, EPI, 5>(a, st);
+        case 6: return launch_abl<BM, BN, AK, BK_, EPI, 6>(a, st);
+        case 7: return launch_abl<BM, BN, AK, BK_, EPI, 7>(a, st);
+        case 8: return launch_abl<BM, BN, AK, BK_, EPI, 8>(a, st);
+        case 15: return launch_abl<BM, BN, AK, BK_, EPI, 15>(a, st);
+        case 16: return launch_abl<BM, BN, AK, BK_, EPI, 16>(a, st);
+        case 32: return launch_abl<BM, BN, AK, BK_, EPI, 32>(a, st);
+        case 48: return launch_abl<BM, BN, AK, BK_, EPI, 48>(a, st);
+        case 24: return launch_abl<BM, BN, AK, BK_, EPI, 24>(a, st);
+        default: return hipErrorInvalidValue;
+      }
+    }
+  }
+  return launch_abl<BM, BN, AK, BK_, EPI, 0>(a, st);
+}
+
+template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL>
+static hipError_t launch_abl(const Args& a, hipStream_t st) {
+  using C_ = Cfg<BM, BN, AK, BK_>;
+  const int grid = a.tiles_m * a.tiles_n * a.splitk;
+  if (a.algo % 10 == 4 && a.splitk == 1) {
+    auto k = gemm_persist_kernel<BM, BN, AK, BK_, EPI>;
+    constexpr int lds = 4 * (BM + BN) * 32 * 2;
+    ensure_lds((const void*)k, lds);
+    const int tiles = a.tiles_m * a.tiles_n;
+    hipLaunchKernelGGL(k, dim3(tiles < 256 ? tiles : 256), dim3(NTHR), lds, st, a);
+  } else if (a.algo % 10 >= 1 && a.algo % 10 <= 3) {
+    auto k = (a.algo % 10 == 1) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 2, 2>
+             : (a.algo % 10 == 2) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 2>
+                                  : gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 3>;
+    constexpr int lds = 4 * (BM + BN) * 32 * 2;
+    ensure_lds((const void*)k, lds);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(NTHR), lds, st, a);
+  } else {
+    auto k = gemm_kernel<BM, BN, AK, BK_, EPI, ABL>;
+    ensure_lds((const void*)k, C_::LDS);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(NTHR), C_::LDS, st, a);
+  }
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int EPI>
+static hipError_t launch_layout(int layout, const Args& a, hipStream_t st) {
+  switch (layout) {
+    case 0: return launch_t<BM, BN, true, true, EPI>(a, st);    // NT  (fwd)
+    case 1: return launch_t<BM, BN, true, false, EPI>(a, st);   // NN  (dgrad)
+    case 2: return launch_t<BM, BN, false, false, EPI>(a, st);  // TN  (wgrad)
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int BM, int BN>
+static hipError_t launch_epi(int layout, int epi, const Args& a, hipStream_t st) {
+  switch (epi) {
+    case EPI_BF16: return launch_layout<BM, BN, EPI_BF16>(layout, a, st);
+    case EPI_BF16_ACC: return launch_layout<BM, BN, EPI_BF16_ACC>(layout, a, st);
+    case EPI_F32: return launch_layout<BM, BN, EPI_F32>(layout, a, st);
+    case EPI_BIAS_GELU: return launch_t<BM, BN, true, true, EPI_BIAS_GELU>(a, st);
+    case EPI_DGELU: return launch_t<BM, BN, true, true, EPI_DGELU>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+
+// ---- bf16 transpose (W -> W^T for the dgrad GEMM's K-major B operand) ---------------
+// 64 x 64 tiles through LDS: coalesced 16-byte loads of input rows, 16-byte stores of
+// output rows (each thread gathers 8 input rows of one column from LDS).
+__global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ in,
+                                                             bf16* __restrict__ out, int R, int C) {
+  __shared__ bf16 tile[64][66];
+  const int tiles_c = C / 64;
+  const int tr = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = h * 32 + (t >> 3), c = (t & 7) * 8;
+    bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(in + (size_t)(tr * 64 + r) * C + tc * 64 + c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[r][c + j] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int oc = h * 32 + (t >> 3);  // output row = input column
+    const int orr = (t & 7) * 8;       // output column chunk = input rows
+    bf16x8_t v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = tile[orr + j][oc];
+    *reinterpret_cast<bf16x8_t*>(out + (size_t)(tc * 64 + oc) * R + tr * 64 + orr) = v;
+  }
+}
+
+}  // namespace gemm
+
+// Host entry: shapes are validated by the caller (bindings.cpp).
+hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
+                       const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
+                       int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st) {
+  gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk, M / bm, N / bn,
+               (long long)M * ldc, algo};
+  if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
+  if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);
+  if (bm == 128 && bn == 320) return gemm::launch_epi<128, 320>(layout, epi, a, st);
+  return hipErrorInvalidValue;
+}
+
+void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st) {
+  hipLaunchKernelGGL(gemm::transpose_bf16_kernel, dim3((R / 64) * (C / 64)), dim3(256), 0, st, in, out, R, C);
+}
+
+void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
+                        bool accumulate, hipStream_t st) {
+  const long long total4 = (long long)M * (N / 4);
+  int grid = (int)std::min<long long>((total4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(gemm::splitk_reduce_kernel, dim3(grid), dim3(256), 0, st, part, S, slab, out, M,
+                     N, ldc, accumulate);
+}
+
+}  // namespace caamd

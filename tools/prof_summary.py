@@ -10,7 +10,8 @@ def family(name: str) -> str:
     n = name
     if n.startswith("Cijk_") or n.startswith("Custom_Cijk"):
         return "GEMM (hipBLASLt)"
-    for key, fam in [("fa_fwd", "flash-attn fwd (ours)"), ("fa_bwd_dq", "flash-attn dQ (ours)"),
+    for key, fam in [("gemm_pp_kernel", "GEMM MFMA (ours)"), ("gemm_kernel", "GEMM MFMA (ours)"),
+                     ("transpose_bf16", "weight transpose (ours)"), ("fa_fwd", "flash-attn fwd (ours)"), ("fa_bwd_dq", "flash-attn dQ (ours)"),
                      ("fa_bwd_dkdv", "flash-attn dK/dV (ours)"), ("ln_fwd", "LayerNorm fwd (ours)"),
                      ("ln_bwd", "LayerNorm bwd (ours)"), ("colsum", "column reduce (ours)"),
                      ("bias_gelu", "bias+GELU (ours)"), ("xent", "cross-entropy (ours)"),
