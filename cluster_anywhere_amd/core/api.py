@@ -8,6 +8,7 @@ import atexit
 import inspect
 import json
 import os
+import sys
 import shutil
 import socket
 import tempfile
@@ -163,17 +164,30 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
             for k, v in (resources or {}).items():
                 res[k] = float(v)
             store_name = f"/caamd_{os.getpid()}_{uuid.uuid4().hex[:8]}"
-            head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
-                        namespace=namespace or "default",
-                        worker_env=_worker_env_from(runtime_env),
-                        listen_tcp=kwargs.get("_listen_tcp"))
-            head.start()
-            _head = head
-            address = head.sock_path
+            if os.environ.get("CAAMD_HEAD_IN_PROCESS", "0") == "1":
+                head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
+                            namespace=namespace or "default",
+                            worker_env=_worker_env_from(runtime_env),
+                            listen_tcp=kwargs.get("_listen_tcp"))
+                head.start()
+                _head = head
+                address = head.sock_path
+                tcp = head.tcp_address
+            else:
+                # the head (GCS tables + scheduler loop) runs as its own process so the
+                # control plane never competes with driver code for the GIL
+                info = _spawn_head_process({
+                    "session_dir": session_dir, "node_id": node_id.hex(), "resources": res,
+                    "store_name": store_name, "store_bytes": store_bytes, "gpus": gpus,
+                    "namespace": namespace or "default", "worker_env": _worker_env_from(runtime_env),
+                    "listen_tcp": kwargs.get("_listen_tcp"), "parent_pid": os.getpid(),
+                    "sys_path": [p for p in sys.path if p and os.path.isdir(p)]})
+                address = info["unix"]
+                tcp = info.get("address")
             try:
                 os.makedirs(root, exist_ok=True)
                 with open(os.path.join(root, "latest_address"), "w") as f:
-                    f.write(head.tcp_address or head.sock_path)
+                    f.write(tcp or address)
             except OSError:
                 pass
         elif address == "auto":
@@ -188,7 +202,9 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                          "namespace": cw.namespace, "job_id": job_id.hex(),
                          "object_store_address": getattr(cw.store, "name", ""),
                          "webui_url": None, "gcs_address": (_head.tcp_address if _head is not None and
-                                                             _head.tcp_address else address)})
+                                                             _head.tcp_address else
+                                                             (_head_proc[1].get("address") if _head_proc
+                                                              else None) or address)})
         if runtime_env:
             _session["runtime_env"] = runtime_env
         global _log_monitor
@@ -201,11 +217,54 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
             from ..dashboard import start_dashboard
 
             _session["webui_url"] = start_dashboard(dashboard_host, 8265 if dashboard_port is None else dashboard_port,
-                                                    head=_head, control_address=address)
+                                                    head=_head, control_address=address,
+                                                    session_dir=cw.session_dir)
         return RayContext(dict(_session))
 
 
 _log_monitor = None
+_head_proc = None  # (Popen, info) of the driver-owned head process
+
+
+def _spawn_head_process(cfg: dict) -> dict:
+    import subprocess
+
+    global _head_proc
+    proc = subprocess.Popen([sys.executable, "-m", "cluster_anywhere_amd.core.head_main", "--embedded",
+                             json.dumps(cfg)], stdout=subprocess.PIPE, stdin=subprocess.DEVNULL,
+                            cwd=os.getcwd(), env=_head_env())
+    line = proc.stdout.readline()
+    if not line:
+        proc.wait(timeout=10)
+        raise RuntimeError(f"head process failed to start (exit code {proc.returncode})")
+    info = json.loads(line)
+    proc.stdout.close()
+    _head_proc = (proc, info)
+    return info
+
+
+def _head_env():
+    e = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
+    return e
+
+
+def _stop_head_process():
+    global _head_proc
+    if _head_proc is None:
+        return
+    proc, _ = _head_proc
+    _head_proc = None
+    try:
+        proc.terminate()
+        proc.wait(timeout=15)
+    except Exception:
+        try:
+            proc.kill()
+            proc.wait(timeout=5)
+        except Exception:
+            pass
 
 
 def _mem_bytes():
@@ -281,6 +340,7 @@ def shutdown(_exiting_interpreter: bool = False):
         if _head is not None:
             _head.shutdown()
             _head = None
+        _stop_head_process()
         _session.clear()
 
 

@@ -181,6 +181,10 @@ class Head:
 
         self.objects: Dict[bytes, ObjEntry] = {}
         self.tasks: Dict[bytes, TaskSpec] = {}
+        # owner notifications (reference: the owner's in-process memory store learns its
+        # tasks' results without a GCS round trip): return oid -> submitting client conn
+        self.owner_of = {}
+        self._notify = {}
         self.waiting_deps: Dict[bytes, Set[bytes]] = {}  # task -> unresolved object ids
         self.lineage: Dict[bytes, TaskSpec] = {}  # finished tasks kept for object recovery
         self.num_reconstructions = 0
@@ -282,6 +286,8 @@ class Head:
                     fn()
                 except Exception:
                     traceback.print_exc()
+            if self._notify:
+                self._flush_notify()
             now = time.time()
             if now - self._last_health > 1.0:
                 self._last_health = now
@@ -289,6 +295,19 @@ class Head:
             if self.mem_monitor.enabled and now - self._last_mem >= self.mem_monitor.refresh_s:
                 self._last_mem = now
                 self._check_memory(now)
+
+    def _flush_notify(self):
+        pending, self._notify = self._notify, {}
+        for c, oids in pending.items():
+            rnode = self.clients.get(c, {}).get("node") or self.head_hex
+            items = []
+            for o in oids:
+                e = self.objects.get(o)
+                if e is None or e.state != READY:
+                    continue
+                items.append((o, *self._obj_payload(o, rnode)))
+            if items:
+                self._send(c, ("ready", items))
 
     def _on_readable(self, c: Conn):
         try:
@@ -407,8 +426,11 @@ class Head:
 
     def _seal_object(self, oid, inline, size, node_hex, contained, is_error=False):
         e = self._obj(oid)
+        oc = self.owner_of.pop(oid, None)
         if e.state == READY:
             return
+        if oc is not None and not oc.closed:
+            self._notify.setdefault(oc, []).append(oid)
         e.state = READY
         e.inline = inline
         e.size = size
@@ -728,6 +750,8 @@ class Head:
             e = self._obj(oid)
             e.refcount += 1
             e.owner_task = spec.task_id
+            if spec.generator is None:
+                self.owner_of[oid] = c
         self.events.append(("submit", spec.task_id, spec.fn_name, spec.submit_time))
         for r in spec.arg_refs:
             self._obj(r).pins += 1

@@ -17,6 +17,35 @@ import time
 import uuid
 
 
+def embedded(cfg_json: str):
+    """Head process owned by one driver (``init()`` default): configuration comes
+    from the driver as JSON; prints its addresses on stdout and exits when the
+    driver process goes away (or on SIGTERM from ``shutdown()``)."""
+    import sys
+
+    cfg = json.loads(cfg_json)
+    for p in reversed(cfg.get("sys_path", [])):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from .head import Head
+
+    head = Head(cfg["session_dir"], bytes.fromhex(cfg["node_id"]), cfg["resources"], cfg["store_name"],
+                int(cfg["store_bytes"]), cfg["gpus"], namespace=cfg.get("namespace") or "default",
+                worker_env=cfg.get("worker_env") or {}, listen_tcp=cfg.get("listen_tcp"))
+    head.start()
+    print(json.dumps({"pid": os.getpid(), "unix": head.sock_path, "address": head.tcp_address,
+                      "session_dir": head.session_dir, "node_id": head.head_hex}), flush=True)
+    parent = int(cfg.get("parent_pid", os.getppid()))
+    stop = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: stop.set())
+    signal.signal(signal.SIGINT, signal.SIG_IGN)  # the driver's Ctrl-C is the driver's business
+    while not stop.is_set():
+        stop.wait(0.5)
+        if os.getppid() != parent:
+            break  # the driver died without shutdown(): take the session down with it
+    head.shutdown()
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--port", type=int, default=6380)
@@ -85,4 +114,9 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    import sys
+
+    if len(sys.argv) > 2 and sys.argv[1] == "--embedded":
+        embedded(sys.argv[2])
+    else:
+        main()

@@ -41,6 +41,11 @@ class RefCounter:
         self.counts: Dict[bytes, int] = {}
         self.lock = threading.Lock()
         self.ops: List[tuple] = []
+        # owner-side results of tasks this process submitted, pushed by the head as
+        # they finish: oid -> (kind, payload); ``owned`` = submitted, not yet pushed
+        self.ready: Dict[bytes, tuple] = {}
+        self.owned = set()
+        self.cv = threading.Condition(self.lock)
         # resolved (kind, payload) of immutable objects this process holds refs
         # to: ray.get of them needs no round trip to the head (the reference's
         # in-process memory store for owned/inlined objects)
@@ -61,6 +66,8 @@ class RefCounter:
             if c <= 1:
                 del self.counts[oid]
                 self.cache.pop(oid, None)
+                self.ready.pop(oid, None)
+                self.owned.discard(oid)
                 self.ops.append(("d", oid))
             else:
                 self.counts[oid] = c - 1
@@ -170,6 +177,8 @@ class CoreWorker:
                 msg = self.conn.recv()
             except (ConnectionClosed, OSError):
                 self.alive = False
+                with self.refs.cv:
+                    self.refs.cv.notify_all()
                 for f in list(self.pending.values()):
                     if not f.done():
                         f.set_exception(ConnectionError("connection to the head was lost"))
@@ -180,12 +189,53 @@ class CoreWorker:
                 f = self.pending.get(msg[1])
                 if f is not None and not f.done():
                     f.set_result(msg[2])
+            elif t == "ready":
+                self._on_ready(msg[1])
             elif t == "execute":
                 self._on_execute(msg[1])
             elif t == "cancel":
                 self._on_cancel(msg[1])
             elif t == "exit":
                 self.task_queue.put(None)
+
+    def _on_ready(self, items):
+        r = self.refs
+        with r.cv:
+            for (oid, kind, payload) in items:
+                r.owned.discard(oid)
+                if oid in r.counts:
+                    r.ready[oid] = (kind, payload)
+            r.cv.notify_all()
+
+    def _local_state(self, ids):
+        """None if some id is neither pushed nor owned-pending here (ask the head);
+        else the list of ids already pushed."""
+        r = self.refs
+        ready = r.ready
+        owned = r.owned
+        out = []
+        for i in ids:
+            if i in ready:
+                out.append(i)
+            elif i not in owned:
+                return None
+        return out
+
+    def _wait_local(self, ids, need, timeout):
+        """Block until ``need`` of ``ids`` (all owned by this process) are pushed."""
+        r = self.refs
+        deadline = None if timeout is None else time.monotonic() + timeout
+        with r.cv:
+            while True:
+                ready = [i for i in ids if i in r.ready]
+                if len(ready) >= need or not self.alive:
+                    return ready
+                if any(i not in r.ready and i not in r.owned for i in ids):
+                    return None  # a ref was dropped meanwhile: fall back to the head
+                left = None if deadline is None else deadline - time.monotonic()
+                if left is not None and left <= 0:
+                    return ready
+                r.cv.wait(left if left is not None else 1.0)
 
     def close(self):
         self.alive = False
@@ -243,7 +293,10 @@ class CoreWorker:
         if kind in ("remote", "err_remote"):
             from .object_server import pull
 
-            data = pull(payload[0], oid)
+            try:
+                data = pull(payload[0], oid)
+            except OSError as e:
+                raise ObjectLostError(oid.hex(), f"object's node {payload[0]} is unreachable: {e}")
             if data is None:
                 raise ObjectLostError(oid.hex(), f"object is gone from its node ({payload[0]})")
             if kind == "remote":
@@ -272,6 +325,29 @@ class CoreWorker:
         out = self._get_cached(ids)
         if out is not None:
             return out[0] if single else out
+        st = self._local_state(ids)
+        if st is not None:
+            blocked = self._maybe_blocked(True) if len(st) < len(ids) else False
+            try:
+                got = self._wait_local(ids, len(ids), timeout) if len(st) < len(ids) else st
+            finally:
+                if blocked:
+                    self._maybe_blocked(False)
+            if got is not None and len(got) == len(ids):
+                ready = self.refs.ready
+                res = [(o, *ready[o]) for o in ids if o in ready]
+                # remote copies go through the head, which knows whether their node is alive
+                if len(res) == len(ids) and all(k in ("inline", "store", "err", "err_store") for _, k, _ in res):
+                    cache, counts = self.refs.cache, self.refs.counts
+                    for (o, k, p) in res:
+                        if k in ("inline", "store") and o in counts:
+                            cache[o] = (k, p)
+                    out = [self._materialize_or_recover(o, k, p, timeout) for (o, k, p) in res]
+                    return out[0] if single else out
+            elif got is not None and timeout is not None:
+                from ..exceptions import GetTimeoutError
+
+                raise GetTimeoutError(f"get() timed out after {timeout}s")
         blocked = self._maybe_blocked(True)
         try:
             res = self.request(lambda req: ("get", req, ids, timeout))
@@ -347,6 +423,19 @@ class CoreWorker:
             raise ValueError("wait() requires a list of unique object refs")
         if num_returns > len(ids):
             raise ValueError("num_returns cannot exceed the number of refs")
+        st = self._local_state(ids)
+        if st is not None:
+            got = st if (len(st) >= num_returns or timeout == 0) else None
+            if got is None:
+                blocked = self._maybe_blocked(True)
+                try:
+                    got = self._wait_local(ids, num_returns, timeout)
+                finally:
+                    if blocked:
+                        self._maybe_blocked(False)
+            if got is not None:
+                ready = set(got[:num_returns]) if len(got) >= num_returns else set(got)
+                return [x for x in refs if x.binary() in ready], [x for x in refs if x.binary() not in ready]
         blocked = self._maybe_blocked(True)
         try:
             ready = set(self.request(lambda req: ("wait", req, ids, num_returns, timeout)))
@@ -421,11 +510,14 @@ class CoreWorker:
                         runtime_env=runtime_env, name=name, job_id=self.job_id,
                         generator=generator, parent=ctx.task_id if ctx else None,
                         concurrency_group=concurrency_group)
+        refs = [] if generator == "streaming" else [ObjectRef(o, _owned=True) for o in return_ids]
+        if generator is None:
+            with self.refs.lock:
+                self.refs.owned.update(return_ids)
         self.send(("submit", spec))
         del keep
         if generator == "streaming":
             return ObjectRefGenerator(task_id)
-        refs = [ObjectRef(o, _owned=True) for o in return_ids]
         return refs
 
     # ------------------------------------------------------------- execution
