@@ -87,7 +87,7 @@ class ObjEntry:
 class WorkerInfo:
     __slots__ = ("worker_id", "conn", "pid", "node", "gpu_key", "idle", "actor_id", "task",
                  "proc", "fns", "alive", "kind", "started", "tasks_inflight", "env_key", "client_id",
-                 "oom_killed")
+                 "oom_killed", "direct_addr")
 
     def __init__(self, **kw):
         for s in self.__slots__:
@@ -185,6 +185,8 @@ class Head:
         # tasks' results without a GCS round trip): return oid -> submitting client conn
         self.owner_of = {}
         self._notify = {}
+        self.dpins = {}
+        self.dsealed_early = set()
         self.waiting_deps: Dict[bytes, Set[bytes]] = {}  # task -> unresolved object ids
         self.lineage: Dict[bytes, TaskSpec] = {}  # finished tasks kept for object recovery
         self.num_reconstructions = 0
@@ -370,6 +372,7 @@ class Head:
             w.alive = True
             w.started = time.time()
             w.client_id = worker_id
+            w.direct_addr = (extra or {}).get("direct")
             self.conn_worker[c] = w
             key = (w.node, w.gpu_key)
             self.starting[key] = max(0, self.starting[key] - 1)
@@ -1202,6 +1205,54 @@ class Head:
         he.state = READY
         he.inline = b""
         self.handle_objs[hid] = spec.actor_id
+
+    # ----------------------------------------------------- direct actor calls
+    def _h_actor_addr(self, c, req, actor_id):
+        """Where to send direct calls (core/direct.py): (state, unix address, node)."""
+        a = self.actors.get(actor_id)
+        if a is None:
+            self._reply(c, req, (None, None, None))
+            return
+        w = self.workers.get(a.worker) if a.worker is not None else None
+        if a.state == "ALIVE" and w is not None and w.alive:
+            self._reply(c, req, ("ALIVE", w.direct_addr, w.node))
+        else:
+            self._reply(c, req, (a.state, None, None))
+
+    def _h_dpin(self, c, task_id, oids):
+        if task_id in self.dsealed_early:  # the caller's seal (which pins them) came first
+            self.dsealed_early.discard(task_id)
+            return
+        for o in oids:
+            self._obj(o).pins += 1
+        self.dpins.setdefault(task_id, []).extend(oids)
+
+    def _h_dseal(self, c, task_id, fn_name, results, dropped, t0, t1, pid):
+        """A caller registers the results of a direct actor call (it holds one
+        reference to each return object unless it already dropped it)."""
+        drop = set(dropped or ())
+        self.events.append(("start", task_id, fn_name, t0, pid))
+        self.events.append(("end", task_id, fn_name, t1, pid))
+        for (oid, inline, size, node_hex, contained, is_err) in results:
+            e = self._obj(oid)
+            if oid not in drop:
+                e.refcount += 1
+            self._seal_object(oid, inline, size, node_hex, contained, is_err)
+            self._maybe_free(oid)
+        pinned = self.dpins.pop(task_id, None)
+        if pinned is None:
+            if any(r[4] for r in results):
+                self.dsealed_early.add(task_id)
+            return
+        for o in pinned:
+            e = self.objects.get(o)
+            if e is not None:
+                e.pins -= 1
+                self._maybe_free(o)
+
+    def _h_dseal_batch(self, c, items):
+        for it in items:
+            self._h_dseal(c, *it)
 
     def _h_check_name(self, c, req, namespace, name):
         aid = self.named_actors.get((namespace or self.namespace, name))

@@ -46,6 +46,11 @@ class RefCounter:
         self.ready: Dict[bytes, tuple] = {}
         self.owned = set()
         self.cv = threading.Condition(self.lock)
+        # return oids of direct actor calls not yet sealed at the head; decrefs of
+        # those dropped meanwhile are held back until the seal (see core/direct.py)
+        self.direct_pending = set()
+        self.direct_dropped = set()
+        self.dseal_buf: List[tuple] = []
         # resolved (kind, payload) of immutable objects this process holds refs
         # to: ray.get of them needs no round trip to the head (the reference's
         # in-process memory store for owned/inlined objects)
@@ -68,13 +73,19 @@ class RefCounter:
                 self.cache.pop(oid, None)
                 self.ready.pop(oid, None)
                 self.owned.discard(oid)
-                self.ops.append(("d", oid))
+                if oid in self.direct_pending:
+                    self.direct_dropped.add(oid)
+                else:
+                    self.ops.append(("d", oid))
             else:
                 self.counts[oid] = c - 1
 
     def drain(self):
         with self.lock:
-            ops, self.ops = self.ops, []
+            return self.drain_locked()
+
+    def drain_locked(self):
+        ops, self.ops = self.ops, []
         msgs = []
         for kind, group in itertools.groupby(ops, key=lambda x: x[0]):
             ids = [o for _, o in group]
@@ -109,6 +120,19 @@ class CoreWorker:
         self.async_loop = None
         self.thread_pool = None
         self.alive = True
+        # direct actor-call transport (core/direct.py)
+        self.direct_origin: Dict[bytes, Any] = {}
+        self.actor_direct: Dict[bytes, Any] = {}
+        self.actor_head_inflight: Dict[bytes, set] = {}
+        self.head_inflight_actor: Dict[bytes, bytes] = {}
+        self.actor_head_only = set()
+        self._direct_lock = threading.Lock()
+        self.direct_server = None
+        if kind == "worker" and os.environ.get("CAAMD_DIRECT_CALLS", "1") == "1":
+            from .direct import DirectServer
+
+            self.direct_server = DirectServer(self)
+            extra = dict(extra or {}, direct=self.direct_server.path)
         self.conn.send(("register", kind, worker_id, os.getpid(), node_hex, dict(extra or {}, job_id=job_id)))
         msg = self.conn.recv()
         assert msg[0] == "registered", msg
@@ -119,6 +143,7 @@ class CoreWorker:
         self.store = self._attach_store(info["store_name"])
         self._reader = threading.Thread(target=self._read_loop, name="caamd-reader", daemon=True)
         self._reader.start()
+        self._flush_evt = threading.Event()
         self._flusher = threading.Thread(target=self._flush_loop, name="caamd-flush", daemon=True)
         self._flusher.start()
 
@@ -159,9 +184,38 @@ class CoreWorker:
         self.send(build(req))
         return fut
 
+    def _flush_dseals(self):
+        """Register finished direct calls with the head: ONE message per batch. The
+        held-back decrefs of their return refs are released atomically with it."""
+        r = self.refs
+        with self.send_lock:
+            with r.cv:
+                buf, r.dseal_buf = r.dseal_buf, []
+                if not buf:
+                    return
+                items = []
+                for (tid, name, results, rids, timing) in buf:
+                    dropped = []
+                    for oid in rids:
+                        r.direct_pending.discard(oid)
+                        if oid in r.direct_dropped:
+                            r.direct_dropped.discard(oid)
+                            dropped.append(oid)
+                    items.append((tid, name, results, dropped, *timing))
+                ops = r.drain_locked()
+            msgs = [m for m in ops if m[0] == "addref"] + [("dseal_batch", items)] + \
+                   [m for m in ops if m[0] == "decref"]
+            self.conn.send_many(msgs)
+
     def _flush_loop(self):
         while self.alive:
-            time.sleep(0.05)
+            self._flush_evt.wait(0.005 if self.refs.dseal_buf else 0.05)
+            self._flush_evt.clear()
+            if self.refs.dseal_buf:
+                try:
+                    self._flush_dseals()
+                except (ConnectionClosed, OSError):
+                    return
             if self.refs.ops:
                 try:
                     with self.send_lock:
@@ -206,6 +260,92 @@ class CoreWorker:
                 if oid in r.counts:
                     r.ready[oid] = (kind, payload)
             r.cv.notify_all()
+        if self.head_inflight_actor:
+            with self._direct_lock:
+                for (oid, _k, _p) in items:
+                    aid = self.head_inflight_actor.pop(oid, None)
+                    if aid is not None:
+                        s_ = self.actor_head_inflight.get(aid)
+                        if s_ is not None:
+                            s_.discard(oid)
+
+    # ------------------------------------------------------ direct actor calls
+    def _direct_for(self, actor_id):
+        """The actor's DirectClient, or None to use the head path (see core/direct.py)."""
+        from .direct import DirectClient, addr_usable
+
+        st = self.actor_direct.get(actor_id)
+        if st is not None and not isinstance(st, tuple):
+            if st.alive:
+                return st
+            st = None
+        if actor_id in self.actor_head_only or self.actor_head_inflight.get(actor_id):
+            return None
+        now = time.monotonic()
+        if st is not None and now - st[1] < 0.05:
+            return None
+        try:
+            state, addr, node = self.request(lambda r: ("actor_addr", r, actor_id), timeout=30)
+        except Exception:
+            return None
+        if state == "ALIVE" and node == self.node_hex and addr_usable(addr):
+            try:
+                dc = DirectClient(self, actor_id, addr)
+            except OSError:
+                dc = None
+            if dc is not None:
+                self.actor_direct[actor_id] = dc
+                return dc
+        self.actor_direct[actor_id] = ("head", now)
+        return None
+
+    def _on_direct_done(self, spec, results, timing):
+        from .direct import result_kinds
+
+        r = self.refs
+        kinds = result_kinds(results, self.node_hex)
+        with r.cv:
+            for (oid, kind, payload) in kinds:
+                if kind is None:
+                    continue  # resolved through the head once sealed
+                r.owned.discard(oid)
+                if oid in r.counts:
+                    r.ready[oid] = (kind, payload)
+            r.cv.notify_all()
+            # registered with the head in batches by the flush thread (_flush_dseals)
+            r.dseal_buf.append((spec.task_id, spec.fn_name, results, spec.return_ids, timing))
+            if len(r.dseal_buf) >= 512:
+                self._flush_evt.set()
+
+    def _on_direct_lost(self, actor_id, specs):
+        """The actor's direct connection broke: resubmit through the head when the
+        call may be retried, else fail it with ActorDiedError."""
+        from ..exceptions import ActorDiedError
+
+        self.actor_direct[actor_id] = ("head", 0.0)
+        r = self.refs
+        for spec in specs:
+            if spec.max_retries:
+                with r.cv:
+                    dropped = [o for o in spec.return_ids if o in r.direct_dropped]
+                    for o in spec.return_ids:
+                        r.direct_pending.discard(o)
+                        r.direct_dropped.discard(o)
+                with self._direct_lock:
+                    self.actor_head_inflight.setdefault(actor_id, set()).update(spec.return_ids)
+                    for o in spec.return_ids:
+                        self.head_inflight_actor[o] = actor_id
+                try:
+                    self.send(("submit", spec))
+                    if dropped:
+                        self.send(("decref", dropped))
+                except (ConnectionClosed, OSError):
+                    pass
+                continue
+            err = ActorDiedError(actor_id.hex(), "the actor's worker died while the call was running")
+            blob = serialization.serialize(err).to_bytes()
+            results = [(o, blob, len(blob), None, (), True) for o in spec.return_ids]
+            self._on_direct_done(spec, results, (time.time(), time.time(), None))
 
     def _local_state(self, ids):
         """None if some id is neither pushed nor owned-pending here (ask the head);
@@ -239,6 +379,14 @@ class CoreWorker:
 
     def close(self):
         self.alive = False
+        if self.direct_server is not None:
+            self.direct_server.close()
+        for dc in list(self.actor_direct.values()):
+            if dc is not None and not isinstance(dc, tuple):
+                try:
+                    dc.close()
+                except Exception:
+                    pass
         try:
             with self.send_lock:
                 ops = self.refs.drain()
@@ -514,6 +662,22 @@ class CoreWorker:
         if generator is None:
             with self.refs.lock:
                 self.refs.owned.update(return_ids)
+        if kind == ACTOR_METHOD:
+            if generator is not None:
+                self.actor_head_only.add(actor_id)
+            elif self.actor_direct is not None:
+                dc = self._direct_for(actor_id)
+                if dc is not None:
+                    with self.refs.lock:
+                        self.refs.direct_pending.update(return_ids)
+                    if dc.submit(spec, (keep, [ObjectRef(o) for o in arg_refs])):
+                        return refs
+                    with self.refs.lock:
+                        self.refs.direct_pending.difference_update(return_ids)
+            with self._direct_lock:
+                self.actor_head_inflight.setdefault(actor_id, set()).update(return_ids)
+                for o in return_ids:
+                    self.head_inflight_actor[o] = actor_id
         self.send(("submit", spec))
         del keep
         if generator == "streaming":
@@ -543,6 +707,13 @@ class CoreWorker:
             self.async_loop.call_soon_threadsafe(t.cancel)
 
     def _resolve_args(self, spec, resolved):
+        if resolved is None:  # a direct call: resolve its ref arguments here
+            ids = [a[1] for a in list(spec.args) + list(spec.kwargs.values()) if a[0] != "v"]
+            resolved = {}
+            if ids:
+                res = self.request(lambda req: ("get", req, ids, None))
+                resolved = {o: (k, p) for (o, k, p) in res}
+
         def unpack(a):
             if a[0] == "v":
                 return serialization.deserialize(a[1])
@@ -572,6 +743,8 @@ class CoreWorker:
 
     def execute(self, payload):
         spec, _, resolved = payload
+        if resolved is None and spec.task_id in self.direct_origin:
+            self.__dict__.setdefault("_t_start", {})[spec.task_id] = time.time()
         self.running_tasks[spec.task_id] = threading.current_thread()
         self._set_ctx(spec)
         error_kind, retryable = None, False
@@ -647,6 +820,17 @@ class CoreWorker:
             os._exit(0)
 
     def _reply_done(self, spec, results, error_kind, retryable):
+        dc = self.direct_origin.pop(spec.task_id, None)
+        if dc is not None:
+            nested = [r for res in results for r in (res[4] or ())]
+            try:
+                if nested:  # keep nested refs alive until the caller seals the results
+                    self.send(("dpin", spec.task_id, nested))
+                t0 = getattr(self, "_t_start", {}).pop(spec.task_id, time.time())
+                dc.put(("ddone", spec.task_id, results, error_kind, t0, time.time(), os.getpid()))
+            except (ConnectionClosed, OSError):
+                pass
+            return
         try:
             self.send(("task_done", spec.task_id, results, error_kind, retryable))
         except ConnectionClosed:

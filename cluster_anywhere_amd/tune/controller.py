@@ -216,6 +216,8 @@ class _TrialRunner:
                 pass
             if out or self.done or time.time() >= deadline:
                 break
+        if out:
+            s.consumed.set()
         return out, self.done and s.reports.empty(), self.error
 
     def stop(self):

@@ -38,6 +38,10 @@ class TuneSession:
         self.trial_dir = trial_dir
         self.checkpoint = checkpoint
         self.reports: "queue.Queue" = queue.Queue()
+        # report() parks the trial until the controller has taken the result (the
+        # reference's function trainable does the same: a trial never runs ahead of
+        # its scheduler's decisions; function_trainable.py continue semaphore)
+        self.consumed = threading.Event()
         self.iteration = iteration_start
         self.ckpt_index = ckpt_index_start
         self.start = time.time()
@@ -66,7 +70,11 @@ class TuneSession:
         m.setdefault("time_this_iter_s", now - self.last)
         m.setdefault("time_total_s", now - self.start)
         self.last = now
+        self.consumed.clear()
         self.reports.put((m, path))
+        while not self.consumed.wait(0.5):
+            if self.stop_requested:
+                break
         if self.stop_requested:
             raise StopTrial()
 

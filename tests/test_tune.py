@@ -129,7 +129,9 @@ def long_trial(config):
 
 def test_tuner_asha_and_stop(cluster, tmp_path):
     sched = tune.ASHAScheduler(max_t=20, grace_period=2, reduction_factor=2)
-    tuner = tune.Tuner(long_trial, param_space={"q": tune.grid_search([0.1, 0.2, 0.5, 1.0, 2.0, 3.0])},
+    # best-first grid: trials report in lock-step (report() waits for the controller),
+    # so later, weaker arrivals at each rung meet a recorded cutoff and are stopped
+    tuner = tune.Tuner(long_trial, param_space={"q": tune.grid_search([3.0, 2.0, 1.0, 0.5, 0.2, 0.1])},
                        tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=sched),
                        run_config=tune.RunConfig(storage_path=str(tmp_path), name="asha"))
     grid = tuner.fit()
