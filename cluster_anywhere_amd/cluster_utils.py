@@ -68,8 +68,11 @@ class Cluster:
     def gcs_address(self) -> Optional[str]:
         return self.address
 
-    def _node_args(self, num_cpus=None, num_gpus=None, resources=None, object_store_memory=None):
+    def _node_args(self, num_cpus=None, num_gpus=None, resources=None, object_store_memory=None,
+                   labels=None):
         argv = []
+        if labels:
+            argv += ["--labels", json.dumps(labels)]
         if num_cpus is not None:
             argv += ["--num-cpus", str(num_cpus)]
         argv += ["--num-gpus", str(0 if num_gpus is None else num_gpus)]
@@ -79,8 +82,8 @@ class Cluster:
         return argv
 
     def add_node(self, wait: bool = True, num_cpus=None, num_gpus=None, resources=None,
-                 object_store_memory=None, **_ignored) -> ClusterNode:
-        args = self._node_args(num_cpus, num_gpus, resources, object_store_memory)
+                 object_store_memory=None, labels=None, **_ignored) -> ClusterNode:
+        args = self._node_args(num_cpus, num_gpus, resources, object_store_memory, labels)
         if self.head_node is None:
             log = os.path.join(self._temp, "head.out")
             argv = [sys.executable, "-m", "cluster_anywhere_amd.core.head_main", "--port", "0",

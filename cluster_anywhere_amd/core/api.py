@@ -168,7 +168,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                 head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
                             namespace=namespace or "default",
                             worker_env=_worker_env_from(runtime_env),
-                            listen_tcp=kwargs.get("_listen_tcp"))
+                            listen_tcp=kwargs.get("_listen_tcp"), labels=kwargs.get("labels"))
                 head.start()
                 _head = head
                 address = head.sock_path
@@ -181,6 +181,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                     "store_name": store_name, "store_bytes": store_bytes, "gpus": gpus,
                     "namespace": namespace or "default", "worker_env": _worker_env_from(runtime_env),
                     "listen_tcp": kwargs.get("_listen_tcp"), "parent_pid": os.getpid(),
+                    "labels": kwargs.get("labels") or {},
                     "sys_path": [p for p in sys.path if p and os.path.isdir(p)]})
                 address = info["unix"]
                 tcp = info.get("address")

@@ -42,6 +42,16 @@ NORMAL, ACTOR_CREATE, ACTOR_METHOD = 0, 1, 2
 PENDING, READY, FREED = 0, 1, 2
 
 
+def _node_labels(node_hex, gpu_ids, labels):
+    """Labels of a node: user labels plus the built-in ones (reference:
+    ray.io/node-id and ray.io/accelerator-type node labels)."""
+    out = {"ray.io/node-id": node_hex}
+    if gpu_ids:
+        out["ray.io/accelerator-type"] = "AMD-Instinct-MI355X"
+    out.update({str(k): str(v) for k, v in (labels or {}).items()})
+    return out
+
+
 class TaskSpec:
     """Everything the head needs to schedule, run, retry and report a task."""
 
@@ -114,7 +124,7 @@ class Head:
                  store_name: str, store_capacity: int, gpu_ids: List[int],
                  listen_tcp: Optional[str] = None, namespace: str = "default",
                  worker_env: Optional[Dict[str, str]] = None, prestart: int = 0,
-                 spill_dir: Optional[str] = None):
+                 spill_dir: Optional[str] = None, labels: Optional[Dict[str, str]] = None):
         from .. import _native
 
         self.session_dir = session_dir
@@ -125,12 +135,15 @@ class Head:
         self.store.prefault_async(int(os.environ.get("CAAMD_OBJECT_STORE_PREFAULT_BYTES", str(2 << 30))))
         self.sched = _native.ClusterScheduler(0.5)
         self.sched.add_node(node_id.hex(), resources)
+        self.node_labels = {node_id.hex(): _node_labels(node_id.hex(), gpu_ids, labels)}
+        self.sched.set_labels(node_id.hex(), self.node_labels[node_id.hex()])
         self.node_resources = {node_id.hex(): dict(resources)}
         self.free_gpus = {node_id.hex(): list(gpu_ids)}
         self.gpu_partial: Dict[str, Dict[int, float]] = {}  # node -> gpu id -> fraction in use
         self.node_info = {node_id.hex(): {"NodeID": node_id.hex(), "Alive": True,
                                           "NodeManagerAddress": "127.0.0.1",
-                                          "Resources": dict(resources), "local": True}}
+                                          "Resources": dict(resources), "local": True,
+                                          "Labels": dict(self.node_labels[node_id.hex()])}}
         self.namespace = namespace
         self.worker_env = worker_env or {}
         self.spill_dir = spill_dir or os.path.join(session_dir, "spill")
@@ -846,18 +859,26 @@ class Head:
             if not q:
                 del self.ready_queues[key]
 
+    def _pick(self, spec, demand=None):
+        """Node for a task under its scheduling strategy ('' = not now, '!' = never)."""
+        demand = demand if demand is not None else self._demand(spec)
+        st = spec.strategy or ("default",)
+        strategy, aff, soft, hard_l, soft_l = 0, "", False, [], []
+        if st[0] == "spread":
+            strategy = 1
+        elif st[0] == "node":
+            strategy, aff, soft = 2, st[1], bool(st[2])
+        elif st[0] == "label":
+            strategy, hard_l, soft_l = 3, list(st[1]), list(st[2])
+        return self.sched.pick_node(demand, strategy, aff, soft, self.node_id.hex(), hard_l, soft_l)
+
     def _try_place(self, spec) -> bool:
         demand = self._demand(spec)
         st = spec.strategy or ("default",)
         if st[0] == "pg" and spec.strategy[1] not in self.pgs:
             self._fail_task(spec, ("TaskPlacementGroupRemoved", "placement group was removed"))
             return True
-        strategy, aff, soft = 0, "", False
-        if st[0] == "spread":
-            strategy = 1
-        elif st[0] == "node":
-            strategy, aff, soft = 2, st[1], bool(st[2])
-        node = self.sched.pick_node(demand, strategy, aff, soft, self.node_id.hex())
+        node = self._pick(spec, demand)
         if node == "!":
             if spec not in self.infeasible:
                 self.infeasible.append(spec)
@@ -1125,7 +1146,7 @@ class Head:
             return
         still = []
         for spec in self.infeasible:
-            node = self.sched.pick_node(self._demand(spec), 0, "", False, "")
+            node = self._pick(spec)
             if node == "!":
                 still.append(spec)
             else:
@@ -1744,13 +1765,16 @@ class Head:
         addr = extra.get("address", "127.0.0.1")
         res.setdefault(f"node:{addr}", 1.0)
         self.sched.add_node(node_hex, res)
+        self.node_labels[node_hex] = _node_labels(node_hex, extra.get("gpu_ids", ()), extra.get("labels"))
+        self.sched.set_labels(node_hex, self.node_labels[node_hex])
         self.free_gpus[node_hex] = list(extra.get("gpu_ids", ()))
         self.node_store[node_hex] = extra["store_name"]
         self.node_obj_addr[node_hex] = extra["obj_addr"]
         self.node_conns[node_hex] = c
         self.node_resources[node_hex] = dict(res)
         self.node_info[node_hex] = {"NodeID": node_hex, "Alive": True, "NodeManagerAddress": addr,
-                                    "Resources": dict(res), "local": False, "pid": extra.get("pid")}
+                                    "Resources": dict(res), "local": False, "pid": extra.get("pid"),
+                                    "Labels": dict(self.node_labels[node_hex])}
         self._send(c, ("registered", {"store_name": extra["store_name"], "node_id": node_hex,
                                       "namespace": self.namespace, "session_dir": self.session_dir,
                                       "head_tcp": self.tcp_address}))

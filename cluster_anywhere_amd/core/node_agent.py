@@ -28,6 +28,7 @@ def main(argv=None):
     ap.add_argument("--object-store-memory", type=int, default=None)
     ap.add_argument("--node-ip-address", default="127.0.0.1")
     ap.add_argument("--node-id", default=None)
+    ap.add_argument("--labels", default="{}", help="node labels (JSON)")
     a = ap.parse_args(argv)
 
     from .. import _native
@@ -50,7 +51,8 @@ def main(argv=None):
     conn = connect(a.address)
     conn.send(("register", "node", os.urandom(16), os.getpid(), node_hex,
                {"resources": res, "gpu_ids": gpus, "store_name": store_name,
-                "obj_addr": osrv.address(a.node_ip_address), "address": a.node_ip_address, "pid": os.getpid()}))
+                "obj_addr": osrv.address(a.node_ip_address), "address": a.node_ip_address, "pid": os.getpid(),
+                "labels": json.loads(a.labels)}))
     msg = conn.recv()
     assert msg[0] == "registered", msg
     session_dir = msg[1]["session_dir"]

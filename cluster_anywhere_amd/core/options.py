@@ -88,8 +88,53 @@ def resource_demand(o: Dict[str, Any], actor: bool = False) -> Dict[str, float]:
     return d
 
 
+def label_conditions(spec: Dict[str, Any]):
+    """{key: In(..)|NotIn(..)|Exists()|DoesNotExist()|"v"|"!v"|"in(a,b)"|"!in(a,b)"}
+    -> [(key, op, values)] with op 0 in, 1 not-in, 2 exists, 3 does-not-exist."""
+    from ..util.scheduling_strategies import DoesNotExist, Exists, In, NotIn
+
+    out = []
+    for k, v in (spec or {}).items():
+        if isinstance(v, In):
+            out.append((k, 0, [str(x) for x in v.values]))
+        elif isinstance(v, NotIn):
+            out.append((k, 1, [str(x) for x in v.values]))
+        elif isinstance(v, Exists) or v is Exists:
+            out.append((k, 2, []))
+        elif isinstance(v, DoesNotExist) or v is DoesNotExist:
+            out.append((k, 3, []))
+        elif isinstance(v, str):
+            neg = v.startswith("!")
+            body = v[1:] if neg else v
+            if body.startswith("in(") and body.endswith(")"):
+                vals = [x.strip() for x in body[3:-1].split(",") if x.strip()]
+            else:
+                vals = [body]
+            out.append((k, 1 if neg else 0, vals))
+        elif isinstance(v, (list, tuple, set)):
+            out.append((k, 0, [str(x) for x in v]))
+        else:
+            raise ValueError(f"unsupported label condition {k}={v!r}")
+    # hashable: the strategy tuple is part of the head's ready-queue key
+    return tuple((k, op, tuple(vals)) for (k, op, vals) in out)
+
+
 def strategy_tuple(o: Dict[str, Any]):
+    st = _strategy_tuple(o)
+    sel = o.get("label_selector")
+    if sel:
+        conds = label_conditions(sel)
+        if st is None:
+            return ("label", conds, ())
+        if st[0] == "label":
+            return ("label", tuple(st[1]) + conds, st[2])
+        raise ValueError("label_selector cannot be combined with a placement-group / node-affinity strategy")
+    return st
+
+
+def _strategy_tuple(o: Dict[str, Any]):
     from ..util.scheduling_strategies import (NodeAffinitySchedulingStrategy,
+                                              NodeLabelSchedulingStrategy,
                                               PlacementGroupSchedulingStrategy)
     from . import context
 
@@ -114,4 +159,6 @@ def strategy_tuple(o: Dict[str, Any]):
     if isinstance(st, NodeAffinitySchedulingStrategy):
         nid = st.node_id if isinstance(st.node_id, str) else st.node_id.hex()
         return ("node", nid, st.soft)
+    if isinstance(st, NodeLabelSchedulingStrategy):
+        return ("label", label_conditions(st.hard), label_conditions(st.soft))
     raise ValueError(f"unsupported scheduling strategy {st!r}")

@@ -40,6 +40,12 @@ class DoesNotExist:
 
 
 class NodeLabelSchedulingStrategy:
+    """Schedule on nodes whose labels satisfy every ``hard`` condition; among those
+    prefer nodes that also satisfy ``soft``. Values: ``In(...)``, ``NotIn(...)``,
+    ``Exists()``, ``DoesNotExist()``. Enforced by the native ClusterScheduler
+    (csrc/runtime/scheduler.cc ``labels_match``); a task no node can ever satisfy
+    is reported infeasible."""
+
     def __init__(self, hard: Dict, *, soft: Optional[Dict] = None):
         self.hard = hard
         self.soft = soft or {}

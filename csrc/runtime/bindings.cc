@@ -1,5 +1,6 @@
 // pybind11 bindings of the native runtime: object store, cluster scheduler,
 // compiled-graph shm channels.
+#include <tuple>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -109,8 +110,23 @@ PYBIND11_MODULE(_native, m) {
       .def("cluster_total", &ClusterScheduler::cluster_total)
       .def("cluster_available", &ClusterScheduler::cluster_available)
       .def("nodes", &ClusterScheduler::nodes)
-      .def("pick_node", &ClusterScheduler::pick_node, py::arg("demand"), py::arg("strategy") = 0,
-           py::arg("affinity_node") = "", py::arg("soft") = false, py::arg("preferred_node") = "")
+      .def("pick_node",
+           [](ClusterScheduler& s, const ResMap& demand, int strategy, const std::string& aff, bool soft,
+              const std::string& pref, const std::vector<std::tuple<std::string, int, std::vector<std::string>>>& hard,
+              const std::vector<std::tuple<std::string, int, std::vector<std::string>>>& softl) {
+             auto conv = [](const std::vector<std::tuple<std::string, int, std::vector<std::string>>>& v) {
+               std::vector<LabelCond> out;
+               for (auto& t : v) out.push_back({std::get<0>(t), std::get<1>(t), std::get<2>(t)});
+               return out;
+             };
+             return s.pick_node(demand, strategy, aff, soft, pref, conv(hard), conv(softl));
+           },
+           py::arg("demand"), py::arg("strategy") = 0, py::arg("affinity_node") = "",
+           py::arg("soft") = false, py::arg("preferred_node") = "",
+           py::arg("hard") = std::vector<std::tuple<std::string, int, std::vector<std::string>>>{},
+           py::arg("soft_labels") = std::vector<std::tuple<std::string, int, std::vector<std::string>>>{})
+      .def("set_labels", &ClusterScheduler::set_labels)
+      .def("labels", &ClusterScheduler::labels)
       .def("acquire", &ClusterScheduler::acquire)
       .def("release", &ClusterScheduler::release)
       .def("reserve_pg", &ClusterScheduler::reserve_pg)

@@ -126,14 +126,68 @@ double ClusterScheduler::utilization(const NodeRes& n) const {
   return u;
 }
 
+void ClusterScheduler::set_labels(const std::string& id, const LabelMap& labels) {
+  auto it = node_idx_.find(id);
+  if (it != node_idx_.end()) nodes_[it->second].labels = labels;
+}
+
+LabelMap ClusterScheduler::labels(const std::string& id) const {
+  auto it = node_idx_.find(id);
+  return it == node_idx_.end() ? LabelMap{} : nodes_[it->second].labels;
+}
+
+bool ClusterScheduler::labels_match(const LabelMap& labels, const std::vector<LabelCond>& conds) {
+  for (const auto& c : conds) {
+    auto it = labels.find(c.key);
+    const bool has = it != labels.end();
+    switch ((LabelOp)c.op) {
+      case LabelOp::kIn:
+        if (!has || std::find(c.values.begin(), c.values.end(), it->second) == c.values.end())
+          return false;
+        break;
+      case LabelOp::kNotIn:
+        if (has && std::find(c.values.begin(), c.values.end(), it->second) != c.values.end())
+          return false;
+        break;
+      case LabelOp::kExists:
+        if (!has) return false;
+        break;
+      case LabelOp::kDoesNotExist:
+        if (has) return false;
+        break;
+    }
+  }
+  return true;
+}
+
 std::string ClusterScheduler::pick_node(const ResMap& demand, int strategy,
                                         const std::string& affinity_node, bool soft,
-                                        const std::string& preferred_node) {
+                                        const std::string& preferred_node,
+                                        const std::vector<LabelCond>& hard,
+                                        const std::vector<LabelCond>& soft_labels) {
   const auto d = to_vec(demand);
   bool feasible_any = false;
   for (auto& n : nodes_)
-    if (n.alive && fits(n, d, true)) feasible_any = true;
+    if (n.alive && fits(n, d, true) && labels_match(n.labels, hard)) feasible_any = true;
   if (!feasible_any) return "!";
+  if ((Strategy)strategy == Strategy::kLabel) {
+    // hard conditions filter; among the matching nodes prefer those that also meet
+    // the soft conditions, then the least utilised one
+    int best = -1, best_soft = -1;
+    double best_u = std::numeric_limits<double>::max();
+    for (int i = 0; i < (int)nodes_.size(); ++i) {
+      auto& n = nodes_[i];
+      if (!n.alive || !labels_match(n.labels, hard) || !fits(n, d, false)) continue;
+      const int s = soft_labels.empty() ? 0 : (labels_match(n.labels, soft_labels) ? 1 : 0);
+      const double u = utilization(n);
+      if (s > best_soft || (s == best_soft && u < best_u)) {
+        best = i;
+        best_soft = s;
+        best_u = u;
+      }
+    }
+    return best < 0 ? "" : nodes_[best].id;
+  }
   if ((Strategy)strategy == Strategy::kNodeAffinity) {
     auto it = node_idx_.find(affinity_node);
     if (it != node_idx_.end() && nodes_[it->second].alive) {

@@ -15,14 +15,25 @@
 namespace caamd_rt {
 
 using ResMap = std::map<std::string, double>;
+using LabelMap = std::map<std::string, std::string>;
 
-enum class Strategy { kHybrid = 0, kSpread = 1, kNodeAffinity = 2 };
+// One node-label condition (reference: python/ray/util/scheduling_strategies.py:135
+// In / NotIn / Exists / DoesNotExist).
+enum class LabelOp { kIn = 0, kNotIn = 1, kExists = 2, kDoesNotExist = 3 };
+struct LabelCond {
+  std::string key;
+  int op;
+  std::vector<std::string> values;
+};
+
+enum class Strategy { kHybrid = 0, kSpread = 1, kNodeAffinity = 2, kLabel = 3 };
 enum class PgStrategy { kPack = 0, kSpread = 1, kStrictPack = 2, kStrictSpread = 3 };
 
 struct NodeRes {
   std::string id;
   std::vector<double> total, avail;
   bool alive = true;
+  LabelMap labels;
 };
 
 class ClusterScheduler {
@@ -40,7 +51,12 @@ class ClusterScheduler {
 
   // "" = not schedulable right now, "!" = infeasible on every node (even when idle)
   std::string pick_node(const ResMap& demand, int strategy, const std::string& affinity_node,
-                        bool soft, const std::string& preferred_node);
+                        bool soft, const std::string& preferred_node,
+                        const std::vector<LabelCond>& hard = {},
+                        const std::vector<LabelCond>& soft_labels = {});
+  void set_labels(const std::string& id, const LabelMap& labels);
+  LabelMap labels(const std::string& id) const;
+  static bool labels_match(const LabelMap& labels, const std::vector<LabelCond>& conds);
   bool acquire(const std::string& node, const ResMap& demand);
   void release(const std::string& node, const ResMap& demand);
 
