@@ -98,6 +98,64 @@ def get_devices():
     return [get_device()]
 
 
+class _Accelerator:
+    """Process-wide settings of ``accelerate()`` (reference: train_loop_utils.py:278
+    ``accelerate`` / ``_TorchAccelerator``): automatic mixed precision for
+    ``prepare_model`` / ``prepare_optimizer`` / ``backward``."""
+
+    def __init__(self):
+        self.amp = False
+        self.dtype = None
+        self.scaler = None
+
+    def autocast_dtype(self, device):
+        if self.dtype is not None:
+            return self.dtype
+        import torch
+
+        # MI355X: bf16 autocast (fp32 range, no loss scaling); fp16 needs GradScaler
+        return torch.bfloat16
+
+
+_ACCEL = _Accelerator()
+
+
+def accelerate(amp: bool = False, amp_dtype=None):
+    """Enable automatic mixed precision for models / optimizers prepared afterwards.
+    ``amp_dtype`` defaults to bfloat16 (no loss scaling needed); ``torch.float16``
+    adds dynamic loss scaling through ``prepare_optimizer`` + ``backward``."""
+    _ACCEL.amp = bool(amp)
+    _ACCEL.dtype = amp_dtype
+    _ACCEL.scaler = None
+
+
+class _AmpForward:
+    """Wraps a module's forward in autocast and returns fp32 floating outputs
+    (the reference's _WrappedModel does the same)."""
+
+    def __init__(self, fwd, device, dtype):
+        self.fwd, self.device, self.dtype = fwd, device, dtype
+
+    def __call__(self, *args, **kwargs):
+        import torch
+
+        with torch.autocast(self.device.type, dtype=self.dtype):
+            out = self.fwd(*args, **kwargs)
+        return _to_fp32(out)
+
+
+def _to_fp32(x):
+    import torch
+
+    if isinstance(x, torch.Tensor):
+        return x.float() if x.is_floating_point() and x.dtype != torch.float32 else x
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_fp32(v) for v in x)
+    if isinstance(x, dict):
+        return {k: _to_fp32(v) for k, v in x.items()}
+    return x
+
+
 def prepare_model(model, move_to_device: bool = True, parallel_strategy: Optional[str] = "ddp",
                   parallel_strategy_kwargs: Optional[Dict[str, Any]] = None):
     import torch
@@ -106,6 +164,8 @@ def prepare_model(model, move_to_device: bool = True, parallel_strategy: Optiona
     dev = get_device()
     if move_to_device:
         model = model.to(dev)
+    if _ACCEL.amp:
+        model.forward = _AmpForward(model.forward, dev, _ACCEL.autocast_dtype(dev))
     if not dist.is_initialized() or dist.get_world_size() == 1 or parallel_strategy is None:
         return model
     kw = dict(parallel_strategy_kwargs or {})
@@ -195,16 +255,41 @@ def prepare_data_loader(data_loader, add_dist_sampler: bool = True, move_to_devi
     return data_loader
 
 
+class _ScaledOptimizer:
+    """fp16 AMP: steps through a GradScaler (skips steps with inf/nan grads)."""
+
+    def __init__(self, optimizer, scaler):
+        self.optimizer, self.scaler = optimizer, scaler
+
+    def step(self, closure=None):
+        self.scaler.step(self.optimizer)
+        self.scaler.update()
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.optimizer.zero_grad(set_to_none=set_to_none)
+
+    def __getattr__(self, name):
+        return getattr(self.optimizer, name)
+
+
 def prepare_optimizer(optimizer):
+    """With ``accelerate(amp=True, amp_dtype=torch.float16)`` the optimizer steps
+    through a dynamic loss scaler; bf16 / no AMP returns it unchanged."""
+    import torch
+
+    if _ACCEL.amp and _ACCEL.dtype == torch.float16:
+        dev = get_device()
+        _ACCEL.scaler = torch.amp.GradScaler(dev.type)
+        return _ScaledOptimizer(optimizer, _ACCEL.scaler)
     return optimizer
 
 
 def backward(tensor):
-    tensor.backward()
-
-
-def accelerate(amp: bool = False):
-    pass
+    """``loss.backward()``, scaled when fp16 AMP is active."""
+    if _ACCEL.scaler is not None:
+        _ACCEL.scaler.scale(tensor).backward()
+    else:
+        tensor.backward()
 
 
 def enable_reproducibility(seed: int = 0):

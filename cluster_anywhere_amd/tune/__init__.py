@@ -3,8 +3,10 @@ from ..train.checkpoint import Checkpoint
 from ..train.config import CheckpointConfig, FailureConfig, RunConfig
 from .callback import Callback, CLIReporter, CSVLoggerCallback, JsonLoggerCallback, LoggerCallback, ProgressReporter
 from .controller import Trial
-from .schedulers import (AsyncHyperBandScheduler, ASHAScheduler, FIFOScheduler, HyperBandScheduler,
-                         MedianStoppingRule, PopulationBasedTraining, TrialScheduler)
+from .schedulers import (PB2, AsyncHyperBandScheduler, ASHAScheduler, DistributeResources, FIFOScheduler,
+                         HyperBandForBOHB, HyperBandScheduler, MedianStoppingRule, PopulationBasedTraining,
+                         ResourceChangingScheduler, TrialScheduler)
+from .search.bohb import TuneBOHB
 from .search import (BasicVariantGenerator, ConcurrencyLimiter, RandomLocalSearch, Repeater, Searcher,
                      choice, grid_search, lograndint, loguniform, qlograndint, qloguniform, qrandint, qrandn,
                      quniform, randint, randn, sample_from, uniform)

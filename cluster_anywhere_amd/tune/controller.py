@@ -249,8 +249,15 @@ class TuneController:
         cc = run_config.checkpoint_config
         self.ckpt_freq = getattr(cc, "checkpoint_frequency", 0) or 0
         self.ckpt_at_end = bool(getattr(cc, "checkpoint_at_end", False))
-        if isinstance(self.scheduler, PopulationBasedTraining) and not self.ckpt_freq:
-            self.ckpt_freq = 1
+        from .schedulers import HyperBandForBOHB, HyperBandScheduler, ResourceChangingScheduler
+
+        if isinstance(self.scheduler, (PopulationBasedTraining, HyperBandScheduler, ResourceChangingScheduler)) \
+                and not self.ckpt_freq:
+            self.ckpt_freq = 1  # pausing schedulers resume trials from checkpoints
+        if isinstance(self.scheduler, ResourceChangingScheduler):
+            self.scheduler.controller = self
+        if isinstance(self.scheduler, HyperBandForBOHB):
+            self.scheduler.searcher = self.searcher
         sp = os.path.join(exp_dir, "searcher_state.pkl")
         if trials is not None and os.path.exists(sp):
             self.searcher = Searcher.load(sp)
@@ -323,15 +330,25 @@ class TuneController:
                 cb.on_trial_start(iteration=0, trials=self.trials, trial=t)
 
     def _fill(self):
+        by_id = {t.trial_id: t for t in self.trials}
+        for tid in self.scheduler.pop_stopped_trials():
+            t = by_id.get(tid)
+            if t is not None and t.status in (Trial.PAUSED, Trial.PENDING):
+                self._complete(t)
         running = [t for t in self.trials if t.status == Trial.RUNNING]
         slots = self.max_concurrent - len(running)
-        # resume paused / pending (restored or exploited) trials first
-        for t in self.trials:
-            if slots <= 0:
-                return
-            if t.status in (Trial.PENDING, Trial.PAUSED) and t.actor is None:
-                self._launch(t)
-                slots -= 1
+        # resume paused / pending (restored or exploited) trials first, in the order
+        # the scheduler allows (synchronous HyperBand gates paused trials)
+        waiting = [t for t in self.trials if t.status in (Trial.PENDING, Trial.PAUSED) and t.actor is None]
+        while slots > 0 and waiting:
+            t = self.scheduler.choose_trial_to_run(waiting)
+            if t is None:
+                break
+            waiting.remove(t)
+            self._launch(t)
+            slots -= 1
+        if slots <= 0:
+            return
         while slots > 0 and not self.searcher_finished:
             tid = uuid.uuid4().hex[:8]
             cfg = self.searcher.suggest(tid)

@@ -78,7 +78,8 @@ def create_scheduler(scheduler: str, **kwargs):
     table = {"fifo": S.FIFOScheduler, "async_hyperband": S.AsyncHyperBandScheduler, "asynchyperband":
              S.AsyncHyperBandScheduler, "asha": S.ASHAScheduler, "hyperband": S.HyperBandScheduler,
              "median_stopping_rule": S.MedianStoppingRule, "medianstopping": S.MedianStoppingRule,
-             "pbt": S.PopulationBasedTraining}
+             "pbt": S.PopulationBasedTraining, "pb2": S.PB2, "hb_bohb": S.HyperBandForBOHB,
+             "resource_changing": S.ResourceChangingScheduler}
     if scheduler not in table:
         raise ValueError(f"unknown scheduler {scheduler!r}; available: {sorted(table)}")
     return table[scheduler](**kwargs)
@@ -87,8 +88,10 @@ def create_scheduler(scheduler: str, **kwargs):
 def create_searcher(search_alg: str, **kwargs):
     from . import search as S
 
+    from .search.bohb import TuneBOHB
+
     table = {"variant_generator": S.BasicVariantGenerator, "random": S.BasicVariantGenerator,
-             "random_local": S.RandomLocalSearch}
+             "random_local": S.RandomLocalSearch, "bohb": TuneBOHB}
     if search_alg not in table:
         raise ValueError(f"unknown searcher {search_alg!r}; available here: {sorted(table)} "
                          "(external optimisation libraries are not installed in this image)")

@@ -42,6 +42,16 @@ class TrialScheduler:
     def on_trial_error(self, trial):
         pass
 
+    # -- which waiting trial runs next (synchronous schedulers gate resumption) --
+    def choose_trial_to_run(self, candidates):
+        """Among PENDING / PAUSED trials without an actor, the one to launch next (None:
+        keep waiting). Reference: trial_scheduler.py ``choose_trial_to_run``."""
+        return candidates[0] if candidates else None
+
+    def pop_stopped_trials(self) -> List[str]:
+        """Trial ids of PAUSED trials the scheduler has decided to terminate."""
+        return []
+
 
 class FIFOScheduler(TrialScheduler):
     pass
@@ -85,14 +95,198 @@ class AsyncHyperBandScheduler(TrialScheduler):
 ASHAScheduler = AsyncHyperBandScheduler
 
 
-class HyperBandScheduler(AsyncHyperBandScheduler):
-    """Synchronous HyperBand approximated by its asynchronous successive-halving
-    form (the reference's HyperBandScheduler pauses whole brackets; ASHA has the
-    same promotion rule without the synchronisation barrier)."""
+class _Bracket:
+    """One HyperBand bracket: n trials, first milestone r, successive halving by eta."""
 
-    def __init__(self, time_attr="training_iteration", metric=None, mode=None, max_t=81,
-                 reduction_factor=3, stop_last_trials=True):
-        super().__init__(time_attr, metric, mode, max_t, 1, reduction_factor)
+    def __init__(self, s: int, n: int, r: float, eta: float, max_t: int):
+        self.s, self.n, self.eta, self.max_t = s, n, eta, max_t
+        self.milestone = min(max_t, max(1, int(round(r))))
+        self.trials: List[str] = []          # members still alive in this bracket
+        self.scores: Dict[str, float] = {}   # trial -> score at the current milestone
+        self.promoted = set()                # may resume past the current milestone
+        self.stopped = set()
+
+    def full(self):
+        return len(self.trials) + len(self.stopped) >= self.n
+
+
+class HyperBandScheduler(TrialScheduler):
+    """Synchronous HyperBand (reference: python/ray/tune/schedulers/hyperband.py:42;
+    Li et al. 2018). Trials are dealt into brackets s = s_max..0 of
+    n_s = ceil((s_max+1)/(s+1) * eta^s) trials whose first milestone is
+    max_t * eta^-s. A trial PAUSES when it reaches its bracket's milestone; once every
+    live member of the bracket is there, the top 1/eta are promoted (milestone x eta,
+    resumed from their checkpoints) and the rest are stopped."""
+
+    def __init__(self, time_attr: str = "training_iteration", metric=None, mode=None,
+                 max_t: int = 81, reduction_factor: float = 3, stop_last_trials: bool = True):
+        super().__init__(metric, mode)
+        self.time_attr, self.max_t, self.eta = time_attr, max_t, reduction_factor
+        self.s_max = int(math.floor(math.log(max_t) / math.log(reduction_factor) + 1e-9))
+        self.brackets: List[_Bracket] = []
+        self.of: Dict[str, _Bracket] = {}
+        self._next_s = self.s_max
+        self._to_stop: List[str] = []
+        self._at_milestone = set()
+
+    def _new_bracket(self):
+        s = self._next_s
+        self._next_s = self._next_s - 1 if self._next_s > 0 else self.s_max
+        n = int(math.ceil((self.s_max + 1) / (s + 1) * self.eta ** s))
+        b = _Bracket(s, n, self.max_t * self.eta ** (-s), self.eta, self.max_t)
+        self.brackets.append(b)
+        return b
+
+    def on_trial_add(self, trial):
+        b = self.brackets[-1] if self.brackets and not self.brackets[-1].full() else self._new_bracket()
+        b.trials.append(trial.trial_id)
+        self.of[trial.trial_id] = b
+
+    def on_trial_result(self, trial, result):
+        b = self.of.get(trial.trial_id)
+        t = result.get(self.time_attr, 0)
+        if t >= self.max_t:
+            return self.STOP
+        if b is None:
+            return self.CONTINUE
+        s = self._score(result)
+        if t < b.milestone or s is None:
+            return self.CONTINUE
+        b.scores[trial.trial_id] = s
+        self._at_milestone.add(trial.trial_id)
+        b.promoted.discard(trial.trial_id)
+        decision = self._maybe_cut(b)
+        if trial.trial_id in self._to_stop:
+            self._to_stop.remove(trial.trial_id)
+            return self.STOP
+        return decision if decision is not None else self.PAUSE
+
+    def _maybe_cut(self, b: _Bracket):
+        live = [tid for tid in b.trials if tid not in b.stopped]
+        if not b.full() or any(tid not in b.scores for tid in live):
+            return None  # wait for the whole bracket to reach the milestone
+        ranked = sorted(live, key=lambda tid: b.scores[tid], reverse=True)
+        keep = max(1, int(len(ranked) / b.eta))
+        for tid in ranked[keep:]:
+            b.stopped.add(tid)
+            self._to_stop.append(tid)
+        b.milestone = min(self.max_t, int(math.ceil(b.milestone * b.eta)))
+        b.scores = {}
+        for tid in ranked[:keep]:
+            b.promoted.add(tid)
+            self._at_milestone.discard(tid)
+        return None
+
+    def on_trial_complete(self, trial, result):
+        b = self.of.get(trial.trial_id)
+        if b is not None and trial.trial_id in b.trials:
+            b.trials.remove(trial.trial_id)
+            b.scores.pop(trial.trial_id, None)
+            self._maybe_cut(b)
+
+    on_trial_error = lambda self, trial: self.on_trial_complete(trial, None)  # noqa: E731
+
+    def choose_trial_to_run(self, candidates):
+        for t in candidates:
+            if getattr(t, "status", None) == "PENDING" and t.trial_id not in self._at_milestone:
+                return t
+        for t in candidates:
+            b = self.of.get(t.trial_id)
+            if b is not None and t.trial_id in b.promoted:
+                return t
+        return None
+
+    def pop_stopped_trials(self):
+        out, self._to_stop = self._to_stop, []
+        return out
+
+
+class HyperBandForBOHB(HyperBandScheduler):
+    """HyperBand whose successive-halving decisions feed the BOHB searcher
+    (reference: python/ray/tune/schedulers/hb_bohb.py:16): every milestone result
+    is reported to ``TuneBOHB`` so its density models are trained per budget."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        self.searcher = None
+
+    def on_trial_result(self, trial, result):
+        d = super().on_trial_result(trial, result)
+        if self.searcher is not None and d in (self.PAUSE, self.STOP) and hasattr(self.searcher, "on_budget_result"):
+            b = self.of.get(trial.trial_id)
+            self.searcher.on_budget_result(trial.trial_id, result, b.milestone if b else None)
+        return d
+
+
+class ResourceChangingScheduler(TrialScheduler):
+    """Wraps a scheduler and re-sizes running trials (reference:
+    python/ray/tune/schedulers/resource_changing_scheduler.py:592). After each
+    result the allocation function proposes resources for the trial; if they
+    differ, the trial is paused and relaunched from its latest checkpoint with the
+    new resources (a Trainable sees them via ``tune.get_trial_resources()``)."""
+
+    def __init__(self, base_scheduler: Optional[TrialScheduler] = None,
+                 resources_allocation_function: Optional[Callable] = None):
+        super().__init__()
+        self.base = base_scheduler or FIFOScheduler()
+        self.alloc = resources_allocation_function or DistributeResources()
+        self.controller = None
+
+    def set_search_properties(self, metric, mode, **spec):
+        super().set_search_properties(metric, mode, **spec)
+        return self.base.set_search_properties(metric, mode, **spec)
+
+    def on_trial_add(self, trial):
+        self.base.on_trial_add(trial)
+
+    def on_trial_result(self, trial, result):
+        d = self.base.on_trial_result(trial, result)
+        if d != self.CONTINUE:
+            return d
+        new = self.alloc(self.controller, trial, result, self)
+        if new and dict(new) != dict(trial.resources) and trial.latest_checkpoint is not None:
+            trial.resources = dict(new)
+            return self.PAUSE
+        return d
+
+    def on_trial_complete(self, trial, result):
+        self.base.on_trial_complete(trial, result)
+
+    def on_trial_error(self, trial):
+        self.base.on_trial_error(trial)
+
+    def choose_trial_to_run(self, candidates):
+        return self.base.choose_trial_to_run(candidates)
+
+    def pop_stopped_trials(self):
+        return self.base.pop_stopped_trials()
+
+
+class DistributeResources:
+    """Default allocation: spread the cluster's CPUs (and GPUs) evenly over the
+    running trials, never below the trial's base request."""
+
+    def __init__(self, add_bundles: bool = False, increase_by: Optional[Dict] = None,
+                 increase_by_times: int = -1, reserve_resources: Optional[Dict] = None):
+        self.reserve = reserve_resources or {}
+
+    def __call__(self, controller, trial, result, scheduler):
+        from ..core import api as core
+
+        if controller is None:
+            return None
+        running = [t for t in controller.trials if t.status == "RUNNING"] or [trial]
+        total = core.cluster_resources()
+        out = dict(trial.resources)
+        base = getattr(trial, "base_resources", None) or dict(trial.resources)
+        trial.base_resources = base
+        for key in ("CPU", "GPU"):
+            avail = float(total.get(key, 0)) - float(self.reserve.get(key, 0))
+            if avail <= 0 or key not in base:
+                continue
+            share = max(float(base[key]), math.floor(avail / len(running)))
+            out[key] = share
+        return out
 
 
 class MedianStoppingRule(TrialScheduler):
@@ -193,5 +387,80 @@ class PopulationBasedTraining(TrialScheduler):
         return self.CONTINUE
 
 
+class PB2(PopulationBasedTraining):
+    """Population Based Bandits (reference: python/ray/tune/schedulers/pb2.py:256;
+    Parker-Holder et al. 2020): PBT's exploit step, but the explore step picks the
+    new hyperparameters with a GP-UCB bandit fitted on (time, hyperparameters) ->
+    reward change observed across the population, inside ``hyperparam_bounds``."""
+
+    def __init__(self, time_attr: str = "training_iteration", metric=None, mode=None,
+                 perturbation_interval: float = 60.0, hyperparam_bounds: Optional[Dict] = None,
+                 quantile_fraction: float = 0.25, log_config: bool = True, seed=None,
+                 custom_explore_fn: Optional[Callable] = None, synch: bool = False):
+        self.bounds = dict(hyperparam_bounds or {})
+        if not self.bounds:
+            raise ValueError("PB2 needs hyperparam_bounds={name: [low, high]}")
+        super().__init__(time_attr, metric, mode, perturbation_interval,
+                         hyperparam_mutations={k: list(v) for k, v in self.bounds.items()},
+                         quantile_fraction=quantile_fraction, custom_explore_fn=custom_explore_fn,
+                         seed=seed, synch=synch)
+        self.data: List[tuple] = []  # (t, x-normalised..., reward delta)
+        self._last = {}              # trial_id -> (t, score)
+        self._np_rng = None
+
+    def _norm(self, cfg):
+        out = []
+        for k, (lo, hi) in self.bounds.items():
+            v = float(cfg.get(k, lo))
+            out.append((v - lo) / (hi - lo) if hi > lo else 0.0)
+        return out
+
+    def on_trial_result(self, trial, result):
+        t = result.get(self.time_attr, 0)
+        s = self._score(result)
+        if s is not None:
+            prev = self._last.get(trial.trial_id)
+            if prev is not None and t > prev[0]:
+                self.data.append((t, *self._norm(trial.config), (s - prev[1]) / (t - prev[0])))
+            self._last[trial.trial_id] = (t, s)
+        return super().on_trial_result(trial, result)
+
+    def _explore(self, config):
+        import numpy as np
+
+        if self._np_rng is None:
+            self._np_rng = np.random.default_rng(self.rng.randrange(1 << 30))
+        new = copy.deepcopy(config)
+        keys = list(self.bounds)
+        cands = self._np_rng.random((256, len(keys)))
+        if len(self.data) >= 3:
+            from sklearn.gaussian_process import GaussianProcessRegressor
+            from sklearn.gaussian_process.kernels import RBF, WhiteKernel
+
+            D = np.asarray(self.data[-500:], dtype=np.float64)
+            X, y = D[:, :-1], D[:, -1]
+            tmax = max(1.0, X[:, 0].max())
+            X = X.copy()
+            X[:, 0] /= tmax
+            y = (y - y.mean()) / (y.std() + 1e-9)
+            gp = GaussianProcessRegressor(kernel=RBF(length_scale=0.5) + WhiteKernel(1e-2), normalize_y=False,
+                                          random_state=0)
+            gp.fit(X, y)
+            tcol = np.full((len(cands), 1), 1.0)  # predict at the latest time
+            mu, sd = gp.predict(np.hstack([tcol, cands]), return_std=True)
+            beta = 2.0
+            best = cands[int(np.argmax(mu + beta * sd))]
+        else:
+            best = cands[0]
+        for k, x in zip(keys, best):
+            lo, hi = self.bounds[k]
+            v = lo + float(x) * (hi - lo)
+            new[k] = type(config[k])(v) if isinstance(config.get(k), int) else v
+        if self.explore_fn:
+            new = self.explore_fn(new)
+        return new
+
+
 __all__ = ["TrialScheduler", "FIFOScheduler", "AsyncHyperBandScheduler", "ASHAScheduler",
-           "HyperBandScheduler", "MedianStoppingRule", "PopulationBasedTraining"]
+           "HyperBandScheduler", "HyperBandForBOHB", "MedianStoppingRule", "PopulationBasedTraining",
+           "PB2", "ResourceChangingScheduler", "DistributeResources"]

@@ -100,3 +100,43 @@ def test_resume_from_checkpoint(cluster, tmp_path):
                       run_config=RunConfig(name="b", storage_path=str(tmp_path)))
     r2 = t2.fit()
     assert [m["epoch"] for m in r2.metrics_dataframe.to_dict("records")] == [2, 3]
+
+
+def test_accelerate_amp_bf16_and_fp16_scaler():
+    """accelerate(amp=True): prepare_model runs forward under autocast and returns
+    fp32 outputs; fp16 AMP steps through a loss scaler (reference
+    train_loop_utils.py:278)."""
+    import torch
+
+    from cluster_anywhere_amd.train import torch as tt
+
+    torch.manual_seed(0)
+    ref = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    m = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    m.load_state_dict(ref.state_dict())
+    try:
+        tt.accelerate(amp=True)
+        pm = tt.prepare_model(m, move_to_device=False, parallel_strategy=None)
+        x = torch.randn(8, 16)
+        seen = []
+        h = pm[0].register_forward_hook(lambda mod, i, o: seen.append(o.dtype))
+        y = pm(x)
+        h.remove()
+        assert seen == [torch.bfloat16] and y.dtype == torch.float32
+        opt = tt.prepare_optimizer(torch.optim.SGD(pm.parameters(), lr=0.1))
+        loss = y.square().mean()
+        tt.backward(loss)
+        yr = ref(x)
+        yr.square().mean().backward()
+        g, gr = pm[0].weight.grad, ref[0].weight.grad
+        assert torch.allclose(g, gr, rtol=0.1, atol=2e-2)
+        opt.step()
+        # fp16: scaled backward, scaler-driven step
+        tt.accelerate(amp=True, amp_dtype=torch.float16)
+        opt2 = tt.prepare_optimizer(torch.optim.SGD(ref.parameters(), lr=0.1))
+        assert hasattr(opt2, "scaler")
+        ref.zero_grad()
+        tt.backward(ref(x).square().mean())
+        opt2.step()
+    finally:
+        tt.accelerate(amp=False)
