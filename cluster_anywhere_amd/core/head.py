@@ -391,7 +391,12 @@ class Head:
             self.starting[key] = max(0, self.starting[key] - 1)
             pending = self.pending_spawn.pop(worker_id, None)
             if pending and pending[0] == "actor":
-                self._start_actor_on(self.actors[pending[1]], w)
+                a = self.actors.get(pending[1])
+                st = a.spec.strategy if a is not None and a.spec else None
+                if a is None or a.state == "DEAD" or (st and st[0] == "pg" and st[1] not in self.pgs):
+                    self._kill_worker(worker_id)  # its actor died (or lost its group) meanwhile
+                    return
+                self._start_actor_on(a, w)
             else:
                 w.idle = True
                 self.idle[key].append(w)
@@ -1619,6 +1624,16 @@ class Head:
                     # group resources vanish with the group; device ids go back to the node
                     self._give_gpus(a.acquired[0], a.gpu_ids or (), float(a.spec.resources.get("GPU", 0) or 0))
                     a.acquired = None
+                w = self.workers.get(a.worker) if a.worker is not None else None
+                if w is None or not w.alive:
+                    # still being spawned / restarted: its worker must never start the actor
+                    # (the device ids above may already belong to someone else)
+                    for wid, pend in list(self.pending_spawn.items()):
+                        if pend == ("actor", a.actor_id):
+                            del self.pending_spawn[wid]
+                            self._kill_worker(wid)
+                    a.state = "DEAD"
+                    self._fail_actor_queue(a, "ActorDiedError", "placement group removed")
                 self._kill_worker(a.worker)
         self.sched.remove_pg(pg_id.hex())
         self._retry_pending_pgs()

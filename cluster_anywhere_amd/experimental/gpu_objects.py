@@ -71,9 +71,28 @@ def reduce_ipc(t):
     return _rebuild_ipc, (rebuild, args, physical_gpu(t.device.index), os.getpid())
 
 
+def _producer_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+        return True
+    except ProcessLookupError:
+        return False
+    except PermissionError:
+        return True
+
+
 def _rebuild_ipc(rebuild, args, phys: int, producer_pid: int):
     import torch
 
+    if producer_pid != os.getpid() and not _producer_alive(producer_pid):
+        # the HBM behind the handle belonged to a process that has exited: mapping it
+        # would read freed memory. Readers must finish with IPC views before the
+        # producer is killed (keep the producer actor alive, or use the default
+        # host-copy transport for objects that outlive it).
+        from ..exceptions import ObjectLostError
+
+        raise ObjectLostError("", f"the producer (pid {producer_pid}) of this tensor_transport='ipc' "
+                                  "object has exited; its GPU memory is gone")
     if not torch.cuda.is_available():
         raise RuntimeError("an object sent with tensor_transport='ipc' can only be read by a GPU "
                            "process on the producer's node")

@@ -202,7 +202,7 @@ int64_t ObjectStore::create(const std::string& id, uint64_t size, uint64_t meta)
     unlock();
     return -3;  // table full
   }
-  if (e->state == 1 || e->state == 2 || e->state == 4) {
+  if (e->state == 1 || e->state == 2 || e->state == 4 || e->state == 5) {
     if (memcmp(e->id, id.data(), kIdBytes) == 0) {
       unlock();
       return -2;
@@ -230,7 +230,14 @@ bool ObjectStore::seal(const std::string& id) {
   lock();
   ObjectEntry* e = find((const uint8_t*)id.data(), false);
   bool ok = e && e->state == 1;
-  if (ok) __atomic_store_n(&e->state, 2u, __ATOMIC_RELEASE);
+  if (ok) {
+    __atomic_store_n(&e->state, 2u, __ATOMIC_RELEASE);
+  } else if (e && e->state == 5) {
+    // removed while its creator was still writing: the block was kept for the
+    // writer; free it now that the copy-in is over
+    free_block(e->offset - sizeof(BlockHdr));
+    e->state = 3;
+  }
   unlock();
   return ok;
 }
@@ -275,10 +282,12 @@ bool ObjectStore::contains(const std::string& id) {
 bool ObjectStore::remove(const std::string& id) {
   lock();
   ObjectEntry* e = find((const uint8_t*)id.data(), false);
-  bool ok = e != nullptr && e->state != 4;
+  bool ok = e != nullptr && e->state != 4 && e->state != 5;
   if (ok) {
     hdr_->num_objects--;
-    if (e->pins > 0) {
+    if (e->state == 1) {
+      e->state = 5;  // unsealed: the creator may still be copying in; freed at its seal/abort
+    } else if (e->pins > 0) {
       e->state = 4;  // zombie: freed by the last unpin
     } else {
       free_block(e->offset - sizeof(BlockHdr));
@@ -292,11 +301,11 @@ bool ObjectStore::remove(const std::string& id) {
 bool ObjectStore::abort(const std::string& id) {
   lock();
   ObjectEntry* e = find((const uint8_t*)id.data(), false);
-  bool ok = e && e->state == 1;
+  bool ok = e && (e->state == 1 || e->state == 5);
   if (ok) {
     free_block(e->offset - sizeof(BlockHdr));
+    if (e->state == 1) hdr_->num_objects--;
     e->state = 3;
-    hdr_->num_objects--;
   }
   unlock();
   return ok;

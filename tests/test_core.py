@@ -531,3 +531,32 @@ def test_gpu_ids_return_when_placement_group_removed():
         assert ray.get(H.remote().f.remote(), timeout=30) == 3
     finally:
         ray.shutdown()
+
+
+def test_pg_removed_while_actor_spawning_or_restarting(cluster):
+    """Removing a placement group while its actor's worker is still starting (or
+    restarting) must kill that worker, not start the actor outside the group
+    (head.py PG-removal race)."""
+    from cluster_anywhere_amd.util.placement_group import placement_group, remove_placement_group
+    from cluster_anywhere_amd.util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+    @ray.remote(num_cpus=1, max_restarts=2)
+    class P:
+        def pid(self):
+            return os.getpid()
+
+    total = ray.cluster_resources().get("CPU")
+    for restart in (False, True):
+        pg = placement_group([{"CPU": 1}])
+        ray.get(pg.ready(), timeout=30)
+        a = P.options(scheduling_strategy=PlacementGroupSchedulingStrategy(pg, 0)).remote()
+        if restart:
+            pid = ray.get(a.pid.remote(), timeout=60)
+            os.kill(pid, 9)
+        remove_placement_group(pg)  # during spawn / during restart
+        with pytest.raises(ray.exceptions.RayActorError):
+            ray.get(a.pid.remote(), timeout=60)
+    deadline = time.time() + 20
+    while time.time() < deadline and ray.available_resources().get("CPU") != total:
+        time.sleep(0.1)
+    assert ray.available_resources().get("CPU") == total

@@ -1,6 +1,8 @@
 """Runtime on a real MI355X: GPU actors (ROCR_VISIBLE_DEVICES isolation, HIP
 kernels inside workers), GPU tensors through the object store, and TorchTrainer
 in actor mode driving the fused GPT-2 step on the GPU."""
+import time
+
 import pytest
 import torch
 
@@ -124,8 +126,16 @@ def test_gpu_object_ipc_zero_copy(cluster):
     x = torch.arange(64, device="cuda", dtype=torch.float32)
     r2 = ray.put(x, _tensor_transport="ipc")
     assert ray.get(c.hold.remote(r2), timeout=60) == (True, float(sum(range(64))))
-    ray.kill(p)
+    # readers release their IPC views BEFORE the producer goes away (the producer's
+    # HBM backs them); a read after the producer died fails loudly instead of
+    # mapping freed memory
     ray.kill(c)
+    del t
+    torch.cuda.synchronize()
+    ray.kill(p)
+    time.sleep(1.0)
+    with pytest.raises(ray.exceptions.ObjectLostError):
+        ray.get(ref, timeout=60)
 
 
 def test_collective_rccl_single_rank(cluster):
