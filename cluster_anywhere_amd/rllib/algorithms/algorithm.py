@@ -1,7 +1,9 @@
 """Algorithm / AlgorithmConfig (reference: rllib/algorithms/algorithm.py,
 algorithm_config.py — builder methods ``environment``, ``env_runners``,
 ``learners``, ``training``, ``rl_module``, ``evaluation``, ``debugging``,
-``reporting``, ``resources``, ``framework``, ``api_stack``).
+``reporting``, ``resources``, ``framework``, ``api_stack``, ``multi_agent``,
+``callbacks``; connector hooks ``env_runners(env_to_module_connector=...,
+module_to_env_connector=...)`` and ``training(learner_connector=...)``).
 
 ``Algorithm`` is a Tune ``Trainable``: ``train()`` runs one
 ``training_step()`` and returns RLlib-style nested metrics
@@ -21,10 +23,13 @@ import numpy as np
 import torch
 
 from ...tune.trainable import Trainable
-from ..core.learner import Learner, LearnerGroup
-from ..core.rl_module import DefaultActorCriticModule
+from ..callbacks import RLlibCallback, make_callbacks
+from ..core.learner import Learner, LearnerGroup, MultiLearner
+from ..core.multi_rl_module import DEFAULT_MODULE_ID, MultiRLModuleSpec
+from ..core.rl_module import DefaultActorCriticModule, RLModuleSpec
 from ..env import make_env
-from ..env.env_runner import EnvRunnerGroup
+from ..env.env_runner import EnvRunner, EnvRunnerGroup
+from ..env.multi_agent_env_runner import MultiAgentEnvRunner
 
 
 class _NotProvided:
@@ -32,6 +37,22 @@ class _NotProvided:
 
 
 NotProvided = _NotProvided()
+
+
+class PolicySpec:
+    """Per-module entry of ``config.multi_agent(policies={...})`` (reference:
+    rllib/policy/policy.py PolicySpec): optional explicit spaces and a model
+    config override for the module."""
+
+    def __init__(self, policy_class=None, observation_space=None, action_space=None, config=None):
+        self.policy_class = policy_class
+        self.observation_space = observation_space
+        self.action_space = action_space
+        self.config = dict(config or {})
+
+
+def _default_mapping(agent_id, episode, **kwargs):
+    return DEFAULT_MODULE_ID
 
 
 class AlgorithmConfig:
@@ -61,6 +82,18 @@ class AlgorithmConfig:
         self.grad_clip = None
         self.model_config: Dict = {}
         self.rl_module_class = None
+        self.learner_connector = None
+        # connectors
+        self.env_to_module_connector = None
+        self.module_to_env_connector = None
+        # multi-agent
+        self.policies: Optional[Dict[str, Any]] = None
+        self.policy_mapping_fn: Callable = _default_mapping
+        self.policies_to_train = None
+        self.multi_rl_module_spec: Optional[MultiRLModuleSpec] = None
+        # callbacks
+        self.callbacks_class = None
+        self.callbacks_functions: Dict[str, Callable] = {}
         # misc
         self.seed = None
         self.evaluation_interval = None
@@ -82,10 +115,13 @@ class AlgorithmConfig:
         return self._set(env=env, env_config=env_config)
 
     def env_runners(self, *, num_env_runners=NotProvided, num_envs_per_env_runner=NotProvided,
-                    rollout_fragment_length=NotProvided, num_cpus_per_env_runner=NotProvided, **_):
+                    rollout_fragment_length=NotProvided, num_cpus_per_env_runner=NotProvided,
+                    env_to_module_connector=NotProvided, module_to_env_connector=NotProvided, **_):
         return self._set(num_env_runners=num_env_runners, num_envs_per_env_runner=num_envs_per_env_runner,
                          rollout_fragment_length=rollout_fragment_length,
-                         num_cpus_per_env_runner=num_cpus_per_env_runner)
+                         num_cpus_per_env_runner=num_cpus_per_env_runner,
+                         env_to_module_connector=env_to_module_connector,
+                         module_to_env_connector=module_to_env_connector)
 
     rollouts = env_runners
 
@@ -107,10 +143,76 @@ class AlgorithmConfig:
         for mc in (model_config, model_config_dict):
             if mc is not NotProvided and mc is not None:
                 self.model_config.update(dict(mc))
-        if rl_module_spec is not NotProvided and rl_module_spec is not None:
+        if isinstance(rl_module_spec, MultiRLModuleSpec):
+            self.multi_rl_module_spec = rl_module_spec
+        elif rl_module_spec is not NotProvided and rl_module_spec is not None:
             self.rl_module_class = getattr(rl_module_spec, "module_class", None)
             self.model_config.update(getattr(rl_module_spec, "model_config", None) or {})
         return self
+
+    def multi_agent(self, *, policies=NotProvided, policy_mapping_fn=NotProvided, policies_to_train=NotProvided,
+                    **_):
+        """``policies``: a set/list of module ids or a dict id -> PolicySpec /
+        RLModuleSpec / (obs_space, act_space) / None; ``policy_mapping_fn(agent_id,
+        episode, **kw)`` -> module id (fixed per episode)."""
+        if policies is not NotProvided:
+            self.policies = {p: None for p in policies} if not isinstance(policies, dict) else dict(policies)
+        if policy_mapping_fn is not NotProvided and policy_mapping_fn is not None:
+            self.policy_mapping_fn = policy_mapping_fn
+        if policies_to_train is not NotProvided:
+            self.policies_to_train = None if policies_to_train is None else list(policies_to_train)
+        return self
+
+    def callbacks(self, callbacks_class=NotProvided, **on_hooks):
+        """A callback class (or list of classes), and/or ``on_<hook>=fn`` functions."""
+        if callbacks_class is not NotProvided:
+            self.callbacks_class = callbacks_class
+        for k, fn in on_hooks.items():
+            if fn is not NotProvided and fn is not None:
+                self.callbacks_functions[k] = fn
+        return self
+
+    @property
+    def is_multi_agent(self) -> bool:
+        return self.policies is not None
+
+    def _module_specs(self) -> MultiRLModuleSpec:
+        specs = dict(self.multi_rl_module_spec.rl_module_specs) if self.multi_rl_module_spec else {}
+        for mid, ps in (self.policies or {}).items():
+            if mid in specs:
+                continue
+            if isinstance(ps, RLModuleSpec):
+                specs[mid] = ps
+            elif isinstance(ps, PolicySpec):
+                specs[mid] = RLModuleSpec(None, ps.config.get("model", ps.config), ps.observation_space,
+                                          ps.action_space)
+            elif isinstance(ps, tuple) and len(ps) == 2:
+                specs[mid] = RLModuleSpec(None, {}, ps[0], ps[1])
+        return MultiRLModuleSpec(specs)
+
+    def module_ids(self):
+        ids = list(self.policies or {})
+        if self.multi_rl_module_spec:
+            ids += [m for m in self.multi_rl_module_spec.rl_module_specs if m not in ids]
+        return ids
+
+    def multi_module_factory(self) -> Callable:
+        spec = self._module_specs()
+        cls = self.rl_module_class or self.default_module_class()
+        mc = dict(self.model_config)
+        return lambda spaces: spec.build(spaces, cls, mc)
+
+    def module_factories(self) -> Dict[str, Callable]:
+        spec = self._module_specs()
+        cls = self.rl_module_class or self.default_module_class()
+        return {mid: spec.module_factory(mid, cls, dict(self.model_config)) for mid in self.module_ids()}
+
+    def policy_spaces(self) -> Dict[str, tuple]:
+        out = {}
+        for mid, sp in self._module_specs().rl_module_specs.items():
+            if sp.observation_space is not None and sp.action_space is not None:
+                out[mid] = (sp.observation_space, sp.action_space)
+        return out
 
     def evaluation(self, *, evaluation_interval=NotProvided, evaluation_duration=NotProvided, **_):
         return self._set(evaluation_interval=evaluation_interval, evaluation_duration=evaluation_duration)
@@ -194,7 +296,13 @@ class AlgorithmConfig:
                 "rollout_fragment_length": self.get_rollout_fragment_length(), "seed": self.seed,
                 "gamma": self.gamma, "module_factory": self.module_factory(),
                 "metrics_num_episodes_for_smoothing": self.metrics_num_episodes_for_smoothing,
-                "need_next_obs": False}
+                "need_next_obs": False,
+                "env_to_module_connector": self.env_to_module_connector,
+                "module_to_env_connector": self.module_to_env_connector,
+                "callbacks_class": self.callbacks_class, "callbacks_functions": dict(self.callbacks_functions),
+                **({"policies": self.module_ids(), "policy_mapping_fn": self.policy_mapping_fn,
+                    "policy_spaces": self.policy_spaces(), "multi_module_factory": self.multi_module_factory()}
+                   if self.is_multi_agent else {})}
 
     def learner_config(self) -> Dict[str, Any]:
         return dict(self.to_dict())
@@ -202,6 +310,11 @@ class AlgorithmConfig:
     def validate(self):
         if self.env is None:
             raise ValueError("config.environment(env=...) is required")
+        if self.is_multi_agent:
+            if not self.module_ids():
+                raise ValueError("config.multi_agent(policies=...) needs at least one module id")
+            if self.algo_class is not None and not getattr(self.algo_class, "supports_multi_agent", False):
+                raise NotImplementedError(f"{self.algo_class.__name__} has no multi-agent training step yet")
 
     def build_algo(self, env=None, logger_creator=None) -> "Algorithm":
         if env is not None:
@@ -215,6 +328,10 @@ class AlgorithmConfig:
 class Algorithm(Trainable):
     config_class = AlgorithmConfig
     learner_class = Learner
+    supports_multi_agent = False
+    is_multi_agent = False
+    callbacks = RLlibCallback()  # replaced per instance in setup()
+    _connector_state = None
 
     @classmethod
     def get_default_config(cls) -> AlgorithmConfig:
@@ -238,14 +355,29 @@ class Algorithm(Trainable):
         if c.seed is not None:
             torch.manual_seed(c.seed)
             np.random.seed(c.seed)
-        self.env_runner_group = EnvRunnerGroup(c.runner_config(), c.num_env_runners, c.num_cpus_per_env_runner)
+        self.callbacks = make_callbacks(c.callbacks_class, c.callbacks_functions)
+        self.is_multi_agent = c.is_multi_agent
+        runner_cls = MultiAgentEnvRunner if self.is_multi_agent else EnvRunner
+        self.env_runner_group = EnvRunnerGroup(c.runner_config(), c.num_env_runners, c.num_cpus_per_env_runner,
+                                               runner_cls=runner_cls)
         self.obs_space, self.act_space = self.env_runner_group.spaces()
-        self.learner_group = LearnerGroup(self.learner_class, c.learner_config(), c.module_factory(),
-                                          self.obs_space, self.act_space)
+        if self.is_multi_agent:
+            self.module_spaces = self.obs_space  # module id -> (obs_space, act_space)
+            train = c.policies_to_train or c.module_ids()
+            facs = c.module_factories()
+            self.learner_group = LearnerGroup(MultiLearner.of(self.learner_class), c.learner_config(),
+                                              {m: facs[m] for m in train},
+                                              {m: self.module_spaces[m][0] for m in train},
+                                              {m: self.module_spaces[m][1] for m in train})
+        else:
+            self.learner_group = LearnerGroup(self.learner_class, c.learner_config(), c.module_factory(),
+                                              self.obs_space, self.act_space)
         self.env_steps_sampled = 0
         self.env_steps_trained = 0
+        self.agent_steps_sampled = 0
         self.setup_algo()
         self._sync_weights()
+        self.callbacks.on_algorithm_init(algorithm=self, metrics_logger=None)
 
     def setup_algo(self):
         pass
@@ -259,45 +391,66 @@ class Algorithm(Trainable):
     def step(self) -> Dict[str, Any]:
         t0 = time.time()
         learner_stats = self.training_step()
+        self._connector_state = self.env_runner_group.sync_connector_states()
         m = self.env_runner_group.metrics()
-        out = {"env_runners": m, "learners": {"default_policy": learner_stats},
+        learners = learner_stats if self.is_multi_agent else {"default_policy": learner_stats}
+        out = {"env_runners": m, "learners": learners,
                "num_env_steps_sampled_lifetime": self.env_steps_sampled,
                "num_env_steps_trained_lifetime": self.env_steps_trained,
                "episode_return_mean": m["episode_return_mean"],
                "timers": dict(getattr(self, "_timers", {}), training_step_s=time.time() - t0)}
+        if self.is_multi_agent:
+            out["num_agent_steps_sampled_lifetime"] = self.agent_steps_sampled
         c = self.algo_config
         if c.evaluation_interval and (self.iteration + 1) % c.evaluation_interval == 0:
             out["evaluation"] = self.evaluate()
+        self.callbacks.on_train_result(algorithm=self, metrics_logger=None, result=out)
         return out
 
-    def evaluate(self) -> Dict[str, Any]:
-        c = self.algo_config
-        env = make_env(c.env, c.env_config)
-        module = c.module_factory()(self.obs_space, self.act_space)
-        module.set_state(self.learner_group.get_module_state())
-        rets = []
-        for ep in range(c.evaluation_duration):
-            obs, _ = env.reset(seed=10_000 + ep)
-            done, ret = False, 0.0
-            while not done:
-                a = module.forward_inference({"obs": torch.from_numpy(np.asarray(obs)[None])})["actions"][0]
-                obs, r, te, tr, _ = env.step(a.numpy())
-                ret += r
-                done = te or tr
-            rets.append(ret)
-        return {"env_runners": {"episode_return_mean": float(np.mean(rets)), "num_episodes": len(rets)}}
+    def _evaluation_runner(self):
+        r = getattr(self, "_eval_runner", None)
+        if r is None:
+            c = self.algo_config
+            cfg = dict(c.runner_config(), num_envs_per_env_runner=1, seed=10_000)
+            cls = MultiAgentEnvRunner if self.is_multi_agent else EnvRunner
+            r = self._eval_runner = cls(cfg, 0)
+        return r
 
-    def compute_single_action(self, obs, explore: bool = False):
-        module = getattr(self, "_inference_module", None)
-        if module is None:
-            module = self._inference_module = self.algo_config.module_factory()(self.obs_space, self.act_space)
-        module.set_state(self.learner_group.get_module_state())
+    def evaluate(self) -> Dict[str, Any]:
+        """``evaluation_duration`` greedy episodes on a local evaluation runner
+        (same connectors, with the training runners' merged connector state)."""
+        c = self.algo_config
+        self.callbacks.on_evaluate_start(algorithm=self, metrics_logger=None)
+        r = self._evaluation_runner()
+        r.set_weights(self.learner_group.get_module_state())
+        if getattr(self, "_connector_state", None):
+            r.set_connector_state(self._connector_state)
+        r.reset_envs(10_000)
+        rets = r.sample_episodes(c.evaluation_duration, explore=False)
+        out = {"env_runners": {"episode_return_mean": float(np.mean(rets)), "num_episodes": len(rets)}}
+        if self.is_multi_agent:
+            m = r.get_metrics()
+            out["env_runners"]["module_episode_returns_mean"] = {
+                k: float(np.mean(v[-len(rets):])) for k, v in m["module_episode_returns_mean"].items() if v}
+        self.callbacks.on_evaluate_end(algorithm=self, metrics_logger=None, evaluation_metrics=out)
+        return out
+
+    def compute_single_action(self, obs, explore: bool = False, policy_id: Optional[str] = None):
+        module = self.get_module(policy_id)
         b = {"obs": torch.from_numpy(np.asarray(obs)[None])}
         out = module.forward_exploration(b) if explore else module.forward_inference(b)
         return out["actions"][0].numpy()
 
-    def get_module(self):
-        m = self.algo_config.module_factory()(self.obs_space, self.act_space)
+    def get_module(self, module_id: Optional[str] = None):
+        c = self.algo_config
+        if self.is_multi_agent:
+            st = self.learner_group.get_module_state()
+            mid = module_id or next(iter(st))
+            obs, act = self.module_spaces[mid]
+            m = c.module_factories()[mid](obs, act)
+            m.set_state(st[mid])
+            return m
+        m = c.module_factory()(self.obs_space, self.act_space)
         m.set_state(self.learner_group.get_module_state())
         return m
 
@@ -325,6 +478,7 @@ class Algorithm(Trainable):
         self.env_steps_trained = a["env_steps_trained"]
         self.load_extra_state(a.get("extra", {}))
         self._sync_weights()
+        self.callbacks.on_checkpoint_loaded(algorithm=self)
 
     def save_to_path(self, path: Optional[str] = None) -> str:
         path = path or os.path.join(self._trial_dir or ".", f"checkpoint_{self.iteration:06d}")

@@ -1,7 +1,9 @@
 """PPO (reference: rllib/algorithms/ppo/ppo.py, ppo_learner.py,
 torch/ppo_torch_learner.py): clipped surrogate + clipped value loss + entropy
-bonus + optional adaptive KL penalty; GAE on the learner's device with the
-``rl_returns.hip`` kernel (one thread per env column, reverse scan over T)."""
+bonus + optional adaptive KL penalty. The train batch comes out of a learner
+connector pipeline (``GeneralAdvantageEstimation``: GAE on the learner's device
+with the ``rl_returns.hip`` kernel, one thread per column, reverse scan over T);
+multi-agent PPO trains one learner per module on its own padded fragment."""
 from __future__ import annotations
 
 from typing import Any, Dict
@@ -66,52 +68,76 @@ class PPOLearner(Learner):
             self.kl_coeff *= 0.5
         return self.kl_coeff
 
+    def build_learner_connector(self):
+        """[user learner connectors..., NumpyToTensor, GeneralAdvantageEstimation, FlattenTimeMajor]."""
+        from ..connectors import (ConnectorPipelineV2, FlattenTimeMajor, GeneralAdvantageEstimation, NumpyToTensor,
+                                  build_pipeline)
+
+        c = self.config
+        user = c.get("learner_connector")
+        p = build_pipeline(user, obs_space=self.obs_space, act_space=self.act_space) if user else ConnectorPipelineV2()
+        p.append(NumpyToTensor(device=self.device))
+        p.append(GeneralAdvantageEstimation(gamma=c["gamma"], lambda_=c.get("lambda_", 1.0)))
+        p.append(FlattenTimeMajor(keys=("obs", "actions", "action_logp", "action_dist_inputs", "advantages",
+                                        "value_targets")))
+        p.set_input_spaces(self.obs_space, self.act_space)
+        return p
+
     @torch.no_grad()
     def postprocess(self, frag: Dict[str, Any]) -> Dict[str, Any]:
-        """Bootstrap values + GAE on device; returns the flattened train batch."""
-        c = self.config
-        dev = self.device
-        T, N = frag["rewards"].shape
-        vf = _to_tensor(frag["vf_preds"], dev).float()
-        last = self.module.compute_values({"obs": _to_tensor(frag["last_obs"], dev)}).float()
-        values = torch.cat([vf, last[None]], 0)
-        rew = _to_tensor(frag["rewards"], dev).float()
-        nonterm = 1.0 - _to_tensor(frag["terminateds"], dev).float()
-        adv, vt = gae(rew, values, nonterm, c["gamma"], c.get("lambda_", 1.0))
-        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-        flat = lambda x: x.reshape((T * N,) + tuple(x.shape[2:]))
-        return {"obs": flat(_to_tensor(frag["obs"], dev)), "actions": flat(_to_tensor(frag["actions"], dev)),
-                "action_logp": flat(_to_tensor(frag["action_logp"], dev)),
-                "action_dist_inputs": flat(_to_tensor(frag["action_dist_inputs"], dev)),
-                "advantages": flat(adv), "value_targets": flat(vt)}
+        """Run the learner connector pipeline (GAE on device) on one time-major
+        fragment; returns the flattened train batch."""
+        if getattr(self, "learner_connector", None) is None:
+            self.learner_connector = self.build_learner_connector()
+        return self.learner_connector(rl_module=self.module, batch=dict(frag), episodes=(), shared_data={})
 
 
 class PPO(Algorithm):
     config_class = PPOConfig
     learner_class = PPOLearner
+    supports_multi_agent = True
 
     def training_step(self):
         import time
 
+        from ..env.multi_agent_env_runner import concat_multi_agent
+
         c = self.algo_config
         t0 = time.perf_counter()
         frags = self.env_runner_group.sample()
-        frag = concat_fragments(frags)
+        if self.is_multi_agent:
+            frag = concat_multi_agent(frags)
+            steps = sum(f["env_steps"] for f in frags)
+            self.agent_steps_sampled += sum(f["agent_steps"] for f in frags)
+        else:
+            frag = concat_fragments(frags)
+            steps = int(frag["rewards"].size)
         t1 = time.perf_counter()
-        steps = int(frag["rewards"].size)
         self.env_steps_sampled += steps
         lg = self.learner_group
+        kl_of = (lambda st: {m: s.get("mean_kl_loss", 0.0) for m, s in st.items()}) if self.is_multi_agent \
+            else (lambda st: st.get("mean_kl_loss", 0.0))
         if lg.local is not None:
             batch = lg.local.postprocess(frag)
             stats = lg.local.update(batch, c.minibatch_size, c.num_epochs)
-            stats["curr_kl_coeff"] = lg.local.update_kl(stats.get("mean_kl_loss", 0.0))
+            kl = lg.local.update_kl(kl_of(stats))
         else:
-            batch = lg.call("postprocess", frag)
-            batch = {k: v.cpu() for k, v in batch.items()}
+            batch = _to_cpu(lg.call("postprocess", frag))
             stats = lg.update(batch, c.minibatch_size, c.num_epochs)
-            stats["curr_kl_coeff"] = lg.call("update_kl", stats.get("mean_kl_loss", 0.0))
+            kl = lg.call("update_kl", kl_of(stats))
+        if self.is_multi_agent:
+            for m, k in kl.items():
+                stats[m]["curr_kl_coeff"] = k
+        else:
+            stats["curr_kl_coeff"] = kl
         self.env_steps_trained += steps
         t2 = time.perf_counter()
         self._sync_weights()
         self._timers = {"sample_s": t1 - t0, "learn_s": t2 - t1, "sync_weights_s": time.perf_counter() - t2}
         return stats
+
+
+def _to_cpu(b):
+    if isinstance(b, dict):
+        return {k: _to_cpu(v) for k, v in b.items()}
+    return b.cpu() if isinstance(b, torch.Tensor) else b

@@ -150,6 +150,73 @@ class Learner:
         return True
 
 
+class MultiLearner:
+    """One inner Learner per trained module of a multi-agent setup (reference
+    role: the multi-module Learner of rllib/core/learner/learner.py). Every
+    module keeps its own flat fp32 parameter buffer and fused AdamW; batches,
+    stats and states are dicts keyed by module id. ``MultiLearner.of(cls)``
+    makes the class for a given algorithm learner (e.g. ``PPOLearner``)."""
+
+    inner_cls = Learner
+
+    @classmethod
+    def of(cls, inner_cls):
+        return type(f"Multi{inner_cls.__name__}", (cls,), {"inner_cls": inner_cls})
+
+    def __init__(self, config, module_factories: Dict[str, Callable], obs_spaces: Dict, act_spaces: Dict,
+                 device: Optional[str] = None, rank: int = 0, world: int = 1):
+        self.config = config
+        self.learners: Dict[str, Learner] = {}
+        for j, mid in enumerate(sorted(module_factories)):
+            c = dict(config)
+            if c.get("seed") is not None:
+                c["seed"] = c["seed"] + 7919 * j  # distinct initial weights per module
+            self.learners[mid] = self.inner_cls(c, module_factories[mid], obs_spaces[mid], act_spaces[mid],
+                                                device, rank, world)
+        self.device = next(iter(self.learners.values())).device if self.learners else torch.device("cpu")
+
+    @property
+    def module(self):
+        from .multi_rl_module import MultiRLModule
+
+        return MultiRLModule({m: l.module for m, l in self.learners.items()})
+
+    def postprocess(self, frags: Dict[str, Dict]) -> Dict[str, Dict]:
+        return {m: self.learners[m].postprocess(f) for m, f in frags.items() if m in self.learners}
+
+    def update(self, batch: Dict[str, Dict], minibatch_size=None, num_epochs=1, shuffle=True):
+        return {m: self.learners[m].update(b, minibatch_size, num_epochs, shuffle)
+                for m, b in batch.items() if m in self.learners}
+
+    def update_kl(self, kls: Dict[str, float]):
+        return {m: self.learners[m].update_kl(k) for m, k in kls.items() if m in self.learners}
+
+    def get_module_state(self):
+        return {m: l.get_module_state() for m, l in self.learners.items()}
+
+    def get_state(self):
+        return {m: l.get_state() for m, l in self.learners.items()}
+
+    def set_state(self, st):
+        for m, s in st.items():
+            if m in self.learners:
+                self.learners[m].set_state(s)
+        return True
+
+
+def _shard_nested(batch, i, n):
+    if isinstance(batch, dict):
+        return {k: _shard_nested(v, i, n) for k, v in batch.items()}
+    per = batch.shape[0] // n
+    return batch[i * per:(i + 1) * per]
+
+
+def _mean_nested(results):
+    if isinstance(results[0], dict):
+        return {k: _mean_nested([r[k] for r in results]) for k in results[0]}
+    return float(np.mean(results))
+
+
 class _LearnerActor:
     def __init__(self, learner_cls, config, module_factory, obs_space, act_space, rank, world, addr, port):
         if world > 1:
@@ -202,9 +269,7 @@ class LearnerGroup:
             core.get([a.call.remote("get_module_state") for a in self.actors])
 
     def _shard(self, batch, i):
-        n = next(iter(batch.values())).shape[0]
-        per = n // self.n
-        return {k: v[i * per:(i + 1) * per] for k, v in batch.items()}
+        return _shard_nested(batch, i, self.n)
 
     def update(self, batch, minibatch_size=None, num_epochs=1, shuffle=True):
         if self.local is not None:
@@ -214,7 +279,7 @@ class LearnerGroup:
         mbs = None if minibatch_size is None else max(1, minibatch_size // self.n)
         res = core.get([a.call.remote("update", self._shard(batch, i), mbs, num_epochs, shuffle)
                         for i, a in enumerate(self.actors)])
-        return {k: float(np.mean([r[k] for r in res])) for k in res[0]}
+        return _mean_nested(res)
 
     def call(self, method, *args, **kwargs):
         """Run a learner method on the local learner / all learner actors (rank 0's result)."""

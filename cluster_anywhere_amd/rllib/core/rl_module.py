@@ -110,6 +110,14 @@ def _act(name):
 class RLModuleSpec:
     module_class: Optional[type] = None
     model_config: Dict = field(default_factory=dict)
+    observation_space: Optional[Space] = None
+    action_space: Optional[Space] = None
+    inference_only: bool = False
+
+    def build(self, observation_space: Optional[Space] = None, action_space: Optional[Space] = None) -> "RLModule":
+        cls = self.module_class or DefaultActorCriticModule
+        return cls(observation_space or self.observation_space, action_space or self.action_space,
+                   dict(self.model_config or {}))
 
 
 class RLModule(nn.Module):

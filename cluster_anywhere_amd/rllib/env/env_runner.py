@@ -17,10 +17,21 @@ import numpy as np
 import torch
 
 from . import VectorEnv
+from .episodes import SingleAgentEpisode
+
+
+def _runner_callbacks(config):
+    from ..callbacks import RLlibCallback, make_callbacks
+
+    cb = make_callbacks(config.get("callbacks_class"), config.get("callbacks_functions"))
+    return cb, type(cb) is not RLlibCallback
 
 
 class EnvRunner:
     def __init__(self, config: Dict[str, Any], worker_index: int = 0):
+        from ..connectors import build_pipeline
+        from ..utils.metrics import MetricsLogger
+
         self.cfg = config
         self.worker_index = worker_index
         seed = config.get("seed")
@@ -28,11 +39,28 @@ class EnvRunner:
         if seed is not None:
             torch.manual_seed(seed + worker_index)
             np.random.seed(seed + worker_index)
+        self.metrics = MetricsLogger()
+        self.callbacks, self._has_cb = _runner_callbacks(config)
         self.env = VectorEnv(config["env"], config.get("num_envs_per_env_runner", 1), config.get("env_config"),
                              None if seed is None else seed + 1000 * worker_index)
-        self.module = config["module_factory"](self.env.observation_space, self.env.action_space)
+        if self._has_cb:
+            self.callbacks.on_environment_created(env_runner=self, metrics_logger=self.metrics, env=self.env,
+                                                  env_context=dict(config.get("env_config") or {},
+                                                                   worker_index=worker_index))
+        env_obs, env_act = self.env.observation_space, self.env.action_space
+        self.env_to_module = build_pipeline(config.get("env_to_module_connector"), self.env)
+        self.env_to_module.set_input_spaces(env_obs, env_act)
+        self.module_to_env = build_pipeline(config.get("module_to_env_connector"), self.env)
+        self.module_to_env.set_input_spaces(env_obs, env_act)
+        self.obs_space = self.env_to_module.recompute_output_observation_space(env_obs, env_act)
+        self.act_space = env_act
+        self.module = config["module_factory"](self.obs_space, self.act_space)
         self.module.eval()
-        self.obs = self.env.reset()
+        self.episodes: List[SingleAgentEpisode] = []
+        raw = self.env.reset()
+        for i in range(self.env.num_envs):
+            self.episodes.append(self._new_episode(i, raw[i]))
+        self.obs = self._to_module(raw, self.episodes)
         self.ep_ret = np.zeros(self.env.num_envs)
         self.ep_len = np.zeros(self.env.num_envs, dtype=np.int64)
         self.done_returns: deque = deque(maxlen=config.get("metrics_num_episodes_for_smoothing", 100))
@@ -40,6 +68,41 @@ class EnvRunner:
         self.new_episodes: List[float] = []
         self.total_steps = 0
         self.explore_extra: Dict[str, Any] = {}
+
+    # ------------------------------------------------------------ episodes / connectors
+    def _new_episode(self, i: int, raw_obs) -> SingleAgentEpisode:
+        ep = SingleAgentEpisode()
+        ep.add_reset(raw_obs)
+        if self._has_cb:
+            kw = dict(episode=ep, env_runner=self, metrics_logger=self.metrics, env=self.env, env_index=i,
+                      rl_module=getattr(self, "module", None))
+            self.callbacks.on_episode_created(**kw)
+            self.callbacks.on_episode_start(**kw)
+        return ep
+
+    def _to_module(self, raw: np.ndarray, episodes, peek: bool = False) -> np.ndarray:
+        if not len(self.env_to_module):
+            return raw
+        b = self.env_to_module(rl_module=getattr(self, "module", None), batch={"obs": raw}, episodes=episodes,
+                               shared_data={"peek": peek}, metrics=self.metrics)
+        return b["obs"]
+
+    def _to_env(self, out: Dict[str, Any], a: np.ndarray, explore: bool) -> np.ndarray:
+        if not len(self.module_to_env):
+            return a
+        b = {k: (v.cpu().numpy() if isinstance(v, torch.Tensor) else v) for k, v in out.items()}
+        b["actions"] = a
+        b = self.module_to_env(rl_module=self.module, batch=b, episodes=self.episodes, explore=explore,
+                               shared_data={}, metrics=self.metrics)
+        return b.get("actions_for_env", b["actions"])
+
+    def get_connector_state(self):
+        return {"env_to_module": self.env_to_module.get_state(), "module_to_env": self.module_to_env.get_state()}
+
+    def set_connector_state(self, state):
+        self.env_to_module.set_state(state.get("env_to_module", {}))
+        self.module_to_env.set_state(state.get("module_to_env", {}))
+        return True
 
     # ------------------------------------------------------------ weights
     def set_weights(self, state, extra: Optional[Dict] = None):
@@ -52,7 +115,7 @@ class EnvRunner:
         return self.module.get_state()
 
     def get_spaces(self):
-        return self.env.observation_space, self.env.action_space
+        return self.obs_space, self.act_space
 
     # ------------------------------------------------------------ sampling
     @torch.no_grad()
@@ -64,6 +127,7 @@ class EnvRunner:
         obs_buf = np.empty((T, N) + self.obs.shape[1:], dtype=self.obs.dtype)
         next_buf = np.empty_like(obs_buf) if need_next else None
         acts, logps, vfs, rews, raw, terms, truncs, dist = [], [], [], [], [], [], [], []
+        track = self._has_cb or len(self.env_to_module) or len(self.module_to_env)
         t0 = time.time()
         for t in range(T):
             obs_buf[t] = self.obs
@@ -71,15 +135,22 @@ class EnvRunner:
             batch.update(self.explore_extra)
             out = self.module.forward_exploration(batch) if explore else self.module.forward_inference(batch)
             a = out["actions"].cpu().numpy()
-            nobs, r, te, tr, final = self.env.step(a)
+            nraw, r, te, tr, final = self.env.step(self._to_env(out, a, explore))
+            done = te | tr
+            if track:
+                for i, ep in enumerate(self.episodes):
+                    ep.add_step(final[i], a[i], r[i], terminated=te[i], truncated=tr[i])
+            mfinal = final
+            if need_next or tr.any():
+                mfinal = self._to_module(final, self.episodes, peek=True) if track else final
             r_aug = r.copy()
             if tr.any() and hasattr(self.module, "compute_values"):
                 idx = np.nonzero(tr & ~te)[0]
                 if len(idx):
-                    v = self.module.compute_values({"obs": torch.from_numpy(final[idx])}).cpu().numpy()
+                    v = self.module.compute_values({"obs": torch.from_numpy(mfinal[idx])}).cpu().numpy()
                     r_aug[idx] += gamma * v
             if need_next:
-                next_buf[t] = final
+                next_buf[t] = mfinal
             acts.append(a)
             if "action_logp" in out:
                 logps.append(out["action_logp"].cpu().numpy())
@@ -89,17 +160,29 @@ class EnvRunner:
                 dist.append(out["action_dist_inputs"].cpu().numpy())
             rews.append(r_aug)
             raw.append(r)
-            terms.append(te | tr)
+            terms.append(done)
             truncs.append(tr)
             self.ep_ret += r
             self.ep_len += 1
-            for i in np.nonzero(te | tr)[0]:
+            for i in np.nonzero(done)[0]:
                 self.done_returns.append(float(self.ep_ret[i]))
                 self.done_lens.append(int(self.ep_len[i]))
                 self.new_episodes.append(float(self.ep_ret[i]))
                 self.ep_ret[i] = 0
                 self.ep_len[i] = 0
-            self.obs = nobs
+                if track:
+                    ep = self.episodes[i]
+                    if self._has_cb:
+                        self.callbacks.on_episode_end(episode=ep, env_runner=self, metrics_logger=self.metrics,
+                                                      env=self.env, env_index=int(i), rl_module=self.module)
+                    self.env_to_module.episode_done(ep)
+                    self.episodes[i] = self._new_episode(int(i), nraw[i])
+            if self._has_cb:
+                for i in np.nonzero(~done)[0]:
+                    self.callbacks.on_episode_step(episode=self.episodes[i], env_runner=self,
+                                                   metrics_logger=self.metrics, env=self.env, env_index=int(i),
+                                                   rl_module=self.module)
+            self.obs = self._to_module(nraw, self.episodes) if track else nraw
         self.total_steps += T * N
         out = {"obs": obs_buf, "actions": np.stack(acts), "rewards": np.stack(rews).astype(np.float32),
                "terminateds": np.stack(terms), "truncateds": np.stack(truncs),
@@ -112,11 +195,36 @@ class EnvRunner:
             out["action_dist_inputs"] = np.stack(dist).astype(np.float32)
         if need_next:
             out["next_obs"] = next_buf
+        if self._has_cb:
+            self.callbacks.on_sample_end(env_runner=self, metrics_logger=self.metrics, samples=out)
         return out
+
+    def reset_envs(self, seed: Optional[int] = None):
+        """Start fresh episodes in every env copy (evaluation: same seeds each time)."""
+        if seed is not None:
+            self.env.seed = seed
+        raw = self.env.reset()
+        for i in range(self.env.num_envs):
+            self.env_to_module.episode_done(self.episodes[i])
+            self.episodes[i] = self._new_episode(i, raw[i])
+        self.obs = self._to_module(raw, self.episodes)
+        self.ep_ret[:] = 0
+        self.ep_len[:] = 0
+        return True
+
+    @torch.no_grad()
+    def sample_episodes(self, num_episodes: int, explore: bool = False) -> List[float]:
+        """Run until ``num_episodes`` episodes finished; returns their returns."""
+        start = len(self.new_episodes)
+        while len(self.new_episodes) - start < num_episodes:
+            self.sample(1, explore)
+        rets = self.new_episodes[start:start + num_episodes]
+        return rets
 
     def get_metrics(self, reset_new: bool = True) -> Dict[str, Any]:
         m = {"num_episodes": len(self.new_episodes), "num_env_steps_sampled_lifetime": self.total_steps,
-             "episode_returns": list(self.done_returns), "episode_lens": list(self.done_lens)}
+             "episode_returns": list(self.done_returns), "episode_lens": list(self.done_lens),
+             "custom": self.metrics.reduce()}
         if reset_new:
             self.new_episodes = []
         return m
@@ -128,20 +236,30 @@ class EnvRunner:
 class EnvRunnerGroup:
     """A local runner (``num_env_runners == 0``) or N remote runner actors."""
 
-    def __init__(self, config: Dict[str, Any], num_env_runners: int = 0, num_cpus_per_env_runner: float = 1):
+    def __init__(self, config: Dict[str, Any], num_env_runners: int = 0, num_cpus_per_env_runner: float = 1,
+                 runner_cls=None):
         self.config = config
+        self.runner_cls = runner_cls or EnvRunner
         self.local = None
         self.remote = []
         if num_env_runners == 0:
-            self.local = EnvRunner(config, 0)
+            self.local = self.runner_cls(config, 0)
         else:
             from ...core import api as core
             from ...core.actor import ActorClass
 
-            Remote = ActorClass(EnvRunner, {})
+            Remote = ActorClass(self.runner_cls, {})
             self.remote = [Remote.options(num_cpus=num_cpus_per_env_runner).remote(config, i + 1)
                            for i in range(num_env_runners)]
             core.get([r.ping.remote() for r in self.remote])
+        self._merger = None
+
+    def _all(self, method, *args):
+        from ...core import api as core
+
+        if self.local is not None:
+            return [getattr(self.local, method)(*args)]
+        return core.get([getattr(r, method).remote(*args) for r in self.remote])
 
     def spaces(self):
         from ...core import api as core
@@ -159,6 +277,21 @@ class EnvRunnerGroup:
         ref = core.put(state)
         core.get([r.set_weights.remote(ref, extra) for r in self.remote])
 
+    def sync_connector_states(self):
+        """Merge the runners' connector statistics (e.g. MeanStdFilter deltas) and
+        broadcast the merged state, so every runner normalises the same way."""
+        from ..connectors import build_pipeline
+
+        if not (self.config.get("env_to_module_connector") or self.config.get("module_to_env_connector")):
+            return None
+        states = self._all("get_connector_state")
+        if self._merger is None:
+            self._merger = {k: build_pipeline(self.config.get(f"{k}_connector"))
+                            for k in ("env_to_module", "module_to_env")}
+        merged = {k: p.merge_states([s[k] for s in states]) for k, p in self._merger.items()}
+        self._all("set_connector_state", merged)
+        return merged
+
     def sample(self, num_timesteps: Optional[int] = None, explore: bool = True) -> List[Dict]:
         from ...core import api as core
 
@@ -170,18 +303,28 @@ class EnvRunnerGroup:
         return [r.sample.remote(num_timesteps) for r in self.remote]
 
     def metrics(self) -> Dict[str, Any]:
-        from ...core import api as core
+        from ..utils.metrics import merge_reduced, strip_meta
 
-        ms = [self.local.get_metrics()] if self.local is not None else \
-            core.get([r.get_metrics.remote() for r in self.remote])
+        ms = self._all("get_metrics")
         rets = [x for m in ms for x in m["episode_returns"]]
         lens = [x for m in ms for x in m["episode_lens"]]
-        return {"episode_return_mean": float(np.mean(rets)) if rets else float("nan"),
-                "episode_return_max": float(np.max(rets)) if rets else float("nan"),
-                "episode_return_min": float(np.min(rets)) if rets else float("nan"),
-                "episode_len_mean": float(np.mean(lens)) if lens else float("nan"),
-                "num_episodes": sum(m["num_episodes"] for m in ms),
-                "num_env_steps_sampled_lifetime": sum(m["num_env_steps_sampled_lifetime"] for m in ms)}
+        out = {"episode_return_mean": float(np.mean(rets)) if rets else float("nan"),
+               "episode_return_max": float(np.max(rets)) if rets else float("nan"),
+               "episode_return_min": float(np.min(rets)) if rets else float("nan"),
+               "episode_len_mean": float(np.mean(lens)) if lens else float("nan"),
+               "num_episodes": sum(m["num_episodes"] for m in ms),
+               "num_env_steps_sampled_lifetime": sum(m["num_env_steps_sampled_lifetime"] for m in ms)}
+        for key in ("agent_episode_returns_mean", "module_episode_returns_mean"):
+            per = {}
+            for m in ms:
+                for k, v in (m.get(key) or {}).items():
+                    per.setdefault(k, []).extend(v)
+            if per:
+                out[key] = {k: float(np.mean(v)) for k, v in per.items()}
+        custom = merge_reduced([m.get("custom") or {} for m in ms])
+        if custom:
+            out.update(strip_meta(custom))
+        return out
 
     def stop(self):
         from ...core import api as core

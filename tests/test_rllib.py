@@ -161,11 +161,12 @@ def test_bc_and_marwil_from_offline_data():
     for cls in (rllib.BCConfig, rllib.MARWILConfig):
         cfg = (cls().environment("CartPole-v1").offline_data(input_=data)
                .training(lr=1e-3, train_batch_size=512, model={"fcnet_hiddens": [32]})
-               .evaluation(evaluation_interval=1, evaluation_duration=3).debugging(seed=0))
+               .evaluation(evaluation_interval=10, evaluation_duration=10).debugging(seed=0))
         algo = cfg.build()
         for _ in range(40):
             r = algo.train()
-        assert r["evaluation"]["env_runners"]["episode_return_mean"] > 100
+        # 10 greedy episodes from seeded starts (the scripted expert itself averages ~200)
+        assert r["evaluation"]["env_runners"]["episode_return_mean"] > 90
 
 
 def test_tune_over_ppo(tmp_path):
