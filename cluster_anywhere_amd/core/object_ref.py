@@ -24,7 +24,7 @@ class ObjectRef:
         w = context.worker
         if w is not None:
             try:
-                w.refs.remove(self._id)
+                w.refs.remove(self._id, blocking=False)
             except Exception:
                 pass
 

@@ -10,6 +10,7 @@ methods), streaming / dynamic generators, cancellation and error propagation.
 from __future__ import annotations
 
 import asyncio
+import collections
 import concurrent.futures
 import ctypes
 import hashlib
@@ -55,36 +56,67 @@ class RefCounter:
         # to: ray.get of them needs no round trip to the head (the reference's
         # in-process memory store for owned/inlined objects)
         self.cache: Dict[bytes, tuple] = {}
+        # releases queued by finalizers that found the lock busy (see remove())
+        self.deferred: collections.deque = collections.deque()
 
     def add(self, oid: bytes, announce: bool):
         with self.lock:
+            if self.deferred:
+                self._run_deferred()
             c = self.counts.get(oid, 0)
             self.counts[oid] = c + 1
             if c == 0 and announce:
                 self.ops.append(("a", oid))
 
-    def remove(self, oid: bytes):
-        with self.lock:
-            c = self.counts.get(oid)
-            if c is None:
+    def remove(self, oid: bytes, blocking: bool = True):
+        """``blocking=False`` (ObjectRef finalizers): a finalizer may run from the
+        garbage collector INSIDE one of this thread's own critical sections (e.g.
+        popping a cached payload that holds nested refs), so it must never wait
+        for the lock; when the lock is busy the release is queued and applied by
+        the next lock holder (the flush loop drains within 50 ms)."""
+        if not self.lock.acquire(blocking):
+            self.deferred.append(oid)
+            return
+        try:
+            if self.deferred:
+                self._run_deferred()
+            self._remove_locked(oid)
+        finally:
+            self.lock.release()
+
+    def _run_deferred(self):
+        while self.deferred:
+            try:
+                oid = self.deferred.popleft()
+            except IndexError:
                 return
-            if c <= 1:
-                del self.counts[oid]
-                self.cache.pop(oid, None)
-                self.ready.pop(oid, None)
-                self.owned.discard(oid)
-                if oid in self.direct_pending:
-                    self.direct_dropped.add(oid)
-                else:
-                    self.ops.append(("d", oid))
+            self._remove_locked(oid)
+
+    def _remove_locked(self, oid: bytes):
+        c = self.counts.get(oid)
+        if c is None:
+            return
+        if c <= 1:
+            del self.counts[oid]
+            # nested refs inside a dropped payload finalize right here, inside the lock:
+            # their (non-blocking) releases are queued in ``deferred``
+            self.cache.pop(oid, None)
+            self.ready.pop(oid, None)
+            self.owned.discard(oid)
+            if oid in self.direct_pending:
+                self.direct_dropped.add(oid)
             else:
-                self.counts[oid] = c - 1
+                self.ops.append(("d", oid))
+        else:
+            self.counts[oid] = c - 1
 
     def drain(self):
         with self.lock:
             return self.drain_locked()
 
     def drain_locked(self):
+        if self.deferred:
+            self._run_deferred()
         ops, self.ops = self.ops, []
         msgs = []
         for kind, group in itertools.groupby(ops, key=lambda x: x[0]):
@@ -216,7 +248,7 @@ class CoreWorker:
                     self._flush_dseals()
                 except (ConnectionClosed, OSError):
                     return
-            if self.refs.ops:
+            if self.refs.ops or self.refs.deferred:
                 try:
                     with self.send_lock:
                         ops = self.refs.drain()

@@ -13,6 +13,10 @@ class DataContext:
     max_tasks_in_flight_per_op: int = int(os.environ.get("CAAMD_DATA_MAX_INFLIGHT", "0"))
     actor_max_tasks_in_flight: int = 4
     execution_preserve_order: bool = True
+    # object-store budget of one execution (resource_manager.py): a fraction of the
+    # store, or an absolute byte count when set
+    execution_object_store_fraction: float = 0.5
+    execution_object_store_bytes: int = 0
     enable_progress_bars: bool = False
     read_op_min_num_blocks: int = 8
     eager_free: bool = True
@@ -35,3 +39,11 @@ class DataContext:
     @property
     def execution_options(self):
         return self
+
+    @property
+    def preserve_order(self) -> bool:
+        return self.execution_preserve_order
+
+    @preserve_order.setter
+    def preserve_order(self, v: bool):
+        self.execution_preserve_order = bool(v)

@@ -23,12 +23,22 @@ from . import block as B
 from .aggregate import AggregateFn, Count, Max, Mean, Min, Std, Sum
 from .context import DataContext
 from .executor import actor_stage, limit_stage, task_stage
+from .resource_manager import ResourceManager
 
 
 class ActorPoolStrategy:
+    """Fixed (``size``) or autoscaling (``min_size``..``max_size``) actor pool
+    (reference: python/ray/data/_internal/compute.py ActorPoolStrategy)."""
+
     def __init__(self, size: Optional[int] = None, min_size: Optional[int] = None,
-                 max_size: Optional[int] = None, max_tasks_in_flight_per_actor: Optional[int] = None):
-        self.size = size or max_size or min_size or 1
+                 max_size: Optional[int] = None, initial_size: Optional[int] = None,
+                 max_tasks_in_flight_per_actor: Optional[int] = None):
+        if size is not None:
+            min_size = max_size = size
+        self.min_size = max(1, min_size or 1)
+        self.max_size = max(self.min_size, max_size or self.min_size)
+        self.initial_size = initial_size
+        self.size = self.max_size
         self.max_tasks_in_flight_per_actor = max_tasks_in_flight_per_actor
 
 
@@ -143,7 +153,7 @@ def _shuffle_reduce(seed, *parts):
 def _range_partition(block, key, bounds, descending):
     if not block:
         return tuple({} for _ in range(len(bounds) + 1)) if bounds else {}
-    k = block[key]
+    k = B.col(block, key)
     idx = np.searchsorted(np.asarray(bounds), k, side="right") if bounds else np.zeros(len(k), dtype=np.int64)
     n = len(bounds) + 1
     if descending:
@@ -155,7 +165,7 @@ def _range_partition(block, key, bounds, descending):
 def _sort_reduce(key, descending, *parts):
     b = B.concat([p for p in parts if p])
     if b:
-        order = np.argsort(b[key], kind="stable")
+        order = np.argsort(B.col(b, key), kind="stable")
         if descending:
             order = order[::-1]
         b = B.take_indices(b, order)
@@ -169,7 +179,7 @@ def _hash_partition(block, keys, n):
         keys = [keys]
     h = np.zeros(B.num_rows(block), dtype=np.uint64)
     for k in keys:
-        col = block[k]
+        col = B.col(block, k)
         hv = np.array([hash(x.item() if isinstance(x, np.generic) else x) for x in col], dtype=np.int64).view(np.uint64)
         h = h * np.uint64(1000003) ^ hv
     idx = (h % np.uint64(n)).astype(np.int64)
@@ -183,7 +193,7 @@ def _group_reduce(keys, aggs, map_fn, batch_format, *parts):
         return {}, _meta({})
     if isinstance(keys, str):
         keys = [keys]
-    keycols = [b[k] for k in keys]
+    keycols = [B.col(b, k) for k in keys]
     tuples = list(zip(*[c.tolist() for c in keycols]))
     groups = collections.OrderedDict()
     for i, t in enumerate(tuples):
@@ -204,12 +214,13 @@ def _group_reduce(keys, aggs, map_fn, batch_format, *parts):
         for k, v in zip(keys, t):
             cols[k].append(v)
         for a in aggs:
-            cols[a.name].append(a.finalize(a.accumulate_block(a.init(t), g)))
+            cols[a.name].append(a.finalize(a.accumulate_block(a.init(t), B.to_numpy(g))))
     out = {k: B._to_array(v) for k, v in cols.items()}
     return out, _meta(out)
 
 
 def _agg_block(block, aggs):
+    block = B.to_numpy(block) if block else block
     return [a.accumulate_block(a.init(None), block) if block else a.init(None) for a in aggs]
 
 
@@ -236,8 +247,8 @@ def _write_block(block, path, fmt, idx, kw):
     elif fmt == "json":
         B.to_batch(block, "pandas").to_json(fn, orient="records", lines=True, **kw)
     elif fmt == "numpy":
-        col = kw.get("column") or next(iter(block))
-        np.save(fn, block[col])
+        col = kw.get("column") or B.columns(block)[0]
+        np.save(fn, B.col(block, col))
     elif fmt in ("tfrecords", "webdataset"):
         from . import formats
 
@@ -273,6 +284,14 @@ class Dataset:
         self._materialized = None
         self._stats = {}
 
+    def __getstate__(self):
+        st = dict(self.__dict__)
+        st.pop("_rm", None)  # per-execution accounting (holds a lock) stays local
+        return st
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+
     def _with(self, op) -> "Dataset":
         return Dataset(self._source if self._materialized is None else ("refs", self._materialized),
                        (self._ops if self._materialized is None else []) + [op])
@@ -288,10 +307,16 @@ class Dataset:
         is_refs = kind == "refs"
         chain: List[Callable] = []
         res = None
+        rm = ResourceManager.for_execution()
+        self._rm = rm
+
+        def _name(fns, read):
+            names = [getattr(f, "__caamd_name__", None) or getattr(f, "__name__", "map") for f in fns]
+            return "->".join((["Read"] if read else []) + names) or "Read"
 
         def flush(stream, chain, res, is_refs):
             if chain or not is_refs:
-                return task_stage(stream, list(chain), res or {}), True
+                return task_stage(stream, list(chain), res or {}, op=rm.op(_name(chain, not is_refs))), True
             return stream, is_refs
 
         for op in self._ops:
@@ -303,7 +328,7 @@ class Dataset:
                     chain = []
                 if conc:
                     stream, is_refs = flush(stream, chain, res, is_refs)
-                    stream = task_stage(stream, [fn], r or {}, max_inflight=conc)
+                    stream = task_stage(stream, [fn], r or {}, max_inflight=conc, op=rm.op(_name([fn], False)))
                     chain, res = [], None
                     continue
                 chain.append(fn)
@@ -311,7 +336,8 @@ class Dataset:
             elif t == "actor":
                 stream, is_refs = flush(stream, chain, res, is_refs)
                 chain, res = [], None
-                stream = actor_stage(stream, op[1])
+                stream = actor_stage(stream, op[1], op=rm.op(
+                    f"ActorPoolMap({getattr(op[1]['ctor'], '__name__', 'udf')})"))
             elif t == "all2all":
                 stream, is_refs = flush(stream, chain, res, is_refs)
                 chain, res = [], None
@@ -375,18 +401,21 @@ class Dataset:
     def _actor_map(self, cls, batch_size, batch_format, fn_args, fn_kwargs, ctor_args, ctor_kwargs,
                    num_cpus, num_gpus, concurrency, compute, row_mode=None, zero_copy_batch=False,
                    resources=None):
+        initial = None
         if isinstance(compute, ActorPoolStrategy):
-            size = compute.size
+            lo, hi, initial = compute.min_size, compute.max_size, compute.initial_size
         elif isinstance(concurrency, tuple):
-            size = concurrency[1]
+            lo, hi = concurrency[0], concurrency[1]
+            initial = concurrency[2] if len(concurrency) > 2 else None
         else:
-            size = concurrency or 1
+            lo = hi = concurrency or 1
+        size = hi
         if row_mode == "map":
             def make(udf):
                 return _row_map(udf)
         else:
             make = _make_class_fn(batch_size, batch_format, tuple(fn_args), fn_kwargs, zero_copy_batch)
-        spec = {"size": size, "ctor": cls, "ctor_args": tuple(ctor_args), "ctor_kwargs": ctor_kwargs,
+        spec = {"size": size, "min_size": lo, "max_size": hi, "initial_size": initial, "ctor": cls, "ctor_args": tuple(ctor_args), "ctor_kwargs": ctor_kwargs,
                 "before": [], "after": [], "make_fn": make,
                 "resources": {"num_cpus": num_cpus if num_cpus is not None else (0 if num_gpus else 1),
                               "num_gpus": num_gpus or 0, "resources": resources},
@@ -528,8 +557,8 @@ class Dataset:
         right_rows = B.concat([get(r) for r, _ in bds._execute()])
         out, off = [], 0
         for (ref, m), c in zip(left, counts):
-            lb = get(ref)
-            rb = B.slice_block(right_rows, off, off + c)
+            lb = B.to_numpy(get(ref))
+            rb = B.to_numpy(B.slice_block(right_rows, off, off + c))
             off += c
             merged = dict(lb)
             for k, v in rb.items():
@@ -663,8 +692,10 @@ class Dataset:
 
     def stats(self) -> str:
         s = self._stats
-        return (f"Dataset: {s.get('num_blocks', '?')} blocks, {s.get('num_rows', '?')} rows, "
+        head = (f"Dataset: {s.get('num_blocks', '?')} blocks, {s.get('num_rows', '?')} rows, "
                 f"executed in {s.get('wall_time_s', 0):.3f}s")
+        rm = getattr(self, "_rm", None)
+        return head + ("\n" + rm.summary() if rm is not None and rm.ops else "")
 
     def to_pandas(self, limit: Optional[int] = None):
         import pandas as pd
@@ -679,7 +710,7 @@ class Dataset:
         out = []
         for r, _ in self._execute():
             b = get(r)
-            out.append(put(b[column] if column else b))
+            out.append(put(B.col(b, column) if column else B.to_numpy(b)))
         return out
 
     def to_arrow_refs(self):

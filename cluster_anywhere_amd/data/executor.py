@@ -44,7 +44,7 @@ def _apply_chain(block, chain):
 def _task_body(src, chain):
     """src: a block (resolved ObjectRef) or a zero-arg read callable."""
     blocks = src() if callable(src) else [src]
-    if isinstance(blocks, dict):
+    if isinstance(blocks, dict) or B.is_arrow(blocks):
         blocks = [blocks]
     out = []
     for b in blocks:
@@ -122,56 +122,162 @@ def _cluster_cpus() -> int:
         return 4
 
 
+def _retire(inflight: collections.deque, preserve_order: bool, block: bool = True):
+    """Pop one finished (ref, meta_ref, tag) entry: the oldest one (order kept) or,
+    without order preservation, whichever finished first (``block=False``: only if
+    one already has)."""
+    from ..core.api import wait
+
+    if preserve_order:
+        if not block:
+            ready, _ = wait([inflight[0][1]], num_returns=1, timeout=0)
+            if not ready:
+                return None
+        return inflight.popleft()
+    ready, _ = wait([e[1] for e in inflight], num_returns=1, timeout=None if block else 0)
+    if not ready:
+        return None
+    r0 = ready[0]
+    for i, e in enumerate(inflight):
+        if e[1] is r0 or e[1] == r0:
+            del inflight[i]
+            return e
+    return inflight.popleft()
+
+
 def task_stage(inputs: Iterator, chain: List[Callable], resources: Dict[str, Any],
-               max_inflight: Optional[int] = None) -> Iterator[Tuple[Any, dict]]:
-    """inputs yield read callables or (block_ref, meta); yields (block_ref, meta)."""
+               max_inflight: Optional[int] = None, op=None) -> Iterator[Tuple[Any, dict]]:
+    """inputs yield read callables or (block_ref, meta); yields (block_ref, meta).
+
+    Submission stops at ``max_inflight`` tasks or when the operator's object-store
+    budget (``op.can_submit``, see resource_manager.py) is used up."""
     from ..core.api import get
 
     ctx = DataContext.get_current()
     max_inflight = max_inflight or ctx.max_tasks_in_flight_per_op or max(2, 2 * _cluster_cpus())
+    keep_order = ctx.execution_preserve_order
+    if op is not None:
+        op.warmup_cap = max(2, min(max_inflight, _cluster_cpus()))
     task = _get_remote_task().options(**resources) if resources else _get_remote_task()
     inflight = collections.deque()
+
+    def out(e):
+        meta = get(e[1])
+        if op is not None:
+            op.on_output(meta)
+            op.on_pulled(meta)
+        return e[0], meta
+
     for item in inputs:
         src = item[0] if isinstance(item, tuple) else item
+        while inflight and (len(inflight) >= max_inflight or (op is not None and not op.can_submit())):
+            yield out(_retire(inflight, keep_order))
         ref, meta_ref = task.remote(src, chain)
-        inflight.append((ref, meta_ref))
-        while len(inflight) >= max_inflight:
-            r, m = inflight.popleft()
-            yield r, get(m)
+        if op is not None:
+            op.on_submit()
+        inflight.append((ref, meta_ref, None))
     while inflight:
-        r, m = inflight.popleft()
-        yield r, get(m)
+        yield out(_retire(inflight, keep_order))
 
 
-def actor_stage(inputs: Iterator, spec: dict) -> Iterator[Tuple[Any, dict]]:
+def actor_stage(inputs: Iterator, spec: dict, op=None) -> Iterator[Tuple[Any, dict]]:
+    """Actor-pool map with autoscaling between ``min_size`` and ``max_size`` actors
+    (reference: actor_pool_map_operator.py + autoscaling_actor_pool.py).
+
+    Starts ``initial`` actors; a new actor is started (one at a time) when every
+    ready actor has ``per_actor`` tasks in flight and more input is waiting; work
+    only goes to actors that are ready, so a slow-starting actor never holds up
+    the first outputs. Once the input is exhausted, actors that have no work left
+    are released immediately (scale-down) instead of at the end of the stage."""
     from ..core.api import get, kill, remote, wait
 
-    size = spec["size"]
-    per_actor = spec.get("max_tasks_in_flight") or DataContext.get_current().actor_max_tasks_in_flight
+    ctx = DataContext.get_current()
+    keep_order = ctx.execution_preserve_order
+    max_size = max(1, int(spec.get("max_size") or spec["size"]))
+    min_size = max(1, min(max_size, int(spec.get("min_size") or spec["size"])))
+    initial = max(min_size, min(max_size, int(spec.get("initial_size") or min_size)))
+    per_actor = spec.get("max_tasks_in_flight") or ctx.actor_max_tasks_in_flight
     opts = {k: v for k, v in spec["resources"].items() if v}
     Actor = remote(**opts)(_MapWorker) if opts else remote(_MapWorker)
-    actors = [Actor.remote(spec["ctor"], spec["ctor_args"], spec["ctor_kwargs"], spec["before"],
-                           spec["after"], spec["make_fn"]) for _ in range(size)]
-    load = [0] * size
-    inflight = collections.deque()  # (ref, meta_ref, actor_idx)
+
+    actors: List[Any] = []        # ready actors
+    load: List[int] = []
+    starting: Dict[Any, Any] = {}  # ready-ref -> actor handle
+    inflight = collections.deque()  # (ref, meta_ref, actor_handle)
+
+    def start_actor():
+        a = Actor.remote(spec["ctor"], spec["ctor_args"], spec["ctor_kwargs"], spec["before"],
+                         spec["after"], spec["make_fn"])
+        starting[a.ready.remote()] = a
+        if op is not None:
+            op.scale_ups += 1
+
+    def poll_starting(block: bool):
+        if not starting:
+            return
+        ready, _ = wait(list(starting), num_returns=1, timeout=None if block else 0)
+        for r in ready:
+            a = starting.pop(r)
+            get(r)  # surfaces constructor errors
+            actors.append(a)
+            load.append(0)
+        if op is not None:
+            op.set_actors(len(actors))
+
+    def retire(block=True):
+        e = _retire(inflight, keep_order, block)
+        if e is None:
+            return None
+        r, m, a = e
+        meta = get(m)
+        load[actors.index(a)] -= 1
+        if op is not None:
+            op.on_output(meta)
+            op.on_pulled(meta)
+        return r, meta
+
+    for _ in range(initial):
+        start_actor()
     try:
         for item in inputs:
             ref_in = item[0]
-            while min(load) >= per_actor:
-                r, m, ai = inflight.popleft()
-                meta = get(m)
-                load[ai] -= 1
-                yield r, meta
-            ai = min(range(size), key=lambda i: load[i])
+            while True:
+                poll_starting(block=not actors and not inflight)
+                free = [i for i in range(len(actors)) if load[i] < per_actor]
+                if free and (op is None or op.can_submit() or not inflight):
+                    break
+                if not free and len(actors) + len(starting) < max_size and not starting:
+                    start_actor()  # every ready actor is saturated: scale up
+                # block until an output (the oldest one if order is kept) or a new actor is ready
+                heads = ([inflight[0][1]] if keep_order else [e[1] for e in inflight]) if inflight else []
+                wait(heads + list(starting), num_returns=1, timeout=None)
+                if inflight:
+                    out = retire(block=False)
+                    if out is not None:
+                        yield out
+            ai = min(free, key=lambda i: load[i])
             r, m = actors[ai].process.options(num_returns=2).remote(ref_in)
             load[ai] += 1
-            inflight.append((r, m, ai))
+            if op is not None:
+                op.on_submit()
+            inflight.append((r, m, actors[ai]))
+        # input exhausted: drain, releasing actors as they go idle
+        for a in starting.values():
+            kill(a)
+        starting.clear()
         while inflight:
-            r, m, ai = inflight.popleft()
-            yield r, get(m)
-            load[ai] -= 1
+            out = retire()
+            yield out
+            for i in range(len(actors) - 1, -1, -1):
+                if load[i] == 0 and not any(e[2] is actors[i] for e in inflight):
+                    kill(actors[i])
+                    del actors[i]
+                    del load[i]
+                    if op is not None:
+                        op.scale_downs += 1
+                        op.set_actors(len(actors))
     finally:
-        for a in actors:
+        for a in list(actors) + list(starting.values()):
             try:
                 kill(a)
             except Exception:

@@ -15,13 +15,14 @@ from . import block as B
 class _Server:
     def __init__(self, block, key):
         self.key = key
+        block = B.to_numpy(block) if block else block
         self.keys = np.asarray(block[key]) if block else np.zeros(0)
         self.block = block
 
     def get(self, k):
         i = int(np.searchsorted(self.keys, k))
         if i < len(self.keys) and self.keys[i] == k:
-            return {c: B._scalar(v[i]) for c, v in self.block.items()}
+            return {c: B._scalar(v[i]) for c, v in B.to_numpy(self.block).items()}
         return None
 
     def multiget(self, ks):

@@ -23,7 +23,7 @@ class DQNModule(RLModule):
         self.image = len(obs.shape) == 3
         hiddens = list(mc.get("fcnet_hiddens", [256, 256]))
         if self.image:
-            self.encoder = NatureCNN(obs.shape[-1])
+            self.encoder = NatureCNN(obs.shape[-1], hw=obs.shape[:2])
             feat = self.encoder.out_dim
         else:
             self.encoder = mlp([int(np.prod(obs.shape))] + hiddens, _act(mc.get("fcnet_activation", "relu")),

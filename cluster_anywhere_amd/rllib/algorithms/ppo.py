@@ -12,7 +12,9 @@ import numpy as np
 import torch
 
 from ...ops.rl import gae
+from ...ops.rl_encoder import ppo_loss_categorical
 from ..core.learner import Learner, _to_tensor
+from ..core.rl_module import Categorical
 from .algorithm import Algorithm, AlgorithmConfig, concat_fragments
 
 
@@ -36,12 +38,28 @@ class PPOConfig(AlgorithmConfig):
 
 
 class PPOLearner(Learner):
+    graph_capturable = True  # compute_loss has no host syncs / host-side state (KL coeff lives on device)
+
     def build(self):
         self.kl_coeff = self.config.get("kl_coeff", 0.2)
+        self._kl_dev = (torch.full((1,), float(self.kl_coeff), device=self.device)
+                        if self.device.type == "cuda" else None)
 
     def compute_loss(self, batch):
         c = self.config
         out = self.module.forward_train(batch)
+        if self.module.dist_cls is Categorical:
+            # one fused kernel on GPU (ops/rl_encoder.py); the same math in torch on CPU
+            use_kl = c.get("use_kl_loss", True)
+            kl_coeff = self.kl_coeff if use_kl and self.kl_coeff > 0 else 0.0
+            loss, st = ppo_loss_categorical(out["action_dist_inputs"], out["vf_preds"], batch["actions"],
+                                            batch["action_logp"], batch["advantages"], batch["value_targets"],
+                                            batch["action_dist_inputs"], c["clip_param"], c["vf_clip_param"],
+                                            c["vf_loss_coeff"], c["entropy_coeff"], kl_coeff,
+                                            self._kl_dev if use_kl else None)
+            st = st / out["vf_preds"].shape[0]
+            return {"default": loss}, {"total_loss": loss.detach(), "policy_loss": -st[0], "vf_loss": st[1],
+                                       "entropy": st[2], "mean_kl_loss": st[3]}
         dist = self.module.dist_cls(out["action_dist_inputs"])
         logp = dist.logp(batch["actions"])
         ratio = torch.exp(logp - batch["action_logp"])
@@ -66,6 +84,8 @@ class PPOLearner(Learner):
             self.kl_coeff *= 1.5
         elif kl < 0.5 * c["kl_target"]:
             self.kl_coeff *= 0.5
+        if self._kl_dev is not None:
+            self._kl_dev.fill_(float(self.kl_coeff))
         return self.kl_coeff
 
     def build_learner_connector(self):

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from ...ops.optim import FusedAdamW
+from ...ops.rl_encoder import accumulate_into_grad
 from ...parallel.flat import FlatParamSpace
 
 
@@ -29,7 +30,23 @@ def _to_tensor(x, device):
     return t
 
 
+def _mean_stats(agg: Dict[str, list]) -> Dict[str, float]:
+    """Per-minibatch stats stay on the device until the end of ``update``: one host
+    sync per update instead of one per statistic per minibatch."""
+    keys = list(agg)
+    tens = [k for k in keys if agg[k] and isinstance(agg[k][0], torch.Tensor)]
+    out = {k: float(np.mean([float(x) for x in agg[k]])) for k in keys if k not in tens}
+    if tens:
+        means = torch.stack([torch.stack([x.detach().float().reshape(()) for x in agg[k]]).mean() for k in tens])
+        out.update(zip(tens, means.tolist()))
+    return out
+
+
 class Learner:
+    # Subclasses whose compute_loss is free of host syncs and host-side mutable state
+    # opt in to running forward+backward of each minibatch as ONE HIP-graph replay.
+    graph_capturable = False
+
     def __init__(self, config: Dict[str, Any], module_factory: Callable, obs_space, act_space,
                  device: Optional[str] = None, rank: int = 0, world: int = 1):
         self.config = config
@@ -59,6 +76,9 @@ class Learner:
                                                eps=config.get("adam_eps", 1e-7), weight_decay=0.0,
                                                max_grad_norm=config.get("grad_clip") or 0.0)
         self.num_updates = 0
+        self._graphs: Dict[tuple, tuple] = {}
+        self._graph_off = not (self.graph_capturable and self.device.type == "cuda" and world == 1
+                               and len(self.flats) == 1 and config.get("learner_cuda_graph", True))
 
     # ---------------------------------------------------------------- hooks
     def build(self):
@@ -90,7 +110,8 @@ class Learner:
         if len(names) == 1:  # .grad of every parameter is a view of the flat grad buffer
             flat = self.flats[names[0]]
             flat.zero_grad()
-            losses[names[0]].backward()
+            with accumulate_into_grad():  # encoder kernels add wgrads straight into .grad
+                losses[names[0]].backward()
             self._allreduce(flat)
             self.optimizers[names[0]].step(inv_world=1.0 / self.world)
             self.num_updates += 1
@@ -117,16 +138,75 @@ class Learner:
         b = {k: _to_tensor(v, self.device) for k, v in batch.items()}
         n = next(iter(b.values())).shape[0]
         mbs = min(minibatch_size or n, n)
-        agg: Dict[str, List[float]] = {}
+        agg: Dict[str, list] = {}
         for _ in range(num_epochs):
             perm = torch.randperm(n, device=self.device) if shuffle else torch.arange(n, device=self.device)
             for s in range(0, n - mbs + 1, mbs):
                 idx = perm[s: s + mbs]
-                mb = {k: v[idx] for k, v in b.items()}
-                st = self.update_once(mb)
+                st = None
+                if not self._graph_off:
+                    st = self._update_graphed(b, idx)
+                if st is None:
+                    st = self.update_once({k: v[idx] for k, v in b.items()})
                 for k, v in st.items():
-                    agg.setdefault(k, []).append(float(v))
-        return {k: float(np.mean(v)) for k, v in agg.items()}
+                    agg.setdefault(k, []).append(v)
+        return _mean_stats(agg)
+
+    # ------------------------------------------------------- HIP-graph step
+    def _update_graphed(self, b: Dict[str, torch.Tensor], idx: torch.Tensor) -> Optional[Dict[str, Any]]:
+        """forward + backward of one minibatch as a single graph replay (captured
+        once per minibatch shape; inputs gathered straight into the graph's static
+        buffers); the fused AdamW step stays eager (its step count / lr change).
+        Returns None (and turns graphs off) if the loss cannot be captured."""
+        key = tuple(sorted((k, (idx.shape[0],) + tuple(v.shape[1:]), v.dtype) for k, v in b.items()))
+        ent = self._graphs.get(key)
+        if ent is None:
+            try:
+                ent = self._capture(b, idx, key)
+            except Exception as e:  # noqa: BLE001 - any capture problem -> eager path
+                import warnings
+
+                warnings.warn(f"learner HIP-graph capture failed ({type(e).__name__}: {e}); running eagerly")
+                self._graph_off = True
+                torch.cuda.synchronize(self.device)
+                return None
+        static_in, graph, stacked, keys, name = ent
+        for k, v in b.items():
+            torch.index_select(v, 0, idx, out=static_in[k])
+        graph.replay()
+        self.optimizers[name].step(inv_world=1.0)
+        self.num_updates += 1
+        self.after_update()
+        st = stacked.clone()
+        return {k: st[i] for i, k in enumerate(keys)}
+
+    def _capture(self, b, idx, key):
+        name = next(iter(self.flats))
+        flat = self.flats[name]
+        static_in = {k: v[idx].clone() for k, v in b.items()}
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):  # warm-up (allocator / kernel selection) outside the capture
+            for _ in range(2):
+                flat.zero_grad()
+                losses, _ = self.compute_loss(static_in)
+                with accumulate_into_grad():
+                    losses[name].backward()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            flat.grad_buffer.zero_()
+            losses, stats = self.compute_loss(static_in)
+            with accumulate_into_grad():
+                losses[name].backward()
+            keys = list(stats)
+            if not all(isinstance(stats[k], torch.Tensor) for k in keys):
+                raise TypeError("compute_loss stats must be tensors to be captured")
+            stacked = torch.stack([stats[k].detach().float().reshape(()) for k in keys])
+        ent = (static_in, graph, stacked, keys, name)
+        self._graphs[key] = ent
+        return ent
 
     # ---------------------------------------------------------------- state
     def get_module_state(self):

@@ -88,18 +88,68 @@ def mlp(sizes: Sequence[int], act=nn.Tanh, out_act=False):
 
 
 class NatureCNN(nn.Module):
-    """84x84xC uint8 -> 512 (Mnih et al. 2015), channels-last input."""
+    """84x84xC uint8 NHWC -> 512 (Mnih et al. 2015). Parameters are kept in the
+    layout of the MFMA kernels (``ops/rl_encoder.py``): conv weights
+    ``[Cout, KH*KW*Cin]`` over NHWC windows, fc input flattened NHWC. On GPU the
+    forward and backward run on those kernels; on CPU (env runners) the same
+    parameters go through the fp32 PyTorch reference."""
 
-    def __init__(self, in_ch: int = 4, out: int = 512):
+    def __init__(self, in_ch: int = 4, out: int = 512, hw=(84, 84)):
         super().__init__()
-        self.conv = nn.Sequential(nn.Conv2d(in_ch, 32, 8, 4), nn.ReLU(), nn.Conv2d(32, 64, 4, 2), nn.ReLU(),
-                                  nn.Conv2d(64, 64, 3, 1), nn.ReLU(), nn.Flatten())
-        self.fc = nn.Sequential(nn.Linear(64 * 7 * 7, out), nn.ReLU())
+        from ...ops.rl_encoder import NATURE_CONVS, nature_shapes
+
+        shapes, flat = nature_shapes(hw[0], hw[1], in_ch)
+        self.convs = nn.ParameterList()
+        for (h, w, cin, cout, k, s, oh, ow) in shapes:
+            wt = nn.Parameter(torch.empty(cout, k * k * cin))
+            b = nn.Parameter(torch.empty(cout))
+            _torch_default_init(wt, b)
+            self.convs.append(wt)
+            self.convs.append(b)
+        self.fc_w = nn.Parameter(torch.empty(out, flat))
+        self.fc_b = nn.Parameter(torch.empty(out))
+        _torch_default_init(self.fc_w, self.fc_b)
         self.out_dim = out
 
+    def params(self):
+        return [*self.convs, self.fc_w, self.fc_b]
+
     def forward(self, x):
-        x = x.permute(0, 3, 1, 2).float() * (1.0 / 255.0)
-        return self.fc(self.conv(x.contiguous(memory_format=torch.channels_last)))
+        from ...ops.rl_encoder import nature_cnn
+
+        return nature_cnn(x, self.params())
+
+
+def _torch_default_init(w: torch.Tensor, b: torch.Tensor):
+    """nn.Linear / nn.Conv2d default init (kaiming-uniform(a=sqrt 5), fan_in = w.shape[1])."""
+    with torch.no_grad():
+        nn.init.kaiming_uniform_(w, a=math.sqrt(5))
+        bound = 1.0 / math.sqrt(w.shape[1])
+        nn.init.uniform_(b, -bound, bound)
+
+
+class TanhMLP(nn.Module):
+    """The default vector-obs encoder (tanh MLP); on GPU via the MFMA kernels
+    when every width is a multiple of 8, else plain torch."""
+
+    def __init__(self, sizes: Sequence[int]):
+        super().__init__()
+        self.ws = nn.ParameterList()
+        for i in range(len(sizes) - 1):
+            w = nn.Parameter(torch.empty(sizes[i + 1], sizes[i]))
+            b = nn.Parameter(torch.empty(sizes[i + 1]))
+            _torch_default_init(w, b)
+            self.ws.append(w)
+            self.ws.append(b)
+        from ...ops.rl_encoder import mlp_kernel_ok
+
+        self.kernel_ok = mlp_kernel_ok(sizes[0], sizes[1:])
+
+    def forward(self, x):
+        from ...ops.rl_encoder import mlp_tanh, mlp_tanh_ref
+
+        ps = list(self.ws)
+        return mlp_tanh(x, ps) if self.kernel_ok else mlp_tanh_ref(x, ps)
 
 
 def _act(name):
@@ -158,14 +208,16 @@ class DefaultActorCriticModule(RLModule):
         self.image = len(obs.shape) == 3
         self.share = mc.get("vf_share_layers", self.image)
         if self.image:
-            self.encoder = NatureCNN(obs.shape[-1])
+            self.encoder = NatureCNN(obs.shape[-1], hw=obs.shape[:2])
             feat = self.encoder.out_dim
             self.vf_encoder = None
         else:
             d = int(np.prod(obs.shape))
-            self.encoder = mlp([d] + hiddens, act, out_act=True)
+            tanh = mc.get("fcnet_activation", "tanh") == "tanh"
+            make = (lambda: TanhMLP([d] + hiddens)) if tanh else (lambda: mlp([d] + hiddens, act, out_act=True))
+            self.encoder = make()
             feat = hiddens[-1]
-            self.vf_encoder = None if self.share else mlp([d] + hiddens, act, out_act=True)
+            self.vf_encoder = None if self.share else make()
         self.pi = nn.Linear(feat, dist_input_dim(self.action_space))
         self.vf = nn.Linear(feat, 1)
         nn.init.normal_(self.pi.weight, std=0.01)

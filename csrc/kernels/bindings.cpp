@@ -35,6 +35,17 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
+void rl_gemm(int layout, const bf16* A, const bf16* B, void* C, const bf16* bias, const bf16* aux, int M, int N,
+             int K, int lda, int ldb, int ldc, int epi, int splits, hipStream_t st);
+void rl_im2col(const void* x, bool u8, bf16* col, int B, int H, int W, int C, int KH, int KW, int S, float scale,
+               hipStream_t st);
+void rl_col2im(const bf16* dcol, const bf16* y, bf16* dz, int B, int H, int W, int C, int KH, int KW, int S, int act,
+               hipStream_t st);
+void rl_colsum(const bf16* x, float* db, int M, int N, hipStream_t st);
+void ppo_loss_cat(const float* logits, const float* vf, const int64_t* act, const float* old_logp,
+                  const float* adv, const float* vt, const float* old_logits, int B, int A, float clip,
+                  float vf_clip, float vf_coeff, float ent_coeff, float kl_coeff, const float* kl_dev,
+                  float* dlogits, float* dvf, float* stats, hipStream_t st);
 }  // namespace caamd
 
 using at::Tensor;
@@ -677,6 +688,149 @@ static Tensor transpose_bf16(const Tensor& x) {
   return y;
 }
 
+// ---- RLlib encoder / PPO loss (rl_encoder.hip) ------------------------------------
+static inline bool aligned16(const Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; }
+
+// layout 0: C[M,N] = A[M,K] . B[N,K]^T ; 1: A[M,K] . B[K,N] ; 2: A[K,M]^T . B[K,N]
+void rl_gemm_(const Tensor& a, const Tensor& b, const Tensor& c, int64_t layout, int64_t epi,
+              std::optional<Tensor> bias, std::optional<Tensor> aux, int64_t M, int64_t N, int64_t K,
+              int64_t lda, int64_t ldb, int64_t ldc, int64_t splits) {
+  CHECK_BF16(a);
+  CHECK_BF16(b);
+  CHECK_GPU(c);
+  CHECK_CONTIG(c);
+  TORCH_CHECK(layout >= 0 && layout <= 2, "rl_gemm: layout must be 0, 1 or 2");
+  TORCH_CHECK(epi >= 0 && epi <= 5, "rl_gemm: bad epilogue");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31),
+              "rl_gemm: bad sizes");
+  TORCH_CHECK(aligned16(a) && aligned16(b), "rl_gemm: operands must be 16-byte aligned");
+  TORCH_CHECK(lda % 8 == 0 && ldb % 8 == 0 && ldc % 4 == 0, "rl_gemm: leading dims must be multiples of 8 (c: 4)");
+  // the contiguous dim of every operand is read in 8-element vectors
+  const int64_t a_vec = layout == 2 ? M : K, b_vec = layout == 0 ? K : N;
+  TORCH_CHECK(a_vec % 8 == 0 && b_vec % 8 == 0 && N % 4 == 0, "rl_gemm: vector dims must be multiples of 8");
+  const int64_t a_need = layout == 2 ? (K - 1) * lda + M : (M - 1) * lda + K;
+  const int64_t b_need = layout == 0 ? (N - 1) * ldb + K : (K - 1) * ldb + N;
+  TORCH_CHECK(a.numel() >= a_need && b.numel() >= b_need, "rl_gemm: operand too small for M/N/K/ld");
+  TORCH_CHECK(c.numel() >= (M - 1) * ldc + N, "rl_gemm: output too small");
+  TORCH_CHECK(c.scalar_type() == (epi == 3 ? at::kFloat : at::kBFloat16),
+              "rl_gemm: c must be fp32 for the atomic epilogue, bf16 otherwise");
+  const caamd::bf16* bp = nullptr;
+  const caamd::bf16* xp = nullptr;
+  if (bias && bias->defined()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() >= N, "rl_gemm: bias too small");
+    bp = reinterpret_cast<const caamd::bf16*>(bias->data_ptr());
+  }
+  if (epi == 4 || epi == 5) {
+    TORCH_CHECK(aux && aux->defined(), "rl_gemm: activation-backward epilogue needs aux");
+    CHECK_BF16(*aux);
+    TORCH_CHECK(aux->numel() >= (M - 1) * ldc + N, "rl_gemm: aux too small");
+    xp = reinterpret_cast<const caamd::bf16*>(aux->data_ptr());
+  }
+  caamd::rl_gemm((int)layout, reinterpret_cast<const caamd::bf16*>(a.data_ptr()),
+                 reinterpret_cast<const caamd::bf16*>(b.data_ptr()), c.data_ptr(), bp, xp, (int)M, (int)N, (int)K,
+                 (int)lda, (int)ldb, (int)ldc, (int)epi, (int)std::max<int64_t>(1, splits), cur_stream());
+  LAUNCH_CHECK();
+}
+
+static void check_conv_geom(int64_t B, int64_t H, int64_t W, int64_t C, int64_t KH, int64_t KW, int64_t S) {
+  TORCH_CHECK(B > 0 && H >= KH && W >= KW && KH > 0 && KW > 0 && S > 0 && C > 0, "rl conv: bad geometry");
+  TORCH_CHECK((KW * C) % 8 == 0 && (S * C) % 8 == 0 && (W * C) % 8 == 0,
+              "rl conv: KW*C, S*C and W*C must be multiples of 8");
+}
+
+void rl_im2col_(const Tensor& x, const Tensor& col, int64_t KH, int64_t KW, int64_t S, double scale) {
+  CHECK_GPU(x);
+  CHECK_CONTIG(x);
+  CHECK_BF16(col);
+  TORCH_CHECK(x.dim() == 4, "rl_im2col: x must be NHWC");
+  const bool u8 = x.scalar_type() == at::kByte;
+  TORCH_CHECK(u8 || x.scalar_type() == at::kBFloat16, "rl_im2col: x must be uint8 or bf16");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  check_conv_geom(B, H, W, C, KH, KW, S);
+  const int64_t OH = (H - KH) / S + 1, OW = (W - KW) / S + 1;
+  TORCH_CHECK(col.numel() == B * OH * OW * KH * KW * C, "rl_im2col: col must be [B*OH*OW, KH*KW*C]");
+  TORCH_CHECK(aligned16(col) && (reinterpret_cast<uintptr_t>(x.data_ptr()) & 15) == 0, "rl_im2col: alignment");
+  caamd::rl_im2col(x.data_ptr(), u8, reinterpret_cast<caamd::bf16*>(col.data_ptr()), (int)B, (int)H, (int)W,
+                   (int)C, (int)KH, (int)KW, (int)S, (float)scale, cur_stream());
+  LAUNCH_CHECK();
+}
+
+void rl_col2im_(const Tensor& dcol, std::optional<Tensor> y, const Tensor& dz, int64_t KH, int64_t KW, int64_t S,
+                int64_t act) {
+  CHECK_BF16(dcol);
+  CHECK_BF16(dz);
+  TORCH_CHECK(dz.dim() == 4, "rl_col2im: dz must be NHWC");
+  const int64_t B = dz.size(0), H = dz.size(1), W = dz.size(2), C = dz.size(3);
+  check_conv_geom(B, H, W, C, KH, KW, S);
+  TORCH_CHECK(C % 8 == 0, "rl_col2im: C must be a multiple of 8");
+  const int64_t OH = (H - KH) / S + 1, OW = (W - KW) / S + 1;
+  TORCH_CHECK(dcol.numel() == B * OH * OW * KH * KW * C, "rl_col2im: dcol must be [B*OH*OW, KH*KW*C]");
+  TORCH_CHECK(act >= 0 && act <= 2, "rl_col2im: act must be 0 (none), 1 (relu) or 2 (tanh)");
+  const caamd::bf16* yp = nullptr;
+  if (act) {
+    TORCH_CHECK(y && y->defined(), "rl_col2im: activation mask needs y");
+    CHECK_BF16(*y);
+    TORCH_CHECK(y->numel() == dz.numel(), "rl_col2im: y must match dz");
+    yp = reinterpret_cast<const caamd::bf16*>(y->data_ptr());
+  }
+  caamd::rl_col2im(reinterpret_cast<const caamd::bf16*>(dcol.data_ptr()), yp,
+                   reinterpret_cast<caamd::bf16*>(dz.data_ptr()), (int)B, (int)H, (int)W, (int)C, (int)KH, (int)KW,
+                   (int)S, (int)act, cur_stream());
+  LAUNCH_CHECK();
+}
+
+void rl_colsum_(const Tensor& x, const Tensor& db) {
+  CHECK_BF16(x);
+  CHECK_F32(db);
+  TORCH_CHECK(x.dim() == 2 && db.numel() == x.size(1), "rl_colsum: x [M,N], db [N]");
+  TORCH_CHECK(x.size(1) % 8 == 0 && x.size(1) <= 2048 && aligned16(x), "rl_colsum: N must be a multiple of 8, <= 2048");
+  if (x.size(0) > 0)
+    caamd::rl_colsum(reinterpret_cast<const caamd::bf16*>(x.data_ptr()), db.data_ptr<float>(), (int)x.size(0),
+                     (int)x.size(1), cur_stream());
+  LAUNCH_CHECK();
+}
+
+// returns (dlogits [B,A], dvf [B], stats [4] = sums of surrogate, vf loss, entropy, kl)
+std::vector<Tensor> ppo_loss_cat_(const Tensor& logits, const Tensor& vf, const Tensor& actions,
+                                  const Tensor& old_logp, const Tensor& adv, const Tensor& vt,
+                                  const Tensor& old_logits, double clip, double vf_clip, double vf_coeff,
+                                  double ent_coeff, double kl_coeff, std::optional<Tensor> kl_dev) {
+  CHECK_F32(logits);
+  CHECK_F32(vf);
+  CHECK_F32(old_logp);
+  CHECK_F32(adv);
+  CHECK_F32(vt);
+  CHECK_F32(old_logits);
+  CHECK_GPU(actions);
+  CHECK_CONTIG(actions);
+  CHECK_DT(actions, at::kLong);
+  TORCH_CHECK(logits.dim() == 2 && old_logits.sizes() == logits.sizes(), "ppo_loss: logits [B,A]");
+  const int64_t B = logits.size(0), A = logits.size(1);
+  TORCH_CHECK(A > 0 && vf.numel() == B && actions.numel() == B && old_logp.numel() == B && adv.numel() == B &&
+                  vt.numel() == B,
+              "ppo_loss: per-sample inputs must have B elements");
+  const float* klp = nullptr;
+  if (kl_dev && kl_dev->defined()) {
+    CHECK_F32(*kl_dev);
+    TORCH_CHECK(kl_dev->numel() >= 1, "ppo_loss: kl_dev must hold the KL coefficient");
+    klp = kl_dev->data_ptr<float>();
+  }
+  auto dlogits = at::empty_like(logits);
+  auto dvf = at::empty_like(vf);
+  auto stats = at::zeros({4}, logits.options());
+  if (B > 0) {
+    // the kernel clamps action indices into [0, A) (no out-of-row reads)
+    caamd::ppo_loss_cat(logits.data_ptr<float>(), vf.data_ptr<float>(), actions.data_ptr<int64_t>(),
+                        old_logp.data_ptr<float>(), adv.data_ptr<float>(), vt.data_ptr<float>(),
+                        old_logits.data_ptr<float>(), (int)B, (int)A, (float)clip, (float)vf_clip, (float)vf_coeff,
+                        (float)ent_coeff, (float)kl_coeff, klp, dlogits.data_ptr<float>(), dvf.data_ptr<float>(),
+                        stats.data_ptr<float>(), cur_stream());
+  }
+  LAUNCH_CHECK();
+  return {dlogits, dvf, stats};
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "cluster_anywhere_amd gfx950 HIP kernels";
   m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
@@ -712,4 +866,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("image_normalize", &image_normalize);
   m.def("add_relu_", &add_relu_);
   m.def("bias_act_", &bias_act_);
+  m.def("rl_gemm", &rl_gemm_);
+  m.def("rl_im2col", &rl_im2col_);
+  m.def("rl_col2im", &rl_col2im_);
+  m.def("rl_colsum", &rl_colsum_);
+  m.def("ppo_loss_cat", &ppo_loss_cat_);
 }

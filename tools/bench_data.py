@@ -60,6 +60,8 @@ def main():
                     help=">1 shares each GPU between actors (fractional num_gpus) so one's H2D "
                          "copy / host work overlaps another's graph replay")
     ap.add_argument("--timeline", default="", help="write a chrome trace + per-function summary here")
+    ap.add_argument("--preserve-order", action="store_true",
+                    help="deliver blocks in input order (off by default, as in the reference's DataContext)")
     args = ap.parse_args()
     import torch
 
@@ -67,6 +69,7 @@ def main():
     from cluster_anywhere_amd import data
 
     gpu = torch.cuda.is_available()
+    data.DataContext.get_current().execution_preserve_order = args.preserve_order
     ncpu = args.cpus or min(os.cpu_count() or 8, 16 * max(1, args.gpus))
     ray.init(num_cpus=ncpu, num_gpus=args.gpus if gpu else 0,
              object_store_memory=min(64 << 30, max(4 << 30, args.batch_size * args.hw * args.hw * 3 * 64)))
@@ -103,17 +106,20 @@ def main():
     from cluster_anywhere_amd.models.resnet import resnet
 
     gflop = resnet(args.model).flops_per_image(args.hw) / 1e9
+    stats = ds.stats()
     print(json.dumps({
         "metric": "Data GPU rows/sec (map_batches ResNet-50 inference)",
         "value": round(rps, 1), "unit": "rows/s", "n_gpus": args.gpus, "rows": n, "warmup_rows": warm,
         "seconds": round(dt, 3), "higher_is_better": True, "scaling": "strong",
         "dtype": "bf16" if gpu else "fp32", "data": "synthetic uint8 224x224x3 images, random-init weights",
         "config": {"model": args.model, "batch_size": args.batch_size, "hw": args.hw, "read_blocks": blocks,
-                   "actors": args.gpus * max(1, args.actors_per_gpu), "cpus": ncpu},
+                   "actors": args.gpus * max(1, args.actors_per_gpu), "cpus": ncpu,
+                   "preserve_order": args.preserve_order},
         "model_tflops_per_gpu": round(rps * gflop / 1e3 / max(1, args.gpus), 1),
         "time_to_first_batch_s": round(t_first - t0, 3),
         "steady_state_rows_per_s": round((n - n_first) / max(1e-9, t_end - t_first), 1),
     }), flush=True)
+    print(stats, flush=True)
     if args.timeline:
         ev = ray.timeline()
         with open(args.timeline, "w") as f:
