@@ -239,6 +239,14 @@ class Head:
 
     # ------------------------------------------------------------------ loop
     def start(self):
+        self._zygote = None
+        from . import zygote
+
+        if zygote.enabled():
+            try:  # forks pre-imported workers (core/zygote.py); Popen until it is ready
+                self._zygote = zygote.Zygote(self.session_dir)
+            except Exception:
+                self._zygote = None
         self.thread = threading.Thread(target=self._loop, name="caamd-head", daemon=True)
         self.thread.start()
         for _ in range(self._prestart):
@@ -1009,11 +1017,15 @@ class Head:
         # workers import user code the way the driver does (reference: the driver's
         # code search path is propagated through the job config)
         e["CAAMD_SYS_PATH"] = os.pathsep.join(p for p in sys.path if p and os.path.isdir(p))
-        log = open(os.path.join(self.session_dir, f"worker-{worker_id.hex()[:8]}.log"), "ab")
-        proc = subprocess.Popen([sys.executable, "-m", "cluster_anywhere_amd.core.worker_main"],
-                                env=e, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
-                                cwd=os.getcwd())
-        log.close()
+        log_path = os.path.join(self.session_dir, f"worker-{worker_id.hex()[:8]}.log")
+        zyg = getattr(self, "_zygote", None)
+        proc = zyg.spawn(e, log_path, os.getcwd()) if zyg is not None else None
+        if proc is None:
+            log = open(log_path, "ab")
+            proc = subprocess.Popen([sys.executable, "-m", "cluster_anywhere_amd.core.worker_main"],
+                                    env=e, stdout=log, stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL,
+                                    cwd=os.getcwd())
+            log.close()
         w = WorkerInfo(worker_id=worker_id, pid=proc.pid, node=node, gpu_key=tuple(gpu_ids),
                        kind="worker", proc=proc, alive=False)
         self.workers[worker_id] = w
@@ -1851,6 +1863,8 @@ class Head:
             pass
         if self.thread is not None:
             self.thread.join(timeout=5)
+        if getattr(self, "_zygote", None) is not None:
+            self._zygote.stop()
         try:
             self.lsock.close()
             os.unlink(self.sock_path)

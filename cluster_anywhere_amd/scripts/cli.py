@@ -251,6 +251,9 @@ def main(argv=None):
     x = jsub.add_parser("list")
     x.add_argument("--address", default=None)
     j.set_defaults(fn=cmd_job)
+    from ..serve.scripts import add_parser as add_serve_parser
+
+    add_serve_parser(sub)
     a = ap.parse_args(argv)
     return a.fn(a) or 0
 

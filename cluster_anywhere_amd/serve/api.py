@@ -31,9 +31,12 @@ def _get_controller(create: bool = True):
 
 
 def start(http_options: Union[None, dict, HTTPOptions] = None, detached: bool = True,
-          proxy_location: str = "HeadOnly", **_ignored):
-    """Start the controller and (unless ``proxy_location='Disabled'``) the HTTP proxy."""
+          proxy_location: str = "HeadOnly", grpc_options=None, **_ignored):
+    """Start the controller and (unless ``proxy_location='Disabled'``) the HTTP proxy;
+    with ``grpc_options`` (a ``gRPCOptions`` or dict) also the gRPC proxy."""
     ctl = _get_controller()
+    if grpc_options is not None:
+        _start_grpc(ctl, grpc_options)
     if proxy_location in ("Disabled", "disabled", None):
         return ctl
     proxy, port = core.get(ctl.get_proxy.remote())
@@ -50,6 +53,34 @@ def start(http_options: Union[None, dict, HTTPOptions] = None, detached: bool = 
         port = core.get(proxy.ready.remote())
         core.get(ctl.set_proxy.remote(proxy, port))
     return ctl
+
+
+def _start_grpc(ctl, grpc_options):
+    from .grpc_proxy import gRPCOptions, gRPCProxy
+
+    if isinstance(grpc_options, dict):
+        grpc_options = gRPCOptions(**grpc_options)
+    proxy, port = core.get(ctl.get_grpc_proxy.remote())
+    if proxy is not None:
+        return port
+    from ..core.actor import ActorClass
+
+    fns = [f if isinstance(f, str) else f"{f.__module__}.{f.__qualname__}" if f.__module__ != "__main__" else f
+           for f in grpc_options.grpc_servicer_functions]
+    P = ActorClass(gRPCProxy, {})
+    proxy = P.options(num_cpus=0, max_concurrency=8, name="SERVE_GRPC_PROXY", namespace=NAMESPACE,
+                      lifetime="detached").remote(grpc_options.host, grpc_options.port, fns,
+                                                  grpc_options.request_timeout_s)
+    port = core.get(proxy.ready.remote())
+    core.get(ctl.set_grpc_proxy.remote(proxy, port))
+    return port
+
+
+def grpc_port() -> Optional[int]:
+    ctl = _get_controller(create=False)
+    if ctl is None:
+        return None
+    return core.get(ctl.get_grpc_proxy.remote())[1]
 
 
 def http_port() -> Optional[int]:
@@ -117,9 +148,10 @@ def run(target: Union[Application, Deployment], *, name: str = "default", route_
         time.sleep(0.05)
     for key in [k for k in _routers if k[0] == name]:
         _routers[key].invalidate()
-    proxy, _ = core.get(ctl.get_proxy.remote())
-    if proxy is not None:
-        core.get(proxy.refresh.remote())
+    for getter in (ctl.get_proxy, ctl.get_grpc_proxy):
+        proxy, _ = core.get(getter.remote())
+        if proxy is not None:
+            core.get(proxy.refresh.remote())
     handle = DeploymentHandle(ingress, name)
     if blocking:
         try:

@@ -173,6 +173,21 @@ class ServeController:
     def get_proxy(self):
         return self.proxy, self.proxy_port
 
+    def set_grpc_proxy(self, proxy, port):
+        self.grpc_proxy, self.grpc_port = proxy, port
+        return True
+
+    def get_grpc_proxy(self):
+        return getattr(self, "grpc_proxy", None), getattr(self, "grpc_port", None)
+
+    def set_deploy_config(self, cfg: Optional[dict]):
+        """Last config applied by ``serve deploy`` (returned by ``serve config``)."""
+        self.deploy_config = cfg
+        return True
+
+    def get_deploy_config(self):
+        return getattr(self, "deploy_config", None)
+
     def record_handle_metrics(self, app, deployment, queued):
         with self.lock:
             a = self.apps.get(app)
@@ -190,12 +205,14 @@ class ServeController:
                 if not self._orphans:
                     break
             time.sleep(0.05)
-        if self.proxy is not None:
-            try:
-                core.kill(self.proxy)
-            except Exception:
-                pass
-            self.proxy = None
+        for attr in ("proxy", "grpc_proxy"):
+            p = getattr(self, attr, None)
+            if p is not None:
+                try:
+                    core.kill(p)
+                except Exception:
+                    pass
+                setattr(self, attr, None)
         self.alive = False
         return True
 

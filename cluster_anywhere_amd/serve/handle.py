@@ -142,7 +142,18 @@ class DeploymentResponse:
             return again.result(timeout_s, _retries - 1)
 
     def __await__(self):
-        return asyncio.wrap_future(self._future()).__await__()
+        return self._await_retrying(1).__await__()
+
+    async def _await_retrying(self, retries: int):
+        from ..exceptions import RayActorError
+
+        try:
+            return await asyncio.wrap_future(self._future())
+        except RayActorError:
+            if retries <= 0:
+                raise
+            self._router.invalidate()  # the replica died (e.g. redeploy): pick again
+            return await self._resend()._await_retrying(retries - 1)
 
     def _to_object_ref(self):
         return self._ref
@@ -204,20 +215,23 @@ class DeploymentResponseGenerator:
 
 class DeploymentHandle:
     def __init__(self, deployment_name: str, app_name: str = "default", *, method_name: str = "__call__",
-                 multiplexed_model_id: str = "", stream: bool = False):
+                 multiplexed_model_id: str = "", stream: bool = False, _grpc: Optional[tuple] = None):
         self.deployment_name = deployment_name
         self.app_name = app_name
         self._method = method_name
         self._model_id = multiplexed_model_id
         self._stream = stream
+        self._grpc = _grpc  # (request type name, request id): serialized protobuf in/out (grpc_proxy.py)
 
     def options(self, *, method_name: Optional[str] = None, multiplexed_model_id: Optional[str] = None,
-                stream: Optional[bool] = None, use_new_handle_api: bool = True, **_ignored) -> "DeploymentHandle":
+                stream: Optional[bool] = None, use_new_handle_api: bool = True, _grpc: Optional[tuple] = None,
+                **_ignored) -> "DeploymentHandle":
         return DeploymentHandle(self.deployment_name, self.app_name,
                                 method_name=method_name if method_name is not None else self._method,
                                 multiplexed_model_id=multiplexed_model_id if multiplexed_model_id is not None
                                 else self._model_id,
-                                stream=self._stream if stream is None else stream)
+                                stream=self._stream if stream is None else stream,
+                                _grpc=_grpc if _grpc is not None else self._grpc)
 
     def __getattr__(self, name):
         if name.startswith("_"):
@@ -229,6 +243,10 @@ class DeploymentHandle:
         args = tuple(_unwrap(a) for a in args)
         kwargs = {k: _unwrap(v) for k, v in kwargs.items()}
         meta = {"method": self._method, "model_id": self._model_id, "request_id": uuid.uuid4().hex[:12]}
+        if self._grpc is not None:
+            meta["grpc"] = self._grpc[0]
+            if self._grpc[1]:
+                meta["request_id"] = self._grpc[1]
 
         if self._stream:
             tag, h, _ = router.choose(self._model_id)

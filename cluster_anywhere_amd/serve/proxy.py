@@ -105,12 +105,21 @@ class HTTPProxy:
 
         router = _router(app_name, ingress)
         loop = asyncio.get_event_loop()
+        from ..exceptions import RayActorError
+
         try:
-            tag, h, _ = await loop.run_in_executor(None, router.choose, model_id)
-            try:
-                status, hdrs, body = await h.handle_http.remote(req)
-            finally:
-                router.done(tag)
+            for attempt in range(3):
+                tag, h, _ = await loop.run_in_executor(None, router.choose, model_id)
+                try:
+                    status, hdrs, body = await h.handle_http.remote(req)
+                    break
+                except RayActorError:
+                    # the replica went away (redeploy / downscale / crash): re-resolve and retry
+                    if attempt == 2:
+                        raise
+                    router.invalidate()
+                finally:
+                    router.done(tag)
         except Exception as e:  # noqa
             return await _respond(send, 500, f"{type(e).__name__}: {e}".encode())
         await send({"type": "http.response.start", "status": status,

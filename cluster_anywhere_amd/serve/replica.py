@@ -126,9 +126,18 @@ class ServeReplica:
         tok = _request_context.set(RequestContext(meta.get("route", ""), meta.get("request_id", ""),
                                                   self.app_name, meta.get("model_id", "")))
         try:
+            grpc_t = meta.get("grpc")
+            if grpc_t:  # serialized protobuf request from the gRPC proxy
+                from .grpc_proxy import decode_request
+
+                args = (decode_request(grpc_t, args[0]),) + tuple(args[1:])
             r = await self._invoke(self._method(meta.get("method", "__call__")), args, kwargs)
             if inspect.isgenerator(r) or inspect.isasyncgen(r):
                 raise TypeError("method returned a generator: call it with handle.options(stream=True)")
+            if grpc_t:
+                from .grpc_proxy import encode_response
+
+                return encode_response(r)
             return r
         finally:
             _request_context.reset(tok)
@@ -141,6 +150,14 @@ class ServeReplica:
                                                   self.app_name, meta.get("model_id", "")))
         try:
             m = self._method(meta.get("method", "__call__"))
+            grpc_t = meta.get("grpc")
+            if grpc_t:  # serialized protobuf in, each streamed message serialized out
+                from .grpc_proxy import decode_request, encode_response
+
+                args = (decode_request(grpc_t, args[0]),) + tuple(args[1:])
+                async for x in self._stream_items(m, args, kwargs):
+                    yield encode_response(x)
+                return
             if inspect.isasyncgenfunction(m):
                 async for x in m(*args, **kwargs):
                     yield x
@@ -162,6 +179,26 @@ class ServeReplica:
         finally:
             _request_context.reset(tok)
             self.ongoing -= 1
+
+    async def _stream_items(self, m, args, kwargs):
+        if inspect.isasyncgenfunction(m):
+            async for x in m(*args, **kwargs):
+                yield x
+            return
+        r = await self._invoke(m, args, kwargs)
+        if inspect.isasyncgen(r):
+            async for x in r:
+                yield x
+        elif inspect.isgenerator(r):
+            loop = asyncio.get_event_loop()
+            sentinel = object()
+            while True:
+                x = await loop.run_in_executor(self.pool, next, r, sentinel)
+                if x is sentinel:
+                    break
+                yield x
+        else:
+            yield r
 
     async def handle_http(self, req: Dict):
         """``req``: method, path, query_string, headers, body, route_prefix."""
