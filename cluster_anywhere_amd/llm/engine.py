@@ -62,6 +62,10 @@ class _Seq:
         return self.prompt + self.out
 
     @property
+    def last_token(self):
+        return self.out[-1] if self.out else self.prompt[-1]
+
+    @property
     def ctx(self):
         return len(self.prompt) + len(self.out)
 
@@ -121,6 +125,9 @@ class LLMEngine:
         self.use_graphs = use_graphs and self.device.type == "cuda"
         self.graphs: Dict[int, tuple] = {}
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "preemptions": 0, "steps": 0}
+        # (batch size, seconds) of every decode step: forward + sampling, host included
+        self.decode_times: List[tuple] = []
+        self._pinned: Dict[int, Dict[str, torch.Tensor]] = {}
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(0)
 
@@ -226,19 +233,33 @@ class LLMEngine:
         return logits
 
     def _decode_inputs(self, batch: List[_Seq], B: int):
-        toks = torch.zeros(B, dtype=torch.long)
-        pos = torch.zeros(B, dtype=torch.int32)
-        slots = torch.full((B,), -1, dtype=torch.int32)
-        ctx = torch.zeros(B, dtype=torch.int32)
-        bt = torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32)
+        """Decode inputs built with numpy in (pinned, reused) host buffers: no
+        per-sequence tensor construction, and the H2D copies are truly async."""
+        import numpy as np
+
+        buf = self._pinned.get(B)
+        if buf is None:
+            pin = self.device.type == "cuda"
+            buf = self._pinned[B] = {
+                "toks": torch.zeros(B, dtype=torch.long, pin_memory=pin),
+                "pos": torch.zeros(B, dtype=torch.int32, pin_memory=pin),
+                "slots": torch.full((B,), -1, dtype=torch.int32, pin_memory=pin),
+                "ctx": torch.zeros(B, dtype=torch.int32, pin_memory=pin),
+                "bt": torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)}
+        n = len(batch)
+        toks, pos, slots, ctx, bt = (buf[k].numpy() for k in ("toks", "pos", "slots", "ctx", "bt"))
+        c = np.fromiter((s.ctx for s in batch), np.int32, n)
+        p = c - 1  # position of the newest (not yet cached) token
+        toks[:n] = np.fromiter((s.last_token for s in batch), np.int64, n)
+        toks[n:] = 0
+        pos[:n], pos[n:] = p, 0
+        ctx[:n], ctx[n:] = c, 0
+        bt[:n] = 0
         for i, s in enumerate(batch):
-            p = s.ctx - 1  # position of the newest (not yet cached) token
-            toks[i] = s.tokens[-1]
-            pos[i] = p
-            slots[i] = s.blocks[p // self.bs] * self.bs + p % self.bs
-            ctx[i] = s.ctx
-            bt[i, : len(s.blocks)] = torch.tensor(s.blocks, dtype=torch.int32)
-        return toks, pos, slots, bt, ctx
+            bt[i, : len(s.blocks)] = s.blocks
+        slots[:n] = bt[np.arange(n), p // self.bs] * self.bs + p % self.bs
+        slots[n:] = -1
+        return buf["toks"], buf["pos"], buf["slots"], buf["bt"], buf["ctx"]
 
     def _bucket(self, n):
         b = 1
@@ -288,7 +309,7 @@ class LLMEngine:
             st["ctx"].copy_(ctx, non_blocking=True)
             graph.replay()
             return out[:n]
-        toks, pos, slots, bt, ctx = self._decode_inputs(batch, n)
+        toks, pos, slots, bt, ctx = (t.clone() for t in self._decode_inputs(batch, n))
         dev = self.device
         max_ctx = max(s.ctx for s in batch)
         return self.model.decode(toks.to(dev), pos.to(dev), slots.to(dev), self.k_caches, self.v_caches,
@@ -363,8 +384,10 @@ class LLMEngine:
             batch = list(self.running)
             if not batch:
                 return []
+            t0 = time.perf_counter()
             logits = self._run_decode(batch)
             toks = self._sample(logits, batch)
+            self.decode_times.append((len(batch), time.perf_counter() - t0))
             return self._append(batch, toks, time.time())
 
     def generate(self, prompts: List[List[int]], params: Optional[SamplingParams] = None) -> List[RequestOutput]:

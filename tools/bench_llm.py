@@ -45,6 +45,7 @@ def main():
         if b <= a.max_num_seqs and eng.use_graphs:
             eng._graph_for(b)
     torch.cuda.synchronize()
+    eng.decode_times.clear()
     t0 = time.time()
     outs = eng.generate(prompts, sp)
     torch.cuda.synchronize()
@@ -60,7 +61,20 @@ def main():
         "elapsed_s": round(dt, 2), "ttft_p50_s": round(ttft[len(ttft) // 2], 3),
         "tpot_p50_ms": round(1000 * tpot[len(tpot) // 2], 2), "kv_blocks": eng.num_blocks,
         "preemptions": eng.stats["preemptions"], "graphs": eng.use_graphs, "dtype": "bf16",
+        "max_num_seqs": a.max_num_seqs, **_steady(eng.decode_times, a.max_num_seqs),
         "data": "synthetic prompts, random-init weights"}))
+
+
+def _steady(times, max_seqs):
+    """Steady-state decode: steps that ran with (nearly) the full batch; the step
+    latency there is the time between two tokens of every running sequence."""
+    full = sorted(t for b, t in times if b >= 0.9 * max_seqs)
+    if not full:
+        return {"steady_decode_steps": 0}
+    return {"steady_decode_steps": len(full), "steady_batch": max_seqs,
+            "steady_tpot_p50_ms": round(1000 * full[len(full) // 2], 2),
+            "steady_tpot_p90_ms": round(1000 * full[int(len(full) * 0.9)], 2),
+            "steady_decode_tokens_per_s": round(max_seqs / full[len(full) // 2], 1)}
 
 
 if __name__ == "__main__":
