@@ -123,6 +123,10 @@ class LLMEngine:
         self._ids = itertools.count()
         self.lock = threading.RLock()
         self.use_graphs = use_graphs and self.device.type == "cuda"
+        if self.device.type == "cuda":
+            from ..ops.gemm_tuning import use_tuned_gemms
+
+            use_tuned_gemms()  # shipped per-shape hipBLASLt selections (decode GEMMs are skinny)
         self.graphs: Dict[int, tuple] = {}
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "preemptions": 0, "steps": 0}
         # (batch size, seconds) of every decode step: forward + sampling, host included

@@ -6,6 +6,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace caamd {
 typedef __bf16 bf16;
 void ln_fwd_launch(const bf16*, const bf16*, bf16*, const bf16*, const bf16*, bf16*, float*, float*,
@@ -403,6 +405,9 @@ void rope_cache_launch(bf16*, const float*, const int*, const int*, bf16*, bf16*
 bool paged_decode_launch(const bf16*, int, const bf16*, const bf16*, const int*, int, const int*, bf16*, float*,
                          float*, int, int, int, int, int, int, float, hipStream_t);
 int paged_max_parts(int);
+int paged_mfma_max_parts(int);
+bool paged_decode_mfma_launch(const bf16*, int, const bf16*, const bf16*, const int*, int, const int*, bf16*,
+                              float*, float*, int, int, int, int, int, int, float, hipStream_t);
 void fa_fwd_gqa_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
                        int, hipStream_t);
 }
@@ -481,8 +486,10 @@ void rope_cache_(Tensor& qkv, const Tensor& cos_sin, const Tensor& positions, co
   }
 }
 
+// impl: -1 auto (MFMA kernel for D=128 / 16-token pages / G <= 16 unless CAAMD_PAGED_MFMA=0),
+//        0 the VALU kernel, 1 the MFMA kernel
 Tensor paged_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
-                    const Tensor& ctx_lens, int64_t max_ctx, int64_t H, double scale) {
+                    const Tensor& ctx_lens, int64_t max_ctx, int64_t H, double scale, int64_t impl) {
   CHECK_GPU(q);
   CHECK_DT(q, at::kBFloat16);
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "paged_decode: q must be [B, >=H*D] with unit inner stride");
@@ -501,14 +508,22 @@ Tensor paged_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cach
   TORCH_CHECK(block_tables.size(0) == B && ctx_lens.numel() == B, "paged_decode: batch mismatch");
   TORCH_CHECK(max_ctx <= block_tables.size(1) * BS, "paged_decode: max_ctx exceeds block table capacity");
   auto out = at::empty({B, H * D}, q.options());
-  const int mp = caamd::paged_max_parts((int)max_ctx);
+  const int G = (int)(H / KVH);
+  const bool mfma_ok = D == 128 && BS == 16 && (G == 1 || G == 2 || G == 4 || G == 8 || G == 16);
+  if (impl < 0) {
+    const char* e = std::getenv("CAAMD_PAGED_MFMA");
+    impl = (mfma_ok && !(e && e[0] == '0')) ? 1 : 0;
+  }
+  TORCH_CHECK(impl == 0 || mfma_ok, "paged_decode: the MFMA kernel needs D=128, 16-token pages, H/KVH in {1..16}");
+  const int mp = impl == 1 ? caamd::paged_mfma_max_parts((int)max_ctx) : caamd::paged_max_parts((int)max_ctx);
   Tensor pacc, pml;
   if (mp > 1) {
     pacc = at::empty({B, H, mp, D}, q.options().dtype(at::kFloat));
     pml = at::empty({B, H, mp, 2}, q.options().dtype(at::kFloat));
   }
   if (B > 0) {
-    const bool ok = caamd::paged_decode_launch(
+    auto launch = impl == 1 ? caamd::paged_decode_mfma_launch : caamd::paged_decode_launch;
+    const bool ok = launch(
         bp(q), (int)q.stride(0), bp(k_cache), bp(v_cache), block_tables.data_ptr<int>(), (int)block_tables.size(1),
         ctx_lens.data_ptr<int>(), bp(out), mp > 1 ? pacc.data_ptr<float>() : nullptr,
         mp > 1 ? pml.data_ptr<float>() : nullptr, B, (int)H, KVH, D, BS, (int)max_ctx, (float)scale, cur_stream());
@@ -861,7 +876,9 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("residual") = pybind11::none());
   m.def("silu_mul", &silu_mul);
   m.def("rope_cache_", &rope_cache_);
-  m.def("paged_decode", &paged_decode);
+  m.def("paged_decode", &paged_decode, pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
+        pybind11::arg("block_tables"), pybind11::arg("ctx_lens"), pybind11::arg("max_ctx"), pybind11::arg("H"),
+        pybind11::arg("scale"), pybind11::arg("impl") = -1);
   m.def("flash_attn_gqa", &flash_attn_gqa);
   m.def("image_normalize", &image_normalize);
   m.def("add_relu_", &add_relu_);

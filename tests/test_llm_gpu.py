@@ -73,9 +73,32 @@ def test_paged_decode(C, H, KVH, D, lens):
     bt = perm[: B * maxb].view(B, maxb).contiguous()
     ctx = torch.tensor(lens, device="cuda", dtype=torch.int32)
     q = torch.randn(B, (H + 2 * KVH) * D, device="cuda", dtype=torch.bfloat16)  # fused-qkv row stride
-    out = C.paged_decode(q, kc, vc, bt, ctx, max(lens), H, 1 / math.sqrt(D))
     ref = L.paged_decode_ref(q, kc, vc, bt, ctx, H, 1 / math.sqrt(D))
+    out = C.paged_decode(q, kc, vc, bt, ctx, max(lens), H, 1 / math.sqrt(D))  # default: MFMA for D=128
     assert _rel(out, ref) < 2e-2
+    if D == 128:  # both implementations against the fp32 reference
+        for impl in (0, 1):
+            o = C.paged_decode(q, kc, vc, bt, ctx, max(lens), H, 1 / math.sqrt(D), impl)
+            assert _rel(o, ref) < 2e-2, impl
+
+
+@pytest.mark.parametrize("lens", [[1, 15, 16, 17, 31, 32, 33], [255, 256, 257, 511, 512, 600, 1500]])
+def test_paged_decode_mfma_edges(C, lens):
+    torch.manual_seed(1)
+    H, KVH, D, BS = 32, 8, 128, 16
+    B = len(lens)
+    maxb = max(math.ceil(n / BS) for n in lens)
+    kc = torch.randn(B * maxb + 2, KVH, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.randperm(B * maxb + 2, device="cuda").int()[: B * maxb].view(B, maxb).contiguous()
+    ctx = torch.tensor(lens, device="cuda", dtype=torch.int32)
+    q = torch.randn(B, H * D, device="cuda", dtype=torch.bfloat16) * 3  # peaked softmax
+    ref = L.paged_decode_ref(q, kc, vc, bt, ctx, H, 1 / math.sqrt(D))
+    out = C.paged_decode(q, kc, vc, bt, ctx, max(lens), H, 1 / math.sqrt(D), 1)
+    assert _rel(out, ref) < 2e-2
+    # max_ctx larger than any sequence (graph replays pass max_model_len)
+    out2 = C.paged_decode(q, kc, vc, bt, ctx, maxb * BS, H, 1 / math.sqrt(D), 1)
+    assert torch.equal(out, out2)
 
 
 @pytest.mark.parametrize("H,KVH,D,T", [(32, 8, 128, 300), (8, 2, 64, 1024), (4, 4, 128, 77)])
@@ -106,4 +129,9 @@ def test_llama_engine_gpu():
     dense = m(torch.tensor([seq], device="cuda"))[0, len(prompts[1]) - 1: -1].float()
     gen = torch.tensor(o1[1].output_token_ids, device="cuda")
     agree = (dense.argmax(-1) == gen).float().mean().item()
-    assert agree > 0.9
+    # random-init weights give near-tied logits: where the paged decode (bf16 P in the
+    # MFMA P.V) picks another token than the dense forward, it must be a near tie
+    top = dense.max(-1).values
+    gap = top - dense.gather(1, gen[:, None]).squeeze(1)
+    spread = top - dense.median(-1).values
+    assert agree > 0.75 and bool((gap <= 0.05 * spread).all()), (agree, (gap / spread).max().item())
