@@ -278,9 +278,14 @@ class AlgorithmConfig:
 
     def get_rollout_fragment_length(self):
         if self.rollout_fragment_length != "auto":
-            return int(self.rollout_fragment_length)
-        per = max(1, self.num_env_runners) * self.num_envs_per_env_runner
-        return max(1, int(np.ceil(self.total_train_batch_size / per)))
+            n = int(self.rollout_fragment_length)
+        else:
+            per = max(1, self.num_env_runners) * self.num_envs_per_env_runner
+            n = max(1, int(np.ceil(self.total_train_batch_size / per)))
+        if self.model_config.get("use_lstm"):  # fragments are cut into whole max_seq_len sequences
+            L = int(self.model_config.get("max_seq_len", 20))
+            n = ((n + L - 1) // L) * L
+        return n
 
     def module_factory(self) -> Callable:
         cls = self.rl_module_class or self.default_module_class()
@@ -313,6 +318,8 @@ class AlgorithmConfig:
         if self.is_multi_agent:
             if not self.module_ids():
                 raise ValueError("config.multi_agent(policies=...) needs at least one module id")
+            if self.model_config.get("use_lstm"):
+                raise NotImplementedError("recurrent modules are single-agent only for now")
             if self.algo_class is not None and not getattr(self.algo_class, "supports_multi_agent", False):
                 raise NotImplementedError(f"{self.algo_class.__name__} has no multi-agent training step yet")
 
@@ -509,8 +516,11 @@ class Algorithm(Trainable):
 
 
 def concat_fragments(frags, keys=None):
-    """Concatenate time-major fragments along the env axis."""
-    keys = keys or [k for k, v in frags[0].items() if isinstance(v, np.ndarray) and k != "last_obs"]
+    """Concatenate time-major fragments along the env axis (``last_*`` entries,
+    one row per env, along axis 0)."""
+    keys = keys or [k for k, v in frags[0].items() if isinstance(v, np.ndarray) and not k.startswith("last_")]
     out = {k: np.concatenate([f[k] for f in frags], axis=1) for k in keys}
-    out["last_obs"] = np.concatenate([f["last_obs"] for f in frags], axis=0)
+    for k in frags[0]:
+        if k.startswith("last_") and isinstance(frags[0][k], np.ndarray):
+            out[k] = np.concatenate([f[k] for f in frags], axis=0)
     return out

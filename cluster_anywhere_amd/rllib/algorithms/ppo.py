@@ -37,6 +37,9 @@ class PPOConfig(AlgorithmConfig):
         self.train_batch_size = 4000
 
 
+_SEQ_KEYS = ("actions", "action_logp", "action_dist_inputs", "advantages", "value_targets")
+
+
 class PPOLearner(Learner):
     graph_capturable = True  # compute_loss has no host syncs / host-side state (KL coeff lives on device)
 
@@ -45,9 +48,17 @@ class PPOLearner(Learner):
         self._kl_dev = (torch.full((1,), float(self.kl_coeff), device=self.device)
                         if self.device.type == "cuda" else None)
 
+    def _stateful(self) -> bool:
+        return bool(getattr(self.module, "is_stateful", lambda: False)())
+
     def compute_loss(self, batch):
         c = self.config
-        out = self.module.forward_train(batch)
+        if self._stateful():  # sequences [S, L]: the module unrolls them; the loss sees flat steps
+            st = {k[len("state_in_"):]: v for k, v in batch.items() if k.startswith("state_in_")}
+            out = self.module.forward_train(dict(batch, state_in=st))
+            batch = {k: (v.reshape((-1,) + tuple(v.shape[2:])) if k in _SEQ_KEYS else v) for k, v in batch.items()}
+        else:
+            out = self.module.forward_train(batch)
         if self.module.dist_cls is Categorical:
             # one fused kernel on GPU (ops/rl_encoder.py); the same math in torch on CPU
             use_kl = c.get("use_kl_loss", True)
@@ -98,8 +109,13 @@ class PPOLearner(Learner):
         p = build_pipeline(user, obs_space=self.obs_space, act_space=self.act_space) if user else ConnectorPipelineV2()
         p.append(NumpyToTensor(device=self.device))
         p.append(GeneralAdvantageEstimation(gamma=c["gamma"], lambda_=c.get("lambda_", 1.0)))
-        p.append(FlattenTimeMajor(keys=("obs", "actions", "action_logp", "action_dist_inputs", "advantages",
-                                        "value_targets")))
+        if self._stateful():  # recurrent module: train on max_seq_len sequences
+            from ..connectors import ChunkSequences
+
+            p.append(ChunkSequences(max_seq_len=c.get("model_config", {}).get("max_seq_len", 20)))
+        else:
+            p.append(FlattenTimeMajor(keys=("obs", "actions", "action_logp", "action_dist_inputs", "advantages",
+                                            "value_targets")))
         p.set_input_spaces(self.obs_space, self.act_space)
         return p
 
@@ -135,15 +151,18 @@ class PPO(Algorithm):
         t1 = time.perf_counter()
         self.env_steps_sampled += steps
         lg = self.learner_group
+        mbs = c.minibatch_size
+        if c.model_config.get("use_lstm"):  # minibatches of whole sequences
+            mbs = max(1, mbs // int(c.model_config.get("max_seq_len", 20)))
         kl_of = (lambda st: {m: s.get("mean_kl_loss", 0.0) for m, s in st.items()}) if self.is_multi_agent \
             else (lambda st: st.get("mean_kl_loss", 0.0))
         if lg.local is not None:
             batch = lg.local.postprocess(frag)
-            stats = lg.local.update(batch, c.minibatch_size, c.num_epochs)
+            stats = lg.local.update(batch, mbs, c.num_epochs)
             kl = lg.local.update_kl(kl_of(stats))
         else:
             batch = _to_cpu(lg.call("postprocess", frag))
-            stats = lg.update(batch, c.minibatch_size, c.num_epochs)
+            stats = lg.update(batch, mbs, c.num_epochs)
             kl = lg.call("update_kl", kl_of(stats))
         if self.is_multi_agent:
             for m, k in kl.items():

@@ -54,7 +54,10 @@ class GeneralAdvantageEstimation(ConnectorV2):
     @torch.no_grad()
     def __call__(self, *, rl_module=None, batch, **kw):
         vf = batch["vf_preds"].float()
-        last = rl_module.compute_values({"obs": batch["last_obs"]}).float()
+        vb = {"obs": batch["last_obs"]}
+        if "last_state_h" in batch:  # recurrent module: V after the fragment's last state
+            vb["state_in"] = {"h": batch["last_state_h"], "c": batch["last_state_c"]}
+        last = rl_module.compute_values(vb).float()
         values = torch.cat([vf, last[None]], 0)
         nonterm = 1.0 - batch["terminateds"].float()
         mask = batch.get("mask")
@@ -100,4 +103,35 @@ class FlattenTimeMajor(ConnectorV2):
         return out
 
 
-__all__ = ["NumpyToTensor", "GeneralAdvantageEstimation", "FlattenTimeMajor"]
+class ChunkSequences(ConnectorV2):
+    """Recurrent modules: cut the time-major fragment ``[T, N, ...]`` into
+    ``max_seq_len`` sequences ``[N*T/L, L, ...]`` (each env column cut along time),
+    with the recurrent state at every sequence start (``state_in_*`` ``[S, cell]``)
+    and ``resets [S, L]`` marking steps that begin a new episode inside a sequence."""
+
+    KEYS = ("obs", "actions", "action_logp", "action_dist_inputs", "advantages", "value_targets")
+
+    def __init__(self, input_observation_space=None, input_action_space=None, *, max_seq_len: int = 20, **kw):
+        super().__init__(input_observation_space, input_action_space)
+        self.L = int(max_seq_len)
+
+    def _seq(self, v, T, N):
+        L = self.L
+        v = v.transpose(0, 1).contiguous()  # [N, T, ...]
+        return v.reshape((N * (T // L), L) + tuple(v.shape[2:]))
+
+    def __call__(self, *, batch, **kw):
+        T, N = batch["rewards"].shape[:2]
+        if T % self.L:
+            raise ValueError(f"fragment length {T} is not a multiple of max_seq_len {self.L}")
+        out = {k: self._seq(batch[k], T, N) for k in self.KEYS if k in batch}
+        prev_term = torch.zeros_like(batch["terminateds"], dtype=torch.float32)
+        prev_term[1:] = batch["terminateds"][:-1].float()
+        out["resets"] = self._seq(prev_term, T, N)
+        for k in [k for k in batch if k.startswith("state_in_")]:
+            st = batch[k][:: self.L]  # [T/L, N, cell] state at each sequence start
+            out[k] = st.transpose(0, 1).reshape(N * (T // self.L), -1).float()
+        return out
+
+
+__all__ = ["NumpyToTensor", "GeneralAdvantageEstimation", "FlattenTimeMajor", "ChunkSequences"]

@@ -198,7 +198,14 @@ class RLModule(nn.Module):
 
 class DefaultActorCriticModule(RLModule):
     """Encoder (MLP or Nature-CNN for image obs) + pi head + value head; the
-    encoder is shared unless ``vf_share_layers`` is False."""
+    encoder is shared unless ``vf_share_layers`` is False.
+
+    ``model_config["use_lstm"]`` adds a recurrent core (reference: the catalog's
+    ``use_lstm`` / ``lstm_cell_size`` / ``max_seq_len``): encoder -> LSTM cell ->
+    heads, with state ``{"h", "c"}``. Acting takes ``state_in`` ([B, cell]) and
+    returns ``state_out``; training takes sequences ``obs [S, L, ...]`` with the
+    state at each sequence start and ``resets [S, L]`` (1 where a new episode
+    begins inside the sequence: the state is zeroed there)."""
 
     def setup(self):
         mc = self.model_config
@@ -206,7 +213,8 @@ class DefaultActorCriticModule(RLModule):
         hiddens = list(mc.get("fcnet_hiddens", [256, 256]))
         act = _act(mc.get("fcnet_activation", "tanh"))
         self.image = len(obs.shape) == 3
-        self.share = mc.get("vf_share_layers", self.image)
+        self.use_lstm = bool(mc.get("use_lstm", False))
+        self.share = mc.get("vf_share_layers", self.image or self.use_lstm)
         if self.image:
             self.encoder = NatureCNN(obs.shape[-1], hw=obs.shape[:2])
             feat = self.encoder.out_dim
@@ -218,6 +226,11 @@ class DefaultActorCriticModule(RLModule):
             self.encoder = make()
             feat = hiddens[-1]
             self.vf_encoder = None if self.share else make()
+        if self.use_lstm:
+            self.cell = int(mc.get("lstm_cell_size", 256))
+            self.lstm = nn.LSTMCell(feat, self.cell)
+            feat = self.cell
+            self.vf_encoder = None  # value head shares the recurrent core
         self.pi = nn.Linear(feat, dist_input_dim(self.action_space))
         self.vf = nn.Linear(feat, 1)
         nn.init.normal_(self.pi.weight, std=0.01)
@@ -233,35 +246,95 @@ class DefaultActorCriticModule(RLModule):
         else:
             self.log_std = None
 
+    # ------------------------------------------------------------------ state
+    def is_stateful(self) -> bool:
+        return self.use_lstm
+
+    def get_initial_state(self) -> Dict[str, torch.Tensor]:
+        if not self.use_lstm:
+            return {}
+        return {"h": torch.zeros(self.cell), "c": torch.zeros(self.cell)}
+
+    def _state(self, batch, B, dev):
+        st = batch.get("state_in")
+        if st is None:
+            z = torch.zeros(B, self.cell, device=dev)
+            return z, z
+        return st["h"].to(dev).float(), st["c"].to(dev).float()
+
+    # ------------------------------------------------------------------ forward
     def _obs(self, batch):
         o = batch["obs"]
         return o if self.image else o.reshape(o.shape[0], -1).float()
 
-    def _heads(self, obs):
-        z = self.encoder(obs)
+    def _head_out(self, z):
         logits = self.pi(z)
         if self.log_std is not None:
             logits = torch.cat([logits, self.log_std.expand_as(logits)], -1)
+        return logits
+
+    def _heads(self, obs):
+        z = self.encoder(obs)
         zv = z if self.vf_encoder is None else self.vf_encoder(obs)
-        return logits, self.vf(zv).squeeze(-1)
+        return self._head_out(z), self.vf(zv).squeeze(-1)
+
+    def _step_lstm(self, batch):
+        obs = self._obs(batch)
+        z = self.encoder(obs)
+        h, c = self._state(batch, obs.shape[0], z.device)
+        h, c = self.lstm(z, (h, c))
+        return h, c
+
+    def _seq_lstm(self, batch):
+        """obs [S, L, ...] -> core outputs [S*L, cell] (state zeroed at ``resets``)."""
+        o = batch["obs"]
+        S, L = o.shape[0], o.shape[1]
+        flat = o.reshape((S * L,) + tuple(o.shape[2:]))
+        z = self.encoder(flat if self.image else flat.reshape(S * L, -1).float()).view(S, L, -1)
+        h, c = self._state(batch, S, z.device)
+        resets = batch.get("resets")
+        outs = []
+        for t in range(L):
+            if resets is not None and t > 0:
+                keep = (1.0 - resets[:, t].float())[:, None]
+                h, c = h * keep, c * keep
+            h, c = self.lstm(z[:, t], (h, c))
+            outs.append(h)
+        return torch.stack(outs, 1).reshape(S * L, -1)
 
     def forward_train(self, batch):
+        if self.use_lstm:
+            core = self._seq_lstm(batch)
+            return {"action_dist_inputs": self._head_out(core), "vf_preds": self.vf(core).squeeze(-1)}
         logits, v = self._heads(self._obs(batch))
         return {"action_dist_inputs": logits, "vf_preds": v}
 
     @torch.no_grad()
     def forward_exploration(self, batch):
-        logits, v = self._heads(self._obs(batch))
+        if self.use_lstm:
+            h, c = self._step_lstm(batch)
+            logits, v = self._head_out(h), self.vf(h).squeeze(-1)
+        else:
+            logits, v = self._heads(self._obs(batch))
         d = self.dist_cls(logits)
         a = d.sample()
-        return {"actions": a, "action_logp": d.logp(a), "vf_preds": v, "action_dist_inputs": logits}
+        out = {"actions": a, "action_logp": d.logp(a), "vf_preds": v, "action_dist_inputs": logits}
+        if self.use_lstm:
+            out["state_out"] = {"h": h, "c": c}
+        return out
 
     @torch.no_grad()
     def forward_inference(self, batch):
+        if self.use_lstm:
+            h, c = self._step_lstm(batch)
+            return {"actions": self.dist_cls(self._head_out(h)).deterministic(), "state_out": {"h": h, "c": c}}
         logits, _ = self._heads(self._obs(batch))
         return {"actions": self.dist_cls(logits).deterministic()}
 
     def compute_values(self, batch):
+        if self.use_lstm:  # V of the state reached after ``state_in`` consumes ``obs``
+            h, _ = self._step_lstm(batch)
+            return self.vf(h).squeeze(-1)
         obs = self._obs(batch)
         z = self.encoder(obs) if self.vf_encoder is None else self.vf_encoder(obs)
         return self.vf(z).squeeze(-1)

@@ -194,7 +194,63 @@ class FakeAtariEnv(Env):
         return self.frame.copy(), r, False, self.t >= self.max_steps, {}
 
 
+class StatelessCartPoleEnv(CartPoleEnv):
+    """CartPole without the velocity entries (x, theta only): partially observed, so
+    a policy needs memory (reference: rllib/examples/envs/classes/stateless_cartpole.py)."""
+
+    def __init__(self, config: Optional[Dict] = None):
+        super().__init__(config)
+        high = np.array([4.8, 0.418], dtype=np.float32)
+        self.observation_space = Box(-high, high)
+
+    def reset(self, *, seed=None, options=None):
+        o, i = super().reset(seed=seed, options=options)
+        return o[[0, 2]], i
+
+    def step(self, action):
+        o, r, te, tr, i = super().step(action)
+        return o[[0, 2]], r, te, tr, i
+
+
+class RepeatAfterMeEnv(Env):
+    """Each step shows a random bit; the reward is +1 for playing the bit shown
+    ``delay`` steps EARLIER (default 1), so only a policy with memory beats
+    chance. Episodes are ``episode_len`` steps (default 20): chance ~= 0.5/step.
+    (reference role: rllib/examples/envs/classes/repeat_after_me_env.py)"""
+
+    def __init__(self, config: Optional[Dict] = None):
+        config = config or {}
+        self.delay = int(config.get("delay", 1))
+        self.episode_len = int(config.get("episode_len", 20))
+        self.observation_space = Box(0.0, 1.0, (2,))
+        self.action_space = Discrete(2)
+        self.rng = np.random.default_rng(config.get("seed"))
+        self.hist: List[int] = []
+
+    def _obs(self, b):
+        o = np.zeros(2, np.float32)
+        o[b] = 1.0
+        return o
+
+    def reset(self, *, seed=None, options=None):
+        if seed is not None:
+            self.rng = np.random.default_rng(seed)
+        b = int(self.rng.integers(2))
+        self.hist = [b]
+        return self._obs(b), {}
+
+    def step(self, action):
+        want = self.hist[-1 - self.delay] if len(self.hist) > self.delay else None
+        r = 1.0 if want is not None and int(action) == want else 0.0
+        b = int(self.rng.integers(2))
+        self.hist.append(b)
+        done = len(self.hist) > self.episode_len
+        return self._obs(b), r, False, done, {}
+
+
 _REGISTRY: Dict[str, Callable[[Dict], Env]] = {
+    "StatelessCartPole": lambda cfg: StatelessCartPoleEnv(cfg),
+    "RepeatAfterMe-v0": lambda cfg: RepeatAfterMeEnv(cfg),
     "CartPole-v1": lambda cfg: CartPoleEnv(cfg),
     "CartPole-v0": lambda cfg: CartPoleEnv(dict({"max_episode_steps": 200}, **(cfg or {}))),
     "Pendulum-v1": lambda cfg: PendulumEnv(cfg),
@@ -257,5 +313,6 @@ class VectorEnv:
         return (np.stack(obs), np.asarray(rew, np.float32), np.asarray(term), np.asarray(trunc), np.stack(final))
 
 
-__all__ = ["Space", "Discrete", "Box", "Env", "CartPoleEnv", "PendulumEnv", "FakeAtariEnv", "register_env",
+__all__ = ["Space", "Discrete", "Box", "Env", "CartPoleEnv", "StatelessCartPoleEnv", "RepeatAfterMeEnv",
+           "PendulumEnv", "FakeAtariEnv", "register_env",
            "make_env", "VectorEnv"]

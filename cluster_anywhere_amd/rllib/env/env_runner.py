@@ -128,12 +128,23 @@ class EnvRunner:
         next_buf = np.empty_like(obs_buf) if need_next else None
         acts, logps, vfs, rews, raw, terms, truncs, dist = [], [], [], [], [], [], [], []
         track = self._has_cb or len(self.env_to_module) or len(self.module_to_env)
+        stateful = getattr(self.module, "is_stateful", lambda: False)()
+        if stateful:
+            if getattr(self, "state", None) is None:
+                init = self.module.get_initial_state()
+                self.state = {k: np.repeat(v.numpy()[None], N, 0) for k, v in init.items()}
+            st_buf = {k: np.empty((T,) + v.shape, np.float32) for k, v in self.state.items()}
         t0 = time.time()
         for t in range(T):
             obs_buf[t] = self.obs
             batch = {"obs": torch.from_numpy(self.obs)}
+            if stateful:
+                for k, v in self.state.items():
+                    st_buf[k][t] = v
+                batch["state_in"] = {k: torch.from_numpy(v) for k, v in self.state.items()}
             batch.update(self.explore_extra)
             out = self.module.forward_exploration(batch) if explore else self.module.forward_inference(batch)
+            new_state = {k: v.cpu().numpy() for k, v in out["state_out"].items()} if stateful else None
             a = out["actions"].cpu().numpy()
             nraw, r, te, tr, final = self.env.step(self._to_env(out, a, explore))
             done = te | tr
@@ -147,7 +158,10 @@ class EnvRunner:
             if tr.any() and hasattr(self.module, "compute_values"):
                 idx = np.nonzero(tr & ~te)[0]
                 if len(idx):
-                    v = self.module.compute_values({"obs": torch.from_numpy(mfinal[idx])}).cpu().numpy()
+                    vb = {"obs": torch.from_numpy(mfinal[idx])}
+                    if stateful:
+                        vb["state_in"] = {k: torch.from_numpy(v[idx]) for k, v in new_state.items()}
+                    v = self.module.compute_values(vb).cpu().numpy()
                     r_aug[idx] += gamma * v
             if need_next:
                 next_buf[t] = mfinal
@@ -183,6 +197,10 @@ class EnvRunner:
                                                    metrics_logger=self.metrics, env=self.env, env_index=int(i),
                                                    rl_module=self.module)
             self.obs = self._to_module(nraw, self.episodes) if track else nraw
+            if stateful:  # episodes that ended start again from the initial state
+                for k in new_state:
+                    new_state[k][done] = 0.0
+                self.state = new_state
         self.total_steps += T * N
         out = {"obs": obs_buf, "actions": np.stack(acts), "rewards": np.stack(rews).astype(np.float32),
                "terminateds": np.stack(terms), "truncateds": np.stack(truncs),
@@ -195,6 +213,10 @@ class EnvRunner:
             out["action_dist_inputs"] = np.stack(dist).astype(np.float32)
         if need_next:
             out["next_obs"] = next_buf
+        if stateful:  # recurrent state at every step (sequence starts) and after the fragment
+            for k, v in st_buf.items():
+                out[f"state_in_{k}"] = v
+                out[f"last_state_{k}"] = self.state[k].copy()
         if self._has_cb:
             self.callbacks.on_sample_end(env_runner=self, metrics_logger=self.metrics, samples=out)
         return out
@@ -204,6 +226,7 @@ class EnvRunner:
         if seed is not None:
             self.env.seed = seed
         raw = self.env.reset()
+        self.state = None  # recurrent state restarts with the episodes
         for i in range(self.env.num_envs):
             self.env_to_module.episode_done(self.episodes[i])
             self.episodes[i] = self._new_episode(i, raw[i])
