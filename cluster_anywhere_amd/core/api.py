@@ -443,7 +443,7 @@ def cancel(ref, *, force: bool = False, recursive: bool = True):
         raise TypeError("cancel() expects an ObjectRef")
     if context.local_mode:
         return
-    _w().send(("cancel", tid, force, recursive))
+    _w().cancel(tid, force, recursive)
 
 
 def free(refs):

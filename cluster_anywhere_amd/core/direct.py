@@ -49,6 +49,7 @@ class DirectServer:
         self.sock = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
         self.sock.bind(self.path)
         self.sock.listen(256)
+        self.senders = []
         threading.Thread(target=self._accept, name="caamd-direct-accept", daemon=True).start()
 
     def _accept(self):
@@ -63,6 +64,7 @@ class DirectServer:
     def _serve(self, c: Conn):
         w = self.worker
         out = BatchSender(c, "caamd-direct-reply")  # replies coalesce into few sends
+        self.senders.append(out)
         while True:
             try:
                 msg = c.recv()
@@ -70,9 +72,17 @@ class DirectServer:
                 out.close()
                 return
             if msg[0] == "dexec":
+                # (spec, resolved args the caller already had, function blob on first use)
                 spec = msg[1]
+                resolved = msg[2] if len(msg) > 2 else None
+                fn_blob = msg[3] if len(msg) > 3 else None
                 w.direct_origin[spec.task_id] = out
-                w._on_execute((spec, None, None))
+                w._on_execute((spec, fn_blob, resolved if resolved is not None else {}))
+            elif msg[0] == "dcancel":
+                _, task_id, force = msg
+                if force and w.actor_id is None:
+                    os._exit(1)  # force-cancel of a leased normal task: the worker goes
+                w._on_cancel(task_id)
 
     def close(self):
         try:
@@ -80,31 +90,42 @@ class DirectServer:
             os.unlink(self.path)
         except OSError:
             pass
+        for out in list(self.senders):  # replies already produced still reach their callers
+            out.drain(2.0)
 
 
 class DirectClient:
-    """Caller side: one connection to one actor."""
+    """Caller side: one connection to one worker (an actor, or a leased task
+    worker when ``sink`` is a lease manager — core/lease.py)."""
 
-    def __init__(self, worker, actor_id: bytes, addr: str):
+    def __init__(self, worker, actor_id: bytes, addr: str, sink=None):
         self.worker = worker
         self.actor_id = actor_id
+        self.sink = sink
         self.conn = connect(addr)
         self.out = BatchSender(self.conn, "caamd-direct-send")
         self.alive = True
         self.lock = threading.Lock()
         self.pending: Dict[bytes, tuple] = {}  # task_id -> (spec, keep-alive refs, t_submit)
+        self.sent_fns = set()
         threading.Thread(target=self._read, name="caamd-direct-client", daemon=True).start()
 
-    def submit(self, spec, keep):
+    def submit(self, spec, keep, resolved=None, fn_blob=None):
         with self.lock:
             if not self.alive:
                 return False
             self.pending[spec.task_id] = (spec, keep, time.time())
         try:
-            self.out.put(("dexec", spec))
+            self.out.put(("dexec", spec, resolved, fn_blob))
         except ConnectionClosed:
             return True  # the reader's failure path resubmits / fails it
         return True
+
+    def cancel(self, task_id: bytes, force: bool = False):
+        try:
+            self.out.put(("dcancel", task_id, force))
+        except ConnectionClosed:
+            pass
 
     def _read(self):
         while True:
@@ -113,16 +134,24 @@ class DirectClient:
             except (ConnectionClosed, OSError):
                 break
             if msg[0] == "ddone":
-                _, task_id, results, error_kind, t0, t1, pid = msg
+                task_id, results, error_kind, t0, t1, pid = msg[1:7]
+                retryable = msg[7] if len(msg) > 7 else False
                 with self.lock:
                     rec = self.pending.pop(task_id, None)
-                if rec is not None:
+                if rec is None:
+                    continue
+                if self.sink is not None:
+                    self.sink._done(self, rec[0], results, error_kind, retryable, (t0, t1, pid))
+                else:
                     self.worker._on_direct_done(rec[0], results, (t0, t1, pid))
         with self.lock:
             self.alive = False
             recs = sorted(self.pending.values(), key=lambda r: r[2])
             self.pending.clear()
-        self.worker._on_direct_lost(self.actor_id, [r[0] for r in recs])
+        if self.sink is not None:
+            self.sink._lost(self, [r[0] for r in recs])
+        else:
+            self.worker._on_direct_lost(self.actor_id, [r[0] for r in recs])
 
     def close(self):
         self.alive = False

@@ -97,7 +97,7 @@ class ObjEntry:
 class WorkerInfo:
     __slots__ = ("worker_id", "conn", "pid", "node", "gpu_key", "idle", "actor_id", "task",
                  "proc", "fns", "alive", "kind", "started", "tasks_inflight", "env_key", "client_id",
-                 "oom_killed", "direct_addr")
+                 "oom_killed", "direct_addr", "lease", "lease_blocked")
 
     def __init__(self, **kw):
         for s in self.__slots__:
@@ -200,6 +200,8 @@ class Head:
         self._notify = {}
         self.dpins = {}
         self.dsealed_early = set()
+        self.lease_waiters: List[tuple] = []  # parked lease requests, FIFO
+        self.oom_killed_ids = set()
         self.waiting_deps: Dict[bytes, Set[bytes]] = {}  # task -> unresolved object ids
         self.lineage: Dict[bytes, TaskSpec] = {}  # finished tasks kept for object recovery
         self.num_reconstructions = 0
@@ -874,6 +876,8 @@ class Head:
 
     def _schedule(self):
         if not self.ready_queues:
+            if self.lease_waiters:
+                self._serve_lease_waiters()
             return
         for key in list(self.ready_queues):
             q = self.ready_queues[key]
@@ -888,6 +892,8 @@ class Head:
                     break
             if not q:
                 del self.ready_queues[key]
+        if self.lease_waiters:
+            self._serve_lease_waiters()
 
     def _pick(self, spec, demand=None):
         """Node for a task under its scheduling strategy ('' = not now, '!' = never)."""
@@ -1309,6 +1315,102 @@ class Head:
         for it in items:
             self._h_dseal(c, *it)
 
+    def _h_lseal(self, c, items):
+        """An owner registers results it kept local so far (core/lease.py: inline
+        direct-call results are sealed at the head only when their ref escapes the
+        owner process). The owner holds one reference to each."""
+        for (oid, inline, size, is_err) in items:
+            self._obj(oid).refcount += 1
+            self._seal_object(oid, inline, size, None, (), is_err)
+
+    # ------------------------------------------------------- task worker leases
+    # Reference role: raylet HandleRequestWorkerLease / ReturnWorker
+    # (src/ray/raylet/node_manager.cc) + direct_task_transport.cc. An owner with a
+    # backlog of normal tasks leases workers of its own node for one resource shape
+    # and pushes tasks straight to them (core/lease.py); the head only grants,
+    # parks (FIFO) and takes back leases.
+    def _grant_leases(self, c, node, demand, want):
+        out = []
+        key = (node, ())
+        while len(out) < want:
+            if not self.sched.acquire(node, demand):
+                break
+            idle = self.idle.get(key)
+            w = None
+            while idle:
+                cand = idle.pop()
+                if cand.alive and cand.idle and cand.direct_addr:
+                    w = cand
+                    break
+            if w is None:
+                self.sched.release(node, demand)
+                if self.starting[key] < max(1, int(self.cpu_count)) and self._num_workers(node) < self.max_workers:
+                    self._spawn_worker(node, ())
+                break
+            w.idle = False
+            w.task = None
+            w.lease = (c, demand, time.time())
+            w.lease_blocked = None
+            out.append((w.worker_id, w.direct_addr))
+        return out
+
+    def _h_lease(self, c, req, resources, want):
+        node = self.clients.get(c, {}).get("node") or self.head_hex
+        demand = {k: float(v) for k, v in resources.items() if v}
+        if node not in self.node_resources and node != self.head_hex:
+            self._reply(c, req, "never")
+            return
+        if self.sched.pick_node(demand, 2, node, False, self.node_id.hex(), [], []) == "!":
+            self._reply(c, req, "never")  # the owner's node can never run this shape
+            return
+        got = self._grant_leases(c, node, demand, max(1, int(want)))
+        if got:
+            self._reply(c, req, got)
+            return
+        other = self.sched.pick_node(demand, 0, "", False, self.node_id.hex(), [], [])
+        if other not in ("", "!") and other != node:
+            self._reply(c, req, "spill")  # another node has room now: send through the head
+            return
+        self.lease_waiters.append((c, req, node, demand, max(1, int(want))))
+
+    def _serve_lease_waiters(self):
+        still = []
+        for ent in self.lease_waiters:
+            c, req, node, demand, want = ent
+            if c.closed:
+                continue
+            got = self._grant_leases(c, node, demand, want)
+            if got:
+                self._reply(c, req, got)
+            else:
+                still.append(ent)
+        self.lease_waiters = still
+
+    def _lease_release(self, w):
+        _c, demand, _t = w.lease
+        rel = dict(demand)
+        for k, v in (w.lease_blocked or {}).items():
+            rel[k] = rel.get(k, 0.0) - v  # lent back while blocked in get()
+        self.sched.release(w.node, rel)
+        w.lease = None
+        w.lease_blocked = None
+        self._retry_pending_pgs()
+        self._retry_infeasible()
+
+    def _h_lease_return(self, c, worker_ids):
+        for wid in worker_ids:
+            w = self.workers.get(wid)
+            if w is None or w.lease is None or w.lease[0] is not c:
+                continue
+            self._lease_release(w)
+            if w.alive and w.actor_id is None:
+                w.idle = True
+                self.idle[(w.node, w.gpu_key)].append(w)
+        self._schedule()
+
+    def _h_worker_fate(self, c, req, worker_id):
+        self._reply(c, req, "oom" if worker_id in self.oom_killed_ids else "crash")
+
     def _h_check_name(self, c, req, namespace, name):
         aid = self.named_actors.get((namespace or self.namespace, name))
         if aid is not None and self.actors.get(aid) and self.actors[aid].state != "DEAD":
@@ -1454,6 +1556,10 @@ class Head:
         c.close()
         info = self.clients.pop(c, {})
         w = self.conn_worker.pop(c, None)
+        for lw in [x for x in self.workers.values() if x.lease is not None and x.lease[0] is c]:
+            # the owner is gone: take its leases back and stop what they were running
+            self._lease_release(lw)
+            self._kill_worker(lw.worker_id)
         if info.get("kind") == "node":
             self._on_node_death(info.get("node"))
             return
@@ -1463,6 +1569,8 @@ class Head:
             return
         w.alive = False
         w.idle = False
+        if w.lease is not None:
+            self._lease_release(w)
         try:
             if w.proc is not None:
                 w.proc.wait(timeout=1)
@@ -1526,10 +1634,13 @@ class Head:
                 spec = next(iter(w.tasks_inflight.values()))
                 mr = spec.max_retries if spec.max_retries is not None else 3
                 cands.append((w, mr < 0 or spec.attempt < mr, spec.start_time or 0.0))
+            elif w.lease is not None:
+                cands.append((w, True, w.lease[2]))
         w = pick_victim(cands)
         if w is None:
             return
         w.oom_killed = True
+        self.oom_killed_ids.add(w.worker_id)
         self.mem_monitor.kills += 1
         self.events.append(("oom_kill", w.worker_id.hex(), time.time(), frac))
         if w.actor_id is not None:
@@ -1562,7 +1673,16 @@ class Head:
         """A worker blocked in get() lends its CPUs back (reference: raylet
         HandleNotifyWorkerBlocked) so nested tasks cannot deadlock the node."""
         spec = self.tasks.get(task_id)
-        if spec is None or spec.kind != NORMAL or not spec.acquired or spec.blocked:
+        if spec is None:
+            w = self.conn_worker.get(c)
+            if w is not None and w.lease is not None and not w.lease_blocked:
+                cpu = {k: v for k, v in w.lease[1].items() if k == "CPU"}
+                if cpu:  # a leased worker's task blocked: lend its CPUs back
+                    self.sched.release(w.node, cpu)
+                    w.lease_blocked = cpu
+                    self._schedule()
+            return
+        if spec.kind != NORMAL or not spec.acquired or spec.blocked:
             return
         node, demand = spec.acquired
         cpu = {k: v for k, v in demand.items() if k == "CPU" or k.startswith("CPU_group_")}
@@ -1573,7 +1693,13 @@ class Head:
 
     def _h_unblocked(self, c, task_id):
         spec = self.tasks.get(task_id)
-        if spec is None or not spec.blocked:
+        if spec is None:
+            w = self.conn_worker.get(c)
+            if w is not None and w.lease is not None and w.lease_blocked:
+                self.sched.release(w.node, {k: -v for k, v in w.lease_blocked.items()})
+                w.lease_blocked = None
+            return
+        if not spec.blocked:
             return
         node, _ = spec.acquired
         # take the CPUs back even if that oversubscribes the node for a moment

@@ -52,6 +52,9 @@ class ObjectRef:
         return f"ObjectRef({self._id.hex()})"
 
     def __reduce__(self):
+        w = context.worker
+        if w is not None and (w.refs.local_only or w.refs.direct_pending):
+            w._escape((self._id,))  # the ref leaves this process: the head must know it
         return (_rebuild_ref, (self._id,))
 
     # -- futures / asyncio -------------------------------------------------------

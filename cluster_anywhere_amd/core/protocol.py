@@ -120,7 +120,8 @@ class BatchSender:
         self._q = []
         self._cv = threading.Condition()
         self.closed = False
-        threading.Thread(target=self._run, name=name, daemon=True).start()
+        self._thread = threading.Thread(target=self._run, name=name, daemon=True)
+        self._thread.start()
 
     def put(self, msg) -> None:
         d = pickle.dumps(msg, protocol=5)
@@ -152,6 +153,12 @@ class BatchSender:
         with self._cv:
             self.closed = True
             self._cv.notify()
+
+    def drain(self, timeout: float = 2.0):
+        """Close, then wait until everything queued so far has been sent."""
+        self.close()
+        if self._thread is not threading.current_thread():
+            self._thread.join(timeout)
 
 
 def connect(address: str) -> Conn:

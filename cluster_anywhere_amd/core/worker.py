@@ -16,6 +16,7 @@ import ctypes
 import hashlib
 import inspect
 import itertools
+import operator
 import os
 import queue
 import sys
@@ -58,6 +59,12 @@ class RefCounter:
         self.cache: Dict[bytes, tuple] = {}
         # releases queued by finalizers that found the lock busy (see remove())
         self.deferred: collections.deque = collections.deque()
+        # inline results of direct calls / leased tasks the head has not been told
+        # about: oid -> (inline, size, is_err). Sealed at the head (``lseal``) only
+        # when the ref escapes this process; dropping it needs no message at all.
+        self.local_only: Dict[bytes, tuple] = {}
+        # direct results still in flight whose refs already escaped: sealed normally
+        self.must_seal = set()
 
     def add(self, oid: bytes, announce: bool):
         with self.lock:
@@ -103,12 +110,27 @@ class RefCounter:
             self.cache.pop(oid, None)
             self.ready.pop(oid, None)
             self.owned.discard(oid)
-            if oid in self.direct_pending:
+            if oid in self.local_only:
+                del self.local_only[oid]
+            elif oid in self.direct_pending:
                 self.direct_dropped.add(oid)
             else:
                 self.ops.append(("d", oid))
         else:
             self.counts[oid] = c - 1
+
+    def escape(self, oids) -> List[tuple]:
+        """Owner-local results among ``oids`` that must now be sealed at the head."""
+        out = []
+        with self.lock:
+            lo, dp = self.local_only, self.direct_pending
+            for o in oids:
+                ent = lo.pop(o, None)
+                if ent is not None:
+                    out.append((o, *ent))
+                elif o in dp:
+                    self.must_seal.add(o)
+        return out
 
     def drain(self):
         with self.lock:
@@ -138,12 +160,15 @@ class CoreWorker:
         self.job_id = job_id
         self.conn = connect(address)
         self.refs = RefCounter()
-        self.send_lock = threading.Lock()
+        # re-entrant: pickling a message may seal an escaping owner-local ref first
+        self.send_lock = threading.RLock()
         self._req = itertools.count(1)
         self.pending: Dict[int, concurrent.futures.Future] = {}
         self.task_queue: "queue.Queue" = queue.Queue()
         self.fn_cache: Dict[bytes, Any] = {}
         self.sent_fns = set()
+        self.fn_blobs: Dict[bytes, bytes] = {}
+        self._ready_cbs: Dict[bytes, list] = {}  # oid -> callbacks when it completes here
         self.running_tasks: Dict[bytes, threading.Thread] = {}
         self.cancelled_tasks = set()
         self.actor_instance = None
@@ -160,6 +185,9 @@ class CoreWorker:
         self.actor_head_only = set()
         self._direct_lock = threading.Lock()
         self.direct_server = None
+        from . import lease
+
+        self.leases = lease.LeaseManager(self) if lease.enabled() and kind in ("driver", "worker") else None
         if kind == "worker" and os.environ.get("CAAMD_DIRECT_CALLS", "1") == "1":
             from .direct import DirectServer
 
@@ -208,6 +236,26 @@ class CoreWorker:
         finally:
             self.pending.pop(req, None)
 
+    def request_cb(self, build, cb):
+        """Send a request; ``cb(value)`` runs in the reader thread (None on failure)."""
+        req = next(self._req)
+        fut = concurrent.futures.Future()
+
+        def done(f, r=req):
+            self.pending.pop(r, None)
+            cb(None if f.exception() is not None else f.result())
+
+        fut.add_done_callback(done)
+        self.pending[req] = fut
+        self.send(build(req))
+
+    def _escape(self, oids):
+        """Seal owner-local results at the head before their refs leave this
+        process (ordered ahead of whatever message carries them)."""
+        items = self.refs.escape(oids)
+        if items:
+            self.send(("lseal", items))
+
     def request_async(self, build) -> concurrent.futures.Future:
         req = next(self._req)
         fut = concurrent.futures.Future()
@@ -230,6 +278,7 @@ class CoreWorker:
                     dropped = []
                     for oid in rids:
                         r.direct_pending.discard(oid)
+                        r.must_seal.discard(oid)
                         if oid in r.direct_dropped:
                             r.direct_dropped.discard(oid)
                             dropped.append(oid)
@@ -292,6 +341,10 @@ class CoreWorker:
                 if oid in r.counts:
                     r.ready[oid] = (kind, payload)
             r.cv.notify_all()
+        if self._ready_cbs:
+            for (oid, _k, _p) in items:
+                for f in self._ready_cbs.pop(oid, None) or ():
+                    f()
         if self.head_inflight_actor:
             with self._direct_lock:
                 for (oid, _k, _p) in items:
@@ -335,6 +388,33 @@ class CoreWorker:
         from .direct import result_kinds
 
         r = self.refs
+        lazy = bool(results) and all(res[1] is not None and not res[4] for res in results)
+        if lazy:
+            # all inline, nothing nested: the results stay owner-local until a ref
+            # escapes (RefCounter.local_only); the head only gets the task events
+            with r.cv:
+                if r.must_seal and any(res[0] in r.must_seal for res in results):
+                    lazy = False  # a ref already left this process: seal at the head
+                else:
+                    for (oid, inline, size, _n, _c, is_err) in results:
+                        r.owned.discard(oid)
+                        r.direct_pending.discard(oid)
+                        if oid in r.direct_dropped:
+                            r.direct_dropped.discard(oid)
+                            continue
+                        if oid in r.counts:
+                            r.ready[oid] = ("err" if is_err else "inline", inline)
+                            r.local_only[oid] = (inline, size, is_err)
+                    r.cv.notify_all()
+                    r.dseal_buf.append((spec.task_id, spec.fn_name, [], (), timing))
+                    if len(r.dseal_buf) >= 512:
+                        self._flush_evt.set()
+            if lazy:
+                if self._ready_cbs:
+                    for res in results:
+                        for f in self._ready_cbs.pop(res[0], None) or ():
+                            f()
+                return
         kinds = result_kinds(results, self.node_hex)
         with r.cv:
             for (oid, kind, payload) in kinds:
@@ -348,6 +428,11 @@ class CoreWorker:
             r.dseal_buf.append((spec.task_id, spec.fn_name, results, spec.return_ids, timing))
             if len(r.dseal_buf) >= 512:
                 self._flush_evt.set()
+        if self._ready_cbs:
+            for (oid, kind, _p) in kinds:
+                if kind is not None:
+                    for f in self._ready_cbs.pop(oid, None) or ():
+                        f()
 
     def _on_direct_lost(self, actor_id, specs):
         """The actor's direct connection broke: resubmit through the head when the
@@ -355,29 +440,44 @@ class CoreWorker:
         from ..exceptions import ActorDiedError
 
         self.actor_direct[actor_id] = ("head", 0.0)
-        r = self.refs
         for spec in specs:
             if spec.max_retries:
-                with r.cv:
-                    dropped = [o for o in spec.return_ids if o in r.direct_dropped]
-                    for o in spec.return_ids:
-                        r.direct_pending.discard(o)
-                        r.direct_dropped.discard(o)
                 with self._direct_lock:
                     self.actor_head_inflight.setdefault(actor_id, set()).update(spec.return_ids)
                     for o in spec.return_ids:
                         self.head_inflight_actor[o] = actor_id
-                try:
-                    self.send(("submit", spec))
-                    if dropped:
-                        self.send(("decref", dropped))
-                except (ConnectionClosed, OSError):
-                    pass
+                self._resubmit_via_head(spec)
                 continue
-            err = ActorDiedError(actor_id.hex(), "the actor's worker died while the call was running")
-            blob = serialization.serialize(err).to_bytes()
-            results = [(o, blob, len(blob), None, (), True) for o in spec.return_ids]
-            self._on_direct_done(spec, results, (time.time(), time.time(), None))
+            self._fail_direct(spec, ActorDiedError(actor_id.hex(),
+                                                   "the actor's worker died while the call was running"))
+
+    def _resubmit_via_head(self, spec):
+        """A direct call / leased task goes (back) through the head: its return refs
+        stop being direct-pending; ones dropped meanwhile are released after it."""
+        r = self.refs
+        with r.cv:
+            dropped = [o for o in spec.return_ids if o in r.direct_dropped]
+            for o in spec.return_ids:
+                r.direct_pending.discard(o)
+                r.direct_dropped.discard(o)
+        try:
+            if r.local_only or r.direct_pending:
+                self._escape(spec.arg_refs)
+            self.send(("submit", spec))
+            if dropped:
+                self.send(("decref", dropped))
+        except (ConnectionClosed, OSError):
+            pass
+
+    def _submit_via_head(self, spec, keep):
+        self._resubmit_via_head(spec)
+        del keep
+
+    def _fail_direct(self, spec, exc):
+        blob = serialization.serialize(exc).to_bytes()
+        results = [(o, blob, len(blob), None, (), True) for o in spec.return_ids]
+        now = time.time()
+        self._on_direct_done(spec, results, (now, now, None))
 
     def _local_state(self, ids):
         """None if some id is neither pushed nor owned-pending here (ask the head);
@@ -398,21 +498,30 @@ class CoreWorker:
         r = self.refs
         deadline = None if timeout is None else time.monotonic() + timeout
         with r.cv:
+            rd = r.ready
+            waiting = [i for i in ids if i not in rd]
+            n_ready = len(ids) - len(waiting)
             while True:
-                ready = [i for i in ids if i in r.ready]
-                if len(ready) >= need or not self.alive:
-                    return ready
-                if any(i not in r.ready and i not in r.owned for i in ids):
+                if waiting:
+                    still = [i for i in waiting if i not in rd]
+                    n_ready += len(waiting) - len(still)
+                    waiting = still
+                if n_ready >= need or not self.alive:
+                    return [i for i in ids if i in rd]
+                owned = r.owned
+                if any(i not in owned and i not in rd for i in waiting):
                     return None  # a ref was dropped meanwhile: fall back to the head
                 left = None if deadline is None else deadline - time.monotonic()
                 if left is not None and left <= 0:
-                    return ready
+                    return [i for i in ids if i in rd]
                 r.cv.wait(left if left is not None else 1.0)
 
     def close(self):
         self.alive = False
         if self.direct_server is not None:
             self.direct_server.close()
+        if self.leases is not None:
+            self.leases.close()
         for dc in list(self.actor_direct.values()):
             if dc is not None and not isinstance(dc, tuple):
                 try:
@@ -501,7 +610,7 @@ class CoreWorker:
         for r in refs:
             if not isinstance(r, ObjectRef):
                 raise TypeError(f"get() expects ObjectRefs, got {type(r).__name__}")
-        ids = [r.binary() for r in refs]
+        ids = [r._id for r in refs]
         out = self._get_cached(ids)
         if out is not None:
             return out[0] if single else out
@@ -528,6 +637,8 @@ class CoreWorker:
                 from ..exceptions import GetTimeoutError
 
                 raise GetTimeoutError(f"get() timed out after {timeout}s")
+        if self.refs.local_only or self.refs.direct_pending:
+            self._escape(ids)
         blocked = self._maybe_blocked(True)
         try:
             res = self.request(lambda req: ("get", req, ids, timeout))
@@ -584,7 +695,29 @@ class CoreWorker:
 
     def get_future(self, ref: ObjectRef) -> concurrent.futures.Future:
         out = concurrent.futures.Future()
-        inner = self.request_async(lambda req: ("get", req, [ref.binary()], None))
+        oid = ref.binary()
+        r = self.refs
+
+        def local(_keep=ref):  # the closure keeps the ref (and so its result) alive
+            try:
+                k, p = r.ready[oid]
+                out.set_result(self._materialize(oid, k, p))
+            except BaseException as e:  # noqa
+                out.set_exception(e)
+
+        with r.cv:
+            ent = r.ready.get(oid)
+            pending_here = ent is None and oid in r.owned
+            if pending_here:  # completes here (owner-side store): no head round trip
+                self._ready_cbs.setdefault(oid, []).append(local)
+        if ent is not None and ent[0] in ("inline", "store", "err", "err_store"):
+            local()
+            return out
+        if pending_here:
+            return out
+        if r.local_only or r.direct_pending:
+            self._escape([oid])
+        inner = self.request_async(lambda req: ("get", req, [oid], None))
 
         def done(f):
             try:
@@ -598,11 +731,27 @@ class CoreWorker:
         return out
 
     def wait(self, refs, num_returns=1, timeout=None, fetch_local=True):
-        ids = [r.binary() for r in refs]
+        ids = list(map(_ref_id, refs))
         if len(set(ids)) != len(ids):
             raise ValueError("wait() requires a list of unique object refs")
         if num_returns > len(ids):
             raise ValueError("num_returns cannot exceed the number of refs")
+        # fast path: enough of them already completed here (owner-side store);
+        # stops scanning at the num_returns-th ready ref
+        rd = self.refs.ready
+        if num_returns == 1:
+            for idx, i in enumerate(ids):
+                if i in rd:
+                    refs = list(refs)
+                    return [refs[idx]], refs[:idx] + refs[idx + 1:]
+        else:
+            got = []
+            for i in ids:
+                if i in rd:
+                    got.append(i)
+                    if len(got) >= num_returns:
+                        gs = set(got)
+                        return [x for x in refs if x._id in gs], [x for x in refs if x._id not in gs]
         st = self._local_state(ids)
         if st is not None:
             got = st if (len(st) >= num_returns or timeout == 0) else None
@@ -616,6 +765,8 @@ class CoreWorker:
             if got is not None:
                 ready = set(got[:num_returns]) if len(got) >= num_returns else set(got)
                 return [x for x in refs if x.binary() in ready], [x for x in refs if x.binary() not in ready]
+        if self.refs.local_only or self.refs.direct_pending:
+            self._escape(ids)
         blocked = self._maybe_blocked(True)
         try:
             ready = set(self.request(lambda req: ("wait", req, ids, num_returns, timeout)))
@@ -636,13 +787,20 @@ class CoreWorker:
     def free(self, refs):
         self.send(("free", [r.binary() for r in refs]))
 
+    def cancel(self, task_id: bytes, force: bool, recursive: bool):
+        if self.leases is not None and self.leases.cancel(task_id, force):
+            return
+        self.send(("cancel", task_id, force, recursive))
+
     def gen_next(self, task_id, index):
         return self.request(lambda req: ("gen_next", req, task_id, index))
 
     # ------------------------------------------------------------- submission
     def register_function(self, fn_id: bytes, blob_fn):
         if fn_id not in self.sent_fns:
-            self.send(("fn", fn_id, blob_fn()))
+            blob = blob_fn()
+            self.fn_blobs[fn_id] = blob
+            self.send(("fn", fn_id, blob))
             self.sent_fns.add(fn_id)
 
     def _pack_args(self, args, kwargs):
@@ -691,25 +849,47 @@ class CoreWorker:
                         generator=generator, parent=ctx.task_id if ctx else None,
                         concurrency_group=concurrency_group)
         refs = [] if generator == "streaming" else [ObjectRef(o, _owned=True) for o in return_ids]
+        r = self.refs
+        busy = bool(r.owned)
         if generator is None:
-            with self.refs.lock:
-                self.refs.owned.update(return_ids)
-        if kind == ACTOR_METHOD:
+            with r.lock:
+                r.owned.update(return_ids)
+        if kind == NORMAL and self.leases is not None and generator is None:
+            from .lease import eligible, resolved_args
+
+            resolved = resolved_args(r, arg_refs) if arg_refs else {}
+            if resolved is not None and eligible(spec):
+                with r.lock:
+                    r.direct_pending.update(return_ids)
+                if self.leases.submit(spec, (keep, [ObjectRef(o) for o in arg_refs + pinned]), resolved, busy):
+                    return refs
+                with r.lock:
+                    r.direct_pending.difference_update(return_ids)
+        elif kind == ACTOR_METHOD:
             if generator is not None:
                 self.actor_head_only.add(actor_id)
             elif self.actor_direct is not None:
                 dc = self._direct_for(actor_id)
                 if dc is not None:
-                    with self.refs.lock:
-                        self.refs.direct_pending.update(return_ids)
-                    if dc.submit(spec, (keep, [ObjectRef(o) for o in arg_refs])):
+                    resolved = None
+                    if arg_refs:
+                        from .lease import resolved_args
+
+                        resolved = resolved_args(r, arg_refs)
+                        if resolved is None and (r.local_only or r.direct_pending):
+                            self._escape(arg_refs)  # the actor resolves them through the head
+                    with r.lock:
+                        r.direct_pending.update(return_ids)
+                    if dc.submit(spec, (keep, [ObjectRef(o) for o in arg_refs]), resolved):
                         return refs
-                    with self.refs.lock:
-                        self.refs.direct_pending.difference_update(return_ids)
+                    with r.lock:
+                        r.direct_pending.difference_update(return_ids)
             with self._direct_lock:
                 self.actor_head_inflight.setdefault(actor_id, set()).update(return_ids)
                 for o in return_ids:
                     self.head_inflight_actor[o] = actor_id
+        if arg_refs and (r.local_only or r.direct_pending):
+            self._escape(arg_refs)
         self.send(("submit", spec))
         del keep
         if generator == "streaming":
@@ -739,12 +919,14 @@ class CoreWorker:
             self.async_loop.call_soon_threadsafe(t.cancel)
 
     def _resolve_args(self, spec, resolved):
-        if resolved is None:  # a direct call: resolve its ref arguments here
-            ids = [a[1] for a in list(spec.args) + list(spec.kwargs.values()) if a[0] != "v"]
+        if resolved is None:
             resolved = {}
-            if ids:
-                res = self.request(lambda req: ("get", req, ids, None))
-                resolved = {o: (k, p) for (o, k, p) in res}
+        # a direct call / leased task: ref arguments the caller did not send resolved
+        ids = [a[1] for a in list(spec.args) + list(spec.kwargs.values()) if a[0] != "v" and a[1] not in resolved]
+        if ids:
+            res = self.request(lambda req: ("get", req, ids, None))
+            resolved = dict(resolved)
+            resolved.update({o: (k, p) for (o, k, p) in res})
 
         def unpack(a):
             if a[0] == "v":
@@ -775,7 +957,7 @@ class CoreWorker:
 
     def execute(self, payload):
         spec, _, resolved = payload
-        if resolved is None and spec.task_id in self.direct_origin:
+        if spec.task_id in self.direct_origin:
             self.__dict__.setdefault("_t_start", {})[spec.task_id] = time.time()
         self.running_tasks[spec.task_id] = threading.current_thread()
         self._set_ctx(spec)
@@ -859,7 +1041,7 @@ class CoreWorker:
                 if nested:  # keep nested refs alive until the caller seals the results
                     self.send(("dpin", spec.task_id, nested))
                 t0 = getattr(self, "_t_start", {}).pop(spec.task_id, time.time())
-                dc.put(("ddone", spec.task_id, results, error_kind, t0, time.time(), os.getpid()))
+                dc.put(("ddone", spec.task_id, results, error_kind, t0, time.time(), os.getpid(), retryable))
             except (ConnectionClosed, OSError):
                 pass
             return
@@ -1016,6 +1198,9 @@ class CoreWorker:
             if item is None:
                 break
             self.execute(item)
+
+
+_ref_id = operator.attrgetter("_id")
 
 
 def _retryable(retry_exceptions, e) -> bool:

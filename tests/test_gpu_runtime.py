@@ -114,6 +114,16 @@ def test_gpu_object_ipc_zero_copy(cluster):
             torch.cuda.synchronize()
             return float(self.t[0])
 
+        def drop(self):
+            import gc
+
+            import torch
+
+            self.t = None
+            gc.collect()
+            torch.cuda.synchronize()
+            return True
+
     p, c = Producer.remote(), Consumer.remote()
     ref = p.get.remote()
     assert ray.get(c.hold.remote(ref), timeout=300) == (True, 0.0)
@@ -129,6 +139,8 @@ def test_gpu_object_ipc_zero_copy(cluster):
     # readers release their IPC views BEFORE the producer goes away (the producer's
     # HBM backs them); a read after the producer died fails loudly instead of
     # mapping freed memory
+    # (a SIGKILLed reader never releases its mapping: let it drop its views first)
+    assert ray.get(c.drop.remote(), timeout=60)
     ray.kill(c)
     del t
     torch.cuda.synchronize()

@@ -1,0 +1,156 @@
+"""Normal-task worker leases (core/lease.py; reference role:
+src/ray/core_worker/transport/direct_task_transport.cc): bursts of tasks run on
+leased workers without the head on the per-task path; owner-local results are
+sealed at the head when their refs escape; retries, crashes, cancel and nested
+blocking tasks behave as on the head path."""
+import os
+import time
+
+import pytest
+
+import cluster_anywhere_amd as ray
+from cluster_anywhere_amd.core import context
+from cluster_anywhere_amd.exceptions import TaskCancelledError, WorkerCrashedError
+
+
+@pytest.fixture(scope="module")
+def cluster():
+    ray.init(num_cpus=4, object_store_memory=256 << 20)
+    yield
+    ray.shutdown()
+
+
+@ray.remote
+def sq(x):
+    return x * x
+
+
+@ray.remote
+def add(a, b):
+    return a + b
+
+
+@ray.remote
+def big(n):
+    return bytes(n)
+
+
+def _leased():
+    return context.worker.leases.n_leased_tasks
+
+
+def test_burst_runs_on_leases(cluster):
+    before = _leased()
+    refs = [sq.remote(i) for i in range(300)]
+    assert ray.get(refs) == [i * i for i in range(300)]
+    assert _leased() - before > 200  # all but the first few went through leases
+    # large results land in the object store and are registered with the head
+    out = ray.get([big.remote(1 << 20) for _ in range(8)])
+    assert all(len(b) == 1 << 20 for b in out)
+
+
+def test_owner_local_results_escape(cluster):
+    refs = [sq.remote(i) for i in range(50)]
+    ray.wait(refs, num_returns=len(refs))
+    # top-level args (resolved locally), nested refs (sealed at the head on pickling)
+    assert ray.get(add.remote(refs[3], refs[4])) == 9 + 16
+    holder = ray.put({"r": refs[5]})
+    assert ray.get(ray.get(holder)["r"]) == 25
+
+    @ray.remote
+    def deref(d):
+        return ray.get(d["x"]) + 1
+
+    assert ray.get(deref.remote({"x": refs[6]})) == 37
+
+    @ray.remote
+    class A:
+        def get(self, d):
+            return ray.get(d[0])
+
+    a = A.remote()
+    assert ray.get(a.get.remote([refs[7]])) == 49
+    ray.kill(a)
+    # chained while the producer is still in flight
+    r1 = [sq.remote(i) for i in range(20)]
+    r2 = [add.remote(r, 1) for r in r1]
+    assert ray.get(r2) == [i * i + 1 for i in range(20)]
+    # awaiting an owner-local result
+    import asyncio
+
+    async def aw():
+        return await sq.remote(12)
+
+    _ = [sq.remote(i) for i in range(10)]
+    assert asyncio.run(aw()) == 144
+
+
+def test_nested_blocking_tasks_do_not_deadlock(cluster):
+    @ray.remote
+    def outer(i):
+        return sum(ray.get([sq.remote(i + j) for j in range(4)]))
+
+    refs = [outer.remote(i) for i in range(12)]
+    assert ray.get(refs, timeout=120) == [sum((i + j) ** 2 for j in range(4)) for i in range(12)]
+
+
+def test_retries_and_crashes(cluster, tmp_path):
+    @ray.remote(max_retries=2)
+    def flaky(marker, i):
+        p = f"{marker}-{i}"
+        if not os.path.exists(p):
+            open(p, "w").close()
+            os._exit(1)
+        return i
+
+    @ray.remote(max_retries=0)
+    def dies():
+        os._exit(1)
+
+    @ray.remote(max_retries=3, retry_exceptions=[ValueError])
+    def raises_once(marker, i):
+        p = f"{marker}-e{i}"
+        if not os.path.exists(p):
+            open(p, "w").close()
+            raise ValueError("first attempt")
+        return -i
+
+    m = str(tmp_path / "m")
+    warm = [sq.remote(i) for i in range(20)]  # in flight: the next ones take leases
+    assert ray.get([flaky.remote(m, i) for i in range(6)], timeout=120) == list(range(6))
+    assert ray.get([raises_once.remote(m, i) for i in range(6)], timeout=120) == [-i for i in range(6)]
+    ray.get(warm)
+    warm = [sq.remote(i) for i in range(20)]
+    with pytest.raises(WorkerCrashedError):
+        ray.get([dies.remote() for _ in range(3)], timeout=120)
+    ray.get(warm)
+
+
+def test_leases_are_returned(cluster):
+    ray.get([sq.remote(i) for i in range(200)])
+    deadline = time.time() + 10
+    while time.time() < deadline and ray.available_resources().get("CPU") != 4.0:
+        time.sleep(0.05)
+    assert ray.available_resources().get("CPU") == 4.0
+
+
+def test_cancel_leased_task(cluster):
+    @ray.remote
+    def sleepy(t):
+        time.sleep(t)
+        return t
+
+    refs = [sleepy.remote(5.0) for _ in range(12)]  # more than the CPUs: some stay queued
+    time.sleep(0.5)
+    for r in refs:
+        ray.cancel(r)
+    for r in refs:
+        with pytest.raises(TaskCancelledError):
+            ray.get(r, timeout=60)
+    refs = [sleepy.remote(30.0) for _ in range(3)]
+    time.sleep(0.5)
+    ray.cancel(refs[-1], force=True)
+    with pytest.raises(TaskCancelledError):
+        ray.get(refs[-1], timeout=60)
+    for r in refs[:-1]:
+        ray.cancel(r)
