@@ -109,16 +109,18 @@ class Conn:
 
 
 class BatchSender:
-    """Coalescing sender for one Conn: ``put`` pickles in the calling thread and
-    appends to a queue; a daemon thread sends everything queued in ONE sendall.
-    A burst of small messages (pipelined actor calls / replies) then costs one
-    syscall and one GIL hand-off instead of one per message; a lone message is
-    sent as soon as the producer blocks (e.g. in get())."""
+    """Coalescing sender for one Conn. ``put`` pickles in the calling thread; when
+    nothing is queued or being sent it also SENDS in the calling thread (a lone
+    message — a sync actor call, its reply — costs no thread hand-off); otherwise
+    it queues, and a daemon thread sends everything queued in ONE sendall, so a
+    burst of small messages costs one syscall and one GIL hand-off instead of one
+    per message. FIFO order holds: at most one send is in progress at a time."""
 
     def __init__(self, conn: Conn, name: str = "caamd-sender"):
         self.conn = conn
         self._q = []
         self._cv = threading.Condition()
+        self._busy = False
         self.closed = False
         self._thread = threading.Thread(target=self._run, name=name, daemon=True)
         self._thread.start()
@@ -128,18 +130,33 @@ class BatchSender:
         with self._cv:
             if self.closed:
                 raise ConnectionClosed("sender closed")
-            self._q.append(_LEN.pack(len(d)))
-            self._q.append(d)
-            self._cv.notify()
+            if self._q or self._busy:
+                self._q.append(_LEN.pack(len(d)))
+                self._q.append(d)
+                self._cv.notify()
+                return
+            self._busy = True
+        try:
+            with self.conn._send_lock:
+                self.conn.sock.sendall(_LEN.pack(len(d)) + d)
+        except OSError:
+            self.conn.closed = True
+            with self._cv:
+                self.closed = True
+        finally:
+            with self._cv:
+                self._busy = False
+                self._cv.notify()
 
     def _run(self):
         while True:
             with self._cv:
-                while not self._q and not self.closed:
+                while (not self._q and not self.closed) or self._busy:
                     self._cv.wait()
-                if self.closed and not self._q:
-                    return
+                if not self._q:
+                    return  # closed and drained
                 parts, self._q = self._q, []
+                self._busy = True
             try:
                 with self.conn._send_lock:
                     self.conn.sock.sendall(b"".join(parts))
@@ -147,12 +164,17 @@ class BatchSender:
                 self.conn.closed = True
                 with self._cv:
                     self.closed = True
+                    self._busy = False
+                    self._cv.notify_all()
                 return
+            with self._cv:
+                self._busy = False
+                self._cv.notify_all()
 
     def close(self):
         with self._cv:
             self.closed = True
-            self._cv.notify()
+            self._cv.notify_all()
 
     def drain(self, timeout: float = 2.0):
         """Close, then wait until everything queued so far has been sent."""
