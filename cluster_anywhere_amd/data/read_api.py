@@ -277,6 +277,160 @@ def read_sql(sql: str, connection_factory, *, parallelism: int = -1, **kw) -> Da
     return Dataset(("read", [rd]))
 
 
+def read_avro(paths, **kw) -> Dataset:
+    """Avro object-container files, one block per file (own decoder: data/avro.py;
+    reference: datasource/avro_datasource.py)."""
+    from .avro import read_avro_file
+
+    files = _expand(paths, [".avro"])
+    return _file_ds(files, lambda f: B.from_rows(list(read_avro_file(f))))
+
+
+def _read_wav(path):
+    import wave
+
+    with wave.open(path, "rb") as w:
+        ch, width, rate, n = w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()
+        raw = w.readframes(n)
+    if width == 1:
+        a = (np.frombuffer(raw, np.uint8).astype(np.float32) - 128.0) / 128.0
+    elif width == 2:
+        a = np.frombuffer(raw, "<i2").astype(np.float32) / 32768.0
+    elif width == 3:
+        b = np.frombuffer(raw, np.uint8).reshape(-1, 3).astype(np.int32)
+        v = b[:, 0] | (b[:, 1] << 8) | (b[:, 2] << 16)
+        v = np.where(v >= 1 << 23, v - (1 << 24), v)
+        a = v.astype(np.float32) / float(1 << 23)
+    elif width == 4:
+        a = np.frombuffer(raw, "<i4").astype(np.float32) / float(1 << 31)
+    else:
+        raise ValueError(f"unsupported WAV sample width {width}")
+    return a.reshape(-1, ch).T.copy(), rate
+
+
+def read_audio(paths, *, include_paths: bool = False, **kw) -> Dataset:
+    """PCM WAV files -> ``amplitude [channels, samples]`` float32 in [-1, 1] and
+    ``sample_rate`` (reference: datasource/audio_datasource.py; decoded with the
+    standard-library ``wave`` module, no soundfile)."""
+    files = _expand(paths, [".wav", ".wave"])
+
+    def rd(f):
+        amp, rate = _read_wav(f)
+        b = {"amplitude": amp[None], "sample_rate": np.asarray([rate], dtype=np.int64)}
+        if include_paths:
+            b["path"] = np.asarray([f], dtype=object)
+        return b
+
+    return _file_ds(files, rd)
+
+
+def _local(uri: str) -> str:
+    return uri[len("file://"):] if uri.startswith("file://") else (uri[5:] if uri.startswith("file:") else uri)
+
+
+def read_iceberg(table_identifier: str, *, snapshot_id: Optional[int] = None,
+                 selected_fields: Optional[List[str]] = None, row_filter=None, **kw) -> Dataset:
+    """An Iceberg table on a local / mounted filesystem (``table_identifier`` =
+    the table directory): latest (or ``snapshot_id``) snapshot -> manifest list
+    -> manifests (Avro, decoded by data/avro.py) -> live Parquet data files, one
+    read task per file. Delete files (v2 row-level deletes) are refused.
+    Reference: datasource/iceberg_datasource.py (which drives pyiceberg)."""
+    import json as _json
+
+    from .avro import read_avro_file
+
+    root = _local(table_identifier)
+    mdir = os.path.join(root, "metadata")
+    hint = os.path.join(mdir, "version-hint.text")
+    cands = sorted(glob.glob(os.path.join(mdir, "*.metadata.json")))
+    if not cands:
+        raise ValueError(f"no Iceberg metadata under {mdir}")
+    meta_path = cands[-1]
+    if os.path.exists(hint):
+        v = open(hint).read().strip()
+        for c in cands:
+            b = os.path.basename(c)
+            if b == f"v{v}.metadata.json" or b.startswith(f"{int(v):05d}-"):
+                meta_path = c
+    else:
+        def ver(p):
+            b = os.path.basename(p)
+            head = b.split(".")[0].split("-")[0].lstrip("v")
+            return int(head) if head.isdigit() else -1
+
+        meta_path = max(cands, key=ver)
+    with open(meta_path) as f:
+        meta = _json.load(f)
+    sid = snapshot_id if snapshot_id is not None else meta.get("current-snapshot-id")
+    if sid is None or sid == -1:
+        return from_items([])
+    snap = next((s for s in meta.get("snapshots", []) if s["snapshot-id"] == sid), None)
+    if snap is None:
+        raise ValueError(f"snapshot {sid} not found in {meta_path}")
+    files = []
+    for m in read_avro_file(_local(snap["manifest-list"])):
+        if int(m.get("content", 0) or 0) != 0:
+            raise NotImplementedError("Iceberg row-level delete files are not supported")
+        for ent in read_avro_file(_local(m["manifest_path"])):
+            if int(ent.get("status", 1)) == 2:
+                continue  # deleted in this snapshot
+            df = ent["data_file"]
+            if int(df.get("content", 0) or 0) != 0:
+                raise NotImplementedError("Iceberg row-level delete files are not supported")
+            if str(df.get("file_format", "PARQUET")).upper() != "PARQUET":
+                raise NotImplementedError(f"Iceberg data file format {df.get('file_format')}")
+            files.append(_local(df["file_path"]))
+    if not files:
+        return from_items([])
+
+    def rd(f):
+        import pyarrow.parquet as pq
+
+        return B.from_batch(pq.read_table(f, columns=selected_fields, filters=row_filter))
+
+    return _file_ds(sorted(set(files)), rd)
+
+
+def read_hudi(table_uri: str, **kw) -> Dataset:
+    """Snapshot query of a copy-on-write Hudi table on a local filesystem: for
+    every file group the Parquet base file of the latest COMPLETED commit
+    (``.hoodie/<instant>.commit``); merge-on-read log files are refused.
+    Reference: datasource/hudi_datasource.py (which drives hudi-rs)."""
+    root = _local(table_uri)
+    hoodie = os.path.join(root, ".hoodie")
+    if not os.path.isdir(hoodie):
+        raise ValueError(f"{root} is not a Hudi table (no .hoodie directory)")
+    done = {n.split(".")[0] for n in os.listdir(hoodie)
+            if n.endswith(".commit") or n.endswith(".replacecommit")}
+    latest: Dict[tuple, tuple] = {}
+    for dirpath, dirnames, filenames in os.walk(root):
+        dirnames[:] = [d for d in dirnames if d != ".hoodie"]
+        for fn in filenames:
+            if fn.endswith(".log") or ".log." in fn:
+                raise NotImplementedError("Hudi merge-on-read log files are not supported")
+            if not fn.endswith(".parquet"):
+                continue
+            parts = fn[: -len(".parquet")].split("_")
+            if len(parts) < 3:
+                continue
+            file_id, instant = parts[0], parts[-1]
+            if instant not in done:
+                continue  # inflight / rolled back write
+            key = (os.path.relpath(dirpath, root), file_id)
+            if key not in latest or instant > latest[key][0]:
+                latest[key] = (instant, os.path.join(dirpath, fn))
+    files = sorted(p for _, p in latest.values())
+    if not files:
+        return from_items([])
+
+    def rd(f):
+        import pyarrow.parquet as pq
+
+        return B.from_batch(pq.read_table(f))
+
+    return _file_ds(files, rd)
+
+
 def _unavailable(name: str, lib: str):
     def fn(*a, **k):
         raise ImportError(f"{name} needs {lib}, which is not installed in this image "
@@ -288,10 +442,10 @@ def _unavailable(name: str, lib: str):
 
 for _n, _lib in (("from_dask", "dask"), ("from_spark", "pyspark"), ("from_modin", "modin"),
                  ("from_mars", "mars"), ("from_tf", "tensorflow"), ("read_bigquery", "google-cloud-bigquery"),
-                 ("read_mongo", "pymongo"), ("read_lance", "lance"), ("read_iceberg", "pyiceberg"),
-                 ("read_hudi", "hudi"), ("read_delta_sharing_tables", "delta-sharing"),
+                 ("read_mongo", "pymongo"), ("read_lance", "lance"),
+                 ("read_delta_sharing_tables", "delta-sharing"),
                  ("read_databricks_tables", "databricks-sql-connector"), ("read_clickhouse", "clickhouse-connect"),
-                 ("read_avro", "fastavro"), ("read_audio", "soundfile"), ("read_videos", "decord")):
+                 ("read_videos", "decord")):
     globals()[_n] = _unavailable(_n, _lib)
 
 
