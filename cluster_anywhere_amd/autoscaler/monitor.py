@@ -13,6 +13,12 @@ def main(argv=None):
     ap.add_argument("--config", required=True)
     ap.add_argument("--interval", type=float, default=5.0)
     a = ap.parse_args(argv)
+    import signal
+
+    def _term(*_):
+        raise KeyboardInterrupt  # `down` sends SIGTERM: terminate our node agents first
+
+    signal.signal(signal.SIGTERM, _term)
     from ..core import api
     from .autoscaler import Monitor, StandardAutoscaler
     from .node_provider import LocalNodeProvider

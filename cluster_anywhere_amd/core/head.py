@@ -1863,7 +1863,8 @@ class Head:
         if what == "objects":
             return [{"object_id": o.hex(), "state": ["PENDING", "READY", "FREED"][e.state],
                      "size": e.size, "inline": e.inline is not None, "ref_count": e.refcount,
-                     "pins": e.pins, "spilled": e.spilled_path is not None}
+                     "pins": e.pins, "spilled": e.spilled_path is not None,
+                     "node_id": "inline" if e.inline is not None else (e.node or self.head_hex)}
                     for o, e in self.objects.items()]
         if what == "workers":
             return [{"worker_id": w.worker_id.hex(), "pid": w.pid, "node_id": w.node,

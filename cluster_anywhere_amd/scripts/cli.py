@@ -9,6 +9,9 @@ python/ray/dashboard/modules/job/cli.py — ``ray job submit/status/logs/stop/li
     python -m cluster_anywhere_amd summary tasks|actors
     python -m cluster_anywhere_amd job submit [--submission-id ID] [--no-wait] -- <entrypoint>
     python -m cluster_anywhere_amd job status|logs|stop ID ; job list
+    python -m cluster_anywhere_amd up|down|get-head-ip|attach cluster.yaml ; exec cluster.yaml <cmd>
+    python -m cluster_anywhere_amd submit cluster.yaml script.py [args] ; rsync-up|rsync-down cluster.yaml SRC DST
+    python -m cluster_anywhere_amd memory [--top N] ; logs [GLOB] [--tail N]
 """
 from __future__ import annotations
 
@@ -108,7 +111,8 @@ def cmd_stop(a):
 def _connect(a):
     import cluster_anywhere_amd as ray
 
-    ray.init(address=a.address or "auto", _temp_dir=getattr(a, "temp_dir", None))
+    addr = a.address or os.environ.get("CAAMD_ADDRESS") or os.environ.get("RAY_ADDRESS") or "auto"
+    ray.init(address=addr, _temp_dir=getattr(a, "temp_dir", None))
     return ray
 
 
@@ -200,6 +204,124 @@ def cmd_job(a):
     return 0
 
 
+def _launcher_cfg(a):
+    from ..autoscaler import commands
+
+    return commands.load_cluster_config(a.cluster_config)
+
+
+def cmd_up(a):
+    from ..autoscaler import commands
+
+    st = commands.create_or_update_cluster(a.cluster_config, no_restart=a.no_restart)
+    print(f"Cluster {st['cluster_name']!r} is up: address={st['address']}")
+    print(f"  run on it:   python -m cluster_anywhere_amd exec {a.cluster_config} '<cmd>'")
+    print(f"  tear down:   python -m cluster_anywhere_amd down {a.cluster_config}")
+    return 0
+
+
+def cmd_down(a):
+    from ..autoscaler import commands
+
+    commands.teardown_cluster(a.cluster_config, workers_only=a.workers_only)
+    print("Cluster torn down." if not a.workers_only else "Worker nodes terminated.")
+    return 0
+
+
+def cmd_exec(a):
+    from ..autoscaler import commands
+
+    return commands.exec_cluster(a.cluster_config, " ".join(a.cmd)).returncode
+
+
+def cmd_submit(a):
+    from ..autoscaler import commands
+
+    return commands.submit(a.cluster_config, a.script, a.script_args).returncode
+
+
+def cmd_get_head_ip(a):
+    from ..autoscaler import commands
+
+    print(commands.get_head_node_ip(a.cluster_config))
+    return 0
+
+
+def cmd_rsync(a):
+    from ..autoscaler import commands
+
+    commands.rsync(a.cluster_config, a.source, a.target, down=a.cmd == "rsync-down")
+    return 0
+
+
+def cmd_attach(a):
+    from ..autoscaler import commands
+
+    cfg = _launcher_cfg(a)
+    st = commands._load_state(cfg["cluster_name"])
+    if st is None:
+        print("cluster is not running", file=sys.stderr)
+        return 1
+    if st["provider"] == "local":
+        return subprocess.call([os.environ.get("SHELL", "bash")], env=dict(os.environ, CAAMD_ADDRESS=st["address"]))
+    auth = cfg.get("auth", {})
+    tgt = f"{auth['ssh_user']}@{st['head_ip']}" if auth.get("ssh_user") else st["head_ip"]
+    return subprocess.call(["ssh", "-t", tgt])
+
+
+def cmd_memory(a):
+    """Object-store usage by node and the largest live objects (reference: ``ray memory``)."""
+    from ..util import state
+
+    ray = _connect(a)
+    objs = state.list_objects(limit=100000)
+    per_node = {}
+    for o in objs:
+        n = o.get("node_id") or o.get("node") or "inline"
+        sz = int(o.get("object_size") or o.get("size") or 0)
+        c, b = per_node.get(n, (0, 0))
+        per_node[n] = (c + 1, b + sz)
+    print("======== Object references ========")
+    print(f"{'node':34s} {'objects':>8s} {'bytes':>14s}")
+    for n, (c, b) in sorted(per_node.items(), key=lambda kv: -kv[1][1]):
+        print(f"{str(n)[:34]:34s} {c:8d} {b:14d}")
+    top = sorted(objs, key=lambda o: -int(o.get("object_size") or o.get("size") or 0))[: a.top]
+    if top:
+        print(f"\nLargest {len(top)} objects:")
+        for o in top:
+            print(f"  {str(o.get('object_id', ''))[:48]:48s} {int(o.get('object_size') or o.get('size') or 0):14d}"
+                  f"  refs={o.get('ref_count', '?')}")
+    total = ray.cluster_resources().get("object_store_memory", 0)
+    print(f"\nObject store capacity: {int(total)} bytes")
+    ray.shutdown()
+    return 0
+
+
+def cmd_logs(a):
+    """List the session's log files, or print one (``--tail`` lines; reference: ``ray logs``)."""
+    import fnmatch
+
+    ray = _connect(a)
+    from ..core.api import _session
+
+    sdir = _session.get("session_dir")
+    ray.shutdown()
+    if not sdir or not os.path.isdir(sdir):
+        print("no session directory", file=sys.stderr)
+        return 1
+    files = sorted(f for f in os.listdir(sdir) if f.endswith((".log", ".out", ".err")))
+    if a.glob:
+        files = [f for f in files if fnmatch.fnmatch(f, a.glob)]
+    if not a.glob or len(files) != 1:
+        for f in files:
+            print(f"{os.path.getsize(os.path.join(sdir, f)):10d}  {f}")
+        return 0
+    with open(os.path.join(sdir, files[0]), errors="replace") as fh:
+        lines = fh.readlines()
+    sys.stdout.writelines(lines[-a.tail:] if a.tail else lines)
+    return 0
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="cluster_anywhere_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -251,6 +373,40 @@ def main(argv=None):
     x = jsub.add_parser("list")
     x.add_argument("--address", default=None)
     j.set_defaults(fn=cmd_job)
+    for name, fn in (("up", cmd_up), ("down", cmd_down), ("get-head-ip", cmd_get_head_ip), ("attach", cmd_attach)):
+        x = sub.add_parser(name)
+        x.add_argument("cluster_config")
+        if name == "up":
+            x.add_argument("--no-restart", action="store_true")
+            x.add_argument("-y", "--yes", action="store_true")
+        if name == "down":
+            x.add_argument("--workers-only", action="store_true")
+            x.add_argument("-y", "--yes", action="store_true")
+        x.set_defaults(fn=fn)
+    x = sub.add_parser("exec")
+    x.add_argument("cluster_config")
+    x.add_argument("cmd", nargs=argparse.REMAINDER)
+    x.set_defaults(fn=cmd_exec)
+    x = sub.add_parser("submit")
+    x.add_argument("cluster_config")
+    x.add_argument("script")
+    x.add_argument("script_args", nargs=argparse.REMAINDER)
+    x.set_defaults(fn=cmd_submit)
+    for name in ("rsync-up", "rsync-down"):
+        x = sub.add_parser(name)
+        x.add_argument("cluster_config")
+        x.add_argument("source")
+        x.add_argument("target")
+        x.set_defaults(fn=cmd_rsync, cmd=name)
+    x = sub.add_parser("memory")
+    x.add_argument("--address", default=None)
+    x.add_argument("--top", type=int, default=10)
+    x.set_defaults(fn=cmd_memory)
+    x = sub.add_parser("logs")
+    x.add_argument("glob", nargs="?", default=None)
+    x.add_argument("--address", default=None)
+    x.add_argument("--tail", type=int, default=0)
+    x.set_defaults(fn=cmd_logs)
     from ..serve.scripts import add_parser as add_serve_parser
 
     add_serve_parser(sub)
