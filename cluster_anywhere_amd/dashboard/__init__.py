@@ -75,10 +75,10 @@ def render_prometheus(state: Callable) -> str:
     return "\n".join(lines) + "\n"
 
 
-def build_app(state: Callable, jobs: JobManager):
+def build_app(state: Callable, jobs: JobManager, session_dir: Optional[str] = None):
     from starlette.applications import Starlette
     from starlette.requests import Request
-    from starlette.responses import JSONResponse, PlainTextResponse, Response
+    from starlette.responses import HTMLResponse, JSONResponse, PlainTextResponse, Response
     from starlette.routing import Route
 
     def j(x, status=200):
@@ -136,7 +136,41 @@ def build_app(state: Callable, jobs: JobManager):
 
         return j(_timeline_events(state("events")))
 
-    routes = [Route("/api/version", version), Route("/api/cluster_status", cluster_status),
+    async def ui(req):
+        # single-page UI over the REST endpoints below (reference: dashboard/client)
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "ui.html")) as f:
+            return HTMLResponse(f.read())
+
+    def _log_dir():
+        return session_dir if session_dir and os.path.isdir(session_dir) else None
+
+    async def list_logs(req):
+        d = _log_dir()
+        files = []
+        if d:
+            for root, _, names in os.walk(d):
+                for n in sorted(names):
+                    if n.endswith((".log", ".out", ".err")):
+                        p = os.path.join(root, n)
+                        files.append({"name": os.path.relpath(p, d), "size": os.path.getsize(p)})
+        return j({"files": files})
+
+    async def log_file(req):
+        d = _log_dir()
+        name = req.query_params.get("name", "")
+        lines = int(req.query_params.get("lines", "1000"))
+        if not d or not name:
+            return j({"error": "not found"}, 404)
+        p = os.path.realpath(os.path.join(d, name))
+        if not p.startswith(os.path.realpath(d) + os.sep) or not os.path.isfile(p):
+            return j({"error": "not found"}, 404)  # no escaping the session directory
+        with open(p, errors="replace") as f:
+            text = "".join(f.readlines()[-lines:])
+        return j({"name": name, "text": text})
+
+    routes = [Route("/", ui), Route("/ui", ui), Route("/api/v0/logs", list_logs),
+              Route("/api/v0/logs/file", log_file),
+              Route("/api/version", version), Route("/api/cluster_status", cluster_status),
               Route("/api/v0/nodes", lister("nodes")), Route("/api/v0/actors", lister("actors")),
               Route("/api/v0/tasks", lister("tasks")), Route("/api/v0/objects", lister("objects")),
               Route("/api/v0/workers", lister("workers")),
@@ -166,7 +200,7 @@ def start_dashboard(host: str = "127.0.0.1", port: int = 8265, head=None, contro
     if session_dir is None:
         session_dir = head.session_dir if head is not None else "/tmp/caamd"
     jobs = JobManager(control_address, os.path.join(session_dir, "jobs"))
-    app = build_app(state, jobs)
+    app = build_app(state, jobs, session_dir)
     cfg = uvicorn.Config(app, host=host, port=port, log_level="warning", lifespan="off", access_log=False)
     server = uvicorn.Server(cfg)
     t = threading.Thread(target=server.run, name="caamd-dashboard", daemon=True)
