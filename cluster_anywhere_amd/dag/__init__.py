@@ -40,7 +40,8 @@ class DAGNode:
 
     def with_tensor_transport(self, transport: str = "auto", **_kw):
         """Mark this node's output for out-of-band tensor transfer in a compiled
-        graph: ``"nccl"``/``"rccl"`` (GPU→GPU over xGMI) or ``"gloo"`` (CPU)."""
+        graph: ``"nccl"``/``"rccl"`` (GPU→GPU over xGMI), ``"ipc"`` (same-node GPU
+        actors through shared HBM buffers, HIP IPC) or ``"gloo"`` (CPU)."""
         self._transport = transport
         return self
 
@@ -138,6 +139,23 @@ class ClassMethodNode(DAGNode):
         return getattr(h, self._method).remote(*a, **k)
 
 
+class CollectiveOutputNode(ClassMethodNode):
+    """One participant's output of a collective op across several actors' node
+    outputs (reference: python/ray/dag/collective_node.py): it runs on the
+    actor that produced its input; all participants execute the op together
+    inside a compiled graph (``experimental.collective.allreduce.bind``)."""
+
+    METHOD = "__caamd_collective__"
+
+    def __init__(self, inp: ClassMethodNode, coll: dict, rank: int):
+        super().__init__(inp._target, self.METHOD, (inp,), {}, 1)
+        self._coll = coll
+        self._rank = rank
+
+    def _run(self, cache, inp):
+        raise ValueError("collective nodes run only inside a compiled graph (dag.experimental_compile())")
+
+
 class MultiOutputNode(DAGNode):
     def __init__(self, outputs: List[DAGNode]):
         super().__init__(tuple(outputs), {})
@@ -146,4 +164,5 @@ class MultiOutputNode(DAGNode):
         return [x._exec(cache, inp) if isinstance(x, DAGNode) else x for x in self._args]
 
 
-__all__ = ["DAGNode", "InputNode", "FunctionNode", "ClassNode", "ClassMethodNode", "MultiOutputNode"]
+__all__ = ["DAGNode", "InputNode", "FunctionNode", "ClassNode", "ClassMethodNode", "MultiOutputNode",
+           "CollectiveOutputNode"]

@@ -15,6 +15,13 @@ standing pipeline:
   ``"gloo"`` for CPU) sends only tensor metadata through the ring and the tensor
   payload point-to-point over an RCCL communicator spanning the graph's actors
   — on MI355X that is a direct xGMI GPU→GPU copy, never a host bounce;
+* ``with_tensor_transport("ipc")`` keeps GPU tensors on the GPU between actors
+  of one node: the producer copies each output tensor into one of ``depth + 1``
+  HBM buffers it shares once by HIP IPC handle, the ring carries only metadata,
+  and the consumer maps the buffers once and copies out of them on its GPU;
+* collective nodes (``experimental.collective.allreduce/allgather/reducescatter``,
+  reference: dag/collective_node.py) run an op across several actors' outputs
+  over a collective group set up at compile time;
 * up to ``_max_inflight_executions`` executions are pipelined (the ring depth);
   ``execute()`` returns a :class:`CompiledDAGRef`; ``ray.get`` on it reads the
   outputs in submission order. An exception inside a node is forwarded through
@@ -51,6 +58,15 @@ class _TensorSlot:
 
     def __init__(self, i, shape, dtype):
         self.i, self.shape, self.dtype = i, tuple(shape), dtype
+
+
+class _IpcSlot(_TensorSlot):
+    """Placeholder for a tensor left in shared HBM buffer ``buf`` (``handle`` is
+    sent with a buffer's first use / reallocation)."""
+
+    def __init__(self, i, shape, dtype, buf, handle):
+        super().__init__(i, shape, dtype)
+        self.buf, self.handle = buf, handle
 
 
 # --------------------------------------------------------------------- refs
@@ -120,8 +136,20 @@ class _ActorLoop:
         self.inst = instance
         self.plan = plan
         self.group = None
+        self.cgroups = {}
+        self.ipc_out = {}   # (out key, tensor index) -> [buffers]
+        self.ipc_seq = {}   # out key -> executions written
+        self.ipc_maps = {}  # (channel name, tensor index, buffer) -> mapped uint8 tensor
 
     def _setup_group(self):
+        from ..util.collective import collective as col
+
+        for cg in self.plan.get("cgroups", []):
+            backend = cg["backend"]
+            if backend == "auto":
+                backend = "nccl" if os.environ.get("CAAMD_GPU_IDS") else "gloo"
+            col.init_collective_group(cg["world"], cg["rank"], backend=backend, group_name=cg["name"])
+            self.cgroups[cg["name"]] = backend
         g = self.plan.get("group")
         if not g:
             return
@@ -136,6 +164,8 @@ class _ActorLoop:
 
     def _read(self, ch, reader, producer_rank):
         v = ch.read(reader)
+        if producer_rank == "ipc" and not isinstance(v, (_Stop, _DagError)):
+            return self._read_ipc(ch, v)
         if producer_rank is not None and not isinstance(v, (_Stop, _DagError)):
             import torch
 
@@ -147,7 +177,104 @@ class _ActorLoop:
             v = _fill_tensors(v, {s.i: b for s, b in zip(slots, bufs)})
         return v
 
+    # -- HIP IPC edges: shared HBM buffer ring (depth + 1 buffers per tensor) ----
+    def _write_ipc(self, out, value):
+        import torch
+
+        from ..experimental.gpu_objects import reduce_ipc
+
+        key = id(out)
+        seq = self.ipc_seq.get(key, 0)
+        self.ipc_seq[key] = seq + 1
+        nbuf = out["ipc_depth"] + 1
+        j = seq % nbuf
+
+        def sub_all(skel, tensors):
+            def sub(v):
+                if not isinstance(v, _TensorSlot):
+                    return v
+                t = tensors[v.i]
+                if not t.is_cuda:
+                    return t  # CPU tensors travel in the ring itself
+                nbytes = t.numel() * t.element_size()
+                bufs = self.ipc_out.setdefault((key, v.i), [None] * nbuf)
+                handle = None
+                if bufs[j] is None or bufs[j].numel() < nbytes or bufs[j].device != t.device:
+                    bufs[j] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=t.device)
+                    handle = reduce_ipc(bufs[j])
+                bufs[j][:nbytes].copy_(t.reshape(-1).view(torch.uint8))
+                return _IpcSlot(v.i, t.shape, t.dtype, j, handle)
+
+            if isinstance(skel, (list, tuple)):
+                return type(skel)(sub(x) for x in skel)
+            if isinstance(skel, dict):
+                return {k: sub(x) for k, x in skel.items()}
+            return sub(skel)
+
+        skel, tensors = _split_tensors(value)
+        msg = sub_all(skel, tensors)
+        if any(t.is_cuda for t in tensors):
+            torch.cuda.current_stream().synchronize()  # data in HBM before the consumer sees the slot
+        out["chan"].write(msg)
+
+    def _read_ipc(self, ch, v):
+        import torch
+
+        def sub(x):
+            if not isinstance(x, _IpcSlot):
+                return x
+            k = (ch.name, x.i, x.buf)
+            if x.handle is not None:
+                fn, args = x.handle
+                self.ipc_maps[k] = fn(*args)
+            src = self.ipc_maps[k]
+            n = 1
+            for d in x.shape:
+                n *= d
+            nbytes = n * torch.empty((), dtype=x.dtype).element_size()
+            t = src[:nbytes].view(x.dtype).view(x.shape).clone()
+            return t
+
+        if isinstance(v, (list, tuple)):
+            out = type(v)(sub(x) for x in v)
+        elif isinstance(v, dict):
+            out = {k: sub(x) for k, x in v.items()}
+        else:
+            out = sub(v)
+        if torch.cuda.is_available() and self.ipc_maps:
+            # copies done before the next read lets the producer reuse the buffer
+            torch.cuda.current_stream().synchronize()
+        return out
+
+    def _collective(self, spec, x):
+        import torch
+
+        from ..util.collective import collective as col
+
+        name, kind, op = spec["group"], spec["kind"], spec["op"]
+        if not isinstance(x, torch.Tensor):
+            raise TypeError(f"collective {kind} needs a torch.Tensor input, got {type(x).__name__}")
+        world = spec["world"]
+        if kind == "allreduce":
+            t = x.clone()
+            col.allreduce(t, name, op)
+            return t
+        if kind == "allgather":
+            outs = [torch.empty_like(x) for _ in range(world)]
+            col.allgather(outs, x.contiguous(), name)
+            return outs
+        if kind == "reducescatter":
+            if x.shape[0] % world:
+                raise ValueError(f"reducescatter: dim 0 ({x.shape[0]}) must divide by {world}")
+            chunks = [c.contiguous() for c in x.chunk(world, 0)]
+            t = torch.empty_like(chunks[0])
+            col.reducescatter(t, chunks, name, op)
+            return t
+        raise ValueError(kind)
+
     def _write(self, out, value):
+        if out.get("ipc") and not isinstance(value, (_Stop, _DagError)):
+            return self._write_ipc(out, value)
         ch, dst_ranks = out["chan"], out.get("dst_ranks")
         if dst_ranks and not isinstance(value, (_Stop, _DagError)):
             skel, tensors = _split_tensors(value)
@@ -218,7 +345,10 @@ class _ActorLoop:
                         res = err
                     else:
                         try:
-                            res = self._call(t["method"], a, k)
+                            if t.get("coll") is not None:
+                                res = self._collective(t["coll"], a[0])
+                            else:
+                                res = self._call(t["method"], a, k)
                         except Exception as e:
                             res = _DagError(RayTaskError(t["method"], traceback.format_exc(), e))
                 local[t["idx"]] = res
@@ -228,11 +358,12 @@ class _ActorLoop:
                     except ChannelClosedError:
                         return
             if stop:
-                if self.group is not None:
-                    from ..util import collective as col
+                from ..util import collective as col
 
+                names = list(self.cgroups) + ([self.plan["group"]["name"]] if self.group is not None else [])
+                for nm in names:
                     try:
-                        col.destroy_collective_group(self.plan["group"]["name"])
+                        col.destroy_collective_group(nm)
                     except Exception:
                         pass
                 return
@@ -336,8 +467,9 @@ class CompiledDAG:
         if not input_readers:
             raise ValueError("a compiled graph must consume its InputNode")
 
-        # collective group for tensor-transport edges (ranks = actor order)
-        transports = {getattr(t, "_transport", None) for t in tasks} - {None, "auto", "shm"}
+        # collective group for tensor-transport edges (ranks = actor order); "ipc"
+        # edges need no group (shared HBM buffers between same-node actors)
+        transports = {getattr(t, "_transport", None) for t in tasks} - {None, "auto", "shm", "ipc"}
         bad = transports - set(COLLECTIVE_TRANSPORTS)
         if bad:
             raise ValueError(f"unknown tensor transport(s) {sorted(bad)}")
@@ -359,11 +491,26 @@ class CompiledDAG:
         for o in outputs:
             self._out_specs.append((chans[id(o)], consumers[id(o)].index("driver")))
 
-        plans = {a: {"tasks": [], "group": None} for a in range(len(actors))}
+        plans = {a: {"tasks": [], "group": None, "cgroups": []} for a in range(len(actors))}
         if backend:
             for a in plans:
                 plans[a]["group"] = {"world": len(actors), "rank": a, "backend": backend,
                                      "name": self._group}
+        # collective nodes: one group per collective op, ranks = participant order
+        from . import CollectiveOutputNode
+
+        colls: Dict[int, dict] = {}
+        for t in tasks:
+            if isinstance(t, CollectiveOutputNode) and t._coll["id"] not in colls:
+                c = t._coll
+                parts = [akey[id(o)] for o in c["outputs"]]
+                if any(id(o) not in akey for o in c["outputs"]):
+                    raise ValueError("every output of a collective must be part of the compiled graph")
+                name = f"cdag-{os.getpid()}-{os.urandom(3).hex()}-c{c['id']}"
+                colls[c["id"]] = {"group": name, "kind": c["kind"], "op": c["op"], "world": len(parts)}
+                tr = {"rccl": "nccl"}.get(c["transport"], c["transport"])
+                for r, a in enumerate(parts):
+                    plans[a]["cgroups"].append({"name": name, "world": len(parts), "rank": r, "backend": tr})
 
         def spec(d, a):
             if isinstance(d, InputNode):
@@ -373,7 +520,10 @@ class CompiledDAG:
             if isinstance(d, ClassMethodNode):
                 if akey[id(d)] == a:
                     return ("loc", tidx[id(d)])
-                tr = getattr(d, "_transport", None) if backend else None
+                tr = getattr(d, "_transport", None)
+                if tr == "ipc":
+                    return ("ch", chans[id(d)], consumers[id(d)].index(a), None, "ipc")
+                tr = tr if backend else None
                 src = akey[id(d)] if tr in COLLECTIVE_TRANSPORTS else None
                 return ("ch", chans[id(d)], consumers[id(d)].index(a), None, src)
             return ("const", d)
@@ -384,6 +534,11 @@ class CompiledDAG:
             if id(t) in chans:
                 out = {"chan": chans[id(t)]}
                 tr = getattr(t, "_transport", None)
+                if tr == "ipc":
+                    if "driver" in consumers[id(t)]:
+                        raise ValueError("an ipc tensor-transport node cannot be a graph output")
+                    out["ipc"] = True
+                    out["ipc_depth"] = self._slots
                 if backend and tr in COLLECTIVE_TRANSPORTS:
                     if "driver" in consumers[id(t)]:
                         raise ValueError("a tensor-transport node cannot be a graph output "
@@ -391,6 +546,7 @@ class CompiledDAG:
                     out["dst_ranks"] = list(consumers[id(t)])
             plans[a]["tasks"].append({
                 "idx": tidx[id(t)], "method": t._method, "out": out,
+                "coll": colls[t._coll["id"]] if isinstance(t, CollectiveOutputNode) else None,
                 "args": [spec(d, a) for d in t._args],
                 "kwargs": {k: spec(d, a) for k, d in t._kwargs.items()},
             })

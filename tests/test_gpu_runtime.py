@@ -169,3 +169,41 @@ def test_collective_rccl_single_rank(cluster):
             return float(t.sum())
 
     assert ray.get(M.remote().run.remote(), timeout=120) == 2048.0
+
+
+def test_compiled_dag_ipc_gpu_edge(cluster):
+    """Compiled graph with a HIP-IPC tensor edge: the producer's HBM buffers are
+    mapped once by the consumer (two actors sharing the GPU); values stay exact
+    across pipelined executions (buffer reuse is safe)."""
+    from cluster_anywhere_amd.dag import InputNode
+
+    @ray.remote(num_gpus=0.4)
+    class Prod:
+        def make(self, x):
+            import torch
+
+            return {"t": torch.arange(1 << 16, device="cuda", dtype=torch.float32) * x, "tag": x}
+
+    @ray.remote(num_gpus=0.4)
+    class Cons:
+        def use(self, d):
+            t = d["t"]
+            assert t.is_cuda
+            return float(t.sum()), d["tag"]
+
+    p, c = Prod.remote(), Cons.remote()
+    with InputNode() as inp:
+        dag = c.use.bind(p.make.bind(inp).with_tensor_transport("ipc"))
+    cdag = dag.experimental_compile(_max_inflight_executions=4)
+    try:
+        base = float(sum(range(1 << 16)))
+        refs = [cdag.execute(float(i)) for i in range(4)]
+        outs = [ray.get(r, timeout=120) for r in refs]
+        for i in range(4, 24):
+            outs.append(ray.get(cdag.execute(float(i)), timeout=120))
+        for i, (s, tag) in enumerate(outs):
+            assert tag == float(i) and s == pytest.approx(base * i, rel=1e-6)
+    finally:
+        cdag.teardown()
+    ray.kill(c)
+    ray.kill(p)
