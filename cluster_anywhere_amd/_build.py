@@ -57,6 +57,13 @@ def native_path() -> str:
     return os.path.join(PKG_DIR, "_native" + EXT_SUFFIX)
 
 
+# Per-source extra hipcc flags. The D = 64 attention kernels are VALU-issue-bound
+# next to their MFMAs; packed f32 ops (v_pk_add/mul_f32, formed by SLP
+# vectorisation of adjacent scalar adds/multiplies) cost more issue cycles there
+# than the scalar pair (cdna_hip_programming.md: packed f32 VALU beside MFMAs).
+PER_FILE_FLAGS = {"flash_attn_d64.hip": ["-fno-slp-vectorize"]}
+
+
 def build_kernels(verbose: bool = False, force: bool = False) -> str:
     import torch
     import torch.utils.cpp_extension as ce
@@ -84,7 +91,7 @@ def build_kernels(verbose: bool = False, force: bool = False) -> str:
         objs.append(o)
         if force or _newer(o, [s] + headers):
             jobs.append([HIPCC, f"--offload-arch={ARCH}", *common, "-munsafe-fp-atomics",
-                         "-I", src_dir, "-c", s, "-o", o])
+                         *PER_FILE_FLAGS.get(os.path.basename(s), []), "-I", src_dir, "-c", s, "-o", o])
     for s in cpp_srcs:
         o = os.path.join(BUILD_DIR, os.path.basename(s) + ".o")
         objs.append(o)

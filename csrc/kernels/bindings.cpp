@@ -387,7 +387,8 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, 
   TORCH_CHECK(dout.sizes() == out.sizes(), "flash_attn_bwd: dout shape");
   TORCH_CHECK(lse.numel() == (int64_t)B * H * T, "flash_attn_bwd: lse shape");
   auto dqkv = at::empty_like(qkv);
-  auto delta = at::empty_like(lse);
+  // workspace: Delta = rowsum(dO * O) and lse * log2(e), [2, B, H, T]
+  auto delta = at::empty({2, (int64_t)B * H * T}, lse.options());
   if (B > 0 && T > 0)
     caamd::fa_bwd_launch(bp(qkv), bp(out), bp(dout), lse.data_ptr<float>(),
                          delta.data_ptr<float>(), bp(dqkv), B, T, (int)H, D, causal ? 1 : 0,

@@ -23,7 +23,23 @@
 // XCD (shared K/V in that XCD's L2), heaviest causal blocks first.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace caamd {
+
+// D = 64 second-generation kernels (flash_attn_d64.hip); CAAMD_FA_V1=1 selects
+// the first-generation D = 64 kernels below (A/B timing).
+void fa64_fwd_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
+                     hipStream_t);
+void fa64_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, float*, bf16*, int, int, int, int,
+                     hipStream_t);
+static bool fa_v1() {
+  static const bool v = [] {
+    const char* e = std::getenv("CAAMD_FA_V1");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -627,6 +643,10 @@ static void fa_set_attrs() {
 
 void fa_fwd_gqa_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int kv_rs, int group,
                        bf16* out, float* lse, int B, int T, int H, int D, int causal, hipStream_t st) {
+  if (D == 64 && !fa_v1()) {
+    fa64_fwd_launch(q, k, v, q_rs, kv_rs, group, out, lse, B, T, H, causal, st);
+    return;
+  }
   const int qblk = D == 64 ? qblk_for<64>() : qblk_for<128>();
   const int nqb = (T + qblk - 1) / qblk;
   const float scale_log2 = 1.44269504089f / sqrtf((float)D);
@@ -650,6 +670,10 @@ void fa_fwd_launch(const bf16* qkv, bf16* out, float* lse, int B, int T, int H, 
 void fa_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse,
                    float* delta, bf16* dqkv, int B, int T, int H, int D, int causal,
                    hipStream_t st) {
+  if (D == 64 && !fa_v1()) {  // delta: 2 * B * H * T floats
+    fa64_bwd_launch(qkv, out, dout, lse, delta, dqkv, B, T, H, causal, st);
+    return;
+  }
   const int qblk = D == 64 ? qblk_for<64>() : qblk_for<128>();
   const int nqb = (T + qblk - 1) / qblk;
   const int nkb = (T + 127) / 128;

@@ -1,0 +1,774 @@
+// Causal flash attention for head_dim 64 on gfx950 (v_mfma_f32_32x32x16_bf16),
+// second generation: the D = 64 path of GPT-2-XL training (25 heads x 64).
+//
+// Why a separate D = 64 design: at D = 64 every score costs only 4*D = 256 MFMA
+// flops but ~5 VALU instructions (max, fma, exp, sum, cvt), so the kernels are
+// VALU-issue-bound, not MFMA-bound. A rocprofv3 PMC pass of the first-generation
+// kernels (flash_attention.hip) measured 13-15 VALU instructions per MFMA
+// (profiles/attn_pmc_v1.md): operand tiles were staged through registers and
+// the transposed operands (V^T, K^T, Q^T, dO^T) were written into LDS with
+// 16-32 ds_write_b16 + v_perm per thread per tile, and the online softmax
+// rescaled O on every tile. This generation removes that overhead:
+//
+//  * Every K/V/Q/dO tile (64 rows x 128 B) reaches LDS by LDS-DMA
+//    (global_load_lds_dwordx4, 16 B per lane, no VGPR staging) into ONE
+//    row-major image, XOR-swizzled on the DMA source address:
+//       16-B chunk c of row r sits at chunk position c ^ f((r >> 1) & 7),
+//       f(x) = x ^ ((x & 1) << 2)
+//    f is a bijection of x, so the ds_read_b128 row reads of the 32x32x16
+//    operand (lane: row R0 + (l & 31), chunk 2s + (l >> 5)) hit 16 distinct
+//    16-B slots in each of the four b128 lane groups, and bit 2 of f flips
+//    between rows 4k+{0,1} and 4k+{2,3}, so the ds_read_b64_tr_b16 transposed
+//    reads (per 32-lane half: 4 rows x 64 B) cover all 64 banks exactly once.
+//    The same image serves row reads AND transposed reads (dq: K; dkdv: Q, dO).
+//  * Transposed operands come from ds_read_b64_tr_b16 (hardware transpose),
+//    no transposed copies.
+//  * Lazy softmax rescale (forward): the running max used for exp2 is only
+//    raised when some query's max grew by more than 8 (log2 units), so O and l
+//    are rescaled on a few early tiles instead of every tile; P <= 2^8 stays
+//    exact to bf16 relative precision and l/O stay in fp32.
+//  * Per-lane partial row sums (both lanes of a query keep their own half and
+//    combine once at the end).
+//  * The backward keeps two kernels (dQ and dK/dV). A fused single kernel
+//    needs dQ summed across key blocks: at D = 64 that is one f32 atomic byte
+//    per 640 flops, ~0.9 GB of atomics per GPT-2-XL layer at B=32, T=1024,
+//    which at the ~1.3 TB/s chip-wide float-atomic rate costs more than the
+//    whole two-kernel backward; recomputing S and dP in the dQ kernel is cheaper.
+//
+// Layout (same as flash_attention.hip): packed qkv [B, T, 3, H, D] in place,
+// o [B, T, H, D], dqkv packed like qkv. GQA forward via q/kv row strides.
+#include "common.h"
+
+#include <cstdlib>
+#include <type_traits>
+#include <utility>
+
+namespace caamd {
+namespace fa64 {
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// compile-time unrolled loop: f(std::integral_constant<int, i>) for i = 0..N-1
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) char lds_t;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int D = 64;
+constexpr int IMG = 64 * 128;  // one 64-row bf16 tile image (bytes)
+constexpr float kThr = 8.f;    // lazy-rescale threshold (log2 units)
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+// C/D layout of 32x32: reg i of lane l -> row (i&3) + 8*(i>>2) + 4*(l>>5), col l&31.
+__device__ __forceinline__ int crow(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// accumulator registers 8s..8s+7 -> bf16 operand fragment for k-step s
+__device__ __forceinline__ bf16x8 acc_frag(const f32x16& x, int s) {
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = (bf16)x[8 * s + j];
+  return f;
+}
+
+__device__ __forceinline__ int swz(int row) {
+  const int x = (row >> 1) & 7;
+  return x ^ ((x & 1) << 2);
+}
+
+// 64-row tile rows [row0, row0 + 64) of g (row stride rs elements, 64 bf16 per
+// row) -> swizzled LDS image; 256 threads, two 1-KiB DMA pieces per wave. Rows
+// past T are clamped to T - 1 (finite data; masked by the caller).
+__device__ __forceinline__ void dma_tile(const bf16* __restrict__ g, size_t rs, int row0, int T,
+                                         lds_t* dst, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int lin = j * 256 + wave * 64 + lane;
+    const int row = lin >> 3, pos = lin & 7;
+    const int c = pos ^ swz(row);
+    const int gr = min(row0 + row, T - 1);
+    const bf16* src = g + (size_t)gr * rs + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (void __attribute__((address_space(3)))*)(dst + (j * 256 + wave * 64) * 16),
+                                     16, 0, 0);
+  }
+}
+// 64 floats st[row0 .. row0 + 64) -> LDS (one wave, 4 B per lane)
+__device__ __forceinline__ void dma_stats(const float* __restrict__ st, int row0, int T, lds_t* dst,
+                                          int lane) {
+  const int gr = min(row0 + lane, T - 1);
+  __builtin_amdgcn_global_load_lds((const void*)(st + gr), (void __attribute__((address_space(3)))*)dst, 4, 0,
+                                   0);
+}
+
+// Row fragment of the 32x32x16 operand: lane (r, h) gets X[row][16 s + 8 h .. +7].
+__device__ __forceinline__ bf16x8 rd_row(const lds_t* img, int row, int s, int h) {
+  const int c = 2 * s + h;
+  typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+  return *(lds_bf16x8*)(img + row * 128 + ((c ^ swz(row)) << 4));
+}
+
+// Transposed fragment: lane (r, h) gets X[rb + 8 (j >> 2) + 4 h + (j & 3)][c0 + r],
+// j = 0..7 -- the k order of acc_frag(., s) when rb = 32 kb + 16 s. Two
+// ds_read_b64_tr_b16 (rows rb + 4h + q and rb + 8 + 4h + q of a 16-lane group).
+//
+// Issued by inline asm: hipcc treats the tr16 builtin as possibly aliasing the
+// in-flight LDS-DMA of the NEXT tiles and puts an s_waitcnt vmcnt(0) before it,
+// which would expose the whole prefetch latency on every tile. The asm reads are
+// invisible to the compiler's counters, so every batch ends with tr_wait*, an
+// lgkmcnt(0) that also names the destination registers (nothing reads them
+// before it). LDS reads complete in order, so the compiler's own counted
+// lgkmcnt waits stay correct with these extra reads in flight.
+struct TrFrag {
+  s16x4 lo, hi;
+};
+__device__ __forceinline__ void tr_issue(TrFrag& t, const lds_t* img, int rb, int c0, int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = rb + 4 * (G >> 1) + q;
+  const int col = c0 + 16 * (G & 1) + 4 * p;
+  const int c = col >> 3, within = (col & 7) * 2;
+  const int row2 = row + 8;
+  const unsigned a0 = (unsigned)(size_t)(img + row * 128 + ((c ^ swz(row)) << 4) + within);
+  const unsigned a1 = (unsigned)(size_t)(img + row2 * 128 + ((c ^ swz(row2)) << 4) + within);
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(t.lo) : "v"(a0) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(t.hi) : "v"(a1) : "memory");
+}
+__device__ __forceinline__ void tr_wait2(TrFrag& a, TrFrag& b) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a.lo), "+v"(a.hi), "+v"(b.lo), "+v"(b.hi)::"memory");
+}
+__device__ __forceinline__ void tr_wait4(TrFrag& a, TrFrag& b, TrFrag& c, TrFrag& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(a.lo), "+v"(a.hi), "+v"(b.lo), "+v"(b.hi), "+v"(c.lo), "+v"(c.hi), "+v"(d.lo), "+v"(d.hi)::"memory");
+}
+// Lane-constant parts of the transposed-read addresses. For a block starting
+// at row rb (a multiple of 16) swz() is unchanged, and row + 8 flips bit 2 of
+// swz(), which maps the d = 0 hi read onto the d = 1 lo pattern and vice versa:
+// two lane offsets (A: d = 0 lo, B: d = 1 lo) serve every transposed read of an
+// image, the rest is the instruction's immediate offset (rb * 128, + 1024).
+struct TrBase {
+  unsigned a, b;
+};
+__device__ __forceinline__ TrBase tr_base(int lane) {
+  const int G = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = 4 * (G >> 1) + q;
+  const int c = 2 * (G & 1) + (p >> 1), within = (p & 1) * 8;
+  return {(unsigned)(row * 128 + ((c ^ swz(row)) << 4) + within),
+          (unsigned)(row * 128 + (((c + 4) ^ swz(row)) << 4) + within)};
+}
+template <int OFF>
+__device__ __forceinline__ s16x4 tr_at(unsigned addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+  return v;
+}
+// fragment rows [RB, RB + 16), head-dim block DD (columns 32 DD .. 32 DD + 31) of
+// the image at LDS byte address `img` (lane bases from tr_base)
+template <int RB, int DD>
+__device__ __forceinline__ void tr_frag(TrFrag& t, unsigned img, const TrBase& tb) {
+  if constexpr (DD == 0) {
+    t.lo = tr_at<RB * 128>(img + tb.a);
+    t.hi = tr_at<RB * 128 + 1024>(img + tb.b);
+  } else {
+    t.lo = tr_at<RB * 128>(img + tb.b);
+    t.hi = tr_at<RB * 128 + 1024>(img + tb.a);
+  }
+}
+
+__device__ __forceinline__ bf16x8 tr_join(const TrFrag& t) {
+  const s16x8 v = {t.lo[0], t.lo[1], t.lo[2], t.lo[3], t.hi[0], t.hi[1], t.hi[2], t.hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// x (op) x[lane ^ 32] with v_permlane32_swap (VALU, no LDS bpermute)
+__device__ __forceinline__ float max_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// Three-stage ring, DMA two tiles ahead: at the end of step t, tile t + 1 must
+// have landed while tile t + 2's N pieces (issued this step) stay in flight.
+template <int N>
+__device__ __forceinline__ void wait_next(bool t2_issued) {
+  if (t2_issued) wait_vm<N>();
+  else wait_dma();
+}
+
+__device__ __forceinline__ int xcd_remap(int id, int n) {
+  const int xcd = id & 7, q = n >> 3, r = n & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (id >> 3);
+}
+
+// ----------------------------------------------------------------------------
+// forward: 4 waves x 64 queries (two 32-query sub-blocks) per block, 64-key tiles
+// double-buffered in LDS ({K image, V image} per stage, three stages, DMA two tiles ahead).
+// ----------------------------------------------------------------------------
+template <int QS>
+__global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void fwd_kernel(const bf16* __restrict__ qp, const bf16* __restrict__ kp,
+                                                     const bf16* __restrict__ vp, int q_rs, int kv_rs, int group,
+                                                     bf16* __restrict__ out, float* __restrict__ lse, int T,
+                                                     int H, int nqb, float scale_log2, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_t* smem = (lds_t*)smem_raw;
+  constexpr int STAGE = 2 * IMG;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = id / nqb;
+  const int qb = nqb - 1 - (id % nqb);  // heavy (late) query blocks first
+  const int b = bh / H, hh = bh % H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const size_t rs = (size_t)q_rs, krs = (size_t)kv_rs;
+  const bf16* qbase = qp + (size_t)b * T * rs + (size_t)hh * D;
+  const bf16* kbase = kp + (size_t)b * T * krs + (size_t)(hh / group) * D;
+  const bf16* vbase = vp + (size_t)b * T * krs + (size_t)(hh / group) * D;
+  constexpr int QBLK = 128 * QS;  // queries per block (4 waves x QS x 32)
+  const int q0w = qb * QBLK + wave * 32 * QS;
+
+  const int qend = min(T, qb * QBLK + QBLK);
+  const int nkt = causal ? (qend + 63) / 64 : (T + 63) / 64;
+  dma_tile(kbase, krs, 0, T, smem, wave, lane);
+  dma_tile(vbase, krs, 0, T, smem + IMG, wave, lane);
+  if (nkt > 1) {
+    dma_tile(kbase, krs, 64, T, smem + STAGE, wave, lane);
+    dma_tile(vbase, krs, 64, T, smem + STAGE + IMG, wave, lane);
+  }
+
+  // lane-constant LDS offsets: K row reads (k-step s) and V transposed reads
+  int koff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) koff[s] = r * 128 + (((2 * s + h) ^ swz(r)) << 4);
+  const TrBase vtb = tr_base(lane);
+
+  bf16x8 qf[QS][4];
+  f32x16 o[QS][2];
+  float m[QS], l[QS];
+#pragma unroll
+  for (int qs = 0; qs < QS; ++qs) {
+    const int q = q0w + qs * 32 + r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (q < T) qf[qs][s] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * s + 8 * h);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qs][s][j] = (bf16)0.f;
+      }
+    }
+    o[qs][0] = o[qs][1] = zero16();
+    m[qs] = -INFINITY;
+    l[qs] = 0.f;
+  }
+  wait_dma();
+  __syncthreads();
+
+  // one 64-key tile; need_mask (wave-uniform): causal diagonal / sequence tail.
+  // The mask compares kb*32 + crow(i, h) (an immediate + 4h) against one
+  // per-lane limit, so the unmasked tiles carry no index arithmetic.
+  auto tile = [&](bool need_mask, const lds_t* kimg, unsigned vimg, int k0) {
+    typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+    f32x16 sacc[QS][2];
+    // all eight K fragments of the tile in flight at once (one LDS latency)
+    bf16x8 kf[2][4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kf[kb][s] = *(lds_bf16x8*)(kimg + koff[s] + kb * 4096);
+    __builtin_amdgcn_sched_barrier(0);  // keep the reads batched (counted lgkmcnt per use)
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[kb][0], qf[qs][0], zero16());
+#pragma unroll
+      for (int s = 1; s < 4; ++s)
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[kb][s], qf[qs][s], sacc[qs][kb]);
+    }
+    // V^T fragments requested now, consumed after the softmax (latency hidden)
+    __builtin_amdgcn_sched_barrier(0);
+    TrFrag vt[2][2][2];
+    static_for<2>([&](auto kb_c) {
+      constexpr int kb = decltype(kb_c)::value;
+      static_for<2>([&](auto s_c) {
+        constexpr int s = decltype(s_c)::value;
+        tr_frag<kb * 32 + s * 16, 0>(vt[kb][s][0], vimg, vtb);
+        tr_frag<kb * 32 + s * 16, 1>(vt[kb][s][1], vimg, vtb);
+      });
+    });
+#pragma unroll
+    for (int qs = 0; qs < QS; ++qs) {
+      if (need_mask) {
+        const int q = q0w + qs * 32 + r;
+        const int lim = (causal ? min(q, T - 1) : T - 1) - k0 - 4 * h;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            sacc[qs][kb][i] = (kb * 32 + crow(i, 0) > lim) ? -INFINITY : sacc[qs][kb][i];
+      }
+      float mxa = sacc[qs][0][0], mxb = sacc[qs][1][0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) {
+        mxa = fmaxf(mxa, sacc[qs][0][i]);
+        mxb = fmaxf(mxb, sacc[qs][1][i]);
+      }
+      float mx = fmaxf(mxa, mxb);
+      mx = max_xor32(mx) * scale_log2;  // scale > 0 commutes with max
+      // lazy rescale: raise the reference max only when it grew by > kThr somewhere
+      if (__builtin_amdgcn_ballot_w64(mx > m[qs] + kThr) != 0) {
+        asm volatile("");  // keep this a real (rarely taken) branch: no speculated rescale
+        const float mnew = fmaxf(m[qs], mx);
+        const float alpha = m[qs] == -INFINITY ? 0.f : fexp2(m[qs] - mnew);
+        l[qs] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 2; ++d)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[qs][d][i] *= alpha;
+        m[qs] = mnew;
+      }
+      const float muse = m[qs] == -INFINITY ? 0.f : m[qs];
+      float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fexp2(__builtin_fmaf(sacc[qs][kb][i], scale_log2, -muse));
+          sacc[qs][kb][i] = p;
+          rs4[i & 3] += p;
+        }
+      l[qs] += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);  // this lane's key half only
+    }
+    // O^T += V^T P^T ; each V^T fragment feeds both query sub-blocks
+    tr_wait4(vt[0][0][0], vt[0][0][1], vt[0][1][0], vt[0][1][1]);
+    tr_wait4(vt[1][0][0], vt[1][0][1], vt[1][1][0], vt[1][1][1]);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pf[QS];
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) pf[qs] = acc_frag(sacc[qs][kb], s);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const bf16x8 vf = tr_join(vt[kb][s][d]);
+#pragma unroll
+          for (int qs = 0; qs < QS; ++qs) o[qs][d] = mfma32(vf, pf[qs], o[qs][d]);
+        }
+      }
+  };
+
+  const unsigned smem_u = (unsigned)(size_t)smem;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const int st = kt % 3;
+    const lds_t* kimg = smem + st * STAGE;
+    const unsigned vimg = smem_u + st * STAGE + IMG;
+    const bool ahead = kt + 2 < nkt;
+    if (ahead) {
+      lds_t* nb = smem + ((kt + 2) % 3) * STAGE;
+      dma_tile(kbase, krs, k0 + 128, T, nb, wave, lane);
+      dma_tile(vbase, krs, k0 + 128, T, nb + IMG, wave, lane);
+    }
+    const bool active = !(causal && k0 > q0w + 32 * QS - 1) && q0w < T;  // wave-uniform
+    if (active) {
+      tile((causal && k0 + 63 > q0w) || (k0 + 64 > T), kimg, vimg, k0);
+    }
+    wait_next<4>(ahead);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qs = 0; qs < QS; ++qs) {
+    const int q = q0w + qs * 32 + r;
+    const float lt = sum_xor32(l[qs]);
+    if (q < T) {
+      const float inv_l = lt > 0.f ? 1.f / lt : 0.f;
+      bf16* orow = out + ((size_t)b * T + q) * H * D + (size_t)hh * D;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[qs][d][4 * g + j] * inv_l);
+          *reinterpret_cast<bf16x4*>(orow + d * 32 + 8 * g + 4 * h) = v;
+        }
+      if (h == 0) lse[(size_t)bh * T + q] = (m[qs] + __log2f(lt)) * 0.69314718056f;
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// backward dQ (+ Delta = rowsum(dO * O), lse2 = lse * log2 e for the dK/dV
+// kernel): 4 waves x 64 queries per block, 64-key tiles {K image, V image}.
+// ----------------------------------------------------------------------------
+template <int QS>
+__global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o,
+                                                        const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                        float* __restrict__ delta, float* __restrict__ lse2o,
+                                                        bf16* __restrict__ dqkv, int T, int H, int nqb,
+                                                        float scale_log2, float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_t* smem = (lds_t*)smem_raw;
+  constexpr int STAGE = 2 * IMG;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = id / nqb;
+  const int qb = nqb - 1 - (id % nqb);
+  const int b = bh / H, hh = bh % H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const size_t rs = (size_t)3 * H * D, ors = (size_t)H * D;
+  const bf16* qbase = qkv + (size_t)b * T * rs + (size_t)hh * D;
+  const bf16* kbase = qbase + (size_t)H * D;
+  const bf16* vbase = kbase + (size_t)H * D;
+  constexpr int QBLK = 128 * QS;
+  const int q0w = qb * QBLK + wave * 32 * QS;
+  const int qend = min(T, qb * QBLK + QBLK);
+  const int nkt = causal ? (qend + 63) / 64 : (T + 63) / 64;
+  dma_tile(kbase, rs, 0, T, smem, wave, lane);
+  dma_tile(vbase, rs, 0, T, smem + IMG, wave, lane);
+  if (nkt > 1) {
+    dma_tile(kbase, rs, 64, T, smem + STAGE, wave, lane);
+    dma_tile(vbase, rs, 64, T, smem + STAGE + IMG, wave, lane);
+  }
+
+  bf16x8 qf[QS][4], df[QS][4];
+  float dlt[QS], lse2[QS];
+  f32x16 dq[QS][2];
+#pragma unroll
+  for (int qs = 0; qs < QS; ++qs) {
+    const int q = q0w + qs * 32 + r;
+    float dsum = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (q < T) {
+        qf[qs][s] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * s + 8 * h);
+        const size_t oo = ((size_t)b * T + q) * ors + (size_t)hh * D + 16 * s + 8 * h;
+        df[qs][s] = *reinterpret_cast<const bf16x8*>(dout + oo);
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + oo);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum += (float)df[qs][s][j] * (float)ov[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qs][s][j] = df[qs][s][j] = (bf16)0.f;
+      }
+    }
+    dsum += __shfl_xor(dsum, 32, 64);
+    dlt[qs] = dsum;
+    lse2[qs] = q < T ? lse[(size_t)bh * T + q] * 1.44269504089f : 0.f;
+    if (q < T && h == 0) {
+      delta[(size_t)bh * T + q] = dsum;
+      lse2o[(size_t)bh * T + q] = lse2[qs];
+    }
+    dq[qs][0] = dq[qs][1] = zero16();
+  }
+  int koff[4];  // lane-constant row-read offsets (K and V images share the layout)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) koff[s] = r * 128 + (((2 * s + h) ^ swz(r)) << 4);
+  const TrBase ktb = tr_base(lane);
+  wait_dma();
+  __syncthreads();
+
+  auto tile = [&](bool need_mask, const lds_t* kimg, unsigned kimg_u, int k0) {
+    typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+    static_for<2>([&](auto kb_c) {
+      constexpr int kb = decltype(kb_c)::value;
+      f32x16 sacc[QS], dp[QS];
+      {
+        const bf16x8 kf = *(lds_bf16x8*)(kimg + koff[0] + kb * 4096);
+        const bf16x8 vf = *(lds_bf16x8*)(kimg + IMG + koff[0] + kb * 4096);
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) {
+          sacc[qs] = mfma32(kf, qf[qs][0], zero16());
+          dp[qs] = mfma32(vf, df[qs][0], zero16());
+        }
+      }
+#pragma unroll
+      for (int s = 1; s < 4; ++s) {
+        const bf16x8 kf = *(lds_bf16x8*)(kimg + koff[s] + kb * 4096);
+        const bf16x8 vf = *(lds_bf16x8*)(kimg + IMG + koff[s] + kb * 4096);
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) {
+          sacc[qs] = mfma32(kf, qf[qs][s], sacc[qs]);
+          dp[qs] = mfma32(vf, df[qs][s], dp[qs]);
+        }
+      }
+#pragma unroll
+      for (int qs = 0; qs < QS; ++qs) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[qs][i] = fexp2(__builtin_fmaf(sacc[qs][i], scale_log2, -lse2[qs]));
+        if (need_mask) {
+          const int q = q0w + qs * 32 + r;
+          const int lim = (q >= T ? -1 : (causal ? min(q, T - 1) : T - 1)) - k0 - 4 * h;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sacc[qs][i] = (kb * 32 + crow(i, 0) > lim) ? 0.f : sacc[qs][i];
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[qs][i] *= dp[qs][i] - dlt[qs];  // dS^T
+      }
+      // dQ^T += K^T dS^T
+      static_for<2>([&](auto s_c) {
+        constexpr int s = decltype(s_c)::value;
+        TrFrag t[2];
+        tr_frag<kb * 32 + s * 16, 0>(t[0], kimg_u, ktb);
+        tr_frag<kb * 32 + s * 16, 1>(t[1], kimg_u, ktb);
+        tr_wait2(t[0], t[1]);
+        bf16x8 f[QS];
+#pragma unroll
+        for (int qs = 0; qs < QS; ++qs) f[qs] = acc_frag(sacc[qs], s);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const bf16x8 a = tr_join(t[d]);
+#pragma unroll
+          for (int qs = 0; qs < QS; ++qs) dq[qs][d] = mfma32(a, f[qs], dq[qs][d]);
+        }
+      });
+    });
+  };
+
+  const unsigned smem_u = (unsigned)(size_t)smem;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * 64;
+    const int st = kt % 3;
+    const bool ahead = kt + 2 < nkt;
+    if (ahead) {
+      lds_t* nb = smem + ((kt + 2) % 3) * STAGE;
+      dma_tile(kbase, rs, k0 + 128, T, nb, wave, lane);
+      dma_tile(vbase, rs, k0 + 128, T, nb + IMG, wave, lane);
+    }
+    if (!(causal && k0 > q0w + 32 * QS - 1) && q0w < T)  // wave-uniform
+      tile((causal && k0 + 63 > q0w) || (k0 + 64 > T), smem + st * STAGE, smem_u + st * STAGE, k0);
+    wait_next<4>(ahead);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qs = 0; qs < QS; ++qs) {
+    const int q = q0w + qs * 32 + r;
+    if (q < T) {
+      bf16* row = dqkv + ((size_t)b * T + q) * rs + (size_t)hh * D;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = (bf16)(dq[qs][d][4 * g + j] * scale);
+          *reinterpret_cast<bf16x4*>(row + d * 32 + 8 * g + 4 * h) = v;
+        }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// backward dK, dV: key on the lane, 4 waves x 32 keys per block; 64-query tiles
+// {Q image, dO image, lse2[64], delta[64]} double-buffered. Q and dO are read
+// by rows (S^T, dP^T) and transposed (dK^T, dV^T) from the same image.
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict__ qkv,
+                                                          const bf16* __restrict__ dout,
+                                                          const float* __restrict__ lse2g,
+                                                          const float* __restrict__ delta,
+                                                          bf16* __restrict__ dqkv, int T, int H, int nkb,
+                                                          float scale_log2, float scale, int causal) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_t* smem = (lds_t*)smem_raw;
+  constexpr int STAGE = 2 * IMG + 512;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = id / nkb;
+  const int kb0 = id % nkb;  // early key blocks are the heavy ones under the causal mask
+  const int b = bh / H, hh = bh % H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const size_t rs = (size_t)3 * H * D, ors = (size_t)H * D;
+  const bf16* qbase = qkv + (size_t)b * T * rs + (size_t)hh * D;
+  const bf16* kbase = qbase + (size_t)H * D;
+  const bf16* vbase = kbase + (size_t)H * D;
+  const bf16* dobase = dout + (size_t)b * T * ors + (size_t)hh * D;
+  const float* l2b = lse2g + (size_t)bh * T;
+  const float* dlb = delta + (size_t)bh * T;
+  const int key0w = kb0 * 128 + wave * 32;
+  const int key = key0w + r;
+  const bool kv = key < T;
+  const int qt0 = causal ? (kb0 * 128) / 64 : 0;
+  const int nqt = (T + 63) / 64;
+
+  auto issue = [&](int qt, lds_t* buf) {
+    dma_tile(qbase, rs, qt * 64, T, buf, wave, lane);
+    dma_tile(dobase, ors, qt * 64, T, buf + IMG, wave, lane);
+    if (wave == 0) dma_stats(l2b, qt * 64, T, buf + 2 * IMG, lane);
+    else if (wave == 1) dma_stats(dlb, qt * 64, T, buf + 2 * IMG + 256, lane);
+  };
+  if (qt0 < nqt) issue(qt0, smem);
+  if (qt0 + 1 < nqt) issue(qt0 + 1, smem + STAGE);
+
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (kv) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)key * rs + 16 * s + 8 * h);
+      vf[s] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)key * rs + 16 * s + 8 * h);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[s][j] = vf[s][j] = (bf16)0.f;
+    }
+  }
+  f32x16 dk[2], dv[2];
+  dk[0] = dk[1] = dv[0] = dv[1] = zero16();
+  int qoff[4];  // lane-constant row-read offsets (Q and dO images share the layout)
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qoff[s] = r * 128 + (((2 * s + h) ^ swz(r)) << 4);
+  const TrBase tb = tr_base(lane);
+  wait_dma();
+  __syncthreads();
+
+  // mask: query q0 + 4h + c (c = qh*32 + 8g + j, an immediate) is dropped when
+  // c < key - q0 - 4h (causal) or c > T - 1 - q0 - 4h (tail). Lanes with key >= T
+  // compute on zero K/V and are never stored.
+  auto tile = [&](bool need_mask, const lds_t* qimg, unsigned qimg_u, int q0) {
+    typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+    const float* st = (const float*)(qimg + 2 * IMG);
+    const int lo_lim = causal ? key - q0 - 4 * h : -0x7fffffff;
+    const int hi_lim = T - 1 - q0 - 4 * h;
+    // one 32-query half at a time (S^T, dP^T live for 16 MFMAs only)
+    static_for<2>([&](auto qh_c) {
+      constexpr int qh = decltype(qh_c)::value;
+      f32x16 sacc = mfma32(*(lds_bf16x8*)(qimg + qoff[0] + qh * 4096), kf[0], zero16());
+      f32x16 dp = mfma32(*(lds_bf16x8*)(qimg + IMG + qoff[0] + qh * 4096), vf[0], zero16());
+#pragma unroll
+      for (int s = 1; s < 4; ++s) {
+        sacc = mfma32(*(lds_bf16x8*)(qimg + qoff[s] + qh * 4096), kf[s], sacc);
+        dp = mfma32(*(lds_bf16x8*)(qimg + IMG + qoff[s] + qh * 4096), vf[s], dp);
+      }
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int qi = qh * 32 + 8 * g + 4 * h;
+        const f32x4 l4 = *reinterpret_cast<const f32x4*>(st + qi);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(st + 64 + qi);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j;
+          float p = fexp2(__builtin_fmaf(sacc[i], scale_log2, -l4[j]));
+          if (need_mask) {
+            const int c = qh * 32 + 8 * g + j;
+            p = (c < lo_lim || c > hi_lim) ? 0.f : p;
+          }
+          sacc[i] = p;
+          dp[i] = p * (dp[i] - d4[j]);
+        }
+      }
+      static_for<2>([&](auto s_c) {
+        constexpr int s = decltype(s_c)::value;
+        TrFrag tv[2], tk[2];
+        tr_frag<qh * 32 + s * 16, 0>(tv[0], qimg_u + IMG, tb);
+        tr_frag<qh * 32 + s * 16, 1>(tv[1], qimg_u + IMG, tb);
+        tr_frag<qh * 32 + s * 16, 0>(tk[0], qimg_u, tb);
+        tr_frag<qh * 32 + s * 16, 1>(tk[1], qimg_u, tb);
+        tr_wait4(tv[0], tv[1], tk[0], tk[1]);
+        const bf16x8 pf = acc_frag(sacc, s), sf = acc_frag(dp, s);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = mfma32(tr_join(tv[d]), pf, dv[d]);
+          dk[d] = mfma32(tr_join(tk[d]), sf, dk[d]);
+        }
+      });
+    });
+  };
+
+  const unsigned smem_u = (unsigned)(size_t)smem;
+  for (int qt = qt0; qt < nqt; ++qt) {
+    const int q0 = qt * 64;
+    const int stg = (qt - qt0) % 3;
+    const bool ahead = qt + 2 < nqt;
+    if (ahead) issue(qt + 2, smem + ((qt + 2 - qt0) % 3) * STAGE);
+    if (!(causal && q0 + 63 < key0w) && key0w < T)  // wave-uniform
+      tile((causal && q0 < key0w + 31) || (q0 + 64 > T), smem + stg * STAGE, smem_u + stg * STAGE, q0);
+    if (wave < 2) wait_next<5>(ahead);  // waves 0 / 1 also DMA the lse2 / delta rows
+    else wait_next<4>(ahead);
+    __syncthreads();
+  }
+  if (kv) {
+    bf16* krow = dqkv + ((size_t)b * T + key) * rs + (size_t)(H + hh) * D;
+    bf16* vrow = krow + (size_t)H * D;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        bf16x4 a, c;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = (bf16)(dk[d][4 * g + j] * scale);
+          c[j] = (bf16)dv[d][4 * g + j];
+        }
+        *reinterpret_cast<bf16x4*>(krow + d * 32 + 8 * g + 4 * h) = a;
+        *reinterpret_cast<bf16x4*>(vrow + d * 32 + 8 * g + 4 * h) = c;
+      }
+  }
+}
+
+}  // namespace fa64
+
+void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int kv_rs, int group, bf16* out,
+                     float* lse, int B, int T, int H, int causal, hipStream_t st) {
+  // CAAMD_FA64_QS: 32-query sub-blocks per wave (2: 256-query blocks at 2 waves
+  // per SIMD; 1: 128-query blocks at 3 waves per SIMD)
+  static const int qs = [] {
+    const char* e = std::getenv("CAAMD_FA64_QS");
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  const float scale_log2 = 1.44269504089f / 8.f;
+  if (qs == 2) {
+    const int nqb = (T + 255) / 256;
+    hipLaunchKernelGGL(fa64::fwd_kernel<2>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs,
+                       kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
+  } else {
+    const int nqb = (T + 127) / 128;
+    hipLaunchKernelGGL(fa64::fwd_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs,
+                       kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
+  }
+}
+
+// ws: 2 * B * H * T floats (delta, then lse * log2 e)
+void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse, float* ws, bf16* dqkv,
+                     int B, int T, int H, int causal, hipStream_t st) {
+  const int nkb = (T + 127) / 128;
+  const float scale = 0.125f;
+  const float scale_log2 = 1.44269504089f * scale;
+  float* delta = ws;
+  float* lse2 = ws + (size_t)B * H * T;
+  static const int qs = [] {
+    const char* e = std::getenv("CAAMD_FA64_DQ_QS");
+    return (e && e[0] == '2') ? 2 : 1;
+  }();
+  if (qs == 2) {
+    const int nqb = (T + 255) / 256;
+    hipLaunchKernelGGL(fa64::bwd_dq_kernel<2>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout,
+                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal);
+  } else {
+    const int nqb = (T + 127) / 128;
+    hipLaunchKernelGGL(fa64::bwd_dq_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout,
+                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal);
+  }
+  hipLaunchKernelGGL(fa64::bwd_dkdv_kernel, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
+                     lse2, delta, dqkv, T, H, nkb, scale_log2, scale, causal);
+}
+
+}  // namespace caamd

@@ -227,3 +227,31 @@ def test_flash_attention_fwd_bwd(C, B, T, H, D, causal):
     if causal:
         s = s.masked_fill(~torch.ones(T, T, dtype=torch.bool, device="cuda").tril(), float("-inf"))
     assert torch.allclose(lse, torch.logsumexp(s, -1), atol=2e-2, rtol=1e-3)
+
+
+@pytest.mark.parametrize("B,T,H,causal,amp", [(2, 512, 2, True, 3.0), (1, 320, 3, False, 3.0), (1, 1024, 2, True, 6.0)])
+def test_flash_attention_d64_spiky(C, B, T, H, causal, amp):
+    """Large-magnitude scores, so the D = 64 forward's lazy softmax rescale (raise
+    the reference max only when it grows by > 8 in log2 units) fires on many tiles;
+    keys are scaled up along the sequence so later tiles keep raising the max."""
+    from cluster_anywhere_amd.ops.attention import attention_ref
+    from cluster_anywhere_amd.ops.flash import flash_attention_qkv
+
+    D = 64
+    torch.manual_seed(11)
+    x = torch.randn(B, T, 3, H, D, device="cuda")
+    ramp = torch.linspace(0.5, 2.0, T, device="cuda").view(1, T, 1, 1)
+    x[:, :, 1] = x[:, :, 1] * ramp + 0.5          # keys grow along the sequence
+    x[:, :, 0] = x[:, :, 0].abs() * amp / 2 + 0.5  # positive-leaning queries
+    qkv = x.reshape(B, T, 3 * H * D).bfloat16().requires_grad_()
+    out = flash_attention_qkv(qkv, H, causal)
+    dout = torch.randn_like(out)
+    out.backward(dout)
+    qf = qkv.detach().float().requires_grad_()
+    q, k, v = qf.view(B, T, 3, H, D).permute(2, 0, 3, 1, 4).unbind(0)
+    ref_o = attention_ref(q, k, v, causal).transpose(1, 2).reshape(B, T, H * D)
+    ref_o.backward(dout.float())
+    assert _rel(out, ref_o) < 2e-2, _rel(out, ref_o)
+    g, gr = qkv.grad.view(B, T, 3, H, D), qf.grad.view(B, T, 3, H, D)
+    for i, name in enumerate("qkv"):
+        assert _rel(g[:, :, i], gr[:, :, i]) < 4e-2, (name, _rel(g[:, :, i], gr[:, :, i]))
