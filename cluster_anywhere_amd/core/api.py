@@ -104,6 +104,13 @@ def is_initialized() -> bool:
     return context.worker is not None or context.local_mode
 
 
+def _gcs_storage(kwargs) -> Optional[str]:
+    """Durable GCS table log for head fault tolerance: ``init(_gcs_storage=path)``,
+    ``init(_system_config={"gcs_storage": path})`` or ``CAAMD_GCS_STORAGE``."""
+    sc = kwargs.get("_system_config") or {}
+    return kwargs.get("_gcs_storage") or sc.get("gcs_storage") or os.environ.get("CAAMD_GCS_STORAGE") or None
+
+
 def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
          num_gpus: Optional[int] = None, resources: Optional[Dict[str, float]] = None,
          object_store_memory: Optional[int] = None, local_mode: bool = False,
@@ -168,7 +175,8 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                 head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
                             namespace=namespace or "default",
                             worker_env=_worker_env_from(runtime_env),
-                            listen_tcp=kwargs.get("_listen_tcp"), labels=kwargs.get("labels"))
+                            listen_tcp=kwargs.get("_listen_tcp"), labels=kwargs.get("labels"),
+                            gcs_storage=_gcs_storage(kwargs))
                 head.start()
                 _head = head
                 address = head.sock_path
@@ -181,7 +189,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                     "store_name": store_name, "store_bytes": store_bytes, "gpus": gpus,
                     "namespace": namespace or "default", "worker_env": _worker_env_from(runtime_env),
                     "listen_tcp": kwargs.get("_listen_tcp"), "parent_pid": os.getpid(),
-                    "labels": kwargs.get("labels") or {},
+                    "labels": kwargs.get("labels") or {}, "gcs_storage": _gcs_storage(kwargs),
                     "sys_path": [p for p in sys.path if p and os.path.isdir(p)]})
                 address = info["unix"]
                 tcp = info.get("address")

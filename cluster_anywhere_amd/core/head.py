@@ -124,7 +124,8 @@ class Head:
                  store_name: str, store_capacity: int, gpu_ids: List[int],
                  listen_tcp: Optional[str] = None, namespace: str = "default",
                  worker_env: Optional[Dict[str, str]] = None, prestart: int = 0,
-                 spill_dir: Optional[str] = None, labels: Optional[Dict[str, str]] = None):
+                 spill_dir: Optional[str] = None, labels: Optional[Dict[str, str]] = None,
+                 gcs_storage: Optional[str] = None):
         from .. import _native
 
         self.session_dir = session_dir
@@ -238,6 +239,16 @@ class Head:
         self.mem_monitor = MemoryMonitor()
         self._last_mem = 0.0
         self._oom_quiet_until = 0.0
+        # durable GCS tables (head fault tolerance, core/gcs_persist.py)
+        gcs_storage = gcs_storage or os.environ.get("CAAMD_GCS_STORAGE") or None
+        self.gcs = None
+        self._gcs_actors: Set[bytes] = set()
+        self.gcs_restored = {}
+        if gcs_storage:
+            from .gcs_persist import GcsPersistence
+
+            os.makedirs(os.path.dirname(os.path.abspath(gcs_storage)), exist_ok=True)
+            self.gcs = GcsPersistence(gcs_storage)
 
     # ------------------------------------------------------------------ loop
     def start(self):
@@ -249,6 +260,8 @@ class Head:
                 self._zygote = zygote.Zygote(self.session_dir)
             except Exception:
                 self._zygote = None
+        if self.gcs is not None:
+            self._gcs_restore()
         self.thread = threading.Thread(target=self._loop, name="caamd-head", daemon=True)
         self.thread.start()
         for _ in range(self._prestart):
@@ -429,12 +442,17 @@ class Head:
                 self.idle[key].append(w)
                 self._schedule()
         elif kind == "driver":
-            self.jobs.setdefault(extra.get("job_id", b""), {"start": time.time(), "pid": pid,
-                                                             "driver": worker_id})
+            jid = extra.get("job_id", b"")
+            if jid not in self.jobs:
+                self.jobs[jid] = {"start": time.time(), "pid": pid, "driver": worker_id}
+                if self.gcs is not None:
+                    self.gcs.job_put(jid, self.jobs[jid])
 
     # ------------------------------------------------------------ functions/kv
     def _h_fn(self, c, fn_id, blob):
         self.functions[fn_id] = blob
+        if self.gcs is not None:
+            self.gcs.fn_put(fn_id, blob)
 
     def _h_kv(self, c, req, op, ns, key, value, overwrite):
         k = (ns, key)
@@ -442,6 +460,8 @@ class Head:
             existed = k in self.kv
             if overwrite or not existed:
                 self.kv[k] = value
+                if self.gcs is not None:
+                    self.gcs.kv_put(ns, key, value)
             self._reply(c, req, not existed)
         elif op == "get":
             self._reply(c, req, self.kv.get(k))
@@ -450,10 +470,15 @@ class Head:
                 n = 0
                 for kk in [kk for kk in self.kv if kk[0] == ns and kk[1].startswith(key[:-1])]:
                     del self.kv[kk]
+                    if self.gcs is not None:
+                        self.gcs.kv_del(*kk)
                     n += 1
                 self._reply(c, req, n)
             else:
-                self._reply(c, req, 1 if self.kv.pop(k, None) is not None else 0)
+                gone = self.kv.pop(k, None) is not None
+                if gone and self.gcs is not None:
+                    self.gcs.kv_del(ns, key)
+                self._reply(c, req, 1 if gone else 0)
         elif op == "exists":
             self._reply(c, req, k in self.kv)
         elif op == "keys":
@@ -1259,6 +1284,9 @@ class Head:
         self.actors[spec.actor_id] = a
         if a.name:
             self.named_actors[(a.namespace, a.name)] = spec.actor_id
+        if self.gcs is not None and a.lifetime == "detached" and spec.actor_id not in self._gcs_actors:
+            if self.gcs.actor_put(spec):
+                self._gcs_actors.add(spec.actor_id)
         # the creator's handle: an always-READY object whose refcount = live handles
         hid = spec.actor_id + b"\xac" * 8
         he = self._obj(hid)
@@ -1652,7 +1680,44 @@ class Head:
         # let the kernel reclaim the victim's memory before judging again
         self._oom_quiet_until = now + max(1.0, 4 * self.mem_monitor.refresh_s)
 
+    def _gcs_reconcile(self):
+        """Drop persisted detached actors that are now permanently dead (not while the
+        head is going down: its own shutdown kills every worker)."""
+        if not self.running:
+            return
+        for aid in list(self._gcs_actors):
+            a = self.actors.get(aid)
+            if a is None or a.state == "DEAD":
+                self._gcs_actors.discard(aid)
+                self.gcs.actor_del(aid)
+
+    def _gcs_restore(self):
+        """Reload the durable tables written by a previous head with the same storage
+        (reference: GcsInitData::AsyncLoad + GcsActorManager / GcsPlacementGroupManager
+        Initialize on GCS restart)."""
+        data = self.gcs.load()
+        self.kv.update(data["kv"])
+        self.functions.update(data["fn"])
+        for jid, info in data["job"].items():
+            self.jobs.setdefault(jid, dict(info, restored=True))
+        for pg_id, pg in data["pg"].items():
+            self._h_pg_create(None, pg_id, pg["bundles"], pg["strategy"], pg["name"],
+                              pg_id + b"\xb7" * 4, pg["lifetime"])
+        n_actors = 0
+        for aid, fields in data["actor"].items():
+            spec = TaskSpec(**fields)
+            spec.task_id = os.urandom(16)
+            spec.attempt = 0
+            spec.return_ids = [os.urandom(len(r)) for r in (fields.get("return_ids") or [])]
+            self._gcs_actors.add(aid)  # already persisted: keep the record, do not rewrite it
+            self._h_submit(None, spec)
+            n_actors += 1
+        self.gcs_restored = {"kv": len(data["kv"]), "functions": len(data["fn"]), "jobs": len(data["job"]),
+                             "placement_groups": len(data["pg"]), "actors": n_actors}
+
     def _health_check(self):
+        if self.gcs is not None and self._gcs_actors:
+            self._gcs_reconcile()
         for w in list(self.workers.values()):
             if w.proc is not None and w.proc.poll() is not None and not w.alive and w.conn is None:
                 # died before registering
@@ -1735,6 +1800,8 @@ class Head:
                            "nodes": None, "ready_oid": ready_oid, "code": codes[strategy],
                            "lifetime": lifetime}
         self._obj(ready_oid).refcount += 1
+        if self.gcs is not None and lifetime == "detached":
+            self.gcs.pg_put(pg_id, bundles, strategy, name, lifetime)
         if not self.sched.pg_feasible(bundles, codes[strategy]):
             self.pgs[pg_id]["state"] = "INFEASIBLE"
         self.pending_pgs.append(pg_id)
@@ -1761,6 +1828,8 @@ class Head:
         pg = self.pgs.pop(pg_id, None)
         if pg is None:
             return
+        if self.gcs is not None and pg.get("lifetime") == "detached":
+            self.gcs.pg_del(pg_id)
         if pg_id in self.pending_pgs:
             self.pending_pgs.remove(pg_id)
         # actors placed in the group die with it (reference: ActorPlacementGroupRemoved)

@@ -32,7 +32,7 @@ def embedded(cfg_json: str):
     head = Head(cfg["session_dir"], bytes.fromhex(cfg["node_id"]), cfg["resources"], cfg["store_name"],
                 int(cfg["store_bytes"]), cfg["gpus"], namespace=cfg.get("namespace") or "default",
                 worker_env=cfg.get("worker_env") or {}, listen_tcp=cfg.get("listen_tcp"),
-                labels=cfg.get("labels"))
+                labels=cfg.get("labels"), gcs_storage=cfg.get("gcs_storage"))
     head.start()
     print(json.dumps({"pid": os.getpid(), "unix": head.sock_path, "address": head.tcp_address,
                       "session_dir": head.session_dir, "node_id": head.head_hex}), flush=True)
@@ -60,6 +60,9 @@ def main(argv=None):
     ap.add_argument("--include-dashboard", default="true")
     ap.add_argument("--temp-dir", default=None)
     ap.add_argument("--labels", default="{}", help="node labels (JSON)")
+    ap.add_argument("--gcs-storage", default=None,
+                    help="durable GCS table log (head fault tolerance): a head restarted with the same "
+                         "path restores the KV, function table, jobs, detached actors and placement groups")
     a = ap.parse_args(argv)
 
     from .api import _default_cpus, _default_store_bytes, _mem_bytes, detect_gpus
@@ -79,7 +82,7 @@ def main(argv=None):
     res.update({k: float(v) for k, v in json.loads(a.resources).items()})
     store_name = f"/caamd_{os.getpid()}_{uuid.uuid4().hex[:8]}"
     head = Head(session_dir, os.urandom(16), res, store_name, store_bytes, gpus,
-                listen_tcp=f"{a.host}:{a.port}", labels=json.loads(a.labels))
+                listen_tcp=f"{a.host}:{a.port}", labels=json.loads(a.labels), gcs_storage=a.gcs_storage)
     head.start()
     url = None
     if a.include_dashboard.lower() in ("1", "true", "yes"):

@@ -54,6 +54,8 @@ def cmd_start(a):
                 "--include-dashboard", a.include_dashboard, "--resources", a.resources]
         if a.temp_dir:
             argv += ["--temp-dir", a.temp_dir]
+        if a.gcs_storage:
+            argv += ["--gcs-storage", a.gcs_storage]
     elif a.address:
         argv = [sys.executable, "-m", "cluster_anywhere_amd.core.node_agent", "--address", a.address,
                 "--resources", a.resources, "--node-ip-address", a.node_ip_address]
@@ -337,6 +339,8 @@ def main(argv=None):
     s.add_argument("--dashboard-port", type=int, default=8265)
     s.add_argument("--include-dashboard", default="true")
     s.add_argument("--temp-dir", default=None)
+    s.add_argument("--gcs-storage", default=None,
+                   help="head fault tolerance: durable GCS table log reloaded by a head restarted on it")
     s.add_argument("--block", action="store_true")
     s.set_defaults(fn=cmd_start)
     s = sub.add_parser("stop")

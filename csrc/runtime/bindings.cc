@@ -1,10 +1,11 @@
 // pybind11 bindings of the native runtime: object store, cluster scheduler,
-// compiled-graph shm channels.
+// compiled-graph shm channels, durable GCS table store.
 #include <tuple>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include "channel.h"
+#include "gcs_store.h"
 #include "object_store.h"
 #include "scheduler.h"
 
@@ -177,4 +178,41 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("write_seq", &Channel::write_seq)
       .def("read_seq", &Channel::read_seq)
       .def_property_readonly("name", &Channel::name);
+
+  py::class_<GcsStore>(m, "GcsStore")
+      .def(py::init<const std::string&, bool>(), py::arg("path"), py::arg("fsync_each") = false)
+      .def("put",
+           [](GcsStore& s, const std::string& t, py::bytes k, py::bytes v) {
+             std::string ks(k), vs(v);
+             py::gil_scoped_release g;
+             s.put(t, ks, vs);
+           })
+      .def("delete", [](GcsStore& s, const std::string& t, py::bytes k) { return s.del(t, std::string(k)); })
+      .def("get",
+           [](GcsStore& s, const std::string& t, py::bytes k) -> py::object {
+             std::string v;
+             if (!s.get(t, std::string(k), &v)) return py::none();
+             return py::bytes(v);
+           })
+      .def("keys",
+           [](GcsStore& s, const std::string& t) {
+             py::list out;
+             for (auto& k : s.keys(t)) out.append(py::bytes(k));
+             return out;
+           })
+      .def("items",
+           [](GcsStore& s, const std::string& t) {
+             py::list out;
+             for (auto& kv : s.items(t)) out.append(py::make_tuple(py::bytes(kv.first), py::bytes(kv.second)));
+             return out;
+           })
+      .def("tables", &GcsStore::tables)
+      .def("clear_table", &GcsStore::clear_table)
+      .def("sync", &GcsStore::sync)
+      .def("compact", &GcsStore::compact)
+      .def_property_readonly("log_bytes", &GcsStore::log_bytes)
+      .def_property_readonly("live_bytes", &GcsStore::live_bytes)
+      .def_property_readonly("records_replayed", &GcsStore::records_replayed)
+      .def_property_readonly("torn_bytes_dropped", &GcsStore::torn_bytes_dropped)
+      .def_property_readonly("path", &GcsStore::path);
 }

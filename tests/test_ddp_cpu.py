@@ -52,7 +52,9 @@ def _worker(rank, world, port, zero, bucket_mb, q):
                 grads = st.flat.grad_buffer.clone() / world
     st.wait_params()  # ZeRO-1 defers the weight all-gather into the next forward
     if rank == 0:
-        q.put((st.flat.param_buffer.clone(), grads))
+        # numpy arrays pickle by value: torch tensors would go through a shared-memory
+        # fd that vanishes if this process exits before the parent has received it
+        q.put((st.flat.param_buffer.clone().numpy(), grads.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -81,7 +83,7 @@ def test_dp_matches_single_process(zero, bucket_mb):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, zero, bucket_mb, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got, got_g = q.get(timeout=240)
+    got, got_g = (torch.from_numpy(a) for a in q.get(timeout=240))
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
