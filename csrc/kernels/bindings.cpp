@@ -463,7 +463,7 @@ void rope_cache_(Tensor& qkv, const Tensor& cos_sin, const Tensor& positions, co
   const int N = (int)positions.numel();
   TORCH_CHECK(qkv.numel() % ((int64_t)N * (H + 2 * KVH)) == 0, "rope_cache: qkv shape");
   const int D = (int)(qkv.numel() / ((int64_t)N * (H + 2 * KVH)));
-  TORCH_CHECK(D % 2 == 0 && cos_sin.size(-2) == D / 2 && cos_sin.size(-1) == 2, "rope_cache: cos_sin must be [P, D/2, 2]");
+  TORCH_CHECK(D % 16 == 0 && cos_sin.size(-2) == D / 2 && cos_sin.size(-1) == 2, "rope_cache: head dim must be a multiple of 16 and cos_sin [P, D/2, 2]");
   caamd::bf16 *kc = nullptr, *vc = nullptr;
   const int* sl = nullptr;
   int BS = 1;

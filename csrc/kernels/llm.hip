@@ -70,8 +70,69 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x
   }
 }
 
+// Few rows (decode: one row per sequence, 1..256 rows): the one-wave-per-row
+// grid above would put only rows/4 blocks on 256 CUs, each wave walking a
+// 4096-wide row serially. Here a 256-thread block owns a row (16 elements per
+// thread at D = 4096), the weight load is issued before the reduction, and the
+// four wave partial sums meet in LDS.
+template <int NV, bool HAS_RES>
+__global__ __launch_bounds__(256) void rmsnorm_row_kernel(const bf16* __restrict__ x, const bf16* __restrict__ r,
+                                                          bf16* __restrict__ s_out, const bf16* __restrict__ w,
+                                                          bf16* __restrict__ y, int D, float eps) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, t = threadIdx.x;
+  const int nchunk = D >> 3;
+  const size_t base = (size_t)row * D;
+  float v[NV][8], ww[NV][8];
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int ch = t + c * 256;
+    if (ch < nchunk) {
+      load8(x + base + ch * 8, v[c]);
+      load8(w + ch * 8, ww[c]);
+      if (HAS_RES) {
+        float tr[8];
+        load8(r + base + ch * 8, tr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] += tr[j];
+        store8(s_out + base + ch * 8, v[c]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (float)(bf16)v[c][j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sq += v[c][j] * v[c][j];
+    }
+  }
+  sq = wave_sum(sq);
+  if ((t & 63) == 0) red[t >> 6] = sq;
+  __syncthreads();
+  const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int ch = t + c * 256;
+    if (ch < nchunk) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[c][j] * rs * ww[c][j];
+      store8(y + base + ch * 8, o);
+    }
+  }
+}
+
 void rmsnorm_launch(const bf16* x, const bf16* r, bf16* s_out, const bf16* w, bf16* y, int rows, int D,
                     float eps, hipStream_t st) {
+  if (rows < 1024 && D <= 8 * 256 * 4) {
+    const int nv = (D / 8 + 255) / 256;
+#define RMS_ROW(N)                                                                                        \
+  if (nv <= N) {                                                                                         \
+    if (r) hipLaunchKernelGGL((rmsnorm_row_kernel<N, true>), dim3(rows), dim3(256), 0, st, x, r, s_out, w, y, D, eps); \
+    else hipLaunchKernelGGL((rmsnorm_row_kernel<N, false>), dim3(rows), dim3(256), 0, st, x, r, s_out, w, y, D, eps); \
+    return;                                                                                              \
+  }
+    RMS_ROW(1) RMS_ROW(2) RMS_ROW(4)
+#undef RMS_ROW
+  }
   dim3 grid((rows + 3) / 4), block(256);
   const int nv = (D / 8 + 63) / 64;
 #define RMS_CASE(N)                                                                                       \
@@ -87,46 +148,60 @@ void rmsnorm_launch(const bf16* x, const bf16* r, bf16* s_out, const bf16* w, bf
 // ---------------------------------------------------------------- SwiGLU
 __global__ __launch_bounds__(256) void silu_mul_kernel(const bf16* __restrict__ gu, bf16* __restrict__ out,
                                                        int rows, int F) {
-  const int64_t nvec = (int64_t)rows * (F / 8);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = i / (F / 8), c = (i % (F / 8)) * 8;
-    float g[8], u[8], o[8];
-    load8(gu + row * 2 * F + c, g);
-    load8(gu + row * 2 * F + F + c, u);
+  // grid (column-chunk blocks, rows): no 64-bit index division per element
+  const int row = blockIdx.y;
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= F) return;
+  const bf16* g_row = gu + (size_t)row * 2 * F;
+  float g[8], u[8], o[8];
+  load8(g_row + c, g);
+  load8(g_row + F + c, u);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
-    store8(out + row * F + c, o);
-  }
+  for (int j = 0; j < 8; ++j) o[j] = __fdividef(g[j], 1.f + __expf(-g[j])) * u[j];
+  store8(out + (size_t)row * F + c, o);
 }
 
 void silu_mul_launch(const bf16* gu, bf16* out, int rows, int F, hipStream_t st) {
-  const int64_t nvec = (int64_t)rows * (F / 8);
-  hipLaunchKernelGGL(silu_mul_kernel, dim3(ew_grid(nvec, 256)), dim3(256), 0, st, gu, out, rows, F);
+  for (int r0 = 0; r0 < rows; r0 += 65535) {  // gridDim.y limit
+    const int n = rows - r0 < 65535 ? rows - r0 : 65535;
+    hipLaunchKernelGGL(silu_mul_kernel, dim3((F / 8 + 255) / 256, n), dim3(256), 0, st, gu + (size_t)r0 * 2 * F,
+                       out + (size_t)r0 * F, n, F);
+  }
 }
 
 // ---------------------------------------------------------------- RoPE + cache append
 // qkv: [N, (H + 2*KVH) * D]; cos_sin: [max_pos, D/2, 2] fp32; positions/slots: [N]
+// One thread per (token, head, 8 consecutive rotary pairs): 16-byte loads of both
+// halves, 8 cos/sin pairs, 16-byte stores to qkv and to the paged cache page.
 __global__ __launch_bounds__(256) void rope_cache_kernel(bf16* __restrict__ qkv, const float* __restrict__ cs,
                                                          const int* __restrict__ pos, const int* __restrict__ slot,
                                                          bf16* __restrict__ kc, bf16* __restrict__ vc, int N,
                                                          int H, int KVH, int D, int BS) {
-  const int half = D / 2;
+  const int half = D / 2, ng = half / 8;
   const int heads = H + 2 * KVH;
-  const int64_t total = (int64_t)N * heads * half;
+  const int64_t total = (int64_t)N * heads * ng;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int p = (int)(i % half);
-    const int64_t th = i / half;
+    const int p = (int)(i % ng) * 8;
+    const int64_t th = i / ng;
     const int hd = (int)(th % heads);
     const int t = (int)(th / heads);
     bf16* row = qkv + (size_t)t * heads * D + (size_t)hd * D;
-    float a = (float)row[p], b = (float)row[p + half];
+    float a[8], b[8];
+    load8(row + p, a);
+    load8(row + p + half, b);
     if (hd < H + KVH) {  // q or k: rotate
-      const float2 c = reinterpret_cast<const float2*>(cs)[(size_t)pos[t] * half + p];
-      const float ra = a * c.x - b * c.y, rb = b * c.x + a * c.y;
-      a = ra;
-      b = rb;
-      row[p] = (bf16)a;
-      row[p + half] = (bf16)b;
+      const float4* c4 = reinterpret_cast<const float4*>(cs + ((size_t)pos[t] * half + p) * 2);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 c = c4[j];  // (cos, sin) of pairs p + 2j, p + 2j + 1
+        const float a0 = a[2 * j], b0 = b[2 * j], a1 = a[2 * j + 1], b1 = b[2 * j + 1];
+        a[2 * j] = a0 * c.x - b0 * c.y;
+        b[2 * j] = b0 * c.x + a0 * c.y;
+        a[2 * j + 1] = a1 * c.z - b1 * c.w;
+        b[2 * j + 1] = b1 * c.z + a1 * c.w;
+      }
+      store8(row + p, a);
+      store8(row + p + half, b);
     }
     if (hd >= H && kc != nullptr) {
       const int s = slot[t];
@@ -134,8 +209,8 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(bf16* __restrict__ qkv,
         const int blk = s / BS, off = s % BS;
         const int kvh = hd < H + KVH ? hd - H : hd - H - KVH;
         bf16* dst = (hd < H + KVH ? kc : vc) + (((size_t)blk * KVH + kvh) * BS + off) * D;
-        dst[p] = (bf16)a;
-        dst[p + half] = (bf16)b;
+        store8(dst + p, a);
+        store8(dst + p + half, b);
       }
     }
   }
@@ -143,7 +218,7 @@ __global__ __launch_bounds__(256) void rope_cache_kernel(bf16* __restrict__ qkv,
 
 void rope_cache_launch(bf16* qkv, const float* cs, const int* pos, const int* slot, bf16* kc, bf16* vc, int N,
                        int H, int KVH, int D, int BS, hipStream_t st) {
-  const int64_t total = (int64_t)N * (H + 2 * KVH) * (D / 2);
+  const int64_t total = (int64_t)N * (H + 2 * KVH) * (D / 16);
   hipLaunchKernelGGL(rope_cache_kernel, dim3(ew_grid(total, 256)), dim3(256), 0, st, qkv, cs, pos, slot, kc, vc,
                      N, H, KVH, D, BS);
 }
