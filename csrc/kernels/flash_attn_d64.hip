@@ -94,17 +94,18 @@ __device__ __forceinline__ int swz(int row) {
 // 64-row tile rows [row0, row0 + 64) of g (row stride rs elements, 64 bf16 per
 // row) -> swizzled LDS image; 256 threads, two 1-KiB DMA pieces per wave. Rows
 // past T are clamped to T - 1 (finite data; masked by the caller).
+template <int NT = 256>
 __device__ __forceinline__ void dma_tile(const bf16* __restrict__ g, size_t rs, int row0, int T,
                                          lds_t* dst, int wave, int lane) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int lin = j * 256 + wave * 64 + lane;
+  for (int j = 0; j < 512 / NT; ++j) {
+    const int lin = j * NT + wave * 64 + lane;
     const int row = lin >> 3, pos = lin & 7;
     const int c = pos ^ swz(row);
     const int gr = min(row0 + row, T - 1);
     const bf16* src = g + (size_t)gr * rs + c * 8;
     __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (void __attribute__((address_space(3)))*)(dst + (j * 256 + wave * 64) * 16),
+                                     (void __attribute__((address_space(3)))*)(dst + (j * NT + wave * 64) * 16),
                                      16, 0, 0);
   }
 }
@@ -225,8 +226,11 @@ __device__ __forceinline__ int xcd_remap(int id, int n) {
 // forward: 4 waves x 64 queries (two 32-query sub-blocks) per block, 64-key tiles
 // double-buffered in LDS ({K image, V image} per stage, three stages, DMA two tiles ahead).
 // ----------------------------------------------------------------------------
-template <int QS>
-__global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void fwd_kernel(const bf16* __restrict__ qp, const bf16* __restrict__ kp,
+// ABL (timing ablations, tools/bench_attn.py with CAAMD_FA64_ABL; production 0):
+// bit 0 no DMA inside the loop (stale tiles), bit 1 no per-tile wait + barrier,
+// bit 2 no exp (p = s), bit 3 no tile compute at all.
+template <int QS, int ABL = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_kernel(const bf16* __restrict__ qp, const bf16* __restrict__ kp,
                                                      const bf16* __restrict__ vp, int q_rs, int kv_rs, int group,
                                                      bf16* __restrict__ out, float* __restrict__ lse, int T,
                                                      int H, int nqb, float scale_log2, int causal) {
@@ -243,16 +247,17 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void fwd_kernel(const bf16* _
   const bf16* qbase = qp + (size_t)b * T * rs + (size_t)hh * D;
   const bf16* kbase = kp + (size_t)b * T * krs + (size_t)(hh / group) * D;
   const bf16* vbase = vp + (size_t)b * T * krs + (size_t)(hh / group) * D;
-  constexpr int QBLK = 128 * QS;  // queries per block (4 waves x QS x 32)
+  constexpr int NT = 64 * NW, QBLK = 32 * QS * NW;  // queries per block (NW waves x QS x 32)
+  constexpr int DMA_N = 2 * (512 / NT);  // DMA pieces per wave per tile (K + V)
   const int q0w = qb * QBLK + wave * 32 * QS;
 
   const int qend = min(T, qb * QBLK + QBLK);
   const int nkt = causal ? (qend + 63) / 64 : (T + 63) / 64;
-  dma_tile(kbase, krs, 0, T, smem, wave, lane);
-  dma_tile(vbase, krs, 0, T, smem + IMG, wave, lane);
+  dma_tile<NT>(kbase, krs, 0, T, smem, wave, lane);
+  dma_tile<NT>(vbase, krs, 0, T, smem + IMG, wave, lane);
   if (nkt > 1) {
-    dma_tile(kbase, krs, 64, T, smem + STAGE, wave, lane);
-    dma_tile(vbase, krs, 64, T, smem + STAGE + IMG, wave, lane);
+    dma_tile<NT>(kbase, krs, 64, T, smem + STAGE, wave, lane);
+    dma_tile<NT>(vbase, krs, 64, T, smem + STAGE + IMG, wave, lane);
   }
 
   // lane-constant LDS offsets: K row reads (k-step s) and V transposed reads
@@ -288,32 +293,27 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void fwd_kernel(const bf16* _
   auto tile = [&](bool need_mask, const lds_t* kimg, unsigned vimg, int k0) {
     typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
     f32x16 sacc[QS][2];
-    // all eight K fragments of the tile in flight at once (one LDS latency)
-    bf16x8 kf[2][4];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) kf[kb][s] = *(lds_bf16x8*)(kimg + koff[s] + kb * 4096);
-    __builtin_amdgcn_sched_barrier(0);  // keep the reads batched (counted lgkmcnt per use)
+    // the four K fragments of each 32-key half in flight at once (one LDS latency)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 kf[4];
 #pragma unroll
-      for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[kb][0], qf[qs][0], zero16());
+      for (int s = 0; s < 4; ++s) kf[s] = *(lds_bf16x8*)(kimg + koff[s] + kb * 4096);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[0], qf[qs][0], zero16());
 #pragma unroll
       for (int s = 1; s < 4; ++s)
 #pragma unroll
-        for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[kb][s], qf[qs][s], sacc[qs][kb]);
+        for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[s], qf[qs][s], sacc[qs][kb]);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // V^T fragments requested now, consumed after the softmax (latency hidden)
-    __builtin_amdgcn_sched_barrier(0);
-    TrFrag vt[2][2][2];
-    static_for<2>([&](auto kb_c) {
-      constexpr int kb = decltype(kb_c)::value;
-      static_for<2>([&](auto s_c) {
-        constexpr int s = decltype(s_c)::value;
-        tr_frag<kb * 32 + s * 16, 0>(vt[kb][s][0], vimg, vtb);
-        tr_frag<kb * 32 + s * 16, 1>(vt[kb][s][1], vimg, vtb);
-      });
+    // V^T fragments of the first key half requested now, consumed after the softmax
+    TrFrag vt[2][2];
+    static_for<2>([&](auto s_c) {
+      constexpr int s = decltype(s_c)::value;
+      tr_frag<s * 16, 0>(vt[s][0], vimg, vtb);
+      tr_frag<s * 16, 1>(vt[s][1], vimg, vtb);
     });
 #pragma unroll
     for (int qs = 0; qs < QS; ++qs) {
@@ -352,17 +352,29 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void fwd_kernel(const bf16* _
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = fexp2(__builtin_fmaf(sacc[qs][kb][i], scale_log2, -muse));
+          const float p = (ABL & 4) ? __builtin_fmaf(sacc[qs][kb][i], scale_log2, -muse)
+                                    : fexp2(__builtin_fmaf(sacc[qs][kb][i], scale_log2, -muse));
           sacc[qs][kb][i] = p;
           rs4[i & 3] += p;
         }
       l[qs] += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);  // this lane's key half only
     }
     // O^T += V^T P^T ; each V^T fragment feeds both query sub-blocks
-    tr_wait4(vt[0][0][0], vt[0][0][1], vt[0][1][0], vt[0][1][1]);
-    tr_wait4(vt[1][0][0], vt[1][0][1], vt[1][1][0], vt[1][1][1]);
+    static_for<2>([&](auto kb_c) {
+      constexpr int kb = decltype(kb_c)::value;
+      tr_wait4(vt[0][0], vt[0][1], vt[1][0], vt[1][1]);
+      TrFrag cur[2][2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) cur[s][d] = vt[s][d];
+      if constexpr (kb == 0) {  // second key half's V^T under this half's MFMAs
+        static_for<2>([&](auto s_c) {
+          constexpr int s = decltype(s_c)::value;
+          tr_frag<32 + s * 16, 0>(vt[s][0], vimg, vtb);
+          tr_frag<32 + s * 16, 1>(vt[s][1], vimg, vtb);
+        });
+      }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         bf16x8 pf[QS];
@@ -370,11 +382,12 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void fwd_kernel(const bf16* _
         for (int qs = 0; qs < QS; ++qs) pf[qs] = acc_frag(sacc[qs][kb], s);
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-          const bf16x8 vf = tr_join(vt[kb][s][d]);
+          const bf16x8 vf = tr_join(cur[s][d]);
 #pragma unroll
           for (int qs = 0; qs < QS; ++qs) o[qs][d] = mfma32(vf, pf[qs], o[qs][d]);
         }
       }
+    });
   };
 
   const unsigned smem_u = (unsigned)(size_t)smem;
@@ -383,18 +396,20 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void fwd_kernel(const bf16* _
     const int st = kt % 3;
     const lds_t* kimg = smem + st * STAGE;
     const unsigned vimg = smem_u + st * STAGE + IMG;
-    const bool ahead = kt + 2 < nkt;
+    const bool ahead = kt + 2 < nkt && !(ABL & 1);
     if (ahead) {
       lds_t* nb = smem + ((kt + 2) % 3) * STAGE;
-      dma_tile(kbase, krs, k0 + 128, T, nb, wave, lane);
-      dma_tile(vbase, krs, k0 + 128, T, nb + IMG, wave, lane);
+      dma_tile<NT>(kbase, krs, k0 + 128, T, nb, wave, lane);
+      dma_tile<NT>(vbase, krs, k0 + 128, T, nb + IMG, wave, lane);
     }
-    const bool active = !(causal && k0 > q0w + 32 * QS - 1) && q0w < T;  // wave-uniform
+    const bool active = !(causal && k0 > q0w + 32 * QS - 1) && q0w < T && !(ABL & 8);  // wave-uniform
     if (active) {
       tile((causal && k0 + 63 > q0w) || (k0 + 64 > T), kimg, vimg, k0);
     }
-    wait_next<4>(ahead);
-    __syncthreads();
+    if constexpr (!(ABL & 2)) {
+      wait_next<DMA_N>(ahead);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int qs = 0; qs < QS; ++qs) {
@@ -493,25 +508,34 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
     static_for<2>([&](auto kb_c) {
       constexpr int kb = decltype(kb_c)::value;
       f32x16 sacc[QS], dp[QS];
-      {
-        const bf16x8 kf = *(lds_bf16x8*)(kimg + koff[0] + kb * 4096);
-        const bf16x8 vf = *(lds_bf16x8*)(kimg + IMG + koff[0] + kb * 4096);
+      // the 32-key half's eight row fragments in flight at once
+      bf16x8 kr[4], vr[4];
 #pragma unroll
-        for (int qs = 0; qs < QS; ++qs) {
-          sacc[qs] = mfma32(kf, qf[qs][0], zero16());
-          dp[qs] = mfma32(vf, df[qs][0], zero16());
-        }
+      for (int s = 0; s < 4; ++s) {
+        kr[s] = *(lds_bf16x8*)(kimg + koff[s] + kb * 4096);
+        vr[s] = *(lds_bf16x8*)(kimg + IMG + koff[s] + kb * 4096);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int qs = 0; qs < QS; ++qs) {
+        sacc[qs] = mfma32(kr[0], qf[qs][0], zero16());
+        dp[qs] = mfma32(vr[0], df[qs][0], zero16());
       }
 #pragma unroll
-      for (int s = 1; s < 4; ++s) {
-        const bf16x8 kf = *(lds_bf16x8*)(kimg + koff[s] + kb * 4096);
-        const bf16x8 vf = *(lds_bf16x8*)(kimg + IMG + koff[s] + kb * 4096);
+      for (int s = 1; s < 4; ++s)
 #pragma unroll
         for (int qs = 0; qs < QS; ++qs) {
-          sacc[qs] = mfma32(kf, qf[qs][s], sacc[qs]);
-          dp[qs] = mfma32(vf, df[qs][s], dp[qs]);
+          sacc[qs] = mfma32(kr[s], qf[qs][s], sacc[qs]);
+          dp[qs] = mfma32(vr[s], df[qs][s], dp[qs]);
         }
-      }
+      // K^T fragments for dQ requested now, consumed after the VALU pass
+      __builtin_amdgcn_sched_barrier(0);
+      TrFrag t[2][2];
+      static_for<2>([&](auto s_c) {
+        constexpr int s = decltype(s_c)::value;
+        tr_frag<kb * 32 + s * 16, 0>(t[s][0], kimg_u, ktb);
+        tr_frag<kb * 32 + s * 16, 1>(t[s][1], kimg_u, ktb);
+      });
 #pragma unroll
       for (int qs = 0; qs < QS; ++qs) {
 #pragma unroll
@@ -526,22 +550,19 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
         for (int i = 0; i < 16; ++i) sacc[qs][i] *= dp[qs][i] - dlt[qs];  // dS^T
       }
       // dQ^T += K^T dS^T
-      static_for<2>([&](auto s_c) {
-        constexpr int s = decltype(s_c)::value;
-        TrFrag t[2];
-        tr_frag<kb * 32 + s * 16, 0>(t[0], kimg_u, ktb);
-        tr_frag<kb * 32 + s * 16, 1>(t[1], kimg_u, ktb);
-        tr_wait2(t[0], t[1]);
+      tr_wait4(t[0][0], t[0][1], t[1][0], t[1][1]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
         bf16x8 f[QS];
 #pragma unroll
         for (int qs = 0; qs < QS; ++qs) f[qs] = acc_frag(sacc[qs], s);
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-          const bf16x8 a = tr_join(t[d]);
+          const bf16x8 a = tr_join(t[s][d]);
 #pragma unroll
           for (int qs = 0; qs < QS; ++qs) dq[qs][d] = mfma32(a, f[qs], dq[qs][d]);
         }
-      });
+      }
     });
   };
 
@@ -651,13 +672,31 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
     // one 32-query half at a time (S^T, dP^T live for 16 MFMAs only)
     static_for<2>([&](auto qh_c) {
       constexpr int qh = decltype(qh_c)::value;
-      f32x16 sacc = mfma32(*(lds_bf16x8*)(qimg + qoff[0] + qh * 4096), kf[0], zero16());
-      f32x16 dp = mfma32(*(lds_bf16x8*)(qimg + IMG + qoff[0] + qh * 4096), vf[0], zero16());
+      // the half's eight row fragments in flight at once (one LDS latency)
+      bf16x8 qr[4], dr[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        qr[s] = *(lds_bf16x8*)(qimg + qoff[s] + qh * 4096);
+        dr[s] = *(lds_bf16x8*)(qimg + IMG + qoff[s] + qh * 4096);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 sacc = mfma32(qr[0], kf[0], zero16());
+      f32x16 dp = mfma32(dr[0], vf[0], zero16());
 #pragma unroll
       for (int s = 1; s < 4; ++s) {
-        sacc = mfma32(*(lds_bf16x8*)(qimg + qoff[s] + qh * 4096), kf[s], sacc);
-        dp = mfma32(*(lds_bf16x8*)(qimg + IMG + qoff[s] + qh * 4096), vf[s], dp);
+        sacc = mfma32(qr[s], kf[s], sacc);
+        dp = mfma32(dr[s], vf[s], dp);
       }
+      // transposed dO / Q fragments requested now, consumed after the VALU pass
+      __builtin_amdgcn_sched_barrier(0);
+      TrFrag tv[2][2], tk[2][2];
+      static_for<2>([&](auto s_c) {
+        constexpr int s = decltype(s_c)::value;
+        tr_frag<qh * 32 + s * 16, 0>(tv[s][0], qimg_u + IMG, tb);
+        tr_frag<qh * 32 + s * 16, 1>(tv[s][1], qimg_u + IMG, tb);
+        tr_frag<qh * 32 + s * 16, 0>(tk[s][0], qimg_u, tb);
+        tr_frag<qh * 32 + s * 16, 1>(tk[s][1], qimg_u, tb);
+      });
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int qi = qh * 32 + 8 * g + 4 * h;
@@ -675,21 +714,17 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
           dp[i] = p * (dp[i] - d4[j]);
         }
       }
-      static_for<2>([&](auto s_c) {
-        constexpr int s = decltype(s_c)::value;
-        TrFrag tv[2], tk[2];
-        tr_frag<qh * 32 + s * 16, 0>(tv[0], qimg_u + IMG, tb);
-        tr_frag<qh * 32 + s * 16, 1>(tv[1], qimg_u + IMG, tb);
-        tr_frag<qh * 32 + s * 16, 0>(tk[0], qimg_u, tb);
-        tr_frag<qh * 32 + s * 16, 1>(tk[1], qimg_u, tb);
-        tr_wait4(tv[0], tv[1], tk[0], tk[1]);
+      tr_wait4(tv[0][0], tv[0][1], tk[0][0], tk[0][1]);
+      tr_wait4(tv[1][0], tv[1][1], tk[1][0], tk[1][1]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
         const bf16x8 pf = acc_frag(sacc, s), sf = acc_frag(dp, s);
 #pragma unroll
         for (int d = 0; d < 2; ++d) {
-          dv[d] = mfma32(tr_join(tv[d]), pf, dv[d]);
-          dk[d] = mfma32(tr_join(tk[d]), sf, dk[d]);
+          dv[d] = mfma32(tr_join(tv[s][d]), pf, dv[d]);
+          dk[d] = mfma32(tr_join(tk[s][d]), sf, dk[d]);
         }
-      });
+      }
     });
   };
 
@@ -740,8 +775,34 @@ void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int 
     hipLaunchKernelGGL(fa64::fwd_kernel<2>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs,
                        kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
   } else {
+    static const int abl = [] {
+      const char* e = std::getenv("CAAMD_FA64_ABL");
+      return e ? std::atoi(e) : 0;
+    }();
+    // CAAMD_FA64_FWD_WAVES=8: 256-query blocks of 8 waves (half the K/V re-reads,
+    // 4 waves per SIMD at 128 VGPRs) -- measured 267 vs 243 us at B32 T1024 H25, not default
+    static const int nw = [] {
+      const char* e = std::getenv("CAAMD_FA64_FWD_WAVES");
+      return (e && e[0] == '8') ? 8 : 4;
+    }();
+    if (nw == 8 && abl == 0) {
+      const int nqb = (T + 255) / 256;
+      hipLaunchKernelGGL((fa64::fwd_kernel<1, 0, 8>), dim3(B * H * nqb), dim3(512), 6 * fa64::IMG, st, q, k, v, q_rs,
+                         kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
+      return;
+    }
     const int nqb = (T + 127) / 128;
-    hipLaunchKernelGGL(fa64::fwd_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs,
+    auto kern = fa64::fwd_kernel<1, 0>;
+    switch (abl) {
+      case 1: kern = fa64::fwd_kernel<1, 1>; break;
+      case 2: kern = fa64::fwd_kernel<1, 2>; break;
+      case 3: kern = fa64::fwd_kernel<1, 3>; break;
+      case 4: kern = fa64::fwd_kernel<1, 4>; break;
+      case 7: kern = fa64::fwd_kernel<1, 7>; break;
+      case 8: kern = fa64::fwd_kernel<1, 8>; break;
+      default: break;
+    }
+    hipLaunchKernelGGL(kern, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs,
                        kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
   }
 }

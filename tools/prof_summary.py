@@ -12,7 +12,9 @@ def family(name: str) -> str:
         return "GEMM (hipBLASLt)"
     for key, fam in [("gemm_pp_kernel", "GEMM MFMA (ours)"), ("gemm_kernel", "GEMM MFMA (ours)"),
                      ("transpose_bf16", "weight transpose (ours)"), ("fa_fwd", "flash-attn fwd (ours)"), ("fa_bwd_dq", "flash-attn dQ (ours)"),
-                     ("fa_bwd_dkdv", "flash-attn dK/dV (ours)"), ("ln_fwd", "LayerNorm fwd (ours)"),
+                     ("fa_bwd_dkdv", "flash-attn dK/dV (ours)"), ("fa6410fwd_kernel", "flash-attn fwd (ours)"),
+                     ("fa64::fwd_kernel", "flash-attn fwd (ours)"), ("bwd_dq_kernel", "flash-attn dQ (ours)"),
+                     ("bwd_dkdv_kernel", "flash-attn dK/dV (ours)"), ("rowsum_partial", "column reduce (ours)"), ("ln_fwd", "LayerNorm fwd (ours)"),
                      ("ln_bwd", "LayerNorm bwd (ours)"), ("colsum", "column reduce (ours)"),
                      ("bias_gelu", "bias+GELU (ours)"), ("xent", "cross-entropy (ours)"),
                      ("adamw", "fused AdamW (ours)"), ("sumsq", "grad-norm (ours)"),
