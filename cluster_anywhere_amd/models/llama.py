@@ -161,14 +161,16 @@ class Llama(nn.Module):
             h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
             if res is None:
                 res = x
-            qkv = F.linear(h, layer.w_qkv)  # [B, (H+2KVH)*hd]
+            # decode GEMMs stream the weights once: the skinny MFMA kernel (<= 128 rows)
+            qkv = L.decode_linear(h, layer.w_qkv)  # [B, (H+2KVH)*hd]
             L.rope_cache_(qkv, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
             o = L.paged_decode_attention(qkv, k_caches[i], v_caches[i], block_tables, ctx_lens, max_ctx, H)
-            x = F.linear(o, layer.w_o)
+            x = L.decode_linear(o, layer.w_o)
             h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
-            x = F.linear(L.silu_mul(F.linear(h, layer.w_gate_up)), layer.w_down)
+            x = L.decode_linear(L.silu_mul(L.decode_linear(h, layer.w_gate_up)), layer.w_down)
         h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
-        return self._head(h)
+        w = self.embed if self.lm_head is None else self.lm_head
+        return L.decode_linear(h, w)
 
     # ------------------------------------------------ reference full forward
     @torch.no_grad()

@@ -436,6 +436,35 @@ std::vector<Tensor> rmsnorm(const Tensor& x, const Tensor& w, double eps, const 
   return {y, s_out};
 }
 
+namespace caamd {
+hipError_t skinny_gemm_launch(const bf16*, const bf16*, bf16*, float*, unsigned*, int, int, int, int, int,
+                              hipStream_t);
+}
+
+// decode GEMM: out[M, N] = x[M, K] . w[N, K]^T for M <= 128 (skinny_gemm.hip)
+void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& out, Tensor& part, Tensor& counters, int64_t splits) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(out);
+  CHECK_F32(part);
+  TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.is_contiguous(),
+              "skinny_gemm: counters must be a contiguous int32 CUDA tensor");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && w.is_contiguous(), "skinny_gemm: w must be a contiguous [N, K]");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) >= K, "skinny_gemm: x rows must be dense");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.is_contiguous(), "skinny_gemm: out must be [M, N]");
+  TORCH_CHECK(M >= 1 && M <= 128, "skinny_gemm: 1 <= M <= 128");
+  TORCH_CHECK(N % 64 == 0, "skinny_gemm: N % 64 == 0");
+  TORCH_CHECK(splits >= 1 && K % (128 * splits) == 0, "skinny_gemm: K % (128 * splits) == 0");
+  TORCH_CHECK(splits == 1 || part.numel() >= splits * N * 128, "skinny_gemm: workspace too small");
+  TORCH_CHECK(counters.numel() >= N / 64, "skinny_gemm: counters too small");
+  hipError_t e = caamd::skinny_gemm_launch(bp(x), bp(w), bp(out), part.data_ptr<float>(),
+                                           (unsigned*)counters.data_ptr<int>(), (int)M, (int)N, (int)K,
+                                           (int)x.stride(0), (int)splits, cur_stream());
+  TORCH_CHECK(e == hipSuccess, "skinny_gemm launch failed: ", hipGetErrorString(e));
+}
+
 Tensor silu_mul(const Tensor& gu) {
   CHECK_BF16(gu);
   const int64_t F2 = gu.size(-1);
@@ -876,6 +905,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm", &rmsnorm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("eps"),
         pybind11::arg("residual") = pybind11::none());
   m.def("silu_mul", &silu_mul);
+  m.def("skinny_gemm", &skinny_gemm);
   m.def("rope_cache_", &rope_cache_);
   m.def("paged_decode", &paged_decode, pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
         pybind11::arg("block_tables"), pybind11::arg("ctx_lens"), pybind11::arg("max_ctx"), pybind11::arg("H"),

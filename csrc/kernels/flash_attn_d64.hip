@@ -208,6 +208,16 @@ __device__ __forceinline__ float sum_xor32(float x) {
 __device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// Workgroup barrier that keeps younger LDS-DMA in flight: __syncthreads() compiles
+// to `s_waitcnt vmcnt(0) lgkmcnt(0); s_barrier`, which would drain the tile
+// prefetched two steps ahead at every step (the ring would be one deep). Callers
+// wait for the tile they need with a counted vmcnt first; lgkmcnt(0) finishes this
+// wave's LDS reads before another wave's DMA may overwrite the stage.
+__device__ __forceinline__ void barrier_keep_dma() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 // Three-stage ring, DMA two tiles ahead: at the end of step t, tile t + 1 must
 // have landed while tile t + 2's N pieces (issued this step) stay in flight.
 template <int N>
@@ -408,7 +418,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
     }
     if constexpr (!(ABL & 2)) {
       wait_next<DMA_N>(ahead);
-      __syncthreads();
+      barrier_keep_dma();
     }
   }
 #pragma unroll
@@ -579,7 +589,7 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
     if (!(causal && k0 > q0w + 32 * QS - 1) && q0w < T)  // wave-uniform
       tile((causal && k0 + 63 > q0w) || (k0 + 64 > T), smem + st * STAGE, smem_u + st * STAGE, k0);
     wait_next<4>(ahead);
-    __syncthreads();
+    barrier_keep_dma();
   }
 #pragma unroll
   for (int qs = 0; qs < QS; ++qs) {
@@ -738,7 +748,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
       tile((causal && q0 < key0w + 31) || (q0 + 64 > T), smem + stg * STAGE, smem_u + stg * STAGE, q0);
     if (wave < 2) wait_next<5>(ahead);  // waves 0 / 1 also DMA the lse2 / delta rows
     else wait_next<4>(ahead);
-    __syncthreads();
+    barrier_keep_dma();
   }
   if (kv) {
     bf16* krow = dqkv + ((size_t)b * T + key) * rs + (size_t)(H + hh) * D;
