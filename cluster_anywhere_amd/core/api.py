@@ -437,7 +437,13 @@ def kill(actor, *, no_restart: bool = True):
         raise ValueError("kill() only supports actor handles")
     if context.local_mode:
         return
-    _w().send(("kill_actor", actor._actor_id, no_restart))
+    w = _w()
+    w.send(("kill_actor", actor._actor_id, no_restart))
+    # later calls from this process go through the head, which orders them after the
+    # kill (a still-open direct connection would reach the actor before it dies)
+    head_only = getattr(w, "actor_head_only", None)
+    if head_only is not None:
+        head_only.add(actor._actor_id)
 
 
 def cancel(ref, *, force: bool = False, recursive: bool = True):

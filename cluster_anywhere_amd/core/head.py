@@ -244,6 +244,7 @@ class Head:
         self.gcs = None
         self._gcs_actors: Set[bytes] = set()
         self.gcs_restored = {}
+        self._restored_grace: Dict[bytes, float] = {}  # restored object -> evict-protection deadline
         if gcs_storage:
             from .gcs_persist import GcsPersistence
 
@@ -686,6 +687,8 @@ class Head:
         if e.spilled_path is not None:
             self._restore(oid, e)
             e.node = self.head_hex
+            # the reader maps it after this reply: keep the next evictions off it
+            self._restored_grace[oid] = time.time() + self._RESTORE_GRACE_S
         src = e.node or self.head_hex
         if node is not None and src != node:
             addr = self.node_obj_addr.get(src)
@@ -710,13 +713,29 @@ class Head:
         else:
             e.inline = data  # last resort: serve through the control plane
 
+    _RESTORE_GRACE_S = 2.0
+
     def _evict(self, need):
-        """Spill least-recently-used sealed objects to disk until ``need`` fits."""
+        """Spill least-recently-used sealed objects to disk until ``need`` fits.
+        Objects restored for a reader within the last ``_RESTORE_GRACE_S`` seconds
+        are spilled only when nothing else can make room (otherwise two readers of
+        spilled objects evict each other's copies between the head's reply and the
+        reader's mapping)."""
         os.makedirs(self.spill_dir, exist_ok=True)
+        now = time.time()
+        grace = self._restored_grace
+        for o in [o for o, t in grace.items() if t <= now]:
+            del grace[o]
+        freed = self._evict_pass(need, skip=grace)
+        if freed < need or self.store.largest_free() < need:
+            freed += self._evict_pass(need - freed, skip=None)
+        return freed
+
+    def _evict_pass(self, need, skip):
         freed = 0
         for oid in self.store.lru_candidates(256):
             e = self.objects.get(oid)
-            if e is None:
+            if e is None or (skip and oid in skip):
                 continue
             pb = self.store.get_pinned(oid)
             if pb is None:

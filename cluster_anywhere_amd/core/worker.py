@@ -663,7 +663,21 @@ class CoreWorker:
             try:
                 return self._materialize(oid, kind, payload)
             except ObjectLostError:
-                if kind not in ("remote", "err_remote", "lost") or attempts <= 0:
+                if attempts <= 0:
+                    raise
+                if kind in ("store", "err_store"):
+                    # evicted (spilled) between the head's reply and our mapping:
+                    # ask again, the head restores it
+                    attempts -= 1
+                    self.refs.cache.pop(oid, None)
+                    res = self.request(lambda req: ("get", req, [oid], timeout))
+                    if res is None:
+                        from ..exceptions import GetTimeoutError
+
+                        raise GetTimeoutError(f"get() timed out after {timeout}s")
+                    _o, kind, payload = res[0]
+                    continue
+                if kind not in ("remote", "err_remote", "lost"):
                     raise
                 attempts -= 1
                 if not self.request(lambda req: ("report_lost", req, oid)):
@@ -932,7 +946,7 @@ class CoreWorker:
             if a[0] == "v":
                 return serialization.deserialize(a[1])
             kind, payload = resolved[a[1]]
-            return self._materialize(a[1], kind, payload)
+            return self._materialize_or_recover(a[1], kind, payload, None)
 
         args = [unpack(a) for a in spec.args]
         kwargs = {k: unpack(v) for k, v in spec.kwargs.items()}
