@@ -282,7 +282,7 @@ class AlgorithmConfig:
         else:
             per = max(1, self.num_env_runners) * self.num_envs_per_env_runner
             n = max(1, int(np.ceil(self.total_train_batch_size / per)))
-        if self.model_config.get("use_lstm"):  # fragments are cut into whole max_seq_len sequences
+        if self.model_config.get("use_lstm") or self.model_config.get("use_attention"):  # whole max_seq_len sequences
             L = int(self.model_config.get("max_seq_len", 20))
             n = ((n + L - 1) // L) * L
         return n
@@ -318,7 +318,7 @@ class AlgorithmConfig:
         if self.is_multi_agent:
             if not self.module_ids():
                 raise ValueError("config.multi_agent(policies=...) needs at least one module id")
-            if self.model_config.get("use_lstm"):
+            if self.model_config.get("use_lstm") or self.model_config.get("use_attention"):
                 raise NotImplementedError("recurrent modules are single-agent only for now")
             if self.algo_class is not None and not getattr(self.algo_class, "supports_multi_agent", False):
                 raise NotImplementedError(f"{self.algo_class.__name__} has no multi-agent training step yet")

@@ -152,7 +152,7 @@ class PPO(Algorithm):
         self.env_steps_sampled += steps
         lg = self.learner_group
         mbs = c.minibatch_size
-        if c.model_config.get("use_lstm"):  # minibatches of whole sequences
+        if c.model_config.get("use_lstm") or c.model_config.get("use_attention"):  # whole sequences
             mbs = max(1, mbs // int(c.model_config.get("max_seq_len", 20)))
         kl_of = (lambda st: {m: s.get("mean_kl_loss", 0.0) for m, s in st.items()}) if self.is_multi_agent \
             else (lambda st: st.get("mean_kl_loss", 0.0))

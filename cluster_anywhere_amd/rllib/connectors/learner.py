@@ -55,8 +55,9 @@ class GeneralAdvantageEstimation(ConnectorV2):
     def __call__(self, *, rl_module=None, batch, **kw):
         vf = batch["vf_preds"].float()
         vb = {"obs": batch["last_obs"]}
-        if "last_state_h" in batch:  # recurrent module: V after the fragment's last state
-            vb["state_in"] = {"h": batch["last_state_h"], "c": batch["last_state_c"]}
+        last_st = {k[len("last_state_"):]: v for k, v in batch.items() if k.startswith("last_state_")}
+        if last_st:  # recurrent / attention module: V after the fragment's last state
+            vb["state_in"] = last_st
         last = rl_module.compute_values(vb).float()
         values = torch.cat([vf, last[None]], 0)
         nonterm = 1.0 - batch["terminateds"].float()

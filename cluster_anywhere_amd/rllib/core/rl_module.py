@@ -156,6 +156,80 @@ def _act(name):
     return {"tanh": nn.Tanh, "relu": nn.ReLU, "silu": nn.SiLU, "elu": nn.ELU}[name]
 
 
+class _GRUGate(nn.Module):
+    """GTrXL gating layer: out = (1 - z) * x + z * tanh(W_g y + U_g (r * x))."""
+
+    def __init__(self, d: int, bias_init: float = 2.0):
+        super().__init__()
+        self.w = nn.Linear(d, 3 * d, bias=False)
+        self.u = nn.Linear(d, 2 * d, bias=False)
+        self.ug = nn.Linear(d, d, bias=False)
+        self.bz = nn.Parameter(torch.full((d,), float(bias_init)))
+
+    def forward(self, x, y):
+        wr, wz, wg = self.w(y).chunk(3, -1)
+        ur, uz = self.u(x).chunk(2, -1)
+        r = torch.sigmoid(wr + ur)
+        z = torch.sigmoid(wz + uz - self.bz)
+        h = torch.tanh(wg + self.ug(r * x))
+        return (1 - z) * x + z * h
+
+
+class GTrXLCore(nn.Module):
+    """Gated transformer-XL core for partially observed tasks (reference: RLlib's
+    attention net, ``use_attention`` / ``attention_dim`` / ``attention_num_heads`` /
+    ``attention_num_transformer_units`` / ``attention_memory_inference`` /
+    ``attention_init_gru_gate_bias``; Parisotto et al., "Stabilizing Transformers
+    for RL"). Every unit keeps a memory of its last ``M`` inputs; one step attends
+    from the current input over [memory, current] (pre-LayerNorm multi-head
+    attention, then a position-wise MLP), each sub-layer joined by a GRU gate
+    instead of a residual add. The recurrent state is the flat memory
+    ``[units * M * dim]`` (zeros at episode start)."""
+
+    def __init__(self, d_in: int, dim: int = 64, heads: int = 2, units: int = 1, memory: int = 16,
+                 mlp_dim: int = 64, gate_bias: float = 2.0):
+        super().__init__()
+        self.dim, self.heads, self.units, self.M = dim, heads, units, memory
+        self.inp = nn.Linear(d_in, dim)
+        self.ln1 = nn.ModuleList([nn.LayerNorm(dim) for _ in range(units)])
+        self.ln_kv = nn.ModuleList([nn.LayerNorm(dim) for _ in range(units)])
+        self.q = nn.ModuleList([nn.Linear(dim, dim) for _ in range(units)])
+        self.kv = nn.ModuleList([nn.Linear(dim, 2 * dim) for _ in range(units)])
+        self.o = nn.ModuleList([nn.Linear(dim, dim) for _ in range(units)])
+        self.g1 = nn.ModuleList([_GRUGate(dim, gate_bias) for _ in range(units)])
+        self.ln2 = nn.ModuleList([nn.LayerNorm(dim) for _ in range(units)])
+        self.mlp = nn.ModuleList([nn.Sequential(nn.Linear(dim, mlp_dim), nn.ReLU(), nn.Linear(mlp_dim, dim))
+                                  for _ in range(units)])
+        self.g2 = nn.ModuleList([_GRUGate(dim, gate_bias) for _ in range(units)])
+        # learned position of each memory slot (oldest ... newest, current)
+        self.pos = nn.Parameter(torch.zeros(memory + 1, dim))
+        nn.init.normal_(self.pos, std=0.02)
+
+    @property
+    def state_size(self) -> int:
+        return self.units * self.M * self.dim
+
+    def step(self, z, mem_flat):
+        """z [B, d_in], mem_flat [B, units*M*dim] -> (out [B, dim], new mem_flat)."""
+        B = z.shape[0]
+        mem = mem_flat.view(B, self.units, self.M, self.dim)
+        x = self.inp(z)
+        new = []
+        H, hd = self.heads, self.dim // self.heads
+        for u in range(self.units):
+            new.append(torch.cat([mem[:, u, 1:], x[:, None]], 1))  # this unit's input joins its memory
+            ctx = torch.cat([mem[:, u], x[:, None]], 1) + self.pos  # [B, M+1, dim]
+            q = self.q[u](self.ln1[u](x)).view(B, H, 1, hd)
+            k, v = self.kv[u](self.ln_kv[u](ctx)).chunk(2, -1)
+            k = k.view(B, self.M + 1, H, hd).transpose(1, 2)
+            v = v.view(B, self.M + 1, H, hd).transpose(1, 2)
+            att = torch.softmax((q @ k.transpose(-1, -2)) / hd ** 0.5, -1) @ v  # [B, H, 1, hd]
+            y = self.o[u](att.reshape(B, self.dim))
+            x = self.g1[u](x, torch.relu(y))
+            x = self.g2[u](x, torch.relu(self.mlp[u](self.ln2[u](x))))
+        return x, torch.stack(new, 1).reshape(B, -1)
+
+
 @dataclass
 class RLModuleSpec:
     module_class: Optional[type] = None
@@ -214,7 +288,8 @@ class DefaultActorCriticModule(RLModule):
         act = _act(mc.get("fcnet_activation", "tanh"))
         self.image = len(obs.shape) == 3
         self.use_lstm = bool(mc.get("use_lstm", False))
-        self.share = mc.get("vf_share_layers", self.image or self.use_lstm)
+        self.use_attention = bool(mc.get("use_attention", False)) and not self.use_lstm
+        self.share = mc.get("vf_share_layers", self.image or self.use_lstm or self.use_attention)
         if self.image:
             self.encoder = NatureCNN(obs.shape[-1], hw=obs.shape[:2])
             feat = self.encoder.out_dim
@@ -231,6 +306,15 @@ class DefaultActorCriticModule(RLModule):
             self.lstm = nn.LSTMCell(feat, self.cell)
             feat = self.cell
             self.vf_encoder = None  # value head shares the recurrent core
+        elif self.use_attention:
+            dim = int(mc.get("attention_dim", 64))
+            self.gtrxl = GTrXLCore(feat, dim=dim, heads=int(mc.get("attention_num_heads", 2)),
+                                   units=int(mc.get("attention_num_transformer_units", 1)),
+                                   memory=int(mc.get("attention_memory_inference", mc.get("max_seq_len", 16))),
+                                   mlp_dim=int(mc.get("attention_position_wise_mlp_dim", dim)),
+                                   gate_bias=float(mc.get("attention_init_gru_gate_bias", 2.0)))
+            feat = dim
+            self.vf_encoder = None
         self.pi = nn.Linear(feat, dist_input_dim(self.action_space))
         self.vf = nn.Linear(feat, 1)
         nn.init.normal_(self.pi.weight, std=0.01)
@@ -248,9 +332,11 @@ class DefaultActorCriticModule(RLModule):
 
     # ------------------------------------------------------------------ state
     def is_stateful(self) -> bool:
-        return self.use_lstm
+        return self.use_lstm or self.use_attention
 
     def get_initial_state(self) -> Dict[str, torch.Tensor]:
+        if self.use_attention:
+            return {"mem": torch.zeros(self.gtrxl.state_size)}
         if not self.use_lstm:
             return {}
         return {"h": torch.zeros(self.cell), "c": torch.zeros(self.cell)}
@@ -302,7 +388,36 @@ class DefaultActorCriticModule(RLModule):
             outs.append(h)
         return torch.stack(outs, 1).reshape(S * L, -1)
 
+    def _step_attn(self, batch):
+        obs = self._obs(batch)
+        z = self.encoder(obs)
+        st = batch.get("state_in")
+        mem = (st["mem"].to(z.device).float() if st is not None
+               else torch.zeros(z.shape[0], self.gtrxl.state_size, device=z.device))
+        return self.gtrxl.step(z, mem)
+
+    def _seq_attn(self, batch):
+        """obs [S, L, ...] -> core outputs [S*L, dim]; memory zeroed at ``resets``."""
+        o = batch["obs"]
+        S, L = o.shape[0], o.shape[1]
+        flat = o.reshape((S * L,) + tuple(o.shape[2:]))
+        z = self.encoder(flat if self.image else flat.reshape(S * L, -1).float()).view(S, L, -1)
+        st = batch.get("state_in")
+        mem = (st["mem"].to(z.device).float() if st is not None
+               else torch.zeros(S, self.gtrxl.state_size, device=z.device))
+        resets = batch.get("resets")
+        outs = []
+        for t in range(L):
+            if resets is not None and t > 0:
+                mem = mem * (1.0 - resets[:, t].float())[:, None]
+            y, mem = self.gtrxl.step(z[:, t], mem)
+            outs.append(y)
+        return torch.stack(outs, 1).reshape(S * L, -1)
+
     def forward_train(self, batch):
+        if self.use_attention:
+            core = self._seq_attn(batch)
+            return {"action_dist_inputs": self._head_out(core), "vf_preds": self.vf(core).squeeze(-1)}
         if self.use_lstm:
             core = self._seq_lstm(batch)
             return {"action_dist_inputs": self._head_out(core), "vf_preds": self.vf(core).squeeze(-1)}
@@ -311,7 +426,10 @@ class DefaultActorCriticModule(RLModule):
 
     @torch.no_grad()
     def forward_exploration(self, batch):
-        if self.use_lstm:
+        if self.use_attention:
+            y, mem = self._step_attn(batch)
+            logits, v = self._head_out(y), self.vf(y).squeeze(-1)
+        elif self.use_lstm:
             h, c = self._step_lstm(batch)
             logits, v = self._head_out(h), self.vf(h).squeeze(-1)
         else:
@@ -321,10 +439,15 @@ class DefaultActorCriticModule(RLModule):
         out = {"actions": a, "action_logp": d.logp(a), "vf_preds": v, "action_dist_inputs": logits}
         if self.use_lstm:
             out["state_out"] = {"h": h, "c": c}
+        elif self.use_attention:
+            out["state_out"] = {"mem": mem}
         return out
 
     @torch.no_grad()
     def forward_inference(self, batch):
+        if self.use_attention:
+            y, mem = self._step_attn(batch)
+            return {"actions": self.dist_cls(self._head_out(y)).deterministic(), "state_out": {"mem": mem}}
         if self.use_lstm:
             h, c = self._step_lstm(batch)
             return {"actions": self.dist_cls(self._head_out(h)).deterministic(), "state_out": {"h": h, "c": c}}
@@ -332,6 +455,9 @@ class DefaultActorCriticModule(RLModule):
         return {"actions": self.dist_cls(logits).deterministic()}
 
     def compute_values(self, batch):
+        if self.use_attention:
+            y, _ = self._step_attn(batch)
+            return self.vf(y).squeeze(-1)
         if self.use_lstm:  # V of the state reached after ``state_in`` consumes ``obs``
             h, _ = self._step_lstm(batch)
             return self.vf(h).squeeze(-1)
