@@ -241,6 +241,7 @@ class ResNetPredictor:
         t2 = time.perf_counter()
         self.model = net.fuse_for_inference(torch.bfloat16 if dev.type == "cuda" else torch.float32, dev)
         self.graph = None
+        self._pending_capture = self._ran_eager = False
         self.init_profile.update(cuda_init_s=t1 - t0, model_init_s=t2 - t1, fuse_s=time.perf_counter() - t2)
         if dev.type == "cuda":
             self.copy_stream = torch.cuda.Stream(dev)
@@ -248,34 +249,38 @@ class ResNetPredictor:
                             for _ in range(2)]
             self.static_in = torch.zeros((batch_size, hw, hw, 3), dtype=torch.uint8, device=dev)
             self._flip = 0
-            from ..core.hip_pinning import pin_object_store
-
-            # inside a GPU worker: page-lock the object-store arena so batches DMA
-            # straight from their shm blocks (no staging memcpy)
-            t4 = time.perf_counter()
-            if use_graph:
-                self._capture()
-            self.init_profile.update(capture_s=time.perf_counter() - t4)
-            # page-lock the arena in the background AFTER the capture (registering GBs
-            # of host memory contends with graph capture in the HIP runtime); until it
-            # is registered, arena_contains() is False and batches take the staging copy
-            import threading
-
-            threading.Thread(target=pin_object_store, name="caamd-pin-arena", daemon=True).start()
+            # Lazy capture: the first batch runs eagerly (it doubles as the MIOpen
+            # algorithm warm-up), and the graph is captured at the start of the next
+            # call, so capture (~0.25 s) and a separate warm-up pass (~0.2 s) are off
+            # the time-to-first-batch path of a freshly started actor.
+            self._pending_capture = bool(use_graph)
             self.arena_pinned = None
+            if not use_graph:
+                self._start_pinning()
         self.init_profile["total_s"] = time.perf_counter() - t0
 
     def _run(self, x_u8):
         return self.model.predict_uint8(x_u8).argmax(dim=1)
 
-    def _capture(self):
-        s = torch.cuda.Stream(self.device)
-        s.wait_stream(torch.cuda.current_stream(self.device))
+    def _start_pinning(self):
+        # page-lock the object-store arena in the background AFTER the capture
+        # (registering GBs of host memory contends with graph capture in the HIP
+        # runtime) so batches DMA straight from their shm blocks; until it is
+        # registered, arena_contains() is False and batches take the staging copy
+        import threading
+
+        from ..core.hip_pinning import pin_object_store
+
+        threading.Thread(target=pin_object_store, name="caamd-pin-arena", daemon=True).start()
+
+    def _capture(self, warm: bool = True):
         tw = time.perf_counter()
-        with torch.cuda.stream(s):
-            for _ in range(1):  # warm up MIOpen algorithm selection outside the graph
+        if warm:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):  # warm up MIOpen algorithm selection outside the graph
                 self._run(self.static_in)
-        torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.init_profile["warmup_runs_s"] = time.perf_counter() - tw
         self.graph = torch.cuda.CUDAGraph()
@@ -291,6 +296,12 @@ class ResNetPredictor:
         if self.device.type != "cuda":
             x = torch.from_numpy(np.ascontiguousarray(arr))
             return self._run(x).numpy()
+        if self._pending_capture and self._ran_eager:
+            tc = time.perf_counter()
+            self._capture(warm=False)
+            self._pending_capture = False
+            self.init_profile["capture_s"] = time.perf_counter() - tc
+            self._start_pinning()
         out = []
         st = self._stats
         t0 = time.perf_counter()
@@ -321,6 +332,7 @@ class ResNetPredictor:
                 res = self.static_out
             else:
                 res = self._run(self.static_in)
+                self._ran_eager = True
             out.append(res[:m].to("cpu", non_blocking=False).numpy())
         if st is not None:
             st["calls"] += 1
