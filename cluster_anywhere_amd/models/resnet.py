@@ -222,7 +222,8 @@ class ResNetPredictor:
     """
 
     def __init__(self, name: str = "resnet50", batch_size: int = 256, hw: int = 224,
-                 device: Optional[str] = None, use_graph: bool = True, seed: int = 0):
+                 device: Optional[str] = None, use_graph: bool = True, seed: int = 0,
+                 lazy_capture: Optional[bool] = None):
         t0 = time.perf_counter()
         torch.manual_seed(seed)
         dev = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -241,7 +242,7 @@ class ResNetPredictor:
         t2 = time.perf_counter()
         self.model = net.fuse_for_inference(torch.bfloat16 if dev.type == "cuda" else torch.float32, dev)
         self.graph = None
-        self._pending_capture = self._ran_eager = False
+        self._pending_capture = self._ran_eager = self._early_pin = False
         self.init_profile.update(cuda_init_s=t1 - t0, model_init_s=t2 - t1, fuse_s=time.perf_counter() - t2)
         if dev.type == "cuda":
             self.copy_stream = torch.cuda.Stream(dev)
@@ -249,13 +250,25 @@ class ResNetPredictor:
                             for _ in range(2)]
             self.static_in = torch.zeros((batch_size, hw, hw, 3), dtype=torch.uint8, device=dev)
             self._flip = 0
-            # Lazy capture: the first batch runs eagerly (it doubles as the MIOpen
-            # algorithm warm-up), and the graph is captured at the start of the next
-            # call, so capture (~0.25 s) and a separate warm-up pass (~0.2 s) are off
-            # the time-to-first-batch path of a freshly started actor.
+            # Lazy capture (opt-in): the first batch runs eagerly (it doubles as the
+            # MIOpen warm-up) and the graph is captured at the start of the next call,
+            # taking capture (~0.25 s) and the warm-up pass (~0.2 s) off a fresh
+            # actor's time to first batch. Measured in the Data bench on one box
+            # (tools/gpu/data_ab.sh): time to first batch 0.64-1.19 s lazy vs
+            # 0.91-1.83 s eager, but end-to-end 22.9-24.9k vs 23.9-26.2k rows/s (the
+            # steady state after the first batch ran ~12% slower), so eager capture
+            # stays the default. lazy_capture=None reads CAAMD_PREDICTOR_LAZY_CAPTURE.
+            if lazy_capture is None:
+                lazy_capture = os.environ.get("CAAMD_PREDICTOR_LAZY_CAPTURE", "0") == "1"
             self._pending_capture = bool(use_graph)
             self.arena_pinned = None
-            if not use_graph:
+            if use_graph and not lazy_capture:
+                t4 = time.perf_counter()
+                self._capture()
+                self._pending_capture = False
+                self.init_profile["capture_s"] = time.perf_counter() - t4
+            self._early_pin = os.environ.get("CAAMD_PREDICTOR_EARLY_PIN", "0") == "1"
+            if not self._pending_capture or self._early_pin:
                 self._start_pinning()
         self.init_profile["total_s"] = time.perf_counter() - t0
 
@@ -301,7 +314,8 @@ class ResNetPredictor:
             self._capture(warm=False)
             self._pending_capture = False
             self.init_profile["capture_s"] = time.perf_counter() - tc
-            self._start_pinning()
+            if not self._early_pin:
+                self._start_pinning()
         out = []
         st = self._stats
         t0 = time.perf_counter()

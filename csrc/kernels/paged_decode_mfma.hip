@@ -8,7 +8,7 @@
 //   S^T[tok][head] = K[tok][:] . Q[head][:]    v_mfma_f32_16x16x32_bf16, A = K page
 //                                              rows straight from global memory
 //                                              (lane = token, 16 B = 8 dims),
-//                                              B = pre-scaled Q in registers
+//                                              B = Q in registers (scores scaled after)
 //   online softmax per head (exp2 domain), the 4 lane groups of a head
 //   reduced with two xor-shuffles
 //   O^T[dim][head] += V^T[dim][tok] . P^T[tok][head]
@@ -22,9 +22,9 @@
 //                                              k-slots are exactly the tokens whose
 //                                              scores it already holds: no shuffle)
 //
-// A wave handles 32-token chunks (two pages): 8 x 16 B K loads and 8 x 16 B V
-// loads per lane in flight, then 8 + 8 MFMAs. A 256-thread block covers a
-// partition of 256 tokens (4 waves x 2 chunks); the waves' (max, sum, O) are
+// A wave handles two 32-token chunks (two pages each): 2 x (8 x 16 B K + 8 x 16 B
+// V) loads per lane in flight at once, then 8 + 8 MFMAs per chunk. A 256-thread
+// block covers a partition of 256 tokens (4 waves x 2 chunks); the waves' (max, sum, O) are
 // merged through LDS. Contexts longer than one partition write un-normalised
 // partials that pdm_reduce merges ("flash-decoding"), so long contexts still
 // spread over all 256 CUs.
@@ -72,7 +72,7 @@ __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f3
 }
 
 template <int G>
-__global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
+__global__ __launch_bounds__(256, 3) void paged_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
     float* __restrict__ part_acc, float* __restrict__ part_ml, int KVH, int max_parts, float scale_log2) {
@@ -85,21 +85,19 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
   const int t0 = part * PART;
   if (t0 >= ctx) return;  // uniform for the block (before any barrier)
   const int t1 = min(ctx, t0 + PART);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 4, r16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, g = lane >> 4, r16 = lane & 15;
   const int H = KVH * G;
 
   // Q (B operand of S^T): column = head r16 of the group, k-slots = dims 32s + 8g + j
   bf16x8 qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    bf16x8 v = {};
-    if (r16 < G) {
-      const bf16x8 raw = *reinterpret_cast<const bf16x8*>(q + (size_t)seq * q_stride + (kvh * G + r16) * D +
-                                                         32 * s + 8 * g);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (bf16)((float)raw[j] * scale_log2);
-    }
-    qf[s] = v;
+    // branch-free (a lane-divergent branch around each load serialises the four
+    // loads behind their own waits) and unscaled (scaling here would wait for Q
+    // before the K/V loads issue; the scores are scaled instead): padding columns
+    // load head G-1, their scores land in output columns that are never stored
+    qf[s] = *reinterpret_cast<const bf16x8*>(q + (size_t)seq * q_stride + (kvh * G + min(r16, G - 1)) * D +
+                                             32 * s + 8 * g);
   }
   const int* bt = block_tables + (size_t)seq * max_blocks;
   lds_char* img = (lds_char*)vimg[wave];
@@ -108,50 +106,71 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
 #pragma unroll
   for (int c = 0; c < 8; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int c0 = t0 + wave * CH; c0 < t1; c0 += WAVES * CH) {
-    const int pg = c0 / BS;  // c0 is page aligned (multiple of 32)
-    const bool has1 = c0 + BS < t1;
-    const int b0 = bt[pg], b1 = has1 ? bt[pg + 1] : b0;
-    const size_t page = (size_t)BS * D;
-    const bf16* K0 = kc + ((size_t)b0 * KVH + kvh) * page;
-    const bf16* K1 = kc + ((size_t)b1 * KVH + kvh) * page;
-    const bf16* V0 = vc + ((size_t)b0 * KVH + kvh) * page;
-    const bf16* V1 = vc + ((size_t)b1 * KVH + kvh) * page;
-    bf16x8 k0f[4], k1f[4], vv[8];
+  // A wave owns at most two 32-token chunks of the partition (PART = WAVES * CH * 2).
+  // Both chunks' K and V loads are issued before either is consumed, so the wave
+  // waits on one memory latency instead of a dependent chain of two (the kernel
+  // moves ~10 MB per layer at batch 128: it is latency-bound, not bandwidth-bound).
+  // A missing chunk re-loads a valid one (uniform, branch-free issue) and is masked.
+  const int cA = t0 + wave * CH, cB = cA + WAVES * CH;
+  const bool hasA = cA < t1, hasB = cB < t1;
+  const int cAc = hasA ? cA : t0, cBc = hasB ? cB : cAc;
+  const size_t page = (size_t)BS * D;
+  // the four page ids, loaded together (second page of a chunk past the context
+  // end -> the first page again; its scores are masked)
+  int pb[4];
+  pb[0] = bt[cAc / BS];
+  pb[1] = bt[cAc / BS + (cAc + BS < t1 ? 1 : 0)];
+  pb[2] = bt[cBc / BS];
+  pb[3] = bt[cBc / BS + (cBc + BS < t1 ? 1 : 0)];
+  bf16x8 kf[2][8], vv[2][8];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const bf16* K0 = kc + ((size_t)pb[2 * h] * KVH + kvh) * page;
+    const bf16* K1 = kc + ((size_t)pb[2 * h + 1] * KVH + kvh) * page;
+    const bf16* V0 = vc + ((size_t)pb[2 * h] * KVH + kvh) * page;
+    const bf16* V1 = vc + ((size_t)pb[2 * h + 1] * KVH + kvh) * page;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      k0f[s] = *reinterpret_cast<const bf16x8*>(K0 + r16 * D + 32 * s + 8 * g);
-      k1f[s] = *reinterpret_cast<const bf16x8*>(K1 + r16 * D + 32 * s + 8 * g);
+      kf[h][s] = *reinterpret_cast<const bf16x8*>(K0 + r16 * D + 32 * s + 8 * g);
+      kf[h][4 + s] = *reinterpret_cast<const bf16x8*>(K1 + r16 * D + 32 * s + 8 * g);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int v = lane + 64 * u, t = v >> 4, cc = (v & 15) * 8;
-      vv[u] = *reinterpret_cast<const bf16x8*>((t < 16 ? V0 : V1) + (t & 15) * D + cc);
+      vv[h][u] = *reinterpret_cast<const bf16x8*>((t < 16 ? V0 : V1) + (t & 15) * D + cc);
     }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    // straight-line for both chunks (a branch around chunk B would let the compiler
+    // sink its loads into the branch, behind chunk A's compute): a missing chunk
+    // starts at t1, so all of its scores are masked
+    const int c0 = h == 0 ? (hasA ? cA : t1) : (hasB ? cB : t1);
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      s0 = mfma(k0f[s], qf[s], s0);
-      s1 = mfma(k1f[s], qf[s], s1);
+      s0 = mfma(kf[h][s], qf[s], s0);
+      s1 = mfma(kf[h][4 + s], qf[s], s1);
     }
     // lane holds S^T[token 4g+i][head r16] of page 0 (s0) and page 1 (s1)
     float mt = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      if (c0 + 4 * g + i >= t1) s0[i] = -INFINITY;
-      if (c0 + 16 + 4 * g + i >= t1) s1[i] = -INFINITY;
+      s0[i] = c0 + 4 * g + i >= t1 ? -INFINITY : s0[i] * scale_log2;
+      s1[i] = c0 + 16 + 4 * g + i >= t1 ? -INFINITY : s1[i] * scale_log2;
       mt = fmaxf(mt, fmaxf(s0[i], s1[i]));
     }
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-    const float mn = fmaxf(m, mt);  // finite: every chunk holds at least one valid token
-    const float alpha = __builtin_amdgcn_exp2f(m - mn);
+    const float mn = fmaxf(m, mt);
+    const float mref = mn == -INFINITY ? 0.f : mn;  // nothing valid yet: p = 0, alpha = 0 (o, lsum are 0)
+    const float alpha = __builtin_amdgcn_exp2f(m - mref);
     m = mn;
     bf16x8 pf;
     float ps = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const float p0 = __builtin_amdgcn_exp2f(s0[i] - mn), p1 = __builtin_amdgcn_exp2f(s1[i] - mn);
+      const float p0 = __builtin_amdgcn_exp2f(s0[i] - mref), p1 = __builtin_amdgcn_exp2f(s1[i] - mref);
       ps += p0 + p1;
       pf[i] = (bf16)p0;
       pf[4 + i] = (bf16)p1;
@@ -169,7 +188,7 @@ __global__ __launch_bounds__(256) void paged_decode_mfma_kernel(
       const int v = lane + 64 * u, t = v >> 4, cc = (v & 15) * 8;
       const int tt = t & 15;
       const int row = 8 * (tt >> 2) + (t >= 16 ? 4 : 0) + (tt & 3);
-      st_img(img, row, cc, vv[u]);
+      st_img(img, row, cc, vv[h][u]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();

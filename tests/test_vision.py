@@ -88,14 +88,17 @@ def test_fused_resnet50_gpu_matches_fp32():
 @C
 def test_predictor_hip_graph_matches_eager():
     imgs = np.random.randint(0, 256, (300, 224, 224, 3), dtype=np.uint8)
-    g = ResNetPredictor("resnet50", batch_size=128, use_graph=True)
+    g = ResNetPredictor("resnet50", batch_size=128, use_graph=True, lazy_capture=False)
+    lz = ResNetPredictor("resnet50", batch_size=128, use_graph=True, lazy_capture=True)
     e = ResNetPredictor("resnet50", batch_size=128, use_graph=False)
-    first, b = g(imgs), e(imgs)  # the first call runs eagerly (lazy capture)
-    assert g.graph is None
-    a = g(imgs)  # captured at the start of this call, then replayed per chunk
-    assert g.graph is not None
+    assert g.graph is not None and lz.graph is None
+    a, b = g(imgs), e(imgs)
+    first = lz(imgs)  # lazy: the first call runs eagerly
+    assert lz.graph is None
+    second = lz(imgs)  # captured at the start of this call, then replayed per chunk
+    assert lz.graph is not None
     assert a.shape == (300,)
-    assert (a == b).mean() > 0.98 and (first == b).mean() > 0.98
+    assert (a == b).mean() > 0.98 and (first == b).mean() > 0.98 and (second == b).mean() > 0.98
 
 
 @C
