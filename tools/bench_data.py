@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--hw", type=int, default=224)
     ap.add_argument("--read-blocks", type=int, default=0)
     ap.add_argument("--cpus", type=int, default=0)
-    ap.add_argument("--actors-per-gpu", type=int, default=2,
+    ap.add_argument("--actors-per-gpu", type=int, default=3,
                     help=">1 shares each GPU between actors (fractional num_gpus) so one's H2D "
                          "copy / host work overlaps another's graph replay")
     ap.add_argument("--timeline", default="", help="write a chrome trace + per-function summary here")
