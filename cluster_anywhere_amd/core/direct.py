@@ -33,6 +33,7 @@ import threading
 import time
 from typing import Dict, Optional
 
+from .head import NORMAL
 from .protocol import BatchSender, Conn, ConnectionClosed, connect
 
 
@@ -76,12 +77,29 @@ class DirectServer:
                 spec = msg[1]
                 resolved = msg[2] if len(msg) > 2 else None
                 fn_blob = msg[3] if len(msg) > 3 else None
+                if fn_blob is not None and spec.fn_id not in w.fn_cache:
+                    from . import serialization
+
+                    w.fn_cache[spec.fn_id] = serialization.loads_function(fn_blob)
+                if w.actor_id is None and w._n_blocked > 0 and spec.kind == NORMAL:
+                    # our running task is blocked in get(): a queued task could be what
+                    # it waits for, so the owner re-dispatches it to another lease
+                    try:
+                        out.put(("dreturn", spec.task_id))
+                    except (ConnectionClosed, OSError):
+                        pass
+                    continue
                 w.direct_origin[spec.task_id] = out
                 w._on_execute((spec, fn_blob, resolved if resolved is not None else {}))
             elif msg[0] == "dcancel":
                 _, task_id, force = msg
-                if force and w.actor_id is None:
-                    os._exit(1)  # force-cancel of a leased normal task: the worker goes
+                if force and w.actor_id is None and task_id in w.running_tasks:
+                    # force-cancel of a running leased task ends the worker; the tasks
+                    # queued behind it go back to their owners first (no attempt spent)
+                    w._return_unstarted_leased(exclude=task_id)
+                    for o in list(self.senders):
+                        o.drain(1.0)
+                    os._exit(1)
                 w._on_cancel(task_id)
 
     def close(self):

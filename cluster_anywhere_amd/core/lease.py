@@ -91,19 +91,20 @@ class _Key:
 
 class _Lease:
     __slots__ = ("worker_id", "sock", "key", "pending", "out", "sent_fns", "granted_at", "last_used",
-                 "alive", "rbuf", "writing")
+                 "alive", "rbuf", "writing", "blocked")
 
     def __init__(self, worker_id, sock, key):
         self.worker_id = worker_id
         self.sock = sock
         self.key = key
-        self.pending: Dict[bytes, tuple] = {}  # task_id -> (spec, keep, t_submit)
+        self.pending: Dict[bytes, tuple] = {}  # task_id -> (spec, keep, t_submit, resolved)
         self.out = bytearray()
         self.sent_fns = set()
         self.granted_at = self.last_used = time.monotonic()
         self.alive = True
         self.rbuf = bytearray()
         self.writing = False
+        self.blocked = False  # its running task blocked in get(): no new tasks until it ends
 
 
 class LeaseManager:
@@ -248,17 +249,28 @@ class LeaseManager:
         buf += data
         off = 0
         n_buf = len(buf)
+        returned = []
         while n_buf - off >= 8:
             (n,) = _LEN.unpack_from(buf, off)
             if n_buf - off - 8 < n:
                 break
             msg = pickle.loads(bytes(buf[off + 8: off + 8 + n]))
             off += 8 + n
+            if msg[0] == "dreturn":
+                # not started: the worker's running task is blocked (see worker
+                # _return_unstarted_leased); dispatch it elsewhere, no attempt spent
+                rec = lc.pending.pop(msg[1], None)
+                lc.blocked = True
+                if rec is not None:
+                    self.by_task.pop(msg[1], None)
+                    returned.append(rec)
+                continue
             if msg[0] != "ddone":
                 continue
             task_id, results, error_kind, t0, t1, pid = msg[1:7]
             retryable = msg[7] if len(msg) > 7 else False
             rec = lc.pending.pop(task_id, None)
+            lc.blocked = False
             if rec is None:
                 continue
             self.by_task.pop(task_id, None)
@@ -266,6 +278,21 @@ class LeaseManager:
         if off:
             del buf[:off]
         lc.last_used = time.monotonic()
+        if returned:
+            self._requeue(lc.key, returned)
+
+    def _requeue(self, st: _Key, recs):
+        from ..exceptions import TaskCancelledError
+
+        for rec in sorted(recs, key=lambda r: r[2], reverse=True):  # oldest ends up first
+            spec, keep, _t, resolved = rec
+            if spec.task_id in self.cancelled:
+                self.cancelled.discard(spec.task_id)
+                self.tasks.discard(spec.task_id)
+                self.w._fail_direct(spec, TaskCancelledError(spec.task_id.hex()))
+                continue
+            st.queue.appendleft((spec, keep, resolved))
+        self._pump(st, time.monotonic())
 
     def _complete(self, spec, results, error_kind, retryable, timing):
         tid = spec.task_id
@@ -281,7 +308,7 @@ class LeaseManager:
 
     def _pump(self, st: _Key, now: float):
         q = st.queue
-        live = [lc for lc in st.leases if lc.alive and now - lc.granted_at < SLICE]
+        live = [lc for lc in st.leases if lc.alive and not lc.blocked and now - lc.granted_at < SLICE]
         touched = []
         while q and live:
             lc = min(live, key=lambda x: len(x.pending))
@@ -292,7 +319,7 @@ class LeaseManager:
             if spec.fn_id not in lc.sent_fns:
                 fn_blob = self.w.fn_blobs.get(spec.fn_id)
                 lc.sent_fns.add(spec.fn_id)
-            lc.pending[spec.task_id] = (spec, keep, now)
+            lc.pending[spec.task_id] = (spec, keep, now, resolved)
             self.by_task[spec.task_id] = lc
             self.n_leased_tasks += 1
             lc.out += _frame(("dexec", spec, resolved, fn_blob))

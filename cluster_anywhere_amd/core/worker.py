@@ -179,6 +179,7 @@ class CoreWorker:
         self.alive = True
         # direct actor-call transport (core/direct.py)
         self.direct_origin: Dict[bytes, Any] = {}
+        self._n_blocked = 0  # running normal tasks currently blocked in get()/wait()
         self.actor_direct: Dict[bytes, Any] = {}
         self.actor_head_inflight: Dict[bytes, set] = {}
         self.head_inflight_actor: Dict[bytes, bytes] = {}
@@ -795,8 +796,40 @@ class CoreWorker:
         ctx = context.current_task()
         if self.kind != "worker" or ctx is None or ctx.actor_id is not None:
             return False
+        if on:
+            self._n_blocked += 1
+            # a leased worker must not sit on tasks queued behind a blocked one: one of
+            # them may be what unblocks it (their owners re-dispatch them elsewhere)
+            self._return_unstarted_leased()
+        else:
+            self._n_blocked = max(0, self._n_blocked - 1)
         self.send(("blocked" if on else "unblocked", ctx.task_id))
         return True
+
+    def _return_unstarted_leased(self, exclude: Optional[bytes] = None) -> int:
+        """Hand queued-but-unstarted leased normal tasks back to their owners
+        (``dreturn``): the owner re-queues them without counting an attempt."""
+        q = self.task_queue
+        back = []
+        with q.mutex:
+            keep = []
+            for item in q.queue:
+                if (item is not None and item[0].kind == NORMAL and item[0].task_id != exclude
+                        and item[0].task_id in self.direct_origin):
+                    back.append(item[0].task_id)
+                else:
+                    keep.append(item)
+            if back:
+                q.queue.clear()
+                q.queue.extend(keep)
+        for tid in back:
+            out = self.direct_origin.pop(tid, None)
+            if out is not None:
+                try:
+                    out.put(("dreturn", tid))
+                except (ConnectionClosed, OSError):
+                    pass
+        return len(back)
 
     def free(self, refs):
         self.send(("free", [r.binary() for r in refs]))

@@ -24,6 +24,15 @@ from ._lib import kernels
 
 ALGO = int(os.environ.get("CAAMD_GEMM_ALGO", "2"))
 ENABLED = os.environ.get("CAAMD_MFMA_GEMM", "1") == "1"
+# second-generation kernel (gemm2.hip: 256 x 160 tiles, two workgroups per CU, split-K tail)
+# (opt-in: its mainloop measured ~1.3x slower per MFMA than the ping-pong kernel's,
+# profiles/gemm2_vs_pp.jsonl, so the step keeps gemm.hip + the split tail below)
+GEN2 = os.environ.get("CAAMD_GEMM_GEN", "1") == "2"
+MAX_SPLIT = int(os.environ.get("CAAMD_GEMM2_MAX_SPLIT", "4"))
+# split-K tail of the ping-pong kernel: tiles past the last full round of CUs are
+# split over K-slices so that round is not half empty (N = 1600: 640 tiles = 2.5 rounds)
+TAIL = os.environ.get("CAAMD_GEMM_TAIL", "1") == "1"
+MAX_TAIL_SPLIT = int(os.environ.get("CAAMD_GEMM_TAIL_SPLIT", "4"))
 
 EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_BIAS_GELU, EPI_DGELU = range(5)
 
@@ -51,12 +60,110 @@ def supported(x2: torch.Tensor, w: torch.Tensor) -> bool:
     return tile_for(M, N, K) is not None and tile_for(M, K, N) is not None
 
 
+_PLANS: dict = {}
+_WS: dict = {}
+
+
+def _slots(dev: torch.device) -> int:
+    """Workgroups of gemm2 resident at once: two per CU."""
+    return 2 * torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def plan2(M: int, N: int, K: int, dev: torch.device, max_split: Optional[int] = None):
+    """(full tiles, tail split S, grid, workspace floats, tickets) for a gemm2 launch."""
+    ms = MAX_SPLIT if max_split is None else max_split
+    key = (M, N, K, dev.index, ms)
+    p = _PLANS.get(key)
+    if p is None:
+        p = _PLANS[key] = tuple(kernels().gemm2_plan(M, N, K, _slots(dev), ms))
+    return p
+
+
+def _workspace(dev: torch.device, floats: int, tickets: int):
+    """Per-device split-K slab workspace + zeroed ticket counters (the kernel's last
+    arriver resets its ticket, so the counters stay zero between launches)."""
+    ws, cnt = _WS.get(dev.index, (None, None))
+    if ws is None or ws.numel() < floats or cnt.numel() < tickets:
+        ws = torch.empty(max(floats, 1 << 20), device=dev, dtype=torch.float32)
+        cnt = torch.zeros(max(tickets, 4096), device=dev, dtype=torch.int32)
+        _WS[dev.index] = (ws, cnt)
+    return ws, cnt
+
+
+def gen2_ok(M: int, N: int, K: int) -> bool:
+    return ENABLED and GEN2 and M % 8 == 0 and N % 160 == 0 and K % 32 == 0 and K > 0
+
+
+def run2(a, b, c, layout, epi, bias=None, z=None, zout=None, dbias=None, max_split=None):
+    """gemm2 launch: layout 0 a[M,K] b[N,K]; layout 2 a[K,M] b[K,N]."""
+    M, N = c.shape
+    K = a.shape[0] if layout == 2 else a.shape[1]
+    full, S, grid, wsf, tickets = plan2(M, N, K, c.device, max_split)
+    ws = cnt = None
+    if S > 1:
+        ws, cnt = _workspace(c.device, wsf, tickets)
+    kernels().gemm2_bf16(a, b, c, layout, epi, bias, z, zout, dbias, ws, cnt, full, S, grid)
+    return c
+
+
+def tail_plan(M: int, N: int, K: int, bm: int, bn: int, dev: torch.device, algo: int = None):
+    """(full tiles, tail split) of a ping-pong launch; split 1 = no tail split."""
+    algo = ALGO if algo is None else algo
+    if not TAIL or not (1 <= algo % 10 <= 3) or K < 4096:
+        # K = 1600: the split slices and slab round trip cost more than the half-empty
+        # last round (which the chip runs at a higher clock); profiles/gemm_tail_split.jsonl
+        return (0, 1)
+    key = ("pp", M, N, K, bm, bn, dev.index, MAX_TAIL_SPLIT)
+    p = _PLANS.get(key)
+    if p is None:
+        slots = torch.cuda.get_device_properties(dev).multi_processor_count
+        p = _PLANS[key] = tuple(kernels().gemm_tail_plan((M // bm) * (N // bn), K, 32, slots, MAX_TAIL_SPLIT))
+    return p
+
+
+def run_pp(a, b, c, layout, epi, bm, bn, bias=None, z=None, zout=None, dbias=None, algo=None):
+    """First-generation ping-pong kernel (gemm.hip) with the split-K tail."""
+    M, N = c.shape
+    K = a.shape[0] if layout == 2 else a.shape[1]
+    algo = ALGO if algo is None else algo
+    full, S = tail_plan(M, N, K, bm, bn, c.device, algo)
+    ws = cnt = None
+    if S > 1:
+        ws, cnt = _workspace(c.device, ((M // bm) * (N // bn) - full) * S * bm * bn, (M // bm) * (N // bn) - full)
+    kernels().gemm_bf16(a, b, c, layout, epi, bm, bn, bias, z, zout, dbias, 1, None, False, algo,
+                        ws, cnt, full, S)
+    return c
+
+
+# weight gradients on the stream-K ping-pong kernel (algo 5): dW (+)= dY^T X
+WGRAD_SK = os.environ.get("CAAMD_WGRAD_SK", "1") == "1"
+
+
+def wgrad_ok(M: int, N: int, K: int) -> bool:
+    """dW[M=N_out, N=K_in] over K tokens: 256 x 320 tiles, M may be ragged."""
+    return ENABLED and WGRAD_SK and M % 8 == 0 and N % 320 == 0 and K % 64 == 0 and K >= 2048
+
+
+def run_sk(a, b, c, layout: int, accumulate: bool):
+    """Stream-K launch (one run per CU): layout 2 a[K,M] b[K,N] -> c[M,N] (+)= a^T b."""
+    M, N = c.shape
+    K = a.shape[0] if layout == 2 else a.shape[1]
+    tiles = -(-M // 256) * (N // 320)
+    runs = torch.cuda.get_device_properties(c.device).multi_processor_count // 8 * 8
+    runs = max(8, min(runs, tiles * (K // 32) // 16 // 8 * 8))  # >= 16 K-steps per run
+    ws, cnt = _workspace(c.device, 2 * runs * 256 * 320, tiles)
+    kernels().gemm_bf16(a, b, c, layout, EPI_BF16_ACC if accumulate else EPI_BF16, 256, 320, None, None,
+                        None, None, 1, None, accumulate, 5, ws, cnt, 0, runs)
+    return c
+
+
 def _run(a, b, c, epi, bias=None, z=None, zout=None, dbias=None):
     M, N = c.shape
     K = a.shape[1]
+    if gen2_ok(M, N, K) and M % 256 == 0:
+        return run2(a, b, c, 0, epi, bias, z, zout, dbias)
     bm, bn = tile_for(M, N, K)
-    kernels().gemm_bf16(a, b, c, 0, epi, bm, bn, bias, z, zout, dbias, 1, None, False, ALGO)
-    return c
+    return run_pp(a, b, c, 0, epi, bm, bn, bias, z, zout, dbias)
 
 
 def linear_nt(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -99,6 +206,4 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: int = 0, *, algo: Optional[in
     if not bm:
         raise ValueError(f"no MFMA tile for M={M} N={N} K={K}")
     c = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
-    kernels().gemm_bf16(a, b, c, layout, EPI_BF16, bm, bn, None, None, None, None, 1, None, False,
-                        ALGO if algo is None else algo)
-    return c
+    return run_pp(a, b, c, layout, EPI_BF16, bm, bn, algo=algo)

@@ -33,10 +33,17 @@ void vtrace_launch(const float*, const float*, const float*, const float*, const
                    float*, int, int, float, float, hipStream_t);
 hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
                        const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
-                       int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st);
+                       int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
+                       int tfull, int tS, float* tws, int* tcnt);
+void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
+void gemm2_plan(int M, int N, int K, int slots, int max_split, int* full, int* S, int* grid,
+                long long* ws_floats, int* tickets);
+hipError_t gemm2_launch(int layout, int epi, const bf16* A, const bf16* B, bf16* C, const bf16* bias,
+                        const bf16* Z, bf16* Zout, float* dbias, float* ws, int* cnt, int M, int N, int K,
+                        int lda, int ldb, int ldc, int full, int S, int grid, hipStream_t st);
 void rl_gemm(int layout, const bf16* A, const bf16* B, void* C, const bf16* bias, const bf16* aux, int M, int N,
              int K, int lda, int ldb, int ldc, int epi, int splits, hipStream_t st);
 void rl_im2col(const void* x, bool u8, bf16* col, int B, int H, int W, int C, int KH, int KW, int S, float scale,
@@ -657,7 +664,9 @@ void add_relu_(Tensor& y, const Tensor& r) {
 static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi, int64_t bm,
                       int64_t bn, c10::optional<Tensor> bias, c10::optional<Tensor> z,
                       c10::optional<Tensor> zout, c10::optional<Tensor> dbias, int64_t splitk,
-                      c10::optional<Tensor> ws, bool accumulate, int64_t algo) {
+                      c10::optional<Tensor> ws, bool accumulate, int64_t algo,
+                      c10::optional<Tensor> tail_ws, c10::optional<Tensor> tail_cnt, int64_t tail_full,
+                      int64_t tail_split) {
   CHECK_BF16(a);
   CHECK_BF16(b);
   CHECK_BF16(c);
@@ -670,7 +679,14 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   TORCH_CHECK(Kb == K, "gemm: K mismatch");
   TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: output shape mismatch");
   TORCH_CHECK((bm == 256 && (bn == 256 || bn == 320)) || (bm == 128 && bn == 320), "gemm: tile");
-  TORCH_CHECK(M % bm == 0 && N % bn == 0 && K % 64 == 0, "gemm: M%BM, N%BN, K%64 must be 0");
+  if (algo == 5) {  // stream-K: ragged M allowed (8-aligned), bf16 / accumulate epilogues
+    TORCH_CHECK(M % 8 == 0 && N % bn == 0 && K % 64 == 0, "gemm(stream-K): M%8, N%BN, K%64 must be 0");
+    TORCH_CHECK(epi == 0 || epi == 1, "gemm(stream-K): bf16 epilogues only");
+    TORCH_CHECK(layout == 2 && bm == 256 && bn == 320, "gemm(stream-K): layout 2 with 256 x 320 tiles");
+    TORCH_CHECK(!bias.has_value() && splitk == 1, "gemm(stream-K): no bias / explicit split-K");
+  } else {
+    TORCH_CHECK(M % bm == 0 && N % bn == 0 && K % 64 == 0, "gemm: M%BM, N%BN, K%64 must be 0");
+  }
   TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm: size");
   TORCH_CHECK(splitk >= 1 && splitk <= K / 64, "gemm: splitk");
   using caamd::bf16;
@@ -710,15 +726,121 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   }
   TORCH_CHECK(splitk == 1 || ek == 2, "gemm: split-K only with the f32 partial epilogue");
   const int lda = (int)a.size(1), ldb = (int)b.size(1), ldc = (int)N;
+  float* twp = nullptr;
+  int* tcp = nullptr;
+  if (algo == 5) {
+    const int64_t tiles = ((M + bm - 1) / bm) * (N / bn);
+    const int64_t runs = tail_split;
+    TORCH_CHECK(runs >= 8 && runs % 8 == 0 && runs <= 4096, "gemm(stream-K): runs must be a multiple of 8");
+    TORCH_CHECK(tail_ws.has_value() && tail_cnt.has_value(), "gemm(stream-K): needs slabs and tickets");
+    CHECK_F32(*tail_ws);
+    TORCH_CHECK(tail_cnt->is_cuda() && tail_cnt->scalar_type() == at::kInt && tail_cnt->is_contiguous(),
+                "gemm(stream-K): tickets must be int32");
+    TORCH_CHECK(tail_ws->numel() >= 2 * runs * bm * bn, "gemm(stream-K): slab workspace too small");
+    TORCH_CHECK(tail_cnt->numel() >= tiles, "gemm(stream-K): too few tickets");
+    TORCH_CHECK(tiles * (K / 32) >= runs, "gemm(stream-K): fewer K-steps than runs");
+    twp = tail_ws->data_ptr<float>();
+    tcp = tail_cnt->data_ptr<int>();
+  } else if (tail_split > 1) {
+    const int64_t tiles = (M / bm) * (N / bn);
+    TORCH_CHECK(ek != 2 && splitk == 1, "gemm: split tail is for the bf16 epilogues");
+    TORCH_CHECK(algo % 10 >= 1 && algo % 10 <= 3, "gemm: split tail needs a ping-pong algo (1-3)");
+    TORCH_CHECK(tail_full >= 0 && tail_full < tiles && tail_full % 8 == 0 &&
+                    ((tiles - tail_full) * tail_split) % 8 == 0, "gemm: bad tail plan");
+    TORCH_CHECK(tail_ws.has_value() && tail_cnt.has_value(), "gemm: split tail needs ws and tickets");
+    CHECK_F32(*tail_ws);
+    TORCH_CHECK(tail_cnt->is_cuda() && tail_cnt->scalar_type() == at::kInt && tail_cnt->is_contiguous(),
+                "gemm: tail tickets must be int32");
+    TORCH_CHECK(tail_ws->numel() >= (tiles - tail_full) * tail_split * bm * bn, "gemm: tail workspace too small");
+    TORCH_CHECK(tail_cnt->numel() >= tiles - tail_full, "gemm: too few tail tickets");
+    TORCH_CHECK((K / 32) >= tail_split, "gemm: tail split deeper than K");
+    twp = tail_ws->data_ptr<float>();
+    tcp = tail_cnt->data_ptr<int>();
+  }
   hipError_t e = caamd::gemm_launch((int)layout, ek, (int)bm, (int)bn, (const bf16*)a.data_ptr(),
                                     (const bf16*)b.data_ptr(), cp, bp, zp, zop, dbp, (int)M, (int)N,
-                                    (int)K, lda, ldb, ldc, (int)splitk, (int)algo, cur_stream());
+                                    (int)K, lda, ldb, ldc, (int)splitk, (int)algo, cur_stream(),
+                                    (int)tail_full, (tail_split > 1 || algo == 5) ? (int)tail_split : 1, twp, tcp);
   TORCH_CHECK(e == hipSuccess, "gemm launch failed: ", hipGetErrorString(e));
   if (ek == 2) {
     caamd::gemm_splitk_reduce(ws->data_ptr<float>(), (int)splitk, M * N, (bf16*)c.data_ptr(),
                               (int)M, (int)N, ldc, accumulate, cur_stream());
     LAUNCH_CHECK();
   }
+}
+
+// ---- second-generation GEMM (gemm2.hip): 256 x 160 tiles, 2 workgroups per CU -------------
+// layout 0: a[M,K] b[N,K] · 2: a[K,M] b[K,N]. epi 0: c = acc(+bias) · 1: c += acc(+bias)
+// 3: zout = acc+bias, c = gelu(zout) · 4: c = acc*gelu'(z), dbias += colsum(c)
+static std::vector<int64_t> gemm2_plan_(int64_t M, int64_t N, int64_t K, int64_t slots, int64_t max_split) {
+  int full, S, grid, tickets;
+  long long wsf;
+  caamd::gemm2_plan((int)M, (int)N, (int)K, (int)slots, (int)max_split, &full, &S, &grid, &wsf, &tickets);
+  return {full, S, grid, (int64_t)wsf, tickets};
+}
+
+static void gemm2_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi, c10::optional<Tensor> bias,
+                       c10::optional<Tensor> z, c10::optional<Tensor> zout, c10::optional<Tensor> dbias,
+                       c10::optional<Tensor> ws, c10::optional<Tensor> cnt, int64_t full, int64_t S,
+                       int64_t grid) {
+  CHECK_BF16(a);
+  CHECK_BF16(b);
+  CHECK_BF16(c);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm2: 2-D operands");
+  TORCH_CHECK(layout == 0 || layout == 2, "gemm2: layout 0 (NT) or 2 (TN)");
+  const int64_t M = layout == 2 ? a.size(1) : a.size(0);
+  const int64_t K = layout == 2 ? a.size(0) : a.size(1);
+  const int64_t N = layout == 0 ? b.size(0) : b.size(1);
+  const int64_t Kb = layout == 0 ? b.size(1) : b.size(0);
+  TORCH_CHECK(Kb == K, "gemm2: K mismatch");
+  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm2: output shape mismatch");
+  TORCH_CHECK(M % 8 == 0 && M >= 8 && N % 160 == 0 && K % 32 == 0 && K > 0, "gemm2: M%8, N%160, K%32 must be 0");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm2: size");
+  const int64_t tiles = ((M + 255) / 256) * (N / 160);
+  TORCH_CHECK(S >= 1 && full >= 0 && full <= tiles, "gemm2: bad plan");
+  TORCH_CHECK(grid == (S > 1 ? full + (tiles - full) * S : tiles), "gemm2: grid does not match the plan");
+  TORCH_CHECK(S == 1 || (full % 8 == 0 && (grid - full) % 8 == 0), "gemm2: tail plan must be XCD-divisible");
+  using caamd::bf16;
+  const bf16* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == N, "gemm2: bias size");
+    bp = (const bf16*)bias->data_ptr();
+  }
+  const bf16* zp = nullptr;
+  bf16* zop = nullptr;
+  float* dbp = nullptr;
+  if (epi == 3) {
+    TORCH_CHECK(layout == 0 && zout.has_value() && bp, "gemm2: bias_gelu needs layout 0, bias and zout");
+    CHECK_BF16(*zout);
+    TORCH_CHECK(zout->sizes() == c.sizes(), "gemm2: zout shape");
+    zop = (bf16*)zout->data_ptr();
+  } else if (epi == 4) {
+    TORCH_CHECK(layout == 0 && z.has_value() && dbias.has_value(), "gemm2: dgelu needs layout 0, z, dbias");
+    CHECK_BF16(*z);
+    CHECK_F32(*dbias);
+    TORCH_CHECK(z->sizes() == c.sizes() && dbias->numel() == N, "gemm2: z / dbias shape");
+    zp = (const bf16*)z->data_ptr();
+    dbp = dbias->data_ptr<float>();
+  } else {
+    TORCH_CHECK(epi == 0 || epi == 1, "gemm2: bad epilogue");
+  }
+  float* wsp = nullptr;
+  int* cp = nullptr;
+  if (S > 1) {
+    TORCH_CHECK(ws.has_value() && cnt.has_value(), "gemm2: split tail needs ws and cnt");
+    CHECK_F32(*ws);
+    TORCH_CHECK(cnt->is_cuda() && cnt->scalar_type() == at::kInt && cnt->is_contiguous(), "gemm2: cnt int32");
+    TORCH_CHECK(ws->numel() >= (tiles - full) * S * 256 * 160, "gemm2: workspace too small");
+    TORCH_CHECK(cnt->numel() >= tiles - full, "gemm2: too few tickets");
+    wsp = ws->data_ptr<float>();
+    cp = cnt->data_ptr<int>();
+  }
+  hipError_t e = caamd::gemm2_launch((int)layout, (int)epi, (const bf16*)a.data_ptr(), (const bf16*)b.data_ptr(),
+                                     (bf16*)c.data_ptr(), bp, zp, zop, dbp, wsp, cp, (int)M, (int)N, (int)K,
+                                     (int)a.size(1), (int)b.size(1), (int)N, (int)full, (int)S, (int)grid,
+                                     cur_stream());
+  TORCH_CHECK(e == hipSuccess, "gemm2 launch failed: ", hipGetErrorString(e));
 }
 
 static Tensor transpose_bf16(const Tensor& x) {
@@ -882,7 +1004,16 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("layout"), pybind11::arg("epi"), pybind11::arg("bm"), pybind11::arg("bn"),
         pybind11::arg("bias"), pybind11::arg("z"), pybind11::arg("zout"), pybind11::arg("dbias"),
         pybind11::arg("splitk"), pybind11::arg("ws"), pybind11::arg("accumulate"),
-        pybind11::arg("algo") = 1);
+        pybind11::arg("algo") = 1, pybind11::arg("tail_ws") = pybind11::none(),
+        pybind11::arg("tail_cnt") = pybind11::none(), pybind11::arg("tail_full") = -1,
+        pybind11::arg("tail_split") = 1);
+  m.def("gemm_tail_plan", [](int64_t tiles, int64_t K, int64_t ks, int64_t slots, int64_t max_split) {
+    int full, S;
+    caamd::gemm_tail_plan((int)tiles, (int)K, (int)ks, (int)slots, (int)max_split, &full, &S);
+    return std::vector<int64_t>{full, S};
+  });
+  m.def("gemm2_plan", &gemm2_plan_);
+  m.def("gemm2_bf16", &gemm2_bf16);
   m.def("transpose_bf16", &transpose_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

@@ -161,6 +161,29 @@ __device__ __forceinline__ bf16x8_t frag_mmaj(const lds_char* img, int rr, int k
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// frag_mmaj by inline asm: hipcc treats the tr16 BUILTIN as possibly aliasing an
+// in-flight LDS-DMA and emits s_waitcnt vmcnt(0) before it, which drains the DMA
+// prefetch on every K-step (measured in the stream-K weight-gradient kernel's ISA;
+// the D = 64 attention kernels hit the same). The asm reads are invisible to the
+// compiler's counters: every batch ends in tr_wait(), an lgkmcnt(0) that names the
+// destination registers, so nothing reads them before the data has landed.
+template <int R>
+__device__ __forceinline__ bf16x8_t frag_mmaj_asm(const lds_char* img, int rr, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int m = rr + 4 * p;
+  const int chunk = m >> 3;
+  const int within = (p & 1) * 8;
+  const int k0 = 8 * g + q, k1 = 8 * g + 4 + q;
+  const unsigned a0 = (unsigned)(size_t)(img + k0 * (R * 2) + (chunk ^ mswz<R>(k0)) * 16 + within);
+  const unsigned a1 = (unsigned)(size_t)(img + k1 * (R * 2) + (chunk ^ mswz<R>(k1)) * 16 + within);
+  s16x4 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
 struct Args {
   const bf16* A;
   const bf16* B;
@@ -175,6 +198,12 @@ struct Args {
   int tiles_m, tiles_n;
   long long slab;     // elements between split-K slabs
   int algo;           // 0: 2-stage BK=64 kernel, 1: ping-pong BK=32 4-stage kernel
+  // split-K TAIL (pp kernel): tiles [tfull, T) -- the ones past the last full round
+  // of CUs -- are each split over tS K-slices; slices publish fp32 slabs to tws and
+  // the last arriver (ticket in tcnt, reset by it) combines and runs the epilogue.
+  int tfull, tS;
+  float* tws;
+  int* tcnt;
 };
 
 // Output tile staged through LDS: the MFMA fragments (each lane: 4 columns of one
@@ -237,6 +266,7 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
       if (ir >= HR) break;
       const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
       const int m = m0 + wr_ * (TM * 16) + h * (TMH * 16) + rem;
+      if (m >= p.M) continue;  // ragged M (stream-K weight-gradient tiles)
       bf16x8_t v = *(lds_bf16x8*)(smem + ir * ROWB + c * 16);
       const size_t off = (size_t)m * p.ldc + n;
       float f[8];
@@ -581,14 +611,33 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
 
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
-  int sid;
+  int slice, tile, nsplit;
+  bool tail = false;
   {
     const int xcd = bid & 7, loc = bid >> 3;
-    const int q = nwg >> 3, r = nwg & 7;
-    sid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+    if (p.tS > 1) {
+      // whole tiles: 1/8 per XCD (contiguous); then 1/8 of the tail slices per XCD,
+      // dispatched last on every XCD (the slices of one tile stay on one XCD)
+      const int nfx = p.tfull >> 3, ntx = (nwg - p.tfull) >> 3;
+      if (loc < nfx) {
+        tile = xcd * nfx + loc;
+        slice = 0;
+        nsplit = 1;
+      } else {
+        const int s = xcd * ntx + (loc - nfx);
+        tile = p.tfull + s / p.tS;
+        slice = s - (s / p.tS) * p.tS;
+        nsplit = p.tS;
+        tail = true;
+      }
+    } else {
+      const int q = nwg >> 3, r = nwg & 7;
+      const int sid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+      slice = sid % p.splitk;
+      tile = sid / p.splitk;
+      nsplit = p.splitk;
+    }
   }
-  const int slice = sid % p.splitk;
-  const int tile = sid / p.splitk;
   constexpr int GROUP_M = 8;
   const int group_sz = GROUP_M * p.tiles_n;
   const int g = tile / group_sz;
@@ -600,9 +649,9 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int ns_total = p.K / KS;
-  const int per = (ns_total + p.splitk - 1) / p.splitk;
+  const int per = (ns_total + nsplit - 1) / nsplit;
   const int s0 = slice * per;
-  const int nk = min(ns_total, s0 + per) - s0;
+  const int nk = max(0, min(ns_total, s0 + per) - s0);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -689,6 +738,48 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
       }
     }
     if (lo_grp) __builtin_amdgcn_s_barrier();  // equal barrier counts for both rows
+  }
+  if constexpr (EPI != EPI_F32) {
+    if (tail) {
+      // ---- split-K tail: publish this slice; the last arriver combines -----------
+      // (release/acquire ticket: cdna_hip_programming.md §5 "Projection GEMM" item 2)
+      const int tt = tile - p.tfull;
+      constexpr int SLAB = BM * BN;
+      float* mine = p.tws + ((size_t)tt * p.tS + slice) * SLAB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      typedef __attribute__((address_space(3))) int lds_int;
+      lds_int* flag = (lds_int*)smem;
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(p.tcnt + tt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == p.tS - 1;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          p.tcnt[tt] = 0;  // ready for the next launch
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      const int last = *flag;
+      if (!last) return;
+      for (int s = 0; s < p.tS; ++s) {
+        if (s == slice) continue;
+        const float* other = p.tws + ((size_t)tt * p.tS + s) * SLAB;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] += *reinterpret_cast<const f32x4*>(other + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4);
+      }
+    }
   }
   if constexpr (EPI == EPI_F32) epilogue<BM, BN, TM, TN, EPI>(p, acc, m0, n0, wr, wc, lane, slice);
   else epilogue_staged<BM, BN, TM, TN, EPI, ABL>(p, acc, m0, n0, wr, wc, lane, smem, tid);
@@ -824,6 +915,213 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persist_kernel(Args p) {
   }
 }
 
+
+// ================================================================================
+// Stream-K ping-pong kernel (weight gradients: K = tokens = 32768, only 95-280
+// output tiles of 256 x 320 for 256 CUs). Grid = the CUs (one 147 KB workgroup
+// each); the tiles x K-steps iteration space is cut into gridDim.x equal runs, so
+// every CU streams the same number of K-steps. A run covers the end of one tile,
+// possibly whole tiles, and the start of another; a tile computed by one run gets
+// the normal epilogue, a tile shared by several runs is combined by its LAST
+// arriving contributor (agent-scope release -> ticket -> acquire; the others only
+// publish an fp32 slab and move on), so no workgroup ever waits for another and
+// nothing depends on co-residency. Each run has at most two partial tiles (its
+// first and its last): slab slot 2*g (first) / 2*g+1 (last).
+// Ragged M (1600 / 4800 output rows): A columns past M are clamped on load and
+// never stored. Same R / M segments, counted vmcnt and wave-row stagger as
+// gemm_pp_kernel (one phase per 32-deep K-step, DMA two steps ahead).
+// ================================================================================
+template <int BM, int BN, bool AK, bool BK_, int EPI>
+__global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
+  constexpr int WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int KS = 32, NST = 4, DIST = 2;
+  constexpr int A_ST = BM * KS * 2, B_ST = BN * KS * 2, ST = A_ST + B_ST;
+  static_assert(A_ST % 1024 == 0 && B_ST % 1024 == 0, "stage must be whole KiB");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const bool lo_grp = wr == 0;
+
+  const int G = gridDim.x;  // multiple of 8 (host)
+  const int g = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);  // consecutive runs on one XCD
+  const int nk_tile = p.K / KS;
+  const long long W = (long long)p.tiles_m * p.tiles_n * nk_tile;
+  const long long r0 = (long long)g * W / G, r1 = (long long)(g + 1) * W / G;
+  auto run_start = [&](int gg) { return (long long)gg * W / G; };
+  // first run containing global step x: largest gg with run_start(gg) <= x
+  auto run_of = [&](long long x) { return (int)(((x + 1) * G + W - 1) / W - 1); };
+
+  constexpr int CNT_LO = dma_count32<BM>(0) + dma_count32<BN>(0);
+  constexpr int CNT_HI = dma_count32<BM>(4) + dma_count32<BN>(4);
+  static_assert(dma_count32<BM>(3) == dma_count32<BM>(0) && dma_count32<BN>(3) == dma_count32<BN>(0), "");
+  static_assert(dma_count32<BM>(7) == dma_count32<BM>(4) && dma_count32<BN>(7) == dma_count32<BN>(4), "");
+  auto wait_ahead = [&](int newer) {
+    if (newer >= 1) {
+      if (lo_grp) wait_vm<CNT_LO>(); else wait_vm<CNT_HI>();
+    } else {
+      wait_vm<0>();
+    }
+  };
+  const int a_last = AK ? p.M - 1 : p.M - 8;
+  typedef __attribute__((address_space(3))) int lds_int;
+
+  long long x = r0;
+  while (x < r1) {
+    const int tile = (int)(x / nk_tile);
+    const int s0 = (int)(x - (long long)tile * nk_tile);
+    const long long tile_end = (long long)(tile + 1) * nk_tile;
+    const int nk = (int)((r1 < tile_end ? r1 : tile_end) - x);
+    x += nk;
+    constexpr int GROUP_M = 8;
+    const int group_sz = GROUP_M * p.tiles_n;
+    const int gq = tile / group_sz;
+    const int first_m = gq * GROUP_M;
+    const int gm = min(p.tiles_m - first_m, GROUP_M);
+    const int tin = tile - gq * group_sz;
+    const int m0 = (first_m + tin % gm) * BM, n0 = (tin / gm) * BN;
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto dma = [&](int t) {
+      lds_char* base = smem + (t & (NST - 1)) * ST;
+      const int k0 = (s0 + t) * KS;
+      // A: clamp rows (K-major) / 8-aligned columns (MN-major) past M
+      {
+        constexpr int BYTES = BM * 32 * 2, FULL = BYTES / (NTHR * 16);
+        static_assert(BYTES % (NTHR * 16) == 0, "A stage must be whole rounds");
+#pragma unroll
+        for (int j = 0; j < FULL; ++j) {
+          const int lin = j * NTHR + wid * 64 + lane;
+          const bf16* src;
+          if constexpr (AK) {
+            const int row = lin >> 2, pos = lin & 3;
+            const int c = pos ^ kswz64(row);
+            src = p.A + (size_t)min(m0 + row, a_last) * p.lda + k0 + c * 8;
+          } else {
+            constexpr int CPR = BM / 8;
+            const int k = lin / CPR, pos = lin - k * CPR;
+            const int c = pos ^ mswz<BM>(k);
+            src = p.A + (size_t)(k0 + k) * p.lda + min(m0 + c * 8, a_last);
+          }
+          __builtin_amdgcn_global_load_lds((const void*)src,
+                                           (void __attribute__((address_space(3)))*)(base + (j * NTHR + wid * 64) * 16),
+                                           16, 0, 0);
+        }
+      }
+      dma_step32<BN, BK_>(p.B, p.ldb, n0, k0, base + A_ST, wid, lane);
+    };
+
+    __syncthreads();  // the previous segment's epilogue / slab reads are done with the LDS
+    dma(0);
+    if (nk > 1) dma(1);
+    wait_ahead(min(nk, DIST) - 1);
+    __builtin_amdgcn_s_barrier();
+    if (!lo_grp) __builtin_amdgcn_s_barrier();
+    // two phases per K-step (m-halves), as gemm_pp_kernel with PH = 2: half the A
+    // fragments live at a time (the MN-major tr16 reads otherwise spill at 256 VGPRs)
+    constexpr int PH = 2, TMH = TM / PH;
+    bf16x8_t bf[TN];
+    bf16x8_t af[TMH];
+    for (int t = 0; t < nk; ++t) {
+      const lds_char* As = smem + (t & (NST - 1)) * ST;
+      const lds_char* Bs = As + A_ST;
+#pragma unroll
+      for (int mh = 0; mh < PH; ++mh) {
+        if (mh == 0) {
+          if (t + DIST < nk) dma(t + DIST);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int rr = wc * (TN * 16) + j * 16;
+            if constexpr (BK_) bf[j] = frag_kmaj64(Bs, rr, lane);
+            else bf[j] = frag_mmaj_asm<BN>(Bs, rr, lane);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TMH; ++i) {
+          const int rr = wr * (TM * 16) + (mh * TMH + i) * 16;
+          if constexpr (AK) af[i] = frag_kmaj64(As, rr, lane);
+          else af[i] = frag_mmaj_asm<BM>(As, rr, lane);
+        }
+        if (mh == PH - 1) wait_ahead(min(nk - 1, t + DIST) - (t + 1));
+        static_assert(TN == 5 && TMH == 4, "tr_wait below names 5 B and 4 A fragments");
+        if (mh == 0)
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(bf[0]), "+v"(bf[1]), "+v"(bf[2]), "+v"(bf[3]), "+v"(bf[4]), "+v"(af[0]), "+v"(af[1]),
+                         "+v"(af[2]), "+v"(af[3])::"memory");
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3])::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TMH; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[mh * TMH + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (lo_grp) __builtin_amdgcn_s_barrier();
+
+    if (nk < nk_tile) {
+      // ---- shared tile: publish, and combine if this is the last contributor -----
+      const long long t_first = (long long)tile * nk_tile;
+      const int c0 = run_of(t_first), c1 = run_of(tile_end - 1);
+      constexpr int SLAB = BM * BN;
+      auto slot_of = [&](int gg) {  // a run's first tile uses slot 2g, its last 2g+1
+        return 2 * gg + ((run_start(gg) / nk_tile) == tile ? 0 : 1);
+      };
+      float* mine = p.tws + (size_t)slot_of(g) * SLAB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      lds_int* flag = (lds_int*)smem;
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add(p.tcnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == c1 - c0;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          p.tcnt[tile] = 0;  // ready for the next launch
+        }
+        *flag = last;
+      }
+      __syncthreads();
+      const int last = *flag;
+      if (!last) continue;
+      for (int gg = c0; gg <= c1; ++gg) {
+        if (gg == g) continue;
+        const float* other = p.tws + (size_t)slot_of(gg) * SLAB;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] += *reinterpret_cast<const f32x4*>(other + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4);
+      }
+    }
+    epilogue_staged<BM, BN, TM, TN, EPI, 0>(p, acc, m0, n0, wr, wc, lane, smem, tid);
+  }
+}
+
 // Split-K combine: out(bf16) [+]= sum_s slab_s (+ bias); f32 partials [S][M][ldc].
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S,
                                                             long long slab, bf16* __restrict__ out,
@@ -889,7 +1187,19 @@ static hipError_t launch_t(const Args& a, hipStream_t st) {
 template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL>
 static hipError_t launch_abl(const Args& a, hipStream_t st) {
   using C_ = Cfg<BM, BN, AK, BK_>;
-  const int grid = a.tiles_m * a.tiles_n * a.splitk;
+  const int T = a.tiles_m * a.tiles_n;
+  const int grid = a.tS > 1 ? a.tfull + (T - a.tfull) * a.tS : T * a.splitk;
+  if (a.tS > 1 && !(a.algo % 10 >= 1 && a.algo % 10 <= 3) && a.algo != 5) return hipErrorInvalidValue;
+  if (a.algo == 5) {  // stream-K: the weight-gradient layout (TN) on 256 x 320 tiles only
+    if constexpr ((EPI == EPI_BF16 || EPI == EPI_BF16_ACC) && BM == 256 && BN == 320 && !AK && !BK_) {
+      auto k = gemm_sk_kernel<BM, BN, AK, BK_, EPI>;
+      constexpr int lds = 4 * (BM + BN) * 32 * 2;
+      ensure_lds((const void*)k, lds);
+      hipLaunchKernelGGL(k, dim3(a.tS), dim3(NTHR), lds, st, a);  // tS = number of runs
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (a.algo % 10 == 4 && a.splitk == 1) {
     auto k = gemm_persist_kernel<BM, BN, AK, BK_, EPI>;
     constexpr int lds = 4 * (BM + BN) * 32 * 2;
@@ -967,13 +1277,33 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 // Host entry: shapes are validated by the caller (bindings.cpp).
 hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
                        const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
-                       int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st) {
-  gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk, M / bm, N / bn,
-               (long long)M * ldc, algo};
+                       int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
+                       int tfull, int tS, float* tws, int* tcnt) {
+  gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk,
+               algo == 5 ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt};
   if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
   if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);
   if (bm == 128 && bn == 320) return gemm::launch_epi<128, 320>(layout, epi, a, st);
   return hipErrorInvalidValue;
+}
+
+// Split-K tail plan for a grid of whole tiles over `slots` resident workgroups: the
+// tiles past the last full round are split into S K-slices (S <= max_split, >= 8
+// K-steps of `ks` per slice, tail workgroups divisible over the 8 XCDs).
+void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S) {
+  int f = tiles, s = 1;
+  const int tail = tiles % slots;
+  if (max_split > 1 && tail > 0 && tail * 2 <= slots) {
+    int cand = slots / tail;
+    if (cand > max_split) cand = max_split;
+    while (cand > 1 && ((K / ks) / cand < 8 || (tail * cand) % 8 != 0)) --cand;
+    if (cand > 1 && (tiles - tail) % 8 == 0) {
+      f = tiles - tail;
+      s = cand;
+    }
+  }
+  *full = f;
+  *S = s;
 }
 
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st) {

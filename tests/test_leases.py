@@ -154,3 +154,58 @@ def test_cancel_leased_task(cluster):
         ray.get(refs[-1], timeout=60)
     for r in refs[:-1]:
         ray.cancel(r)
+
+
+@ray.remote
+class _Signal:
+    def __init__(self):
+        self.set_ = False
+
+    def send(self):
+        self.set_ = True
+
+    def is_set(self):
+        return self.set_
+
+
+def test_waiters_then_sender_do_not_deadlock(cluster):
+    """Several waiters and then the task that releases them, all from one owner:
+    queued tasks behind a blocked leased task must not be stranded on its worker
+    (in-flight depth > 1 pipelined the sender behind a waiter)."""
+    sig = _Signal.remote()
+
+    @ray.remote
+    def wait_for(s):
+        deadline = time.time() + 60
+        while not ray.get(s.is_set.remote()):
+            if time.time() > deadline:
+                return "timeout"
+            time.sleep(0.01)
+        return "ok"
+
+    @ray.remote
+    def send(s):
+        ray.get(s.send.remote())
+        return "sent"
+
+    waiters = [wait_for.remote(sig) for _ in range(3)]
+    sender = send.remote(sig)
+    assert ray.get(sender, timeout=60) == "sent"
+    assert ray.get(waiters, timeout=60) == ["ok"] * 3
+
+
+def test_force_cancel_spares_queued_neighbours(cluster):
+    """A force-cancel ends the leased worker; tasks queued behind the victim on that
+    worker go back to the owner without spending an attempt (max_retries=0)."""
+    @ray.remote(max_retries=0)
+    def nap(t, i):
+        time.sleep(t)
+        return i
+
+    victim = nap.remote(30.0, -1)
+    others = [nap.remote(0.2, i) for i in range(16)]
+    time.sleep(0.5)
+    ray.cancel(victim, force=True)
+    with pytest.raises(TaskCancelledError):
+        ray.get(victim, timeout=60)
+    assert ray.get(others, timeout=60) == list(range(16))
