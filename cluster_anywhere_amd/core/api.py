@@ -441,9 +441,8 @@ def kill(actor, *, no_restart: bool = True):
     w.send(("kill_actor", actor._actor_id, no_restart))
     # later calls from this process go through the head, which orders them after the
     # kill (a still-open direct connection would reach the actor before it dies)
-    head_only = getattr(w, "actor_head_only", None)
-    if head_only is not None:
-        head_only.add(actor._actor_id)
+    if getattr(w, "actor_head_only", None) is not None:
+        w._to_head_path(actor._actor_id, drop=True)
 
 
 def cancel(ref, *, force: bool = False, recursive: bool = True):

@@ -124,6 +124,7 @@ class DirectClient:
         self.out = BatchSender(self.conn, "caamd-direct-send")
         self.alive = True
         self.lock = threading.Lock()
+        self.idle = threading.Condition(self.lock)
         self.pending: Dict[bytes, tuple] = {}  # task_id -> (spec, keep-alive refs, t_submit)
         self.sent_fns = set()
         threading.Thread(target=self._read, name="caamd-direct-client", daemon=True).start()
@@ -156,6 +157,8 @@ class DirectClient:
                 retryable = msg[7] if len(msg) > 7 else False
                 with self.lock:
                     rec = self.pending.pop(task_id, None)
+                    if not self.pending:
+                        self.idle.notify_all()
                 if rec is None:
                     continue
                 if self.sink is not None:
@@ -166,10 +169,23 @@ class DirectClient:
             self.alive = False
             recs = sorted(self.pending.values(), key=lambda r: r[2])
             self.pending.clear()
+            self.idle.notify_all()
         if self.sink is not None:
             self.sink._lost(self, [r[0] for r in recs])
         else:
             self.worker._on_direct_lost(self.actor_id, [r[0] for r in recs])
+
+    def wait_idle(self, timeout: float) -> bool:
+        """Block until every call sent on this connection has been answered (or the
+        connection died). False on timeout."""
+        deadline = time.time() + timeout
+        with self.lock:
+            while self.pending and self.alive:
+                left = deadline - time.time()
+                if left <= 0:
+                    return False
+                self.idle.wait(min(left, 1.0))
+        return True
 
     def close(self):
         self.alive = False

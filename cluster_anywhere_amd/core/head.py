@@ -52,6 +52,21 @@ def _node_labels(node_hex, gpu_ids, labels):
     return out
 
 
+
+# Environment variables read when an interpreter (or a library it imports at
+# start-up: torch, OpenMP, MKL, the dynamic loader) starts. A worker forked from the
+# zygote already runs with the zygote's values, so a runtime_env that sets any of
+# them gets a fresh process.
+_START_TIME_ENV = ("PYTHON", "LD_", "OMP_", "MKL_", "OPENBLAS_", "GOMP_", "KMP_", "MALLOC_", "TORCH_")
+
+
+def _needs_fresh_interpreter(renv) -> bool:
+    if not renv:
+        return False
+    if renv.get("pip") or renv.get("uv") or renv.get("conda") or renv.get("py_executable"):
+        return True
+    return any(k.startswith(_START_TIME_ENV) for k in (renv.get("env_vars") or {}))
+
 class TaskSpec:
     """Everything the head needs to schedule, run, retry and report a task."""
 
@@ -1086,6 +1101,8 @@ class Head:
         e["CAAMD_SYS_PATH"] = os.pathsep.join(p for p in sys.path if p and os.path.isdir(p))
         log_path = os.path.join(self.session_dir, f"worker-{worker_id.hex()[:8]}.log")
         zyg = getattr(self, "_zygote", None)
+        if zyg is not None and _needs_fresh_interpreter(renv):
+            zyg = None  # start-time variables / another interpreter: a fork cannot honour them
         proc = zyg.spawn(e, log_path, os.getcwd()) if zyg is not None else None
         if proc is None:
             log = open(log_path, "ab")

@@ -360,12 +360,14 @@ class CoreWorker:
         """The actor's DirectClient, or None to use the head path (see core/direct.py)."""
         from .direct import DirectClient, addr_usable
 
+        if actor_id in self.actor_head_only:
+            return None  # killed, or a streaming call went through the head: stay there
         st = self.actor_direct.get(actor_id)
         if st is not None and not isinstance(st, tuple):
             if st.alive:
                 return st
             st = None
-        if actor_id in self.actor_head_only or self.actor_head_inflight.get(actor_id):
+        if self.actor_head_inflight.get(actor_id):
             return None
         now = time.monotonic()
         if st is not None and now - st[1] < 0.05:
@@ -384,6 +386,21 @@ class CoreWorker:
                 return dc
         self.actor_direct[actor_id] = ("head", now)
         return None
+
+    def _to_head_path(self, actor_id, drop: bool = False):
+        """Route this caller's later calls to ``actor_id`` through the head. Calls
+        already sent on the direct connection finish first, so the caller's FIFO
+        order holds across the switch (the head path cannot overtake them); with
+        ``drop`` (ray.kill) the connection is closed instead of drained."""
+        self.actor_head_only.add(actor_id)
+        dc = self.actor_direct.get(actor_id)
+        if dc is None or isinstance(dc, tuple):
+            return
+        if drop:
+            self.actor_direct[actor_id] = ("head", 0.0)
+            dc.close()
+            return
+        dc.wait_idle(timeout=float(os.environ.get("CAAMD_DIRECT_DRAIN_S", "600")))
 
     def _on_direct_done(self, spec, results, timing):
         from .direct import result_kinds
@@ -914,7 +931,7 @@ class CoreWorker:
                     r.direct_pending.difference_update(return_ids)
         elif kind == ACTOR_METHOD:
             if generator is not None:
-                self.actor_head_only.add(actor_id)
+                self._to_head_path(actor_id)
             elif self.actor_direct is not None:
                 dc = self._direct_for(actor_id)
                 if dc is not None:

@@ -139,18 +139,44 @@ def run_pp(a, b, c, layout, epi, bm, bn, bias=None, z=None, zout=None, dbias=Non
 WGRAD_SK = os.environ.get("CAAMD_WGRAD_SK", "1") == "1"
 
 
-def wgrad_ok(M: int, N: int, K: int) -> bool:
-    """dW[M=N_out, N=K_in] over K tokens: 256 x 320 tiles, M may be ragged."""
-    return ENABLED and WGRAD_SK and M % 8 == 0 and N % 320 == 0 and K % 64 == 0 and K >= 2048
+# (N_out, K_in) -> runs where the kernel measured faster than hipBLASLt at 32768
+# tokens (profiles/wgrad_stream_k.jsonl): GPT-2-XL fc (6400 x 1600, lockstep split-K
+# 2) and attention proj (1600 x 1600, 245 runs). qkv and fc2 stay on hipBLASLt.
+WGRAD_WINNERS = {(6400, 1600): 250, (1600, 1600): 245}
 
 
-def run_sk(a, b, c, layout: int, accumulate: bool):
-    """Stream-K launch (one run per CU): layout 2 a[K,M] b[K,N] -> c[M,N] (+)= a^T b."""
+def wgrad_runs(M: int, N: int, K: int) -> Optional[int]:
+    """Runs for dW[M=N_out, N=K_in] over K tokens on the weight-gradient kernel, or
+    None to keep the library GEMM."""
+    if not (ENABLED and WGRAD_SK) or M % 8 or N % 320 or K % 64 or K < 16384:
+        return None
+    return WGRAD_WINNERS.get((M, N))
+
+
+def sk_runs(M: int, N: int, K: int, dev: torch.device) -> int:
+    """Runs for the weight-gradient kernel: lockstep split-K, tiles x S <= CUs with S
+    dividing the K-steps (every block then streams the same token window at the same
+    time, so the dY / X panels are read from HBM once and shared through L2 / MALL);
+    stream-K over all CUs scatters the runs over the tokens and measured HBM-bound
+    (profiles/wgrad_stream_k.jsonl)."""
+    tiles = -(-M // 256) * (N // 320)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    nk = K // 32
+    S = max(1, cus // tiles)
+    while S > 1 and nk % S:
+        S -= 1
+    return tiles * S
+
+
+def run_sk(a, b, c, layout: int, accumulate: bool, runs: Optional[int] = None):
+    """Weight-gradient launch: layout 2 a[K,M] b[K,N] -> c[M,N] (+)= a^T b, the
+    tiles x K-steps space cut into `runs` equal runs (stream-K; split-K when runs =
+    tiles x S)."""
     M, N = c.shape
     K = a.shape[0] if layout == 2 else a.shape[1]
     tiles = -(-M // 256) * (N // 320)
-    runs = torch.cuda.get_device_properties(c.device).multi_processor_count // 8 * 8
-    runs = max(8, min(runs, tiles * (K // 32) // 16 // 8 * 8))  # >= 16 K-steps per run
+    if runs is None:
+        runs = sk_runs(M, N, K, c.device)
     ws, cnt = _workspace(c.device, 2 * runs * 256 * 320, tiles)
     kernels().gemm_bf16(a, b, c, layout, EPI_BF16_ACC if accumulate else EPI_BF16, 256, 320, None, None,
                         None, None, 1, None, accumulate, 5, ws, cnt, 0, runs)

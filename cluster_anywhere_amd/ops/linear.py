@@ -6,8 +6,10 @@ Forward and input-gradient GEMMs run on the hand-written MFMA kernels
 (GPT-2-XL: every projection), with the bias add fused into the epilogue; the
 input gradient ``dX = dY @ W`` runs as an NT GEMM against ``W^T`` (one 64x64-tile
 transpose per weight per step, ~1 ms for all of GPT-2-XL) so both operands stream
-K-major. ``dW += dY^T X`` accumulates with ``addmm_`` (hipBLASLt, beta = 1)
-directly into ``weight.main_grad`` — a view of the flat grad buffer — and
+K-major. ``dW += dY^T X`` accumulates directly into ``weight.main_grad`` — a view
+of the flat grad buffer — on the split-K / stream-K weight-gradient kernel of
+gemm.hip for the shapes where it measured faster (``gemm.WGRAD_WINNERS``), else
+with ``addmm_`` (hipBLASLt, beta = 1); and
 ``db += colsum(dY)`` with the HIP ``bias_grad_`` kernel, then the parameter is
 signalled ready to the bucketed reducer. Autograd's AccumulateGrad (a
 read-modify-write of every gradient) and torch's generic bias reduction are
@@ -38,7 +40,13 @@ def _ready(p):
 def _wgrad(w, dy2, x2, needs):
     mg = getattr(w, "main_grad", None)
     if mg is not None:
-        mg.addmm_(dy2.t(), x2)
+        runs = None
+        if mg.is_cuda and mg.dtype == torch.bfloat16 and _g._ok(dy2, x2, mg):
+            runs = _g.wgrad_runs(mg.shape[0], mg.shape[1], dy2.shape[0])
+        if runs is not None:
+            _g.run_sk(dy2, x2, mg, 2, True, runs=runs)  # dW += dY^T X (gemm.hip, split-K / stream-K)
+        else:
+            mg.addmm_(dy2.t(), x2)
         _ready(w)
         return None
     return dy2.t() @ x2 if needs else None

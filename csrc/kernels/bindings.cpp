@@ -731,7 +731,7 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   if (algo == 5) {
     const int64_t tiles = ((M + bm - 1) / bm) * (N / bn);
     const int64_t runs = tail_split;
-    TORCH_CHECK(runs >= 8 && runs % 8 == 0 && runs <= 4096, "gemm(stream-K): runs must be a multiple of 8");
+    TORCH_CHECK(runs >= 1 && runs <= 4096, "gemm(stream-K): 1 <= runs <= 4096");
     TORCH_CHECK(tail_ws.has_value() && tail_cnt.has_value(), "gemm(stream-K): needs slabs and tickets");
     CHECK_F32(*tail_ws);
     TORCH_CHECK(tail_cnt->is_cuda() && tail_cnt->scalar_type() == at::kInt && tail_cnt->is_contiguous(),

@@ -947,8 +947,12 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
   const int wr = wid >> 2, wc = wid & 3;
   const bool lo_grp = wr == 0;
 
-  const int G = gridDim.x;  // multiple of 8 (host)
-  const int g = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);  // consecutive runs on one XCD
+  const int G = gridDim.x;
+  int g;  // consecutive runs on one XCD (bijective for any G)
+  {
+    const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q = G >> 3, r = G & 7;
+    g = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
   const int nk_tile = p.K / KS;
   const long long W = (long long)p.tiles_m * p.tiles_n * nk_tile;
   const long long r0 = (long long)g * W / G, r1 = (long long)(g + 1) * W / G;

@@ -210,6 +210,7 @@ PYBIND11_MODULE(_native, m) {
       .def("clear_table", &GcsStore::clear_table)
       .def("sync", &GcsStore::sync)
       .def("compact", &GcsStore::compact)
+      .def("_inject_write_fault", &GcsStore::inject_write_fault)
       .def_property_readonly("log_bytes", &GcsStore::log_bytes)
       .def_property_readonly("live_bytes", &GcsStore::live_bytes)
       .def_property_readonly("records_replayed", &GcsStore::records_replayed)

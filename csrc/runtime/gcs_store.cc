@@ -3,6 +3,7 @@
 // Record layout (little endian):
 //   u32 magic 'GCS1' | u8 op (1 put, 2 del, 3 clear-table) | u32 table_len |
 //   u32 key_len | u32 value_len | table | key | value | u32 crc32(op .. value)
+#include <algorithm>
 #include "gcs_store.h"
 
 #include <fcntl.h>
@@ -149,7 +150,24 @@ void GcsStore::replay() {
 
 void GcsStore::append(uint8_t op, const std::string& table, const std::string& key, const std::string& value) {
   const std::string r = encode(op, table, key, value);
-  write_all(fd_, r);
+  try {
+    if (fault_after_ >= 0) {  // test hook: a short write, then the failure
+      const size_t n = std::min((size_t)fault_after_, r.size());
+      fault_after_ = -1;
+      write_all(fd_, r.substr(0, n));
+      throw std::runtime_error("GcsStore: write failed: injected short write");
+    }
+    write_all(fd_, r);
+  } catch (...) {
+    // A partial record must not stay in the middle of the log: replay stops at the
+    // first bad record, so every later append behind it would be lost on restart.
+    // Cut the file back to the last whole record and put the offset there.
+    if (::ftruncate(fd_, (off_t)log_bytes_) != 0) {
+      throw std::runtime_error("GcsStore: write failed and the partial record could not be removed");
+    }
+    ::lseek(fd_, (off_t)log_bytes_, SEEK_SET);
+    throw;
+  }
   if (fsync_each_) ::fdatasync(fd_);
   log_bytes_ += r.size();
 }

@@ -42,6 +42,9 @@ class GcsStore {
   uint64_t records_replayed() const { return replayed_; }
   uint64_t torn_bytes_dropped() const { return torn_; }
   const std::string& path() const { return path_; }
+  // Test hook: the next append writes only `bytes` bytes of its record and then
+  // fails as a short write / ENOSPC would (-1 disables).
+  void inject_write_fault(int64_t bytes) { fault_after_ = bytes; }
 
  private:
   void replay();
@@ -54,6 +57,7 @@ class GcsStore {
   bool fsync_each_;
   int fd_ = -1;
   uint64_t log_bytes_ = 0, live_bytes_ = 0, replayed_ = 0, torn_ = 0;
+  int64_t fault_after_ = -1;
   std::unordered_map<std::string, std::unordered_map<std::string, std::string>> tables_;
   mutable std::mutex mu_;
 };

@@ -131,3 +131,54 @@ def test_actor_death_with_retries_resubmits(cluster):
     out = ray.get(refs, timeout=120)
     assert len(out) == 20  # every call completed (some on the restarted actor)
     assert ray.get(a.pid.remote(), timeout=60) != pid
+
+
+@ray.remote
+class SlowLog:
+    def __init__(self):
+        self.items = []
+
+    def add(self, x):
+        time.sleep(0.002)
+        self.items.append(x)
+        return x
+
+    def stream(self, n):
+        self.items.append("gen")
+        for i in range(n):
+            yield i
+
+    def get(self):
+        return list(self.items)
+
+
+def test_order_direct_generator_direct(cluster):
+    """A streaming call (head path) between direct calls must not overtake the
+    direct calls sent before it, and later calls must not overtake it."""
+    a = SlowLog.remote()
+    ray.get(a.add.remote(-1))
+    ray.get([a.add.remote(-2) for _ in range(3)])
+    first = [a.add.remote(i) for i in range(40)]
+    gen = a.stream.options(num_returns="streaming").remote(3)
+    later = [a.add.remote(100 + i) for i in range(20)]
+    assert [ray.get(r) for r in gen] == [0, 1, 2]
+    ray.get(first + later)
+    items = ray.get(a.get.remote())[4:]
+    assert items == list(range(40)) + ["gen"] + [100 + i for i in range(20)]
+
+
+def test_calls_after_kill_do_not_reach_actor(cluster):
+    """ray.kill drops the caller's direct connection: later calls go through the
+    head (ordered after the kill) and fail with ActorDiedError."""
+    from cluster_anywhere_amd.exceptions import ActorDiedError, RayActorError
+
+    a = Log.remote()
+    for _ in range(50):
+        ray.get([a.add.remote(i) for i in range(20)])
+        if _direct_client(a) is not None:
+            break
+    assert _direct_client(a) is not None
+    ray.kill(a)
+    assert _direct_client(a) is None
+    with pytest.raises((ActorDiedError, RayActorError)):
+        ray.get(a.add.remote(99), timeout=60)

@@ -60,6 +60,25 @@ class Counter:
         return self.n
 
 
+def test_gcs_store_failed_append_does_not_poison_later_records(tmp_path):
+    """A short write (ENOSPC/EIO mid-record) is cut back off the log, so records
+    appended after it survive a restart (replay stopped at the partial
+    record and dropped everything behind it)."""
+    p = str(tmp_path / "gcs.log")
+    s = _native.GcsStore(p)
+    s.put("kv", b"a", b"1")
+    size = os.path.getsize(p)
+    s._inject_write_fault(7)
+    with pytest.raises(RuntimeError):
+        s.put("kv", b"lost", b"x" * 100)
+    assert os.path.getsize(p) == size and s.log_bytes == size
+    s.put("kv", b"c", b"3")
+    del s
+    s = _native.GcsStore(p)
+    assert sorted(s.items("kv")) == [(b"a", b"1"), (b"c", b"3")]
+    assert s.torn_bytes_dropped == 0
+
+
 @pytest.mark.parametrize("crash", [False, True])
 def test_head_restart_restores_gcs_tables(tmp_path, crash):
     from cluster_anywhere_amd.experimental import internal_kv

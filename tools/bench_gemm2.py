@@ -181,15 +181,18 @@ def bench(rounds, only, wgrad):
             out = torch.zeros(M, N, device=dev, dtype=torch.bfloat16)
             flops = 2.0 * T * M * N
             arms = {}
-            for ms in (4,):
-                arms[f"new_s{ms}"] = (lambda ms=ms: G.run2(dy, x, out, 2, 1, max_split=ms))
-            arms["sk"] = lambda: G.run_sk(dy, x, out, 2, True)
+            tiles = -(-M // 256) * (N // 320)
+            arms["sk256"] = lambda: G.run_sk(dy, x, out, 2, True, runs=256)
+            for S in (1, 2, 3, 4, 7, 8):
+                if tiles * S <= 512 and (1024 % S == 0 or S in (3, 7)):
+                    arms[f"split{S}"] = (lambda S=S: G.run_sk(dy, x, out, 2, True, runs=tiles * S))
+            arms["auto"] = lambda: G.run_sk(dy, x, out, 2, True)
             arms["hipblaslt_addmm"] = lambda: out.addmm_(dy.t(), x)
             t = {k: [] for k in arms}
             for _ in range(rounds):
                 for k, f in arms.items():
                     t[k].append(timeit(f, reps=5))
-            r = {"shape": name, "M": M, "N": N, "K": T, "plans": {ms: G.plan2(M, N, T, dev, ms)[:3] for ms in (4,)}}
+            r = {"shape": name, "M": M, "N": N, "K": T, "auto_runs": G.sk_runs(M, N, T, dev)}
             for k in arms:
                 med = sorted(t[k])[len(t[k]) // 2]
                 r[k + "_us"] = round(med, 1)
