@@ -82,8 +82,11 @@ class Cluster:
         return argv
 
     def add_node(self, wait: bool = True, num_cpus=None, num_gpus=None, resources=None,
-                 object_store_memory=None, labels=None, **_ignored) -> ClusterNode:
+                 object_store_memory=None, labels=None, node_ip_address: str = None,
+                 **_ignored) -> ClusterNode:
         args = self._node_args(num_cpus, num_gpus, resources, object_store_memory, labels)
+        if node_ip_address and self.head_node is not None:
+            args = [*args, "--node-ip-address", node_ip_address]
         if self.head_node is None:
             log = os.path.join(self._temp, "head.out")
             argv = [sys.executable, "-m", "cluster_anywhere_amd.core.head_main", "--port", "0",

@@ -1080,6 +1080,7 @@ class Head:
         e["CAAMD_HEAD"] = self.sock_path if node == self.node_id.hex() else (self.tcp_address or "")
         e["CAAMD_WORKER_ID"] = worker_id.hex()
         e["CAAMD_NODE_ID"] = node
+        e["CAAMD_NODE_IP"] = str((self.node_info.get(node) or {}).get("NodeManagerAddress") or "127.0.0.1")
         e["CAAMD_GPU_IDS"] = ",".join(str(g) for g in gpu_ids)
         renv = env or {}
         noset = (renv.get("env_vars") or {}).get("CAAMD_NOSET_ROCR_VISIBLE_DEVICES")

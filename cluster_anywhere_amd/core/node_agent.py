@@ -88,6 +88,7 @@ def main(argv=None):
                 e["CAAMD_HEAD"] = a.address
                 e["CAAMD_WORKER_ID"] = wid
                 e["CAAMD_NODE_ID"] = node_hex
+                e["CAAMD_NODE_IP"] = a.node_ip_address
                 e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
                 log = open(os.path.join(log_dir, f"worker-{wid[:8]}.log"), "ab")
                 procs.append(subprocess.Popen([sys.executable, "-m", "cluster_anywhere_amd.core.worker_main"],

@@ -22,6 +22,62 @@ from ..session import get_context
 from ..trainer import Backend, DataParallelTrainer, Result
 
 
+_PREFLIGHT = os.environ.get("CAAMD_RCCL_PREFLIGHT", "1") == "1"
+
+
+def rccl_transports(lines) -> Dict[str, int]:
+    """Count the transports RCCL reported for its channels ("Channel 00/0 : 0[0] ->
+    1[1] via P2P/IPC", "... via SHM/direct/direct", "... via NET/IB/0")."""
+    import re
+
+    out: Dict[str, int] = {}
+    pat = re.compile(r"Channel \S+ : .* via (\S+)")
+    for ln in lines:
+        m = pat.search(ln)
+        if m:
+            t = m.group(1).split("/")[0] if m.group(1).startswith("NET") else m.group(1)
+            out[t] = out.get(t, 0) + 1
+    return out
+
+
+def rccl_preflight(rank: int, world_size: int, device_id: Optional[int], debug_file: Optional[str] = None,
+                   nbytes: int = 4 << 20) -> Dict[str, Any]:
+    """RCCL pre-flight after the process group comes up: a checked 4 MiB all-reduce
+    (every rank must see the sum), its time, and the transports RCCL picked (xGMI
+    peers show as P2P/IPC; SHM or NET inside one MI355X node means P2P is off, e.g.
+    IPC not in dmabuf mode). Rank 0 prints one line."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", device_id if device_id is not None else torch.cuda.current_device())
+    t = torch.full((nbytes // 4,), float(rank + 1), device=dev)
+    dist.all_reduce(t)
+    torch.cuda.synchronize(dev)
+    t.fill_(1.0)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    dist.all_reduce(t)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3
+    ok = bool(torch.all(t == float(world_size)).item())
+    transports: Dict[str, int] = {}
+    if debug_file and os.path.exists(debug_file):
+        try:
+            with open(debug_file, errors="replace") as f:
+                transports = rccl_transports(f)
+        except OSError:
+            pass
+    info = {"world_size": world_size, "allreduce_ms": round(ms, 3), "allreduce_MiB": nbytes >> 20,
+            "correct": ok, "transports": transports}
+    if rank == 0:
+        print(f"RCCL pre-flight: {info}", flush=True)
+    if not ok:
+        raise RuntimeError(f"RCCL pre-flight all-reduce returned wrong sums on rank {rank}: {info}")
+    return info
+
+
 class TorchConfig(Backend):
     def __init__(self, backend: Optional[str] = None, init_method: str = "env", timeout_s: int = 1800):
         self.backend = backend
@@ -40,10 +96,22 @@ class TorchConfig(Backend):
         if dist.is_initialized():
             return
         kw = {}
+        debug_file = None
         if backend == "nccl" and device_id is not None:
             kw["device_id"] = torch.device("cuda", int(device_id))
+            if world_size > 1 and _PREFLIGHT and "NCCL_DEBUG" not in os.environ:
+                # RCCL logs the transport of every channel at communicator set-up
+                # ("... via P2P/IPC"); keep that log in a file of its own
+                import tempfile
+
+                debug_file = os.path.join(tempfile.gettempdir(), f"caamd-rccl-{os.getpid()}.log")
+                os.environ.update({"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT,P2P,SHM,NET,GRAPH",
+                                   "NCCL_DEBUG_FILE": debug_file})
         dist.init_process_group(backend, init_method=f"tcp://{master_addr}:{master_port}", rank=rank,
                                 world_size=world_size, timeout=timedelta(seconds=self.timeout_s), **kw)
+        if backend == "nccl" and world_size > 1 and _PREFLIGHT:
+            self.preflight = rccl_preflight(rank, world_size, int(device_id) if device_id is not None else None,
+                                            debug_file)
 
     def on_shutdown(self):
         import torch.distributed as dist

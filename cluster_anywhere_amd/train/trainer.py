@@ -87,9 +87,9 @@ class Backend:
         pass
 
 
-def _free_port() -> int:
+def _free_port(host: str = "") -> int:
     s = socket.socket()
-    s.bind(("127.0.0.1", 0))
+    s.bind((host, 0))
     p = s.getsockname()[1]
     s.close()
     return p
@@ -105,8 +105,13 @@ class _TrainWorker:
 
     def node_info(self):
         gpus = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
+        # the rendezvous runs on rank 0's node: its address as the other nodes reach
+        # it (reference: python/ray/train/torch/config.py:66 uses the rank-0 worker's
+        # node IP as MASTER_ADDR)
+        from ..util import get_node_ip_address
+
         return {"node_id": os.environ.get("CAAMD_NODE_ID", "local"), "gpu_ids": gpus,
-                "port": _free_port(), "addr": "127.0.0.1", "pid": os.getpid()}
+                "port": _free_port(), "addr": get_node_ip_address(), "pid": os.getpid()}
 
     def setup(self, backend, rank, world_size, local_rank, local_world_size, node_rank,
               master_addr, master_port, device_id):

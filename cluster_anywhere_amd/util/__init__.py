@@ -18,6 +18,26 @@ from .scheduling_strategies import (
 
 
 def get_node_ip_address() -> str:
+    """IP address of the node this process runs on (workers: the address their node
+    registered with; drivers: the head's advertised address when attached, else
+    loopback)."""
+    import os
+
+    ip = os.environ.get("CAAMD_NODE_IP")
+    if ip:
+        return ip
+    try:
+        from ..core import context
+
+        w = context.worker
+        if w is not None and getattr(w, "node_hex", None):
+            from ..core.api import nodes
+
+            for n in nodes():
+                if n.get("NodeID") == w.node_hex and n.get("NodeManagerAddress"):
+                    return n["NodeManagerAddress"]
+    except Exception:
+        pass
     return "127.0.0.1"
 
 

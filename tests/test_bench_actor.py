@@ -63,3 +63,30 @@ def test_bench_spmd_mode_under_launcher():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout
     assert lines[0]["config"]["parallelism"] == "dp2-zero1"
+
+
+def test_bench_actor_mode_world8_cpu():
+    """The N=8 scaling run's code path (dp8-zero1 through the actor worker group),
+    rehearsed with gloo on CPU: shard alignment to 8 x world, bucket cuts and the
+    weight all-gather order at the world size of a full MI355X node."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", *TINY],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    j = lines[0]
+    assert j["n_gpus"] == 8 and j["config"]["parallelism"] == "dp8-zero1"
+    assert j["config"]["global_batch"] == 16 and j["value"] > 0
+
+
+def test_bench_actor_mode_under_launcher_world8():
+    """Exactly the driver's N=8 launch line (torch.distributed.run, 8 procs, 127.0.0.1),
+    CPU/gloo: one JSON line, dp8."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", "29647",
+           os.path.join(ROOT, "bench.py"), "--gpus", "8", *TINY]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    assert lines[0]["n_gpus"] == 8 and lines[0]["config"]["parallelism"] == "dp8-zero1"

@@ -1,5 +1,7 @@
-"""Bucketed DDP and ZeRO-1 over gloo, world_size 2, on CPU: both must match a
-single-process run on the concatenated global batch."""
+"""Bucketed DDP and ZeRO-1 over gloo at world sizes 2, 4 and 8, on CPU: both must
+match a single-process run on the concatenated global batch (shard alignment to
+8 x world, bucket cuts, all-gather order and the grad-norm all-reduce are all
+exercised at the world sizes of a full MI355X node)."""
 import os
 import socket
 
@@ -25,6 +27,9 @@ def _make():
     return GPT2(cfg), cfg
 
 
+GLOBAL_BATCH = 8
+
+
 def _worker(rank, world, port, zero, bucket_mb, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -35,10 +40,11 @@ def _worker(rank, world, port, zero, bucket_mb, q):
     m, cfg = _make()
     st = DataParallelStep(m, lr=1e-2, bucket_cap_mb=bucket_mb, zero=zero, max_grad_norm=1.0)
     g = torch.Generator().manual_seed(42)
-    data = torch.randint(0, cfg.vocab_size, (3, 4, 17), generator=g)
+    data = torch.randint(0, cfg.vocab_size, (3, GLOBAL_BATCH, 17), generator=g)
     grads = None
+    per = GLOBAL_BATCH // world
     for it in range(3):
-        x = data[it][rank * 2 : rank * 2 + 2]
+        x = data[it][rank * per : (rank + 1) * per]
         st(x[:, :-1], x[:, 1:])
         if it == 0:
             if zero:
@@ -65,7 +71,7 @@ def _single():
     m, cfg = _make()
     st = DataParallelStep(m, lr=1e-2, max_grad_norm=1.0)
     g = torch.Generator().manual_seed(42)
-    data = torch.randint(0, cfg.vocab_size, (3, 4, 17), generator=g)
+    data = torch.randint(0, cfg.vocab_size, (3, GLOBAL_BATCH, 17), generator=g)
     grads = None
     for it in range(3):
         x = data[it]
@@ -75,12 +81,14 @@ def _single():
     return st.flat.param_buffer.clone(), grads
 
 
-@pytest.mark.parametrize("zero,bucket_mb", [(False, 0.01), (False, 100.0), (True, 0.01)])
-def test_dp_matches_single_process(zero, bucket_mb):
+@pytest.mark.parametrize("world,zero,bucket_mb", [(2, False, 0.01), (2, False, 100.0), (2, True, 0.01),
+                                                  (4, False, 0.01), (4, True, 0.01), (4, True, 100.0),
+                                                  (8, False, 0.05), (8, True, 0.01)])
+def test_dp_matches_single_process(world, zero, bucket_mb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, zero, bucket_mb, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, zero, bucket_mb, q)) for r in range(world)]
     for p in procs:
         p.start()
     got, got_g = (torch.from_numpy(a) for a in q.get(timeout=240))
@@ -89,7 +97,7 @@ def test_dp_matches_single_process(zero, bucket_mb):
         assert p.exitcode == 0
     ref, ref_g = _single()
     n = min(got.numel(), ref.numel())
-    # the mean of two half-batch losses == full-batch loss (equal token counts)
+    # the mean of the per-rank losses == full-batch loss (equal token counts)
     assert torch.allclose(got_g[:n], ref_g[:n], atol=1e-6, rtol=1e-4), (got_g[:n] - ref_g[:n]).abs().max()
     # Adam normalises away tiny summation-order noise only approximately; lr = 1e-2
     assert torch.allclose(got[:n], ref[:n], atol=2e-3), (got[:n] - ref[:n]).abs().max()

@@ -10,7 +10,7 @@ def family(name: str) -> str:
     n = name
     if n.startswith("Cijk_") or n.startswith("Custom_Cijk"):
         return "GEMM (hipBLASLt)"
-    for key, fam in [("gemm_pp_kernel", "GEMM MFMA (ours)"), ("gemm_kernel", "GEMM MFMA (ours)"),
+    for key, fam in [("gemm_pp_kernel", "GEMM MFMA (ours)"), ("gemm_sk_kernel", "GEMM MFMA wgrad (ours)"), ("gemm_kernel", "GEMM MFMA (ours)"),
                      ("transpose_bf16", "weight transpose (ours)"), ("fa_fwd", "flash-attn fwd (ours)"), ("fa_bwd_dq", "flash-attn dQ (ours)"),
                      ("fa_bwd_dkdv", "flash-attn dK/dV (ours)"), ("fa6410fwd_kernel", "flash-attn fwd (ours)"),
                      ("fa64::fwd_kernel", "flash-attn fwd (ours)"), ("bwd_dq_kernel", "flash-attn dQ (ours)"),
