@@ -24,8 +24,10 @@ def _get_controller(create: bool = True):
     from ..core.actor import ActorClass
 
     Ctl = ActorClass(ServeController, {})
+    # restarted without limit (reference: serve/_private/api.py:101 max_restarts=-1); calls
+    # that hit a restart are retried; the state comes back from the KV checkpoint
     h = Ctl.options(name=CONTROLLER_NAME, namespace=NAMESPACE, lifetime="detached", get_if_exists=True,
-                    num_cpus=0, max_concurrency=64).remote()
+                    num_cpus=0, max_concurrency=64, max_restarts=-1, max_task_retries=-1).remote()
     core.get(h.list_apps.remote())
     return h
 

@@ -9,7 +9,15 @@ and replicas. A reconcile thread (every 100 ms):
   * health-checks RUNNING replicas and replaces dead ones,
   * runs the autoscaling policy from replica-reported ongoing requests.
 Handles and the HTTP proxy read ``(version, replicas)`` snapshots; the version
-bumps on every membership change so clients refresh only when needed."""
+bumps on every membership change so clients refresh only when needed.
+
+Fault tolerance (reference: controller.py:123-124, 509 ``_recover_state_from_
+checkpoint``; api.py:101 ``max_restarts=-1``): the controller is restarted by the
+core on death, and every application / deployment change is checkpointed to the
+internal KV (namespace ``serve``). Replicas and proxies are detached named
+actors, so they outlive the controller and keep serving; a restarted controller
+reads the checkpoint, re-attaches to the replicas by name (promoting each after a
+``ready()`` round trip) and starts replacements only for the ones that are gone."""
 from __future__ import annotations
 
 import threading
@@ -23,6 +31,8 @@ from .config import DeploymentConfig
 
 CONTROLLER_NAME = "SERVE_CONTROLLER"
 NAMESPACE = "serve"
+CHECKPOINT_KEY = b"serve:controller_checkpoint"
+REPLICA_PREFIX = "SERVE_REPLICA::"
 
 
 class _ReplicaState:
@@ -77,9 +87,85 @@ class ServeController:
         self.proxy = None
         self.proxy_port = None
         self._orphans: List[_DeploymentState] = []
+        self._ckpt_sig = None
+        self.recovered = False
         self.alive = True
+        self._recover_from_checkpoint()
         self.thread = threading.Thread(target=self._loop, name="serve-reconcile", daemon=True)
         self.thread.start()
+
+    # --------------------------------------------------------- checkpointing
+    def _signature(self):
+        return (tuple(sorted((n, dn, st.version, st.target_replicas, tuple(r.tag for r in st.replicas))
+                             for n, a in self.apps.items() for dn, st in a["deployments"].items())),
+                self.proxy_port, getattr(self, "grpc_port", None), repr(getattr(self, "deploy_config", None)))
+
+    def _checkpoint(self, force: bool = False):
+        """Write the controller state to the internal KV when it changed."""
+        from ..core import serialization
+        from ..experimental import internal_kv
+
+        with self.lock:
+            sig = self._signature()
+            if not force and sig == self._ckpt_sig:
+                return
+            state = {"apps": {}, "proxy_port": self.proxy_port, "grpc_port": getattr(self, "grpc_port", None),
+                     "deploy_config": getattr(self, "deploy_config", None)}
+            for n, a in self.apps.items():
+                deps = {}
+                for dn, st in a["deployments"].items():
+                    deps[dn] = {"target": st.target, "args": st.init_args, "kwargs": st.init_kwargs,
+                                "config": st.config, "target_replicas": st.target_replicas, "counter": st.counter,
+                                "replicas": [r.tag for r in st.replicas if r.state in ("STARTING", "RUNNING")]}
+                state["apps"][n] = {"route_prefix": a["route_prefix"], "ingress": a["ingress"],
+                                    "created": a.get("created", time.time()), "deployments": deps}
+            blob = serialization.dumps_function(state)
+            self._ckpt_sig = sig
+        internal_kv._internal_kv_put(CHECKPOINT_KEY, blob, namespace=NAMESPACE)
+
+    def _recover_from_checkpoint(self):
+        from ..core import serialization
+        from ..experimental import internal_kv
+
+        try:
+            blob = internal_kv._internal_kv_get(CHECKPOINT_KEY, namespace=NAMESPACE)
+        except Exception:
+            blob = None
+        if not blob:
+            return
+        state = serialization.loads_function(blob)
+        for n, a in state["apps"].items():
+            deps = {}
+            for dn, d in a["deployments"].items():
+                st = _DeploymentState(n, dn, d["target"], d["args"], d["kwargs"], d["config"])
+                st.target_replicas = d["target_replicas"]
+                st.counter = d["counter"]
+                for tag in d["replicas"]:
+                    try:
+                        h = core.get_actor(REPLICA_PREFIX + tag, namespace=NAMESPACE)
+                    except ValueError:
+                        continue  # gone with the old controller's node / killed: replaced below
+                    st.replicas.append(_ReplicaState(tag, h))  # STARTING until ready() answers
+                deps[dn] = st
+            self.apps[n] = {"route_prefix": a["route_prefix"], "ingress": a["ingress"],
+                            "deployments": deps, "created": a["created"]}
+        for attr, name, port_key in (("proxy", "SERVE_PROXY", "proxy_port"),
+                                     ("grpc_proxy", "SERVE_GRPC_PROXY", "grpc_port")):
+            try:
+                setattr(self, attr, core.get_actor(name, namespace=NAMESPACE))
+                setattr(self, "proxy_port" if attr == "proxy" else "grpc_port", state.get(port_key))
+            except ValueError:
+                pass
+        self.deploy_config = state.get("deploy_config")
+        self.recovered = True
+
+    def is_recovered(self):
+        return self.recovered
+
+    def pid(self):
+        import os
+
+        return os.getpid()
 
     # ------------------------------------------------------------- public API
     def deploy_application(self, name: str, route_prefix: Optional[str], ingress: str,
@@ -112,6 +198,7 @@ class ServeController:
                         self._orphans.append(st)
             self.apps[name] = {"route_prefix": route_prefix, "ingress": ingress, "deployments": new_deps,
                                "created": time.time()}
+        self._checkpoint(force=True)
         return True
 
     def delete_application(self, name: str):
@@ -121,6 +208,7 @@ class ServeController:
                 for st in app["deployments"].values():
                     st.deleting = True
                     self._orphans.append(st)
+        self._checkpoint(force=True)
         return True
 
     def get_replicas(self, app: str, deployment: str):
@@ -168,6 +256,7 @@ class ServeController:
 
     def set_proxy(self, proxy, port):
         self.proxy, self.proxy_port = proxy, port
+        self._checkpoint(force=True)
         return True
 
     def get_proxy(self):
@@ -175,6 +264,7 @@ class ServeController:
 
     def set_grpc_proxy(self, proxy, port):
         self.grpc_proxy, self.grpc_port = proxy, port
+        self._checkpoint(force=True)
         return True
 
     def get_grpc_proxy(self):
@@ -183,6 +273,7 @@ class ServeController:
     def set_deploy_config(self, cfg: Optional[dict]):
         """Last config applied by ``serve deploy`` (returned by ``serve config``)."""
         self.deploy_config = cfg
+        self._checkpoint(force=True)
         return True
 
     def get_deploy_config(self):
@@ -214,6 +305,12 @@ class ServeController:
                     pass
                 setattr(self, attr, None)
         self.alive = False
+        try:
+            from ..experimental import internal_kv
+
+            internal_kv._internal_kv_del(CHECKPOINT_KEY, namespace=NAMESPACE)
+        except Exception:
+            pass
         return True
 
     # --------------------------------------------------------------- reconcile
@@ -228,6 +325,8 @@ class ServeController:
                         self._reconcile(st)
                         if not st.replicas:
                             self._orphans.remove(st)
+                if self.alive:
+                    self._checkpoint()
             except Exception:  # keep the control loop alive
                 traceback.print_exc()
             time.sleep(0.1)
@@ -242,6 +341,11 @@ class ServeController:
         opts.setdefault("num_cpus", 0)
         opts["max_concurrency"] = max(16, st.config.max_ongoing_requests * 2)
         opts["max_restarts"] = 0
+        # detached + named: replicas outlive a controller crash and the restarted
+        # controller finds them again by name (_recover_from_checkpoint)
+        opts["name"] = REPLICA_PREFIX + tag
+        opts["namespace"] = NAMESPACE
+        opts["lifetime"] = "detached"
         Replica = ActorClass(ServeReplica, {})
         h = Replica.options(**opts).remote(st.app, st.name, tag, st.target, st.init_args, st.init_kwargs,
                                            st.config.user_config, st.config.max_ongoing_requests)

@@ -45,7 +45,12 @@ class _Router:
         if not force and now - self.last_refresh < _REFRESH_S and self.replicas:
             return
         self.last_refresh = now
-        snap = core.get(_controller().get_replicas.remote(self.app, self.deployment))
+        try:
+            snap = core.get(_controller().get_replicas.remote(self.app, self.deployment), timeout=10)
+        except Exception:
+            if self.replicas:
+                return  # controller restarting: keep routing to the last known replicas
+            raise
         if snap is None:
             raise KeyError(f"deployment {self.deployment!r} of application {self.app!r} does not exist")
         version, reps, self.max_ongoing = snap
@@ -58,7 +63,13 @@ class _Router:
     def choose(self, model_id: str = "", timeout_s: float = 60.0):
         deadline = time.time() + timeout_s
         while True:
-            self._refresh(force=not self.replicas)
+            try:
+                self._refresh(force=not self.replicas)
+            except KeyError:
+                raise
+            except Exception:
+                if time.time() > deadline:
+                    raise
             if self.replicas:
                 break
             if time.time() > deadline:

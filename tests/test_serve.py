@@ -281,3 +281,59 @@ def test_llm_openai_app(cluster, tmp_path):
         headers={"content-type": "application/json"})
     assert json.loads(body)["usage"]["completion_tokens"] == 3
     serve.delete("llm")
+
+
+@serve.deployment(num_replicas=2)
+class Stateful:
+    def __init__(self):
+        self.n = 0
+
+    def __call__(self, request):
+        self.n += 1
+        return f"ok {os.getpid()}"
+
+
+def test_controller_crash_recovery(cluster):
+    """The controller checkpoints to the internal KV, restarts without limit and
+    re-attaches to its (detached, named) replicas: HTTP keeps being served while it
+    is down and after it comes back, with the same replicas (reference:
+    serve/_private/controller.py:509 _recover_state_from_checkpoint)."""
+    from cluster_anywhere_amd.serve.controller import CONTROLLER_NAME, NAMESPACE
+
+    serve.run(Stateful.bind(), name="ft", route_prefix="/ft")
+    assert _http("/ft")[0] == 200
+    before = serve.status().applications["ft"].deployments["Stateful"].replica_states
+    assert len(before) == 2
+    ctl = ray.get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
+    old_pid = ray.get(ctl.pid.remote())
+    ray.kill(ctl, no_restart=False)
+    # the proxy and replicas do not depend on the controller for the data path
+    served = 0
+    t_end = time.time() + 3
+    while time.time() < t_end:
+        assert _http("/ft")[0] == 200
+        served += 1
+    assert served > 0
+    ctl = ray.get_actor(CONTROLLER_NAME, namespace=NAMESPACE)
+    deadline = time.time() + 60
+    while time.time() < deadline:
+        try:
+            if ray.get(ctl.is_recovered.remote(), timeout=10):
+                break
+        except Exception:
+            pass
+        time.sleep(0.2)
+    assert ray.get(ctl.is_recovered.remote())
+    assert ray.get(ctl.pid.remote()) != old_pid  # a new controller process
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        st = serve.status().applications.get("ft")
+        if st and st.status == "RUNNING":
+            break
+        time.sleep(0.1)
+    after = serve.status().applications["ft"].deployments["Stateful"].replica_states
+    assert set(after) == set(before), (before, after)  # same replicas, re-attached
+    assert _http("/ft")[0] == 200
+    # the recovered controller keeps managing the app
+    serve.delete("ft")
+    assert "ft" not in serve.status().applications
