@@ -14,14 +14,21 @@ with the same ``gcs_storage`` path restores:
 * the internal KV (all namespaces) and the exported function table;
 * job history;
 * detached placement groups (re-reserved with their ids and names);
-* detached actors: re-created from their creation specs with their actor ids,
-  names and namespaces, so ``get_actor(name)`` resolves to the same actor id.
-  Their worker processes died with the old head, so, as after any actor
-  restart, in-memory actor state starts over from ``__init__``.
+* the head's session identity (session dir, node id, object-store arena name and
+  size, control port): a standalone head restarted on the same storage while the
+  arena still exists re-attaches to it and listens on the same addresses, so the
+  node's workers, actors and drivers RECONNECT instead of dying (reference: raylets
+  and core workers survive a GCS restart and re-register, gcs_server.cc:182
+  DoStart(GcsInitData));
+* every actor's creation record (not only detached ones): a re-registering actor
+  worker is matched to its record and keeps running with its in-memory state;
+  detached actors whose worker does not come back within the re-attach grace are
+  re-created from their specs (same ids and names, state from ``__init__``), other
+  actors are declared dead.
 
-Creation specs that reference object-store arguments (``ObjectRef`` args) are
-not persisted: those objects do not survive the head, so such detached actors
-are not restorable (logged once at registration).
+Creation specs that reference object-store arguments (``ObjectRef`` args) cannot
+be re-created (those objects may not survive); such actors are persisted for
+re-attachment only.
 """
 from __future__ import annotations
 
@@ -58,18 +65,23 @@ class GcsPersistence:
         except Exception:  # noqa: BLE001 - job info is best effort
             pass
 
-    def actor_put(self, spec) -> bool:
-        if spec.arg_refs:
-            log.warning("detached actor %s takes ObjectRef arguments: not restorable after a head restart",
-                        spec.fn_name)
-            return False
+    def actor_put(self, spec, owner=None, lifetime=None) -> bool:
+        restorable = not spec.arg_refs
+        if not restorable and lifetime == "detached":
+            log.warning("detached actor %s takes ObjectRef arguments: re-attachable after a head restart "
+                        "but not re-creatable", spec.fn_name)
         fields = {s: getattr(spec, s) for s in spec.__slots__ if s not in _SPEC_RUNTIME_FIELDS}
         try:
-            self.store.put("actor", spec.actor_id, pickle.dumps(fields))
+            self.store.put("actor", spec.actor_id, pickle.dumps({"fields": fields, "owner": owner,
+                                                                 "lifetime": lifetime,
+                                                                 "restorable": restorable}))
         except Exception as e:  # noqa: BLE001
-            log.warning("detached actor %s not persisted: %s", spec.fn_name, e)
+            log.warning("actor %s not persisted: %s", spec.fn_name, e)
             return False
         return True
+
+    def session_put(self, info: dict):
+        self.store.put("session", b"head", pickle.dumps(info))
 
     def actor_del(self, actor_id: bytes):
         self.store.delete("actor", actor_id)
@@ -98,7 +110,27 @@ class GcsPersistence:
                     out[table][k] = pickle.loads(v)  # records this module wrote itself
                 except Exception as e:  # noqa: BLE001
                     log.warning("GCS %s record %s unreadable: %s", table, k.hex(), e)
+        for k, rec in list(out["actor"].items()):
+            if "fields" not in rec:  # pre-round-3 record: a detached actor's spec fields
+                out["actor"][k] = {"fields": rec, "owner": None, "lifetime": "detached", "restorable": True}
         return out
+
+
+def peek_session(path: str) -> Optional[dict]:
+    """The session record a previous head wrote to ``path`` (None if none). Opens
+    the log, reads and closes it, so the head can open it afterwards."""
+    import os
+
+    from .. import _native
+
+    if not os.path.exists(path):
+        return None
+    st = _native.GcsStore(path)
+    try:
+        v = st.get("session", b"head")
+        return pickle.loads(v) if v else None  # a record this module wrote itself
+    finally:
+        del st
 
 
 def _kv_key(ns, key: bytes) -> bytes:

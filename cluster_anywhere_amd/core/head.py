@@ -124,7 +124,7 @@ class WorkerInfo:
 class ActorInfo:
     __slots__ = ("actor_id", "spec", "state", "worker", "name", "namespace", "restarts_left",
                  "max_task_retries", "queue", "inflight", "node", "gpu_ids", "acquired",
-                 "class_name", "lifetime", "death_cause", "num_restarts", "owner", "pid")
+                 "class_name", "lifetime", "death_cause", "num_restarts", "owner", "pid", "record")
 
     def __init__(self, **kw):
         for s in self.__slots__:
@@ -140,15 +140,26 @@ class Head:
                  listen_tcp: Optional[str] = None, namespace: str = "default",
                  worker_env: Optional[Dict[str, str]] = None, prestart: int = 0,
                  spill_dir: Optional[str] = None, labels: Optional[Dict[str, str]] = None,
-                 gcs_storage: Optional[str] = None):
+                 gcs_storage: Optional[str] = None, reattach: bool = False,
+                 reconnect_s: Optional[float] = None):
         from .. import _native
 
         self.session_dir = session_dir
         os.makedirs(session_dir, exist_ok=True)
         self.node_id = node_id
         self.store_name = store_name
-        self.store = _native.ObjectStore(store_name, store_capacity, 1 << 18, True)
-        self.store.prefault_async(int(os.environ.get("CAAMD_OBJECT_STORE_PREFAULT_BYTES", str(2 << 30))))
+        self.store_capacity = store_capacity
+        self.reattached = False
+        if reattach:
+            # a restarted head on the same node: the arena (and every sealed object in
+            # it) outlived the old head; workers reconnect and re-register (see
+            # _h_reregister). Its mutex is robust, so a lock held by the dead head is
+            # recovered by the next locker.
+            self.store = _native.ObjectStore(store_name, 0, 0, False)
+            self.reattached = True
+        else:
+            self.store = _native.ObjectStore(store_name, store_capacity, 1 << 18, True)
+            self.store.prefault_async(int(os.environ.get("CAAMD_OBJECT_STORE_PREFAULT_BYTES", str(2 << 30))))
         self.sched = _native.ClusterScheduler(0.5)
         self.sched.add_node(node_id.hex(), resources)
         self.node_labels = {node_id.hex(): _node_labels(node_id.hex(), gpu_ids, labels)}
@@ -265,6 +276,25 @@ class Head:
 
             os.makedirs(os.path.dirname(os.path.abspath(gcs_storage)), exist_ok=True)
             self.gcs = GcsPersistence(gcs_storage)
+        # with durable tables, workers and drivers that lose the head keep running and
+        # reconnect for this long (a restarted head re-attaches them); 0 = die with it
+        # (standalone heads: head_main; a driver-embedded head dies with its driver)
+        if reconnect_s is None:
+            reconnect_s = float(os.environ.get("CAAMD_HEAD_RECONNECT_S", "0"))
+        self.reconnect_s = float(reconnect_s) if self.gcs is not None else 0.0
+        if self.reconnect_s > 0:
+            self.worker_env = dict(self.worker_env, CAAMD_HEAD_RECONNECT_S=str(self.reconnect_s))
+        self.reattach_s = float(os.environ.get("CAAMD_GCS_REATTACH_S", "10"))
+        self._reattaching = False
+        self.subscribers: Dict[str, Set[Conn]] = {}  # pubsub channel -> subscriber connections
+        self.reattached_running: Dict[bytes, tuple] = {}  # task id -> (worker, node, demand) of a re-registered run
+        self._held_resubmits: List[tuple] = []  # (conn, spec) replayed by owners during the re-attach grace
+        self.reattach_stats = {"workers": 0, "actors": 0, "objects": 0, "drivers": 0, "lost_objects": 0,
+                               "recreated_actors": 0, "dead_actors": 0}
+        if self.gcs is not None:
+            self.gcs.session_put({"session_dir": session_dir, "node_id": node_id.hex(), "store_name": store_name,
+                                  "store_bytes": int(store_capacity), "tcp_address": self.tcp_address,
+                                  "pid": os.getpid(), "sock_path": self.sock_path})
 
     # ------------------------------------------------------------------ loop
     def start(self):
@@ -430,7 +460,8 @@ class Head:
         self._send(c, ("registered", {"store_name": self.node_store.get(node, self.store_name),
                                       "node_id": node,
                                       "namespace": self.namespace,
-                                      "session_dir": self.session_dir}))
+                                      "session_dir": self.session_dir,
+                                      "reconnect_s": self.reconnect_s}))
         if kind == "worker":
             w = self.workers.get(worker_id)
             if w is None:
@@ -849,6 +880,8 @@ class Head:
 
     # -------------------------------------------------------------------- tasks
     def _h_submit(self, c, spec: TaskSpec):
+        if self.reattached and c is not None and self._resubmitted(c, spec):
+            return
         spec.owner = self.clients.get(c, {}).get("id")
         spec.state = "pending"
         spec.submit_time = time.time()
@@ -867,6 +900,52 @@ class Head:
         if spec.kind == ACTOR_CREATE:
             self._register_actor(spec, c)
         self._enqueue_when_ready(spec)
+
+    def _resubmitted(self, c, spec) -> bool:
+        """An owner re-sends the head-path tasks it had in flight when the previous
+        head died. True if this one needs no new run: its results already exist,
+        its actor is known (a creation), or a re-registered worker is still running
+        (or reporting) it -- then it is adopted as that worker's in-flight task."""
+        if spec.kind == ACTOR_CREATE and spec.actor_id in self.actors:
+            return True
+        rids = spec.return_ids or ()
+        if rids and all((self.objects.get(o) is not None and self.objects[o].state == READY) for o in rids):
+            for o in rids:
+                oc = c
+                if not oc.closed:
+                    self._notify.setdefault(oc, []).append(o)
+            return True
+        run = self.reattached_running.get(spec.task_id)
+        if run is None:
+            held_actor = spec.kind == ACTOR_METHOD and any(
+                h[1].kind == ACTOR_METHOD and h[1].actor_id == spec.actor_id for h in self._held_resubmits)
+            if self._reattaching or held_actor:
+                # its worker may still re-register with it running (then it is adopted,
+                # not run twice); later calls to an actor with held calls queue behind them
+                self._held_resubmits.append((c, spec))
+                return True
+            return False
+        wid, node, held = run
+        spec.owner = self.clients.get(c, {}).get("id")
+        spec.state = "running"
+        spec.submit_time = spec.start_time = time.time()
+        spec.worker, spec.node = wid, node
+        spec.acquired = (node, held) if held else None
+        self.tasks[spec.task_id] = spec
+        for oid in rids:
+            e = self._obj(oid)
+            e.refcount += 1
+            e.owner_task = spec.task_id
+            self.owner_of[oid] = c
+        w = self.workers.get(wid)
+        if w is not None:
+            w.tasks_inflight[spec.task_id] = spec
+        if spec.kind == ACTOR_METHOD:
+            a = self.actors.get(spec.actor_id)
+            if a is not None:
+                a.inflight[spec.task_id] = spec
+        self.reattached_running.pop(spec.task_id, None)
+        return True
 
     def _enqueue_when_ready(self, spec):
         unresolved = {r for r in spec.arg_refs if self._obj(r).state != READY}
@@ -1167,6 +1246,19 @@ class Head:
         if w is not None:
             w.tasks_inflight.pop(task_id, None)
         if spec is None:
+            run = self.reattached_running.pop(task_id, None)
+            if run is not None:
+                # finished on a worker that outlived the previous head before its owner
+                # re-sent the task: keep the results for the owner's resubmission
+                for (oid, inline, size, node_hex, contained, is_err) in results:
+                    self._obj(oid)
+                    self._seal_object(oid, inline, size, node_hex, contained, is_err)
+                if run[2]:
+                    self.sched.release(run[1], run[2])
+                if w is not None and w.actor_id is None and not w.tasks_inflight and w.lease is None:
+                    w.idle = True
+                    self.idle[(w.node, w.gpu_key)].append(w)
+                    self._schedule()
             return
         self.events.append(("end", task_id, spec.fn_name, time.time(), w.pid if w else None))
         if error_kind == "app" and retryable and spec.attempt < (spec.max_retries or 0) and not spec.cancelled:
@@ -1198,13 +1290,13 @@ class Head:
                                 detail = str(serialization.deserialize(inline))
                             except Exception:
                                 pass
-                    a.state = "DEAD"
+                    self._set_actor_state(a, "DEAD")
                     a.death_cause = "creation task failed" + (f": {detail}" if detail else "")
                     self._fail_actor_queue(a, "ActorDiedError",
                                            "actor constructor raised" + (f":\n{detail}" if detail else ""))
                     self._kill_worker(a.worker)
                 else:
-                    a.state = "ALIVE"
+                    self._set_actor_state(a, "ALIVE")
                     self._pump_actor(a)
         else:
             self._finish_worker(w, spec)
@@ -1309,6 +1401,38 @@ class Head:
         if not answer():
             self.gen_waiters[(task_id, index)].append(answer)
 
+    # ------------------------------------------------------------------ pubsub
+    # Reference: src/ray/pubsub/publisher.h:297 -- the GCS publishes actor and node
+    # state changes to subscribers (core workers, raylets, Serve). Here a
+    # subscriber sends ("subscribe", channel); every change is pushed as
+    # ("pub", channel, key, info) on its control connection, in order.
+    CHANNELS = ("actor", "node")
+
+    def _h_subscribe(self, c, channel):
+        if channel in self.CHANNELS:
+            self.subscribers.setdefault(channel, set()).add(c)
+
+    def _h_unsubscribe(self, c, channel):
+        self.subscribers.get(channel, set()).discard(c)
+
+    def _publish(self, channel, key, info):
+        subs = self.subscribers.get(channel)
+        if not subs:
+            return
+        for sc in list(subs):
+            if sc.closed:
+                subs.discard(sc)
+                continue
+            self._send(sc, ("pub", channel, key, info))
+
+    def _set_actor_state(self, a, state):
+        if a.state == state:
+            return
+        a.state = state
+        self._publish("actor", a.actor_id, {"state": state, "name": a.name, "namespace": a.namespace,
+                                            "class_name": a.class_name, "pid": a.pid, "node": a.node,
+                                            "death_cause": a.death_cause if state == "DEAD" else None})
+
     # ------------------------------------------------------------------ actors
     def _register_actor(self, spec, c):
         opts = spec.actor_opts or {}
@@ -1321,8 +1445,9 @@ class Head:
         self.actors[spec.actor_id] = a
         if a.name:
             self.named_actors[(a.namespace, a.name)] = spec.actor_id
-        if self.gcs is not None and a.lifetime == "detached" and spec.actor_id not in self._gcs_actors:
-            if self.gcs.actor_put(spec):
+        if self.gcs is not None and spec.actor_id not in self._gcs_actors:
+            # every actor: a restarted head re-attaches re-registering actor workers to it
+            if self.gcs.actor_put(spec, a.owner, a.lifetime):
                 self._gcs_actors.add(spec.actor_id)
         # the creator's handle: an always-READY object whose refcount = live handles
         hid = spec.actor_id + b"\xac" * 8
@@ -1494,7 +1619,7 @@ class Head:
         spec.node = w.node
         spec.state = "running"
         spec.start_time = time.time()
-        a.state = "PENDING_CREATION" if a.num_restarts == 0 else "RESTARTING"
+        self._set_actor_state(a, "PENDING_CREATION" if a.num_restarts == 0 else "RESTARTING")
         self.events.append(("start", spec.task_id, spec.fn_name, spec.start_time, w.pid))
         w.tasks_inflight[spec.task_id] = spec
         self._send(w.conn, ("execute", self._exec_payload(w, spec)))
@@ -1585,7 +1710,7 @@ class Head:
             if a.restarts_left > 0:
                 a.restarts_left -= 1
             a.num_restarts += 1
-            a.state = "RESTARTING"
+            self._set_actor_state(a, "RESTARTING")
             retry = a.max_task_retries != 0
             for tid, spec in list(a.inflight.items()):
                 if retry:
@@ -1597,7 +1722,7 @@ class Head:
             self.pending_spawn[wid] = ("actor", a.actor_id)
             self._spawn_worker(a.node, a.gpu_ids or (), worker_id=wid, env=a.spec.runtime_env)
             return
-        a.state = "DEAD"
+        self._set_actor_state(a, "DEAD")
         a.death_cause = a.death_cause or "the actor's worker process died"
         self._fail_actor_queue(a, "ActorDiedError", a.death_cause)
         if a.name:
@@ -1619,6 +1744,8 @@ class Head:
         except (KeyError, ValueError):
             pass
         c.close()
+        for subs in self.subscribers.values():
+            subs.discard(c)
         info = self.clients.pop(c, {})
         w = self.conn_worker.pop(c, None)
         for lw in [x for x in self.workers.values() if x.lease is not None and x.lease[0] is c]:
@@ -1741,16 +1868,200 @@ class Head:
             self._h_pg_create(None, pg_id, pg["bundles"], pg["strategy"], pg["name"],
                               pg_id + b"\xb7" * 4, pg["lifetime"])
         n_actors = 0
-        for aid, fields in data["actor"].items():
-            spec = TaskSpec(**fields)
-            spec.task_id = os.urandom(16)
-            spec.attempt = 0
-            spec.return_ids = [os.urandom(len(r)) for r in (fields.get("return_ids") or [])]
+        for aid, rec in data["actor"].items():
             self._gcs_actors.add(aid)  # already persisted: keep the record, do not rewrite it
-            self._h_submit(None, spec)
-            n_actors += 1
+            if self.reattached:
+                # the node outlived the old head: wait for the actor's worker to re-register
+                self._actor_placeholder(aid, rec)
+                n_actors += 1
+            elif rec.get("lifetime") == "detached" and rec.get("restorable", True):
+                self._recreate_actor(rec["fields"])
+                n_actors += 1
+            else:
+                self._gcs_actors.discard(aid)
+                self.gcs.actor_del(aid)
+        if self.reattached:
+            self._reattaching = True
+            self._timer(self.reattach_s, self._reattach_expired)
         self.gcs_restored = {"kv": len(data["kv"]), "functions": len(data["fn"]), "jobs": len(data["job"]),
-                             "placement_groups": len(data["pg"]), "actors": n_actors}
+                             "placement_groups": len(data["pg"]), "actors": n_actors,
+                             "reattach": self.reattached}
+
+    def _recreate_actor(self, fields, queue=()):
+        spec = TaskSpec(**fields)
+        spec.task_id = os.urandom(16)
+        spec.attempt = 0
+        spec.return_ids = [os.urandom(len(r)) for r in (fields.get("return_ids") or [])]
+        self._h_submit(None, spec)
+        a = self.actors.get(spec.actor_id)
+        if a is not None:
+            a.queue.extend(queue)
+
+    def _actor_placeholder(self, aid, rec):
+        fields = rec["fields"]
+        spec = TaskSpec(**fields)
+        opts = spec.actor_opts or {}
+        a = ActorInfo(actor_id=aid, spec=spec, state="RECONNECTING", name=opts.get("name"),
+                      namespace=opts.get("namespace") or self.namespace,
+                      restarts_left=opts.get("max_restarts", 0) or 0,
+                      max_task_retries=opts.get("max_task_retries", 0) or 0, class_name=spec.fn_name,
+                      lifetime=rec.get("lifetime"), owner=rec.get("owner"))
+        a.record = rec
+        self.actors[aid] = a
+        if a.name:
+            self.named_actors[(a.namespace, a.name)] = aid
+        hid = aid + b"\xac" * 8
+        he = self._obj(hid)
+        he.refcount += 1
+        he.state = READY
+        he.inline = b""
+        self.handle_objs[hid] = aid
+
+    # ------------------------------------------------- re-attach after restart
+    def _h_reregister(self, c, kind, worker_id, pid, node_hex, extra):
+        """A worker / driver that outlived the previous head reconnects (reference:
+        core workers and raylets re-registering with a restarted GCS): rebuild its
+        worker record, re-attach its actor, take back the resources it holds, and
+        rebuild the object directory entries it references."""
+        extra = extra or {}
+        node = node_hex or self.head_hex
+        self.clients[c] = {"id": worker_id, "kind": kind, "pid": pid, "node": node}
+        self._send(c, ("registered", {"store_name": self.node_store.get(node, self.store_name), "node_id": node,
+                                      "namespace": self.namespace, "session_dir": self.session_dir,
+                                      "reconnect_s": self.reconnect_s, "reattached": True}))
+        self._reattach_refs(extra)
+        if kind == "driver":
+            self.reattach_stats["drivers"] += 1
+            jid = extra.get("job_id", b"")
+            self.jobs.setdefault(jid, {"start": time.time(), "pid": pid, "driver": worker_id})
+            self._reattach_leases(c, extra.get("leases") or ())
+            return
+        if kind != "worker":
+            return
+        self.reattach_stats["workers"] += 1
+        w = WorkerInfo(worker_id=worker_id, pid=pid, node=node, gpu_key=tuple(extra.get("gpu_ids") or ()),
+                       kind="worker", alive=True, conn=c)
+        w.started = time.time()
+        w.client_id = worker_id
+        w.direct_addr = extra.get("direct")
+        self.workers[worker_id] = w
+        self.conn_worker[c] = w
+        aid = extra.get("actor_id")
+        if aid is not None:
+            a = self.actors.get(aid)
+            if a is None or a.state != "RECONNECTING":
+                self._kill_worker(worker_id)  # an actor this head has no record of (or replaced)
+                return
+            demand = self._demand(a.spec)
+            if self.sched.acquire(node, demand):
+                a.acquired = a.spec.acquired = (node, demand)
+                gamt = float(a.spec.resources.get("GPU", 0) or 0)
+                try:
+                    self._take_gpus(node, w.gpu_key, gamt)
+                except ValueError:
+                    pass
+            a.gpu_ids = w.gpu_key
+            a.spec.gpu_ids = w.gpu_key
+            a.node, a.worker, a.pid = node, worker_id, pid
+            self._set_actor_state(a, "ALIVE")
+            w.actor_id = aid
+            w.idle = False
+            self.reattach_stats["actors"] += 1
+            self._pump_actor(a)
+            return
+        busy = False
+        for (tid, res) in extra.get("running") or ():
+            busy = True
+            demand = {k: float(v) for k, v in (res or {}).items() if v}
+            held = demand if demand and self.sched.acquire(node, demand) else {}
+            self.reattached_running[tid] = (worker_id, node, held)
+        for tid in extra.get("finishing") or ():
+            self.reattached_running.setdefault(tid, (worker_id, node, {}))
+        self._release_held(lambda sp: sp.task_id in self.reattached_running)
+        if not busy:
+            w.idle = True
+            self.idle[(node, w.gpu_key)].append(w)
+            self._schedule()
+
+    def _reattach_refs(self, extra):
+        """Object directory entries from a re-registering process's held refs: sealed
+        in this node's arena, or an inline payload the process still holds."""
+        inline = extra.get("inline") or {}
+        for oid, n in (extra.get("refs") or {}).items():
+            e = self._obj(oid)
+            e.refcount += int(n)
+            if e.state == READY:
+                continue
+            if oid in inline:
+                blob, is_err = inline[oid]
+                self._seal_object(oid, blob, len(blob), None, (), bool(is_err))
+                self.reattach_stats["objects"] += 1
+                continue
+            try:
+                hit = self.store.lookup(oid)
+            except Exception:
+                hit = None
+            if hit is not None:
+                self._seal_object(oid, None, int(hit[1]), self.head_hex, ())
+                self.reattach_stats["objects"] += 1
+
+    def _reattach_leases(self, c, leases):
+        for (wid, res) in leases:
+            w = self.workers.get(wid)
+            if w is None or w.lease is not None:
+                continue
+            demand = {k: float(v) for k, v in (res or {}).items() if v}
+            if w.idle:
+                w.idle = False
+                lst = self.idle.get((w.node, w.gpu_key))
+                if lst and w in lst:
+                    lst.remove(w)
+            if demand:
+                self.sched.acquire(w.node, demand)
+            w.lease = (c, demand, time.time())
+
+    def _release_held(self, pred):
+        keep, go = [], []
+        for (hc, sp) in self._held_resubmits:
+            (go if pred(sp) else keep).append((hc, sp))
+        self._held_resubmits = keep
+        for (hc, sp) in go:
+            if not hc.closed:
+                self._h_submit(hc, sp)
+
+    def _reattach_expired(self):
+        """End of the re-attach grace: actors whose worker did not come back are
+        re-created (detached, restorable) or dead; referenced objects that nothing
+        will produce are lost."""
+        from ..exceptions import ObjectLostError  # noqa: F401  (clients raise it for "lost" payloads)
+
+        self._reattaching = False
+        for a in list(self.actors.values()):
+            if a.state != "RECONNECTING":
+                continue
+            rec = a.record or {}
+            if a.lifetime == "detached" and rec.get("restorable", True):
+                self.reattach_stats["recreated_actors"] += 1
+                q = list(a.queue)
+                a.queue.clear()
+                del self.actors[a.actor_id]
+                self._recreate_actor(rec["fields"], q)
+            else:
+                self.reattach_stats["dead_actors"] += 1
+                self._set_actor_state(a, "DEAD")
+                a.death_cause = "the actor's worker did not reconnect after a head restart"
+                if a.name:
+                    self.named_actors.pop((a.namespace, a.name), None)
+                self._fail_actor_queue(a, "ActorDiedError", a.death_cause)
+        held, self._held_resubmits = self._held_resubmits, []
+        for (hc, sp) in held:  # owners' replayed tasks nobody re-registered as running: run them now
+            if not hc.closed:
+                self._h_submit(hc, sp)
+        for oid, e in list(self.objects.items()):
+            if e.state == PENDING and e.refcount > 0 and e.owner_task is None:
+                e.lost = True
+                self.reattach_stats["lost_objects"] += 1
+                self._seal_object(oid, None, 0, None, ())
 
     def _health_check(self):
         if self.gcs is not None and self._gcs_actors:
@@ -1765,7 +2076,7 @@ class Head:
                 if pending and pending[0] == "actor":
                     a = self.actors.get(pending[1])
                     if a is not None:
-                        a.state = "DEAD"
+                        self._set_actor_state(a, "DEAD")
                         a.death_cause = "worker process failed to start (see session logs)"
                         self._fail_actor_queue(a, "ActorDiedError", a.death_cause)
                 self._schedule()
@@ -1887,7 +2198,7 @@ class Head:
                         if pend == ("actor", a.actor_id):
                             del self.pending_spawn[wid]
                             self._kill_worker(wid)
-                    a.state = "DEAD"
+                    self._set_actor_state(a, "DEAD")
                     self._fail_actor_queue(a, "ActorDiedError", "placement group removed")
                 self._kill_worker(a.worker)
         self.sched.remove_pg(pg_id.hex())
@@ -1940,6 +2251,8 @@ class Head:
             m["series"][key] = cur
 
     def state(self, what, arg=None):
+        if what == "reattach_stats":
+            return dict(self.reattach_stats, reattached=self.reattached, reattaching=self._reattaching)
         if what == "metrics":
             import copy
 
@@ -2048,8 +2361,9 @@ class Head:
                                     "Labels": dict(self.node_labels[node_hex])}
         self._send(c, ("registered", {"store_name": extra["store_name"], "node_id": node_hex,
                                       "namespace": self.namespace, "session_dir": self.session_dir,
-                                      "head_tcp": self.tcp_address}))
+                                      "head_tcp": self.tcp_address, "reconnect_s": self.reconnect_s}))
         self.events.append(("node_added", node_hex, time.time()))
+        self._publish("node", node_hex, {"state": "ALIVE", "address": addr, "resources": dict(res)})
         self._retry_pending_pgs()
         self._retry_infeasible()
         self._schedule()
@@ -2060,6 +2374,7 @@ class Head:
         if node_hex in self.node_info:
             self.node_info[node_hex]["Alive"] = False
         self.events.append(("node_removed", node_hex, time.time()))
+        self._publish("node", node_hex, {"state": "DEAD"})
         # objects whose only copy lived there are lost: re-execute their lineage
         # where possible (reference: object_recovery_manager.cc RecoverObject)
         for oid, e in list(self.objects.items()):

@@ -47,6 +47,28 @@ def embedded(cfg_json: str):
     head.shutdown()
 
 
+def _previous_session(gcs_storage):
+    """The session a previous head on this GCS storage ran, if it can be resumed:
+    its object-store arena still exists and its process is gone."""
+    if not gcs_storage:
+        return None
+    from .gcs_persist import peek_session
+
+    prev = peek_session(gcs_storage)
+    if not prev:
+        return None
+    if not os.path.exists("/dev/shm" + prev["store_name"]):
+        return None
+    try:
+        os.kill(int(prev["pid"]), 0)
+        return None  # that head is still running: never share an arena between two heads
+    except ProcessLookupError:
+        pass
+    except PermissionError:
+        return None
+    return prev
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--port", type=int, default=6380)
@@ -81,8 +103,23 @@ def main(argv=None):
     res["node:__internal_head__"] = 1.0
     res.update({k: float(v) for k, v in json.loads(a.resources).items()})
     store_name = f"/caamd_{os.getpid()}_{uuid.uuid4().hex[:8]}"
-    head = Head(session_dir, os.urandom(16), res, store_name, store_bytes, gpus,
-                listen_tcp=f"{a.host}:{a.port}", labels=json.loads(a.labels), gcs_storage=a.gcs_storage)
+    node_id = os.urandom(16)
+    port = a.port
+    reattach = False
+    prev = _previous_session(a.gcs_storage)
+    if prev is not None:
+        # the node outlived the previous head (its arena is still there and the old
+        # head process is gone): come back as the same node, on the same addresses,
+        # so its workers / actors / drivers reconnect and re-register
+        session_dir, store_name, store_bytes = prev["session_dir"], prev["store_name"], int(prev["store_bytes"])
+        node_id = bytes.fromhex(prev["node_id"])
+        res["object_store_memory"] = float(store_bytes)
+        if prev.get("tcp_address"):
+            port = int(prev["tcp_address"].rsplit(":", 1)[1])
+        reattach = True
+    head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
+                listen_tcp=f"{a.host}:{port}", labels=json.loads(a.labels), gcs_storage=a.gcs_storage,
+                reattach=reattach, reconnect_s=float(os.environ.get("CAAMD_HEAD_RECONNECT_S", "60")))
     head.start()
     url = None
     if a.include_dashboard.lower() in ("1", "true", "yes"):

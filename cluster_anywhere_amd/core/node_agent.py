@@ -48,13 +48,31 @@ def main(argv=None):
     store = _native.ObjectStore(store_name, store_bytes, 1 << 18, True)
     store.prefault_async(int(os.environ.get("CAAMD_OBJECT_STORE_PREFAULT_BYTES", str(2 << 30))))
     osrv = ObjectServer(store, a.node_ip_address)
+    reg = {"resources": res, "gpu_ids": gpus, "store_name": store_name,
+           "obj_addr": osrv.address(a.node_ip_address), "address": a.node_ip_address, "pid": os.getpid(),
+           "labels": json.loads(a.labels)}
     conn = connect(a.address)
-    conn.send(("register", "node", os.urandom(16), os.getpid(), node_hex,
-               {"resources": res, "gpu_ids": gpus, "store_name": store_name,
-                "obj_addr": osrv.address(a.node_ip_address), "address": a.node_ip_address, "pid": os.getpid(),
-                "labels": json.loads(a.labels)}))
+    conn.send(("register", "node", os.urandom(16), os.getpid(), node_hex, reg))
     msg = conn.recv()
     assert msg[0] == "registered", msg
+    reconnect_s = float(msg[1].get("reconnect_s") or 0)
+
+    def reconnect():
+        """The head went away: a restarted head (same GCS storage, same address)
+        takes this node back with its store and running workers (reference: raylets
+        re-registering with a restarted GCS)."""
+        deadline = time.time() + reconnect_s
+        while time.time() < deadline:
+            try:
+                c = connect(a.address)
+                c.send(("register", "node", os.urandom(16), os.getpid(), node_hex, dict(reg, reattach=True)))
+                m = c.recv()
+                if m[0] == "registered":
+                    return c
+            except (ConnectionClosed, OSError):
+                pass
+            time.sleep(0.3)
+        return None
     session_dir = msg[1]["session_dir"]
     log_dir = os.path.join(session_dir, f"node-{node_hex[:8]}")
     os.makedirs(log_dir, exist_ok=True)
@@ -80,7 +98,11 @@ def main(argv=None):
             try:
                 m = conn.recv()
             except (ConnectionClosed, OSError):
-                break
+                nc = reconnect() if reconnect_s > 0 else None
+                if nc is None:
+                    break
+                conn = nc
+                continue
             if m[0] == "spawn":
                 _, wid, gpu_ids, extra = m
                 e = dict(os.environ)

@@ -186,6 +186,18 @@ class CoreWorker:
         self.actor_head_only = set()
         self._direct_lock = threading.Lock()
         self.direct_server = None
+        # head restart (core/gcs_persist.py): with reconnect_s > 0 this process keeps
+        # running when the head goes away, reconnects, re-registers and replays its
+        # outstanding requests and head-path task submissions
+        self.reconnect_s = float(os.environ.get("CAAMD_HEAD_RECONNECT_S", "0") or 0)
+        self._conn_cv = threading.Condition()
+        self._req_builds: Dict[int, Any] = {}
+        self._head_specs: Dict[bytes, Any] = {}  # head-path tasks in flight (replayed on re-attach)
+        self._ret_task: Dict[bytes, bytes] = {}
+        self._running_res: Dict[bytes, dict] = {}
+        self._unsent_done = set()
+        self.reattaches = 0
+        self._subs: Dict[str, List[Any]] = {}  # pubsub channel -> callbacks (run in the reader thread)
         from . import lease
 
         self.leases = lease.LeaseManager(self) if lease.enabled() and kind in ("driver", "worker") else None
@@ -198,6 +210,7 @@ class CoreWorker:
         msg = self.conn.recv()
         assert msg[0] == "registered", msg
         info = msg[1]
+        self.reconnect_s = max(self.reconnect_s, float(info.get("reconnect_s") or 0))
         self.node_hex = info["node_id"]
         self.namespace = info["namespace"]
         self.session_dir = info["session_dir"]
@@ -218,24 +231,45 @@ class CoreWorker:
         # borrow announcements go BEFORE the message, releases AFTER it: a message
         # may pin objects (task_done with nested refs, submit args) whose last
         # local reference died while it was being built.
-        with self.send_lock:
-            ops = self.refs.drain()
-            if ops:
-                adds = [m for m in ops if m[0] == "addref"]
-                decs = [m for m in ops if m[0] == "decref"]
-                self.conn.send_many(adds + [msg] + decs)
-            else:
-                self.conn.send(msg)
+        while True:
+            conn = self.conn
+            try:
+                with self.send_lock:
+                    ops = self.refs.drain()
+                    if ops:
+                        adds = [m for m in ops if m[0] == "addref"]
+                        decs = [m for m in ops if m[0] == "decref"]
+                        conn.send_many(adds + [msg] + decs)
+                    else:
+                        conn.send(msg)
+                return
+            except (ConnectionClosed, OSError):
+                if not self._await_reconnect(conn):
+                    raise
+
+    def _await_reconnect(self, old) -> bool:
+        """Block a sender until the reader thread has re-attached to a restarted head
+        (True) or given up (False)."""
+        if self.reconnect_s <= 0 or threading.current_thread() is getattr(self, "_reader", None):
+            return False
+        deadline = time.time() + self.reconnect_s + 5
+        with self._conn_cv:
+            while self.conn is old and self.alive and time.time() < deadline:
+                self._conn_cv.wait(0.5)
+        return self.conn is not old
 
     def request(self, build, timeout=None):
         req = next(self._req)
         fut = concurrent.futures.Future()
         self.pending[req] = fut
-        self.send(build(req))
+        if self.reconnect_s > 0:
+            self._req_builds[req] = build
         try:
+            self.send(build(req))
             return fut.result(timeout)
         finally:
             self.pending.pop(req, None)
+            self._req_builds.pop(req, None)
 
     def request_cb(self, build, cb):
         """Send a request; ``cb(value)`` runs in the reader thread (None on failure)."""
@@ -244,10 +278,13 @@ class CoreWorker:
 
         def done(f, r=req):
             self.pending.pop(r, None)
+            self._req_builds.pop(r, None)
             cb(None if f.exception() is not None else f.result())
 
         fut.add_done_callback(done)
         self.pending[req] = fut
+        if self.reconnect_s > 0:
+            self._req_builds[req] = build
         self.send(build(req))
 
     def _escape(self, oids):
@@ -261,7 +298,9 @@ class CoreWorker:
         req = next(self._req)
         fut = concurrent.futures.Future()
         self.pending[req] = fut
-        fut.add_done_callback(lambda f, r=req: self.pending.pop(r, None))
+        if self.reconnect_s > 0:
+            self._req_builds[req] = build
+        fut.add_done_callback(lambda f, r=req: (self.pending.pop(r, None), self._req_builds.pop(r, None)))
         self.send(build(req))
         return fut
 
@@ -287,7 +326,15 @@ class CoreWorker:
                 ops = r.drain_locked()
             msgs = [m for m in ops if m[0] == "addref"] + [("dseal_batch", items)] + \
                    [m for m in ops if m[0] == "decref"]
-            self.conn.send_many(msgs)
+        while True:
+            conn = self.conn
+            try:
+                with self.send_lock:
+                    conn.send_many(msgs)
+                return
+            except (ConnectionClosed, OSError):
+                if not self._await_reconnect(conn):
+                    raise
 
     def _flush_loop(self):
         while self.alive:
@@ -299,20 +346,27 @@ class CoreWorker:
                 except (ConnectionClosed, OSError):
                     return
             if self.refs.ops or self.refs.deferred:
+                conn = self.conn
                 try:
                     with self.send_lock:
                         ops = self.refs.drain()
                         if ops:
-                            self.conn.send_many(ops)
+                            conn.send_many(ops)
                 except (ConnectionClosed, OSError):
-                    return
+                    # released refs are re-counted from scratch on re-attach
+                    if not self._await_reconnect(conn):
+                        return
 
     def _read_loop(self):
         while self.alive:
             try:
                 msg = self.conn.recv()
             except (ConnectionClosed, OSError):
+                if self.reconnect_s > 0 and self.alive and self._reconnect():
+                    continue
                 self.alive = False
+                with self._conn_cv:
+                    self._conn_cv.notify_all()
                 with self.refs.cv:
                     self.refs.cv.notify_all()
                 for f in list(self.pending.values()):
@@ -331,10 +385,119 @@ class CoreWorker:
                 self._on_execute(msg[1])
             elif t == "cancel":
                 self._on_cancel(msg[1])
+            elif t == "pub":
+                for cb in list(self._subs.get(msg[1], ())):
+                    try:
+                        cb(msg[2], msg[3])
+                    except Exception:
+                        traceback.print_exc()
             elif t == "exit":
                 self.task_queue.put(None)
 
+    # ------------------------------------------------------------------ pubsub
+    def subscribe(self, channel: str, callback):
+        """``callback(key, info)`` for every state change the head publishes on
+        ``channel`` ("actor": actor id -> state/name/pid/death cause; "node": node id
+        -> ALIVE / DEAD). Runs in the reader thread: keep it short."""
+        first = channel not in self._subs
+        self._subs.setdefault(channel, []).append(callback)
+        if first:
+            self.send(("subscribe", channel))
+
+    def unsubscribe(self, channel: str, callback):
+        cbs = self._subs.get(channel, [])
+        if callback in cbs:
+            cbs.remove(callback)
+        if not cbs and channel in self._subs:
+            del self._subs[channel]
+            self.send(("unsubscribe", channel))
+
+    # ------------------------------------------------ head restart: re-attach
+    def _reconnect(self) -> bool:
+        """The head connection broke: reconnect to the (restarted) head at the same
+        address, re-register with this process's live state and replay what was in
+        flight. False if no head came back within ``reconnect_s``."""
+        old = self.conn
+        deadline = time.time() + self.reconnect_s
+        while self.alive and time.time() < deadline:
+            try:
+                conn = connect(self.address)
+            except OSError:
+                time.sleep(0.2)
+                continue
+            try:
+                conn.send(("reregister", self.kind, self.worker_id, os.getpid(), self.node_hex,
+                           self._reattach_state()))
+                msg = conn.recv()
+            except (ConnectionClosed, OSError):
+                conn.close()
+                time.sleep(0.2)
+                continue
+            if msg[0] != "registered":
+                conn.close()
+                return False
+            with self._conn_cv:
+                self.conn = conn
+                self.reattaches += 1
+                self._conn_cv.notify_all()
+            try:
+                old.close()
+            except Exception:
+                pass
+            try:
+                for ch in list(self._subs):
+                    self.send(("subscribe", ch))
+                for req, build in sorted(self._req_builds.items()):
+                    if req in self.pending:
+                        self.send(build(req))
+                for spec in list(self._head_specs.values()):
+                    self.send(("submit", spec))
+            except (ConnectionClosed, OSError):
+                continue
+            return True
+        return False
+
+    def _reattach_state(self) -> dict:
+        gpus = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
+        st = {"job_id": self.job_id, "gpu_ids": gpus, "actor_id": self.actor_id,
+              "direct": self.direct_server.path if self.direct_server is not None else None}
+        st["running"] = [(tid, self._running_res.get(tid) or {}) for tid in list(self._running_res)
+                         if tid in self.running_tasks]
+        st["finishing"] = list(self._unsent_done)
+        r = self.refs
+        refs, inline = {}, {}
+        with r.lock:
+            for oid, n in r.counts.items():
+                if n <= 0:
+                    continue
+                refs[oid] = 1  # the head counts holders, not local references
+                ent = r.ready.get(oid) or r.cache.get(oid)
+                if ent is not None and ent[0] in ("inline", "err") and ent[1] is not None:
+                    inline[oid] = (ent[1], ent[0] == "err")
+                elif oid in r.local_only:
+                    blob, _size, is_err = r.local_only[oid]
+                    inline[oid] = (blob, is_err)
+        st["refs"], st["inline"] = refs, inline
+        if self.leases is not None:
+            st["leases"] = [(lc.worker_id, dict(k.resources)) for k in list(self.leases.keys.values())
+                            for lc in list(k.leases) if lc.alive]
+        return st
+
+    def _track_head_spec(self, spec):
+        if self.reconnect_s <= 0 or spec.generator is not None or spec.kind == ACTOR_CREATE:
+            return
+        self._head_specs[spec.task_id] = spec
+        for o in spec.return_ids or ():
+            self._ret_task[o] = spec.task_id
+
     def _on_ready(self, items):
+        if self._ret_task:
+            for (oid, _k, _p) in items:
+                tid = self._ret_task.pop(oid, None)
+                if tid is not None:
+                    spec = self._head_specs.pop(tid, None)
+                    for o in (spec.return_ids if spec is not None else ()) or ():
+                        self._ret_task.pop(o, None)
         r = self.refs
         with r.cv:
             for (oid, kind, payload) in items:
@@ -954,6 +1117,7 @@ class CoreWorker:
                     self.head_inflight_actor[o] = actor_id
         if arg_refs and (r.local_only or r.direct_pending):
             self._escape(arg_refs)
+        self._track_head_spec(spec)
         self.send(("submit", spec))
         del keep
         if generator == "streaming":
@@ -1023,6 +1187,8 @@ class CoreWorker:
         spec, _, resolved = payload
         if spec.task_id in self.direct_origin:
             self.__dict__.setdefault("_t_start", {})[spec.task_id] = time.time()
+        elif spec.kind == NORMAL and self.reconnect_s > 0:
+            self._running_res[spec.task_id] = dict(spec.resources or {})
         self.running_tasks[spec.task_id] = threading.current_thread()
         self._set_ctx(spec)
         error_kind, retryable = None, False
@@ -1109,10 +1275,14 @@ class CoreWorker:
             except (ConnectionClosed, OSError):
                 pass
             return
+        self._unsent_done.add(spec.task_id)  # reported on re-attach while this send waits
         try:
             self.send(("task_done", spec.task_id, results, error_kind, retryable))
         except ConnectionClosed:
             pass
+        finally:
+            self._unsent_done.discard(spec.task_id)
+            self._running_res.pop(spec.task_id, None)
 
     def _setup_actor_concurrency(self, cls):
         is_async = any(inspect.iscoroutinefunction(m) or inspect.isasyncgenfunction(m)

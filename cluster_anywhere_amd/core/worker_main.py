@@ -35,7 +35,10 @@ def _apply_runtime_env(renv: dict):
 
 
 def main():
-    _die_with_parent()
+    if float(os.environ.get("CAAMD_HEAD_RECONNECT_S", "0") or 0) <= 0:
+        _die_with_parent()
+    # else: the worker outlives a head crash and re-attaches to the restarted head
+    # (it exits on its own if none comes back within the reconnect window)
     for p in reversed(os.environ.get("CAAMD_SYS_PATH", "").split(os.pathsep)):
         if p and p not in sys.path:
             sys.path.insert(1, p)

@@ -96,6 +96,13 @@ class _Router:
         with self.lock:
             self.inflight[tag] = max(0, self.inflight.get(tag, 0) - 1)
 
+    def drop_actor(self, actor_id):
+        with self.lock:
+            keep = [r for r in self.replicas if getattr(r[1], "_actor_id", None) != actor_id]
+            if len(keep) != len(self.replicas):
+                self.replicas = keep
+                self.version = -1  # take the controller's next snapshot whatever its version
+
     def invalidate(self):
         self.last_refresh = 0.0
         self.version = -1
@@ -104,9 +111,35 @@ class _Router:
 
 _routers: Dict[tuple, _Router] = {}
 _routers_lock = threading.Lock()
+_actor_sub = False
+
+
+def _on_actor_event(actor_id, info):
+    """Head pubsub (core/head.py ``_publish``): a replica that died leaves every
+    router of this process at once, before the controller's next health check."""
+    if info.get("state") != "DEAD":
+        return
+    for r in list(_routers.values()):
+        r.drop_actor(actor_id)
+
+
+def _ensure_actor_sub():
+    global _actor_sub
+    if _actor_sub:
+        return
+    from ..core import context
+
+    w = context.worker
+    if w is not None and hasattr(w, "subscribe"):
+        try:
+            w.subscribe("actor", _on_actor_event)
+            _actor_sub = True
+        except Exception:
+            pass
 
 
 def _router(app, dep) -> _Router:
+    _ensure_actor_sub()
     with _routers_lock:
         r = _routers.get((app, dep))
         if r is None:

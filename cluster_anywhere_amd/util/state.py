@@ -92,3 +92,23 @@ def summarize_objects() -> Dict[str, Any]:
 
 def object_store_stats() -> Dict[str, int]:
     return _state("store")
+
+
+def subscribe(channel: str, callback):
+    """Subscribe to the head's state-change publisher (reference:
+    src/ray/pubsub/publisher.h): ``channel`` "actor" delivers ``callback(actor_id,
+    {"state", "name", "namespace", "class_name", "pid", "node", "death_cause"})`` on
+    every actor state change, "node" delivers ``callback(node_id, {"state", ...})``
+    when nodes join or die. Callbacks run on the driver's reader thread."""
+    from ..core import context
+
+    if context.worker is None:
+        raise RuntimeError("subscribe() needs init()")
+    context.worker.subscribe(channel, callback)
+
+
+def unsubscribe(channel: str, callback):
+    from ..core import context
+
+    if context.worker is not None:
+        context.worker.unsubscribe(channel, callback)
