@@ -46,21 +46,23 @@ def _method_meta(cls) -> Dict[str, Any]:
 
 
 class ActorMethod:
-    def __init__(self, handle: "ActorHandle", name: str, num_returns=1, concurrency_group=None):
+    def __init__(self, handle: "ActorHandle", name: str, num_returns=1, concurrency_group=None, gen_bp=None):
         self._handle = handle
         self._name = name
         self._num_returns = num_returns
         self._cg = concurrency_group
+        self._gen_bp = gen_bp
 
     def __call__(self, *a, **k):
         raise TypeError(f"Actor methods cannot be called directly; use '{self._name}.remote()'.")
 
     def options(self, **kw):
         return ActorMethod(self._handle, self._name, kw.get("num_returns", self._num_returns),
-                           kw.get("concurrency_group", self._cg))
+                           kw.get("concurrency_group", self._cg),
+                           kw.get("_generator_backpressure_num_objects", self._gen_bp))
 
     def remote(self, *args, **kwargs):
-        return self._handle._call(self._name, args, kwargs, self._num_returns, self._cg)
+        return self._handle._call(self._name, args, kwargs, self._num_returns, self._cg, self._gen_bp)
 
     def bind(self, *args, **kwargs):
         from ..dag import ClassMethodNode
@@ -101,7 +103,7 @@ class ActorHandle:
         m = methods.get(name, {"num_returns": 1, "concurrency_group": None})
         return ActorMethod(self, name, m["num_returns"], m.get("concurrency_group"))
 
-    def _call(self, name, args, kwargs, num_returns, cg):
+    def _call(self, name, args, kwargs, num_returns, cg, gen_bp=None):
         if context.local_mode:
             from .local_mode import run_local_method
 
@@ -111,7 +113,8 @@ class ActorHandle:
             name, args, kwargs = "__ray_ready__", (), {}
         refs = w.submit(ACTOR_METHOD, None, self._meta.get("class_name", "Actor"), args, kwargs,
                         num_returns=num_returns, actor_id=self._actor_id, method=name,
-                        concurrency_group=cg, max_retries=self._meta.get("max_task_retries", 0))
+                        concurrency_group=cg, max_retries=self._meta.get("max_task_retries", 0),
+                        gen_bp=gen_bp)
         if num_returns == "streaming":
             return refs
         if num_returns == 1 or num_returns == "dynamic":

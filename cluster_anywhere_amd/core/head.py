@@ -76,7 +76,7 @@ class TaskSpec:
         "actor_id", "method", "actor_opts", "runtime_env", "name", "job_id", "attempt",
         "generator", "node", "worker", "gpu_ids", "state", "submit_time", "start_time",
         "acquired", "pg_id", "cancelled", "parent", "concurrency_group", "pinned_refs",
-        "blocked",
+        "blocked", "gen_bp",
     )
 
     def __init__(self, **kw):
@@ -250,6 +250,9 @@ class Head:
         self.pgs: Dict[bytes, dict] = {}
         self.pending_pgs: List[bytes] = []
         self.gen_waiters: Dict[bytes, list] = collections.defaultdict(list)
+        self.gen_consumed: Dict[bytes, int] = {}  # streaming task -> items handed to its consumer
+        self.gen_consume_waiters: Dict[bytes, list] = {}  # producers waiting for consumption
+        self.gen_stats: Dict[bytes, dict] = {}
         self.handle_objs: Dict[bytes, bytes] = {}  # handle object id -> actor id
         self.events: collections.deque = collections.deque(maxlen=200000)
         self.jobs: Dict[bytes, dict] = {}
@@ -1367,6 +1370,13 @@ class Head:
 
     # ----------------------------------------------------------- generators
     def _h_gen_item(self, c, task_id, index, oid, inline, size, node_hex, contained, is_err=False):
+        st = self.gen_stats.get(task_id)
+        if st is None:
+            if len(self.gen_stats) > 4096:
+                self.gen_stats.pop(next(iter(self.gen_stats)))
+            st = self.gen_stats[task_id] = {"produced": 0, "max_outstanding": 0}
+        st["produced"] = max(st["produced"], index + 1)
+        st["max_outstanding"] = max(st["max_outstanding"], index + 1 - self.gen_consumed.get(task_id, 0))
         self._obj(oid).refcount += 1  # held by the generator object on the owner side
         self._seal_object(oid, inline, size, node_hex, contained, is_err)
         for cb in list(self.gen_waiters.get((task_id, index), [])):
@@ -1376,11 +1386,42 @@ class Head:
     def _gen_end(self, task_id, count, error=None):
         key = ("__gen_end__", task_id)
         self.kv[key] = (count, error)
+        self.gen_consumed.pop(task_id, None)
+        self.gen_consume_waiters.pop(task_id, None)
         for k in [k for k in self.gen_waiters if k[0] == task_id]:
             for cb in self.gen_waiters.pop(k):
                 cb()
 
+    # ---- generator backpressure (reference: remote_function.py:396
+    # _generator_backpressure_num_objects): the consumer asking for item k has taken
+    # items 0..k-1; a producer with k unconsumed items waits in gen_wait.
+    def _gen_consumed_to(self, task_id, n):
+        if n <= self.gen_consumed.get(task_id, 0):
+            return
+        self.gen_consumed[task_id] = n
+        waiters = self.gen_consume_waiters.get(task_id)
+        if waiters:
+            keep = []
+            for (wc, wreq, need) in waiters:
+                if n >= need:
+                    self._reply(wc, wreq, n)
+                else:
+                    keep.append((wc, wreq, need))
+            self.gen_consume_waiters[task_id] = keep
+
+    def _h_gen_wait(self, c, req, task_id, need):
+        have = self.gen_consumed.get(task_id, 0)
+        if have >= need or ("__gen_end__", task_id) in self.kv:
+            self._reply(c, req, have)
+        else:
+            self.gen_consume_waiters.setdefault(task_id, []).append((c, req, need))
+
+    def _h_gen_drop(self, c, task_id):
+        """The consumer dropped its generator: never hold the producer back again."""
+        self._gen_consumed_to(task_id, 1 << 62)
+
     def _h_gen_next(self, c, req, task_id, index):
+        self._gen_consumed_to(task_id, index)
         oid = ObjectID.for_task_return(task_id, index)
 
         def answer():
@@ -2251,6 +2292,9 @@ class Head:
             m["series"][key] = cur
 
     def state(self, what, arg=None):
+        if what == "gen_stats":
+            st = self.gen_stats.get(arg)
+            return dict(st, consumed=self.gen_consumed.get(arg)) if st else None
         if what == "reattach_stats":
             return dict(self.reattach_stats, reattached=self.reattached, reattaching=self._reattaching)
         if what == "metrics":

@@ -114,6 +114,18 @@ class ObjectRefGenerator:
     def completed(self) -> ObjectRef:
         return self._keep
 
+    def __del__(self):
+        # a dropped generator never holds a backpressured producer back again
+        if not self._done:
+            try:
+                w = context.worker
+                if w is not None and getattr(w, "alive", False):
+                    # never send from a finalizer (it may run inside a send's critical
+                    # section): the flush thread delivers it
+                    w.gen_drops.append(self._task_id)
+            except Exception:
+                pass
+
     def __reduce__(self):
         return (ObjectRefGenerator, (self._task_id, None))
 

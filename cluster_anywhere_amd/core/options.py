@@ -21,6 +21,9 @@ TASK_DEFAULTS = {
     "max_calls": 0,
     "label_selector": None,
     "_metadata": None,
+    # streaming generators: pause the producer once this many yielded items are
+    # unconsumed (reference: remote_function.py:396)
+    "_generator_backpressure_num_objects": None,
 }
 
 ACTOR_DEFAULTS = {

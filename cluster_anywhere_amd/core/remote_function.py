@@ -63,6 +63,7 @@ class RemoteFunction:
             num_returns=o["num_returns"], resources=opt_utils.resource_demand(o),
             strategy=opt_utils.strategy_tuple(o), max_retries=o["max_retries"],
             retry_exceptions=o["retry_exceptions"], runtime_env=o.get("runtime_env"),
+            gen_bp=o.get("_generator_backpressure_num_objects"),
         )
         nr = o["num_returns"]
         if nr == "streaming":

@@ -198,6 +198,7 @@ class CoreWorker:
         self._unsent_done = set()
         self.reattaches = 0
         self._subs: Dict[str, List[Any]] = {}  # pubsub channel -> callbacks (run in the reader thread)
+        self.gen_drops: collections.deque = collections.deque()  # dropped generators (finalizers)
         from . import lease
 
         self.leases = lease.LeaseManager(self) if lease.enabled() and kind in ("driver", "worker") else None
@@ -340,6 +341,11 @@ class CoreWorker:
         while self.alive:
             self._flush_evt.wait(0.005 if self.refs.dseal_buf else 0.05)
             self._flush_evt.clear()
+            while self.gen_drops:
+                try:
+                    self.send(("gen_drop", self.gen_drops.popleft()))
+                except (ConnectionClosed, OSError, IndexError):
+                    break
             if self.refs.dseal_buf:
                 try:
                     self._flush_dseals()
@@ -1054,7 +1060,7 @@ class CoreWorker:
 
     def submit(self, kind, fn_id, fn_name, args, kwargs, num_returns=1, resources=None,
                strategy=None, max_retries=0, retry_exceptions=False, actor_id=None, method=None,
-               actor_opts=None, runtime_env=None, name=None, concurrency_group=None):
+               actor_opts=None, runtime_env=None, name=None, concurrency_group=None, gen_bp=None):
         task_id = os.urandom(16)
         pa, pk, arg_refs, pinned, keep = self._pack_args(args, kwargs)
         generator = None
@@ -1074,7 +1080,8 @@ class CoreWorker:
                         actor_id=actor_id, method=method, actor_opts=actor_opts,
                         runtime_env=runtime_env, name=name, job_id=self.job_id,
                         generator=generator, parent=ctx.task_id if ctx else None,
-                        concurrency_group=concurrency_group)
+                        concurrency_group=concurrency_group,
+                        gen_bp=int(gen_bp) if gen_bp and generator == "streaming" else None)
         refs = [] if generator == "streaming" else [ObjectRef(o, _owned=True) for o in return_ids]
         r = self.refs
         busy = bool(r.owned)
@@ -1399,8 +1406,19 @@ class CoreWorker:
 
     def _stream(self, spec, gen):
         i = 0
+        bp = spec.gen_bp or 0
+        consumed = 0
         try:
-            for item in gen:
+            it = iter(gen)
+            while True:
+                if bp > 0 and i - consumed >= bp:
+                    # backpressure: the generator body does not run ahead of its
+                    # consumer by more than bp items
+                    consumed = self.request(lambda r, n=i - bp + 1: ("gen_wait", r, spec.task_id, n))
+                try:
+                    item = next(it)
+                except StopIteration:
+                    break
                 self._stream_item(spec, i, item)
                 i += 1
         except BaseException as e:  # noqa

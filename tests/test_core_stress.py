@@ -170,3 +170,54 @@ def test_concurrent_drivers_share_one_head(tmp_path):
         assert len(jobs) >= 4, jobs
     finally:
         ray.shutdown()
+
+
+def test_streaming_generator_backpressure():
+    """_generator_backpressure_num_objects=N: the producer never runs more than N
+    items ahead of its consumer (reference: python/ray/remote_function.py:396)."""
+    from cluster_anywhere_amd.core.api import _state
+
+    ray.init(num_cpus=2)
+    try:
+        @ray.remote(num_returns="streaming", _generator_backpressure_num_objects=4)
+        def produce(n):
+            for i in range(n):
+                yield i
+
+        gen = produce.remote(10_000)
+        out = [ray.get(r) for r in gen]
+        assert out == list(range(10_000))
+        st = _state("gen_stats", gen._task_id)
+        assert st["produced"] == 10_000 and st["max_outstanding"] <= 4, st
+
+        # without backpressure a fast producer runs far ahead of a slow consumer
+        @ray.remote(num_returns="streaming")
+        def produce_free(n):
+            for i in range(n):
+                yield i
+
+        gen2 = produce_free.remote(200)
+        first = next(gen2)
+        time.sleep(1.0)
+        rest = [ray.get(r) for r in gen2]
+        assert [ray.get(first)] + rest == list(range(200))
+        assert _state("gen_stats", gen2._task_id)["max_outstanding"] > 4
+
+        # actor method generators take the option too
+        @ray.remote
+        class P:
+            def items(self, n):
+                for i in range(n):
+                    yield i * 2
+
+        p = P.remote()
+        g3 = p.items.options(num_returns="streaming", _generator_backpressure_num_objects=2).remote(300)
+        assert [ray.get(r) for r in g3] == [i * 2 for i in range(300)]
+        assert _state("gen_stats", g3._task_id)["max_outstanding"] <= 2
+        # a consumer that drops its generator releases the producer
+        g4 = produce.remote(50)
+        next(g4)
+        del g4
+        time.sleep(0.5)
+    finally:
+        ray.shutdown()
