@@ -286,13 +286,16 @@ def _mem_bytes():
 
 
 def _check_runtime_env(renv):
-    """Validate a runtime_env; ``pip``/``conda``/``uv`` packages must already be
-    importable (no package index on the pods — see runtime_env/__init__.py)."""
+    """Validate a runtime_env. ``pip`` / ``uv`` packages are installed into a cached
+    virtualenv when a worker of that env starts (runtime_env/pip.py: offline, from
+    local wheels / find-links); a failed install surfaces as RuntimeEnvSetupError on
+    the task's result. ``conda`` cannot be installed here (no conda in the image), so
+    its dependencies must already be importable."""
     from ..exceptions import RuntimeEnvSetupError
     from ..runtime_env import RuntimeEnv, missing_packages
 
     RuntimeEnv(**dict(renv))
-    for key in ("pip", "uv", "conda"):
+    for key in ("conda",):
         spec = renv.get(key)
         if spec is None:
             continue

@@ -60,6 +60,18 @@ def _node_labels(node_hex, gpu_ids, labels):
 _START_TIME_ENV = ("PYTHON", "LD_", "OMP_", "MKL_", "OPENBLAS_", "GOMP_", "KMP_", "MALLOC_", "TORCH_")
 
 
+def _env_key(renv) -> Optional[str]:
+    """Worker-pool key of a task's runtime env (None: the job's default workers).
+    Tasks only reuse workers started with the same env (reference: worker_pool.cc
+    keys idle workers by runtime-env hash)."""
+    if not renv:
+        return None
+    import hashlib
+    import json
+
+    return hashlib.sha1(json.dumps(renv, sort_keys=True, default=str).encode()).hexdigest()[:16]
+
+
 def _needs_fresh_interpreter(renv) -> bool:
     if not renv:
         return False
@@ -290,6 +302,7 @@ class Head:
         self.reattach_s = float(os.environ.get("CAAMD_GCS_REATTACH_S", "10"))
         self._reattaching = False
         self.subscribers: Dict[str, Set[Conn]] = {}  # pubsub channel -> subscriber connections
+        self.env_failures: Dict[str, str] = {}  # runtime-env key -> setup error
         self.reattached_running: Dict[bytes, tuple] = {}  # task id -> (worker, node, demand) of a re-registered run
         self._held_resubmits: List[tuple] = []  # (conn, spec) replayed by owners during the re-attach grace
         self.reattach_stats = {"workers": 0, "actors": 0, "objects": 0, "drivers": 0, "lost_objects": 0,
@@ -477,7 +490,7 @@ class Head:
             w.client_id = worker_id
             w.direct_addr = (extra or {}).get("direct")
             self.conn_worker[c] = w
-            key = (w.node, w.gpu_key)
+            key = (w.node, w.gpu_key, w.env_key)
             self.starting[key] = max(0, self.starting[key] - 1)
             pending = self.pending_spawn.pop(worker_id, None)
             if pending and pending[0] == "actor":
@@ -1079,7 +1092,11 @@ class Head:
             self.pending_spawn[wid] = ("actor", spec.actor_id)
             self._spawn_worker(node, gpu_ids, worker_id=wid, env=spec.runtime_env)
             return True
-        key = (node, gpu_ids)
+        ek = _env_key(spec.runtime_env)
+        if ek is not None and ek in self.env_failures:
+            self._fail_task(spec, ("RuntimeEnvSetupError", f"runtime env setup failed: {self.env_failures[ek]}"))
+            return True
+        key = (node, gpu_ids, ek)
         idle = self.idle.get(key)
         w = None
         while idle:
@@ -1088,8 +1105,11 @@ class Head:
                 w = cand
                 break
         if w is None:
-            if self.starting[key] < max(1, int(self.cpu_count)) and self._num_workers(node) < self.max_workers:
-                self._spawn_worker(node, gpu_ids)
+            if self.starting[key] < max(1, int(self.cpu_count)):
+                if self._num_workers(node) >= self.max_workers:
+                    self._evict_idle(node, key)  # an idle worker of another env makes room
+                if self._num_workers(node) < self.max_workers:
+                    self._spawn_worker(node, gpu_ids, env=spec.runtime_env)
             return False
         if not self.sched.acquire(node, demand):
             w.idle = True
@@ -1149,11 +1169,27 @@ class Head:
 
     def _num_workers(self, node):
         return sum(1 for w in self.workers.values() if w.node == node and w.alive) + sum(
-            v for (n, _), v in self.starting.items() if n == node)
+            v for (n, _g, _e), v in self.starting.items() if n == node)
+
+    def _evict_idle(self, node, keep_key):
+        """Stop one idle pooled worker of another runtime env on ``node`` (reference:
+        the raylet worker pool kills idle workers of other runtime envs when full)."""
+        for key, lst in self.idle.items():
+            if key == keep_key or key[0] != node:
+                continue
+            while lst:
+                w = lst.pop()
+                if w.alive and w.idle and w.actor_id is None and w.lease is None:
+                    w.idle = False
+                    self._send(w.conn, ("exit",))
+                    self._kill_worker(w.worker_id)
+                    return True
+        return False
 
     def _spawn_worker(self, node, gpu_ids, worker_id=None, env=None):
         worker_id = worker_id or os.urandom(16)
-        key = (node, tuple(gpu_ids))
+        ek = _env_key(env)
+        key = (node, tuple(gpu_ids), ek)
         self.starting[key] += 1
         if node != self.head_hex:
             return self._spawn_remote(node, gpu_ids, worker_id, env)
@@ -1183,6 +1219,14 @@ class Head:
         # code search path is propagated through the job config)
         e["CAAMD_SYS_PATH"] = os.pathsep.join(p for p in sys.path if p and os.path.isdir(p))
         log_path = os.path.join(self.session_dir, f"worker-{worker_id.hex()[:8]}.log")
+        try:
+            from ..runtime_env import pip as _pip
+
+            pip_cfg = _pip.pip_field(renv)
+        except Exception:  # noqa: BLE001 - a malformed pip field fails at setup below
+            pip_cfg = None
+        if pip_cfg is not None:
+            return self._spawn_in_env(worker_id, node, gpu_ids, ek, e, log_path, pip_cfg, renv)
         zyg = getattr(self, "_zygote", None)
         if zyg is not None and _needs_fresh_interpreter(renv):
             zyg = None  # start-time variables / another interpreter: a fork cannot honour them
@@ -1194,9 +1238,65 @@ class Head:
                                     cwd=os.getcwd())
             log.close()
         w = WorkerInfo(worker_id=worker_id, pid=proc.pid, node=node, gpu_key=tuple(gpu_ids),
-                       kind="worker", proc=proc, alive=False)
+                       kind="worker", proc=proc, alive=False, env_key=ek)
         self.workers[worker_id] = w
         return w
+
+    def _spawn_in_env(self, worker_id, node, gpu_ids, ek, e, log_path, cfg, renv):
+        """Start a worker inside a pip / uv runtime env (runtime_env/pip.py): the env is
+        built (or found in the URI cache) on a thread, then the worker is launched
+        with that env's interpreter (reference: PipPlugin, pip.py:216)."""
+        from ..runtime_env import pip as _pip
+
+        w = WorkerInfo(worker_id=worker_id, pid=None, node=node, gpu_key=tuple(gpu_ids), kind="worker",
+                       proc=None, alive=False, env_key=ek)
+        self.workers[worker_id] = w
+        if ek in self.env_failures:
+            self.call(lambda: self._env_setup_failed(w, ek, self.env_failures[ek]))
+            return w
+
+        def build():
+            try:
+                py = _pip.ensure_env(cfg, _pip.setup_timeout(renv))
+            except Exception as exc:  # noqa: BLE001
+                msg = str(exc)
+                self.call(lambda: self._env_setup_failed(w, ek, msg))
+                return
+
+            def launch():
+                if self.workers.get(worker_id) is not w or not self.running:
+                    return
+                log = open(log_path, "ab")
+                proc = subprocess.Popen([py, "-m", "cluster_anywhere_amd.core.worker_main"], env=e, stdout=log,
+                                        stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, cwd=os.getcwd())
+                log.close()
+                w.proc, w.pid = proc, proc.pid
+
+            self.call(launch)
+
+        threading.Thread(target=build, name="caamd-runtime-env", daemon=True).start()
+        return w
+
+    def _env_setup_failed(self, w, ek, msg):
+        """The runtime env could not be built: fail what waits for it (reference:
+        RuntimeEnvSetupError), and fail later tasks of the same env at once."""
+        self.env_failures[ek] = msg
+        key = (w.node, w.gpu_key, ek)
+        self.starting[key] = max(0, self.starting[key] - 1)
+        self.workers.pop(w.worker_id, None)
+        cause = f"runtime env setup failed: {msg}"
+        pending = self.pending_spawn.pop(w.worker_id, None)
+        if pending and pending[0] == "actor":
+            a = self.actors.get(pending[1])
+            if a is not None:
+                a.restarts_left = 0
+                a.death_cause = cause
+                self._set_actor_state(a, "DEAD")
+                self._fail_actor_queue(a, "RuntimeEnvSetupError", cause)
+        for q in list(self.ready_queues.values()):
+            for spec in [sp for sp in q if _env_key(sp.runtime_env) == ek]:
+                q.remove(spec)
+                self._fail_task(spec, ("RuntimeEnvSetupError", cause))
 
     def _spawn_remote(self, node, gpu_ids, worker_id, env):
         """Ask the node's agent to start a worker (reference: raylet worker pool)."""
@@ -1215,7 +1315,7 @@ class Head:
         extra["CAAMD_SYS_PATH"] = os.pathsep.join(p for p in sys.path if p and os.path.isdir(p))
         self._send(self.node_conns.get(node), ("spawn", worker_id.hex(), list(gpu_ids), extra))
         w = WorkerInfo(worker_id=worker_id, pid=None, node=node, gpu_key=tuple(gpu_ids),
-                       kind="worker", proc=None, alive=False)
+                       kind="worker", proc=None, alive=False, env_key=_env_key(env))
         self.workers[worker_id] = w
         return w
 
@@ -1260,7 +1360,7 @@ class Head:
                     self.sched.release(run[1], run[2])
                 if w is not None and w.actor_id is None and not w.tasks_inflight and w.lease is None:
                     w.idle = True
-                    self.idle[(w.node, w.gpu_key)].append(w)
+                    self.idle[(w.node, w.gpu_key, w.env_key)].append(w)
                     self._schedule()
             return
         self.events.append(("end", task_id, spec.fn_name, time.time(), w.pid if w else None))
@@ -1327,7 +1427,7 @@ class Head:
             return
         w.task = None
         w.idle = True
-        self.idle[(w.node, w.gpu_key)].append(w)
+        self.idle[(w.node, w.gpu_key, w.env_key)].append(w)
 
     def _release(self, spec):
         if spec.acquired and spec.kind != ACTOR_CREATE:
@@ -1355,9 +1455,12 @@ class Head:
                                   TaskPlacementGroupRemoved, WorkerCrashedError)
 
         kind, msg = err
+        from ..exceptions import RuntimeEnvSetupError
+
         cls = {"ActorDiedError": ActorDiedError, "TaskCancelledError": TaskCancelledError,
                "WorkerCrashedError": WorkerCrashedError, "OutOfMemoryError": OutOfMemoryError,
-               "TaskPlacementGroupRemoved": TaskPlacementGroupRemoved}.get(kind, RayError)
+               "TaskPlacementGroupRemoved": TaskPlacementGroupRemoved,
+               "RuntimeEnvSetupError": RuntimeEnvSetupError}.get(kind, RayError)
         exc = cls(msg) if cls is not TaskCancelledError else TaskCancelledError(spec.task_id.hex(), msg)
         blob = serialization.serialize(exc).to_bytes()
         spec.state = "failed"
@@ -1562,7 +1665,7 @@ class Head:
     # parks (FIFO) and takes back leases.
     def _grant_leases(self, c, node, demand, want):
         out = []
-        key = (node, ())
+        key = (node, (), None)
         while len(out) < want:
             if not self.sched.acquire(node, demand):
                 break
@@ -1636,7 +1739,7 @@ class Head:
             self._lease_release(w)
             if w.alive and w.actor_id is None:
                 w.idle = True
-                self.idle[(w.node, w.gpu_key)].append(w)
+                self.idle[(w.node, w.gpu_key, w.env_key)].append(w)
         self._schedule()
 
     def _h_worker_fate(self, c, req, worker_id):
@@ -2021,7 +2124,7 @@ class Head:
         self._release_held(lambda sp: sp.task_id in self.reattached_running)
         if not busy:
             w.idle = True
-            self.idle[(node, w.gpu_key)].append(w)
+            self.idle[(node, w.gpu_key, w.env_key)].append(w)
             self._schedule()
 
     def _reattach_refs(self, extra):
@@ -2054,7 +2157,7 @@ class Head:
             demand = {k: float(v) for k, v in (res or {}).items() if v}
             if w.idle:
                 w.idle = False
-                lst = self.idle.get((w.node, w.gpu_key))
+                lst = self.idle.get((w.node, w.gpu_key, w.env_key))
                 if lst and w in lst:
                     lst.remove(w)
             if demand:
@@ -2110,7 +2213,7 @@ class Head:
         for w in list(self.workers.values()):
             if w.proc is not None and w.proc.poll() is not None and not w.alive and w.conn is None:
                 # died before registering
-                key = (w.node, w.gpu_key)
+                key = (w.node, w.gpu_key, w.env_key)
                 self.starting[key] = max(0, self.starting[key] - 1)
                 self.workers.pop(w.worker_id, None)
                 pending = self.pending_spawn.pop(w.worker_id, None)

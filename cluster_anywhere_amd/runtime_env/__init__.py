@@ -3,11 +3,13 @@
 A :class:`RuntimeEnv` is a validated dict applied by each worker before it runs
 user code (``core/worker_main.py``): ``env_vars`` (exported before HIP starts, so
 ``HIP_VISIBLE_DEVICES``-style variables take effect), ``working_dir`` (chdir +
-``sys.path``), ``py_modules`` (``sys.path``). There is no package index on MI355X
-pods, so ``pip`` / ``conda`` / ``uv`` entries are *verified* instead of installed:
-every listed distribution must already be importable in the image, otherwise the
-task fails with :class:`RuntimeEnvSetupError` (the reference fails the same way
-when installation fails).
+``sys.path``), ``py_modules`` (``sys.path``). Workers are pooled per runtime env
+(a task only reuses a worker started with the same env). ``pip`` / ``uv`` entries
+are INSTALLED offline into a cached virtualenv per requirements hash
+(``runtime_env/pip.py``: ``--no-index`` from local wheels / ``find_links``, LRU URI
+cache) and the env's workers run that env's interpreter; a failed install fails
+the task with :class:`RuntimeEnvSetupError`. ``conda`` is not in the image, so its
+dependencies are verified instead (they must already be importable).
 """
 from __future__ import annotations
 

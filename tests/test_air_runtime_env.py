@@ -1,6 +1,7 @@
 """ray.air namespace, RuntimeEnv / JobConfig (reference: python/ray/air/__init__.py,
 runtime_env/runtime_env.py, job_config.py)."""
 import os
+import time
 
 import pytest
 
@@ -49,8 +50,94 @@ def test_job_config_runtime_env_and_namespace():
         def f():
             return 1
 
+        # not installable offline: the install fails and the task reports it
         with pytest.raises(RuntimeEnvSetupError):
-            f.options(runtime_env={"pip": ["definitely-not-a-package-xyz"]}).remote()
-        assert ray.get(f.options(runtime_env={"pip": ["numpy"]}).remote()) == 1
+            ray.get(f.options(runtime_env={"pip": ["definitely-not-a-package-xyz"]}).remote(), timeout=300)
+        assert ray.get(f.options(runtime_env={"pip": ["numpy"]}).remote()) == 1  # satisfied: no env built
     finally:
         ray.shutdown()
+
+
+def _build_wheel(tmp_path, version="1.2.3"):
+    import subprocess
+    import sys
+
+    src = tmp_path / "src"
+    pkg = src / "caamd_rtenv_probe"
+    pkg.mkdir(parents=True)
+    (pkg / "__init__.py").write_text(f'VERSION = "{version}"\n')
+    (src / "setup.py").write_text(
+        "from setuptools import setup\n"
+        f"setup(name='caamd_rtenv_probe', version='{version}', packages=['caamd_rtenv_probe'])\n")
+    wheels = tmp_path / "wheels"
+    r = subprocess.run([sys.executable, "-m", "pip", "wheel", "--no-index", "--no-deps", "--no-build-isolation",
+                        "-w", str(wheels), str(src)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return str(wheels)
+
+
+def test_pip_runtime_env_installs_offline(tmp_path, monkeypatch):
+    """runtime_env={"pip": ...} installs a local wheel into a cached virtualenv and
+    the task runs inside it, while the driver cannot import the package (reference:
+    _private/runtime_env/pip.py:45,216, uri_cache.py:9)."""
+    import importlib.util
+
+    from cluster_anywhere_amd.runtime_env import pip as rpip
+
+    monkeypatch.setenv("CAAMD_RUNTIME_ENV_DIR", str(tmp_path / "envs"))
+    wheels = _build_wheel(tmp_path)
+    assert importlib.util.find_spec("caamd_rtenv_probe") is None
+    ray.init(num_cpus=2)
+    try:
+        @ray.remote
+        def probe():
+            import sys
+
+            import caamd_rtenv_probe
+
+            return caamd_rtenv_probe.VERSION, sys.prefix
+
+        env = {"pip": {"packages": ["caamd_rtenv_probe==1.2.3"], "find_links": [wheels]}}
+        ver, prefix = ray.get(probe.options(runtime_env=env).remote(), timeout=300)
+        assert ver == "1.2.3" and prefix.startswith(str(tmp_path / "envs"))
+        # the env is cached: the second use starts no build
+        envs = rpip._cache().entries()
+        assert len(envs) == 1
+        t0 = time.time()
+        assert ray.get(probe.options(runtime_env=env).remote(), timeout=120)[0] == "1.2.3"
+        # actors take the env too
+        @ray.remote
+        class A:
+            def v(self):
+                import caamd_rtenv_probe
+
+                return caamd_rtenv_probe.VERSION
+
+        a = A.options(runtime_env=env).remote()
+        assert ray.get(a.v.remote(), timeout=120) == "1.2.3"
+        # the driver's interpreter is untouched
+        assert importlib.util.find_spec("caamd_rtenv_probe") is None
+        # a version that is not among the local wheels fails with RuntimeEnvSetupError
+        bad = {"pip": {"packages": ["caamd_rtenv_probe==9.9"], "find_links": [wheels]}}
+        with pytest.raises(RuntimeEnvSetupError):
+            ray.get(probe.options(runtime_env=bad).remote(), timeout=300)
+        assert time.time() - t0 < 300
+    finally:
+        ray.shutdown()
+
+
+def test_uri_cache_evicts_least_recently_used(tmp_path):
+    from cluster_anywhere_amd.runtime_env.pip import _MARKER, URICache
+
+    root = tmp_path / "pip"
+    for i, name in enumerate(["a", "b", "c"]):
+        d = root / name
+        d.mkdir(parents=True)
+        (d / "blob").write_bytes(b"x" * 1000)
+        (d / _MARKER).write_text("{}")
+        os.utime(d / _MARKER, (1000 + i, 1000 + i))
+    c = URICache(str(root), max_bytes=2100)
+    c.touch(str(root / "a"))  # a becomes the most recently used
+    gone = c.evict()
+    assert gone == [str(root / "b")]
+    assert sorted(os.listdir(root)) == ["a", "c"]
