@@ -57,3 +57,12 @@ __all__ = [
     "from_torch", "from_huggingface", "read_parquet", "read_csv", "read_json", "read_text",
     "read_numpy", "read_binary_files", "read_images", "read_datasource", "preprocessors",
 ] + ['read_parquet_bulk', 'read_tfrecords', 'read_webdataset', 'read_sql', 'from_dask', 'from_spark', 'from_modin', 'from_mars', 'from_tf', 'read_bigquery', 'read_mongo', 'read_lance', 'read_iceberg', 'read_hudi', 'read_delta_sharing_tables', 'read_databricks_tables', 'read_clickhouse', 'read_avro', 'read_audio', 'read_videos']
+
+
+def __getattr__(name):
+    # ``data.llm`` imports pydantic / the LLM stack: load it on first use only
+    if name == "llm":
+        import importlib
+
+        return importlib.import_module(".llm", __name__)
+    raise AttributeError(name)

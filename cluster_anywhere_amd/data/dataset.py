@@ -7,6 +7,7 @@ shared-memory object store.
 """
 from __future__ import annotations
 
+import asyncio
 import builtins
 import collections
 import inspect
@@ -14,6 +15,7 @@ import itertools
 import math
 import os
 import random as _random
+import threading
 import time
 from typing import Any, Callable, Dict, Iterable, Iterator, List, Optional, Tuple, Union
 
@@ -97,12 +99,56 @@ def _batch_map(fn, batch_size, batch_format, fn_args, fn_kwargs, zero_copy_batch
             if not zero_copy_batch and isinstance(batch, dict):
                 batch = {k: np.array(v, copy=True) if not v.flags.writeable else v for k, v in batch.items()}
             out = fn(batch, *fn_args, **fn_kwargs)
-            if inspect.isgenerator(out):
+            if inspect.isasyncgen(out):
+                yield from _drain_async(out, batch_size)
+            elif inspect.iscoroutine(out):
+                yield B.from_batch(_loop().run_until_complete(out))
+            elif inspect.isgenerator(out):
                 for o in out:
                     yield B.from_batch(o)
             else:
                 yield B.from_batch(out)
     return f
+
+
+_tls = threading.local()
+
+
+def _loop():
+    """One event loop per executing thread, kept across batches so async UDF state
+    (HTTP sessions, engine handles) survives between calls."""
+    lp = getattr(_tls, "loop", None)
+    if lp is None or lp.is_closed():
+        lp = asyncio.new_event_loop()
+        _tls.loop = lp
+    return lp
+
+
+def _drain_async(agen, batch_size):
+    """Async-generator UDF (reference: the LLM batch stages stream rows one by one,
+    llm/_internal/batch/stages/base.py:83): outputs are coalesced into blocks of
+    ``batch_size`` rows (all of them when ``batch_size`` is None)."""
+    lp = _loop()
+    pending: List[Any] = []
+    rows = 0
+
+    def flush():
+        blocks = [B.from_batch(o) for o in pending]
+        pending.clear()
+        return blocks[0] if len(blocks) == 1 else B.concat(blocks)
+
+    while True:
+        try:
+            o = lp.run_until_complete(agen.__anext__())
+        except StopAsyncIteration:
+            break
+        pending.append(o)
+        rows += len(next(iter(o.values()))) if isinstance(o, dict) and o else 1
+        if batch_size and rows >= batch_size:
+            yield flush()
+            rows = 0
+    if pending:
+        yield flush()
 
 
 def _make_class_fn(batch_size, batch_format, fn_args, fn_kwargs, zero_copy_batch):

@@ -29,33 +29,11 @@ class LLMConfig:
 
 
 def _build_engine(cfg: LLMConfig):
-    import torch
-
-    from ..llm import LLMEngine
     from ..llm.async_engine import AsyncLLMEngine
-    from ..llm.tokenizer import get_tokenizer
-    from ..models.llama import Llama, LlamaConfig
+    from ..llm.build import build_engine
 
-    dev = "cuda" if torch.cuda.is_available() else "cpu"
-    dtype = getattr(torch, cfg.dtype) if dev == "cuda" else torch.float32
-    if cfg.model_source:
-        from ..llm.weights import load_hf_llama
-
-        model = load_hf_llama(cfg.model_source, dev, dtype)
-    else:
-        lc = LlamaConfig.named(cfg.model_id)
-        with torch.device(dev):
-            model = Llama(lc).to(dtype)
-        torch.manual_seed(cfg.seed)
-        model.init_weights(std=0.02, seed=cfg.seed)
-    tok = get_tokenizer(cfg.tokenizer_source or (cfg.model_source if cfg.tokenizer_source is None and
-                                                 cfg.model_source else None), model.cfg.vocab_size)
-    kw = dict(cfg.engine_kwargs)
-    kw.setdefault("eos_token_id", getattr(tok, "eos_token_id", None))
-    if dev == "cpu":
-        kw.setdefault("num_blocks", 256)
-        kw.setdefault("use_graphs", False)
-    eng = LLMEngine(model, **kw)
+    eng, tok = build_engine(cfg.model_id, cfg.model_source, cfg.tokenizer_source, cfg.dtype,
+                            cfg.engine_kwargs, cfg.seed)
     return AsyncLLMEngine(eng), tok
 
 
@@ -84,7 +62,8 @@ class LLMServer:
         if "prompt_token_ids" in body:
             return list(body["prompt_token_ids"])
         if "messages" in body:
-            text = "".join(f"<|{m['role']}|>{m['content']}\n" for m in body["messages"]) + "<|assistant|>"
+            text = self.tokenizer.apply_chat_template(list(body["messages"]), tokenize=False,
+                                                      add_generation_prompt=True)
         else:
             text = body.get("prompt", "")
         return self.tokenizer.encode(text)
