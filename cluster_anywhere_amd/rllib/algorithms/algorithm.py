@@ -196,16 +196,21 @@ class AlgorithmConfig:
             ids += [m for m in self.multi_rl_module_spec.rl_module_specs if m not in ids]
         return ids
 
+    def algo_model_config(self) -> Dict[str, Any]:
+        """``model_config`` plus the algorithm's own module settings (DQN's
+        dueling flag, SAC's initial temperature ...)."""
+        return dict(self.model_config)
+
     def multi_module_factory(self) -> Callable:
         spec = self._module_specs()
         cls = self.rl_module_class or self.default_module_class()
-        mc = dict(self.model_config)
+        mc = self.algo_model_config()
         return lambda spaces: spec.build(spaces, cls, mc)
 
     def module_factories(self) -> Dict[str, Callable]:
         spec = self._module_specs()
         cls = self.rl_module_class or self.default_module_class()
-        return {mid: spec.module_factory(mid, cls, dict(self.model_config)) for mid in self.module_ids()}
+        return {mid: spec.module_factory(mid, cls, self.algo_model_config()) for mid in self.module_ids()}
 
     def policy_spaces(self) -> Dict[str, tuple]:
         out = {}
@@ -306,7 +311,10 @@ class AlgorithmConfig:
                 "module_to_env_connector": self.module_to_env_connector,
                 "callbacks_class": self.callbacks_class, "callbacks_functions": dict(self.callbacks_functions),
                 **({"policies": self.module_ids(), "policy_mapping_fn": self.policy_mapping_fn,
-                    "policy_spaces": self.policy_spaces(), "multi_module_factory": self.multi_module_factory()}
+                    "policy_spaces": self.policy_spaces(), "multi_module_factory": self.multi_module_factory(),
+                    "max_seq_len": (int(self.model_config.get("max_seq_len", 20))
+                                    if self.model_config.get("use_lstm") or self.model_config.get("use_attention")
+                                    else None)}
                    if self.is_multi_agent else {})}
 
     def learner_config(self) -> Dict[str, Any]:
@@ -318,10 +326,12 @@ class AlgorithmConfig:
         if self.is_multi_agent:
             if not self.module_ids():
                 raise ValueError("config.multi_agent(policies=...) needs at least one module id")
-            if self.model_config.get("use_lstm") or self.model_config.get("use_attention"):
-                raise NotImplementedError("recurrent modules are single-agent only for now")
             if self.algo_class is not None and not getattr(self.algo_class, "supports_multi_agent", False):
-                raise NotImplementedError(f"{self.algo_class.__name__} has no multi-agent training step yet")
+                raise NotImplementedError(f"{self.algo_class.__name__} has no multi-agent training step")
+            if ((self.model_config.get("use_lstm") or self.model_config.get("use_attention"))
+                    and self.algo_class is not None
+                    and not getattr(self.algo_class, "supports_recurrent_multi_agent", False)):
+                raise NotImplementedError(f"{self.algo_class.__name__}: recurrent modules are single-agent only")
 
     def build_algo(self, env=None, logger_creator=None) -> "Algorithm":
         if env is not None:
@@ -524,3 +534,83 @@ def concat_fragments(frags, keys=None):
         if k.startswith("last_") and isinstance(frags[0][k], np.ndarray):
             out[k] = np.concatenate([f[k] for f in frags], axis=0)
     return out
+
+
+class OffPolicyMixin:
+    """Replay-based training step shared by DQN and SAC (reference roles:
+    dqn.py:610 ``training_step``, sac.py). Multi-agent: one replay buffer per
+    trained module, filled from that module's transitions (padding dropped);
+    every update samples each module's buffer and trains all modules in one
+    learner call, priorities go back per module."""
+
+    default_capacity = 50_000
+
+    def _make_buffer(self):
+        from ..utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer
+
+        c = self.algo_config
+        rb = dict(c.replay_buffer_config)
+        cap = rb.get("capacity", self.default_capacity)
+        if "Prioritized" in rb.get("type", ""):
+            return PrioritizedReplayBuffer(cap, rb.get("alpha", 0.6), rb.get("beta", 0.4), seed=c.seed)
+        return ReplayBuffer(cap, seed=c.seed)
+
+    def setup_replay(self):
+        c = self.algo_config
+        if self.is_multi_agent:
+            train = c.policies_to_train or c.module_ids()
+            self.buffers = {m: self._make_buffer() for m in train}
+            self.buffer = None
+        else:
+            self.buffer = self._make_buffer()
+            self.buffers = None
+
+    def sample_into_replay(self) -> int:
+        """One round of sampling into the buffer(s); returns env steps sampled."""
+        from ..utils.replay_buffers import fragments_to_transitions
+
+        frags = self.env_runner_group.sample()
+        if self.is_multi_agent:
+            from ..env.multi_agent_env_runner import concat_multi_agent
+
+            for mid, f in concat_multi_agent(frags).items():
+                if mid in self.buffers:
+                    self.buffers[mid].add(fragments_to_transitions(f))
+            self.agent_steps_sampled += sum(f["agent_steps"] for f in frags)
+            steps = sum(f["env_steps"] for f in frags)
+        else:
+            frag = concat_fragments(frags)
+            steps = int(frag["rewards"].size)
+            self.buffer.add(fragments_to_transitions(frag))
+        self.env_steps_sampled += steps
+        return steps
+
+    def replay_ready(self) -> bool:
+        need = self.algo_config.num_steps_sampled_before_learning_starts
+        if self.is_multi_agent:
+            return all(len(b) >= need for b in self.buffers.values())
+        return len(self.buffer) >= need
+
+    def replay_update(self) -> Dict[str, Any]:
+        """One learner update on a freshly sampled replay batch (per module when
+        multi-agent); priorities are refreshed from the TD errors."""
+        c = self.algo_config
+        lg = self.learner_group
+        call = (lambda b: lg.local.train_on(b)) if lg.local is not None else (lambda b: lg.call("train_on", b))
+        if self.is_multi_agent:
+            batches, idx = {}, {}
+            for m, buf in self.buffers.items():
+                b = buf.sample(c.train_batch_size)
+                idx[m] = b.pop("batch_indexes")
+                batches[m] = b
+            res = call(batches)
+            for m, (_, td) in res.items():
+                self.buffers[m].update_priorities(idx[m], td)
+            self.env_steps_trained += c.train_batch_size
+            return {m: r[0] for m, r in res.items()}
+        b = self.buffer.sample(c.train_batch_size)
+        i = b.pop("batch_indexes")
+        stats, td = call(b)
+        self.buffer.update_priorities(i, td)
+        self.env_steps_trained += c.train_batch_size
+        return stats

@@ -131,6 +131,7 @@ class CQLLearner(SACLearner):
 class CQL(SAC):
     config_class = CQLConfig
     learner_class = CQLLearner
+    supports_multi_agent = False  # offline: one static dataset
 
     def setup_algo(self):
         c = self.algo_config

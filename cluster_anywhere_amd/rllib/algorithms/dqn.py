@@ -11,8 +11,7 @@ import torch.nn.functional as F
 from ..core.learner import Learner, _to_tensor
 from ..core.rl_module import NatureCNN, RLModule, _act, mlp
 from ..env import Discrete
-from ..utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer, fragments_to_transitions
-from .algorithm import Algorithm, AlgorithmConfig, concat_fragments
+from .algorithm import Algorithm, AlgorithmConfig, OffPolicyMixin
 
 
 class DQNModule(RLModule):
@@ -83,9 +82,13 @@ class DQNConfig(AlgorithmConfig):
     def default_module_class(self):
         return DQNModule
 
-    def module_factory(self):
+    def algo_model_config(self):
         mc = dict(self.model_config)
         mc.setdefault("dueling", self.dueling)
+        return mc
+
+    def module_factory(self):
+        mc = self.algo_model_config()
         cls = self.rl_module_class or DQNModule
         return lambda o, a: cls(o, a, mc)
 
@@ -154,18 +157,13 @@ def _schedule(points, t):
     return float(np.interp(t, xs, ys))
 
 
-class DQN(Algorithm):
+class DQN(OffPolicyMixin, Algorithm):
     config_class = DQNConfig
     learner_class = DQNLearner
+    supports_multi_agent = True
 
     def setup_algo(self):
-        c = self.algo_config
-        rb = dict(c.replay_buffer_config)
-        if "Prioritized" in rb.get("type", ""):
-            self.buffer = PrioritizedReplayBuffer(rb.get("capacity", 50_000), rb.get("alpha", 0.6),
-                                                  rb.get("beta", 0.4), seed=c.seed)
-        else:
-            self.buffer = ReplayBuffer(rb.get("capacity", 50_000), seed=c.seed)
+        self.setup_replay()
         self._last_target = 0
 
     def _sync_weights(self, extra=None):
@@ -175,28 +173,23 @@ class DQN(Algorithm):
 
     def training_step(self):
         c = self.algo_config
-        frag = concat_fragments(self.env_runner_group.sample())
-        steps = int(frag["rewards"].size)
-        self.env_steps_sampled += steps
-        self.buffer.add(fragments_to_transitions(frag))
+        steps = self.sample_into_replay()
         stats = {}
-        if len(self.buffer) >= c.num_steps_sampled_before_learning_starts:
+        if self.replay_ready():
             # replay ratio: `training_intensity` trained / sampled steps (default 1 update per fragment)
             n_updates = 1 if not c.training_intensity else max(1, int(round(
                 c.training_intensity * steps / c.train_batch_size)))
             for _ in range(n_updates):
-                b = self.buffer.sample(c.train_batch_size)
-                idx = b.pop("batch_indexes")
-                if self.learner_group.local is not None:
-                    stats, td = self.learner_group.local.train_on(b)
-                else:
-                    stats, td = self.learner_group.call("train_on", b)
-                self.buffer.update_priorities(idx, td)
-                self.env_steps_trained += c.train_batch_size
+                stats = self.replay_update()
             # target sync every `target_network_update_freq` sampled env steps
             if self.env_steps_sampled - self._last_target >= c.target_network_update_freq:
                 self.learner_group.call("update_target")
                 self._last_target = self.env_steps_sampled
         self._sync_weights()
-        stats["epsilon"] = _schedule(c.epsilon, self.env_steps_sampled)
+        eps = _schedule(c.epsilon, self.env_steps_sampled)
+        if self.is_multi_agent:
+            for m in stats:
+                stats[m]["epsilon"] = eps
+        else:
+            stats["epsilon"] = eps
         return stats

@@ -8,7 +8,12 @@ refreshes only those runners' weights and re-launches them. Off-policy
 correction is V-trace on the learner device (``rl_returns.hip`` kernel, one
 thread per env column, reverse scan over T). APPO replaces the IMPALA policy
 gradient by PPO's clipped surrogate on the V-trace advantages, with a target
-network providing the KL anchor."""
+network providing the KL anchor.
+
+Multi-agent: every module learns from its own padded ``[T_m, S_m]`` fragment
+(one column per agent segment, ``mask`` marks real steps; a segment's last
+step is terminal or cut, so V-trace never crosses into the padding); the loss
+averages over real steps only."""
 from __future__ import annotations
 
 import copy
@@ -57,6 +62,12 @@ class IMPALALearner(Learner):
         c = self.config
         T, N = b["rewards"].shape
         flat = lambda x: x.reshape((T * N,) + tuple(x.shape[2:]))
+        mask = b.get("mask")
+        if mask is None:
+            mean = lambda x: x.mean()
+        else:
+            msum = mask.sum().clamp(min=1.0)
+            mean = lambda x: (x * mask.reshape(x.shape)).sum() / msum
         out = self.module.forward_train({"obs": flat(b["obs"])})
         dist = self.module.dist_cls(out["action_dist_inputs"])
         logp = dist.logp(flat(b["actions"])).view(T, N)
@@ -68,20 +79,21 @@ class IMPALALearner(Learner):
                                 c["vtrace_clip_rho_threshold"], c["vtrace_clip_pg_rho_threshold"])
         if self.appo:
             ratio = torch.exp(logp - b["action_logp"])
-            adv = (pg_adv - pg_adv.mean()) / (pg_adv.std() + 1e-8)
+            mu = mean(pg_adv)
+            adv = (pg_adv - mu) / (mean((pg_adv - mu) ** 2).sqrt() + 1e-8)
             cp = c["clip_param"]
-            pi_loss = -torch.min(ratio * adv, ratio.clamp(1 - cp, 1 + cp) * adv).mean()
+            pi_loss = -mean(torch.min(ratio * adv, ratio.clamp(1 - cp, 1 + cp) * adv))
         else:
-            pi_loss = -(logp * pg_adv).mean()
-        vf_loss = 0.5 * ((values - vs) ** 2).mean()
-        ent = dist.entropy().mean()
+            pi_loss = -mean(logp * pg_adv)
+        vf_loss = 0.5 * mean((values - vs) ** 2)
+        ent = mean(dist.entropy().view(T, N))
         loss = pi_loss + c["vf_loss_coeff"] * vf_loss - c["entropy_coeff"] * ent
         stats = {"total_loss": loss.detach(), "policy_loss": pi_loss.detach(), "vf_loss": vf_loss.detach(),
                  "entropy": ent.detach()}
         if self.appo and c.get("use_kl_loss"):
             with torch.no_grad():
                 old = self.target.forward_train({"obs": flat(b["obs"])})["action_dist_inputs"]
-            kl = self.module.dist_cls(old).kl(dist).mean()
+            kl = mean(self.module.dist_cls(old).kl(dist).view(T, N))
             loss = loss + c["kl_coeff"] * kl
             stats["mean_kl_loss"] = kl.detach()
         return {"default": loss}, stats
@@ -98,6 +110,8 @@ class IMPALALearner(Learner):
         b = {k: _to_tensor(frag[k], self.device) for k in keys}
         b["rewards"] = b["rewards"].float()
         b["last_obs"] = _to_tensor(frag["last_obs"], self.device)
+        if "mask" in frag:
+            b["mask"] = _to_tensor(frag["mask"], self.device).float()
         return {k: float(v) for k, v in self.update_once(b).items()}
 
 
@@ -108,6 +122,7 @@ class APPOLearner(IMPALALearner):
 class IMPALA(Algorithm):
     config_class = IMPALAConfig
     learner_class = IMPALALearner
+    supports_multi_agent = True
 
     def setup_algo(self):
         self._inflight: Dict[int, Any] = {}
@@ -144,8 +159,15 @@ class IMPALA(Algorithm):
     def training_step(self):
         c = self.algo_config
         frags = self._collect()
-        frag = concat_fragments(frags)
-        steps = int(frag["rewards"].size)
+        if self.is_multi_agent:
+            from ..env.multi_agent_env_runner import concat_multi_agent
+
+            frag = concat_multi_agent(frags)
+            steps = sum(f["env_steps"] for f in frags)
+            self.agent_steps_sampled += sum(f["agent_steps"] for f in frags)
+        else:
+            frag = concat_fragments(frags)
+            steps = int(frag["rewards"].size)
         self.env_steps_sampled += steps
         lg = self.learner_group
         stats = lg.local.learn_fragments(frag) if lg.local is not None else lg.call("learn_fragments", frag)

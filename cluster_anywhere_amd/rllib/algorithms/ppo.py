@@ -44,6 +44,8 @@ class PPOLearner(Learner):
     graph_capturable = True  # compute_loss has no host syncs / host-side state (KL coeff lives on device)
 
     def build(self):
+        if self._stateful():  # sequence batches with padding masks: dynamic shapes, run eagerly
+            self.graph_capturable = False
         self.kl_coeff = self.config.get("kl_coeff", 0.2)
         self._kl_dev = (torch.full((1,), float(self.kl_coeff), device=self.device)
                         if self.device.type == "cuda" else None)
@@ -57,6 +59,10 @@ class PPOLearner(Learner):
             st = {k[len("state_in_"):]: v for k, v in batch.items() if k.startswith("state_in_")}
             out = self.module.forward_train(dict(batch, state_in=st))
             batch = {k: (v.reshape((-1,) + tuple(v.shape[2:])) if k in _SEQ_KEYS else v) for k, v in batch.items()}
+            if "loss_mask" in batch:  # multi-agent columns are padded to whole sequences
+                keep = batch["loss_mask"].reshape(-1) > 0
+                out = {k: v[keep] for k, v in out.items()}
+                batch = {k: (v[keep] if k in _SEQ_KEYS else v) for k, v in batch.items()}
         else:
             out = self.module.forward_train(batch)
         if self.module.dist_cls is Categorical:
@@ -132,6 +138,7 @@ class PPO(Algorithm):
     config_class = PPOConfig
     learner_class = PPOLearner
     supports_multi_agent = True
+    supports_recurrent_multi_agent = True
 
     def training_step(self):
         import time

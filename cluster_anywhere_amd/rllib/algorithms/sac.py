@@ -13,8 +13,7 @@ import torch.nn as nn
 from ..core.learner import Learner
 from ..core.rl_module import RLModule, _act, mlp
 from ..env import Box
-from ..utils.replay_buffers import PrioritizedReplayBuffer, ReplayBuffer, fragments_to_transitions
-from .algorithm import Algorithm, AlgorithmConfig, concat_fragments
+from .algorithm import Algorithm, AlgorithmConfig, OffPolicyMixin
 
 
 class SACModule(RLModule):
@@ -89,10 +88,18 @@ class SACConfig(AlgorithmConfig):
         self.training_intensity = None
         self.twin_q = True
 
-    def module_factory(self):
+    def default_module_class(self):
+        return SACModule
+
+    def algo_model_config(self):
         mc = dict(self.model_config)
         mc.setdefault("initial_alpha", self.initial_alpha)
-        return lambda o, a: SACModule(o, a, mc)
+        return mc
+
+    def module_factory(self):
+        mc = self.algo_model_config()
+        cls = self.rl_module_class or SACModule
+        return lambda o, a: cls(o, a, mc)
 
     def runner_config(self):
         d = super().runner_config()
@@ -163,36 +170,23 @@ class SACLearner(Learner):
         return True
 
 
-class SAC(Algorithm):
+class SAC(OffPolicyMixin, Algorithm):
     config_class = SACConfig
     learner_class = SACLearner
+    supports_multi_agent = True
+    default_capacity = 100_000
 
     def setup_algo(self):
-        c = self.algo_config
-        rb = dict(c.replay_buffer_config)
-        if "Prioritized" in rb.get("type", ""):
-            self.buffer = PrioritizedReplayBuffer(rb.get("capacity", 100_000), seed=c.seed)
-        else:
-            self.buffer = ReplayBuffer(rb.get("capacity", 100_000), seed=c.seed)
+        self.setup_replay()
 
     def training_step(self):
         c = self.algo_config
-        frag = concat_fragments(self.env_runner_group.sample())
-        steps = int(frag["rewards"].size)
-        self.env_steps_sampled += steps
-        self.buffer.add(fragments_to_transitions(frag))
+        steps = self.sample_into_replay()
         stats = {}
-        if len(self.buffer) >= c.num_steps_sampled_before_learning_starts:
+        if self.replay_ready():
             n_updates = 1 if not c.training_intensity else max(1, int(round(
                 c.training_intensity * steps / c.train_batch_size)))
             for _ in range(n_updates):
-                b = self.buffer.sample(c.train_batch_size)
-                idx = b.pop("batch_indexes")
-                if self.learner_group.local is not None:
-                    stats, td = self.learner_group.local.train_on(b)
-                else:
-                    stats, td = self.learner_group.call("train_on", b)
-                self.buffer.update_priorities(idx, td)
-                self.env_steps_trained += c.train_batch_size
+                stats = self.replay_update()
         self._sync_weights()
         return stats

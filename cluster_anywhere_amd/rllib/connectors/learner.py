@@ -132,6 +132,8 @@ class ChunkSequences(ConnectorV2):
         for k in [k for k in batch if k.startswith("state_in_")]:
             st = batch[k][:: self.L]  # [T/L, N, cell] state at each sequence start
             out[k] = st.transpose(0, 1).reshape(N * (T // self.L), -1).float()
+        if "mask" in batch:  # padded multi-agent columns: the loss skips these steps
+            out["loss_mask"] = self._seq(batch["mask"].float(), T, N)
         return out
 
 

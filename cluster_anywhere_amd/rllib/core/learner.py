@@ -283,6 +283,22 @@ class MultiLearner:
                 self.learners[m].set_state(s)
         return True
 
+    def __getattr__(self, name):
+        """Any other learner method (``train_on``, ``learn_fragments``,
+        ``update_target`` ...): called per module. A first argument keyed by module
+        ids is split so each module gets its own entry; otherwise the call is
+        broadcast. Returns ``{module_id: result}``."""
+        if name.startswith("_") or not callable(getattr(self.inner_cls, name, None)):
+            raise AttributeError(name)
+
+        def call(*args, **kw):
+            learners = self.__dict__.get("learners", {})
+            if args and isinstance(args[0], dict) and args[0] and set(args[0]) <= set(learners):
+                return {m: getattr(learners[m], name)(a, *args[1:], **kw) for m, a in args[0].items()}
+            return {m: getattr(l, name)(*args, **kw) for m, l in learners.items()}
+
+        return call
+
 
 def _shard_nested(batch, i, n):
     if isinstance(batch, dict):

@@ -16,6 +16,16 @@ marked terminal). The fragment for each module is time-major and padded:
 ``[T_m, S_m]`` with one column per segment and a ``mask`` of valid steps, so
 the learner runs GAE over all columns at once (``rl_returns.hip``) and drops
 the padding when flattening.
+
+Off-policy mode (``need_next_obs``, DQN / SAC): segments carry ``next_obs`` and
+true termination flags instead — a truncated or cut segment keeps its last
+observation as ``next_obs`` with ``terminateds=False`` (the TD target
+bootstraps from it), nothing is folded into the rewards.
+
+Recurrent modules (``is_stateful()``): every agent carries its own recurrent
+state (reset with its episode); each step's ``state_in_*`` is recorded, and the
+fragment length is padded to a multiple of ``max_seq_len`` so the learner can
+cut every column into whole sequences.
 """
 from __future__ import annotations
 
@@ -33,15 +43,17 @@ _KEYS = ("action_logp", "vf_preds", "action_dist_inputs")
 
 
 class _Segment:
-    __slots__ = ("mid", "obs", "actions", "rewards", "extra", "closed")
+    __slots__ = ("mid", "obs", "actions", "rewards", "extra", "closed", "final_obs", "terminated")
 
     def __init__(self, mid):
         self.mid = mid
         self.obs: List[np.ndarray] = []
         self.actions: List[Any] = []
         self.rewards: List[float] = []
-        self.extra: Dict[str, List[np.ndarray]] = {k: [] for k in _KEYS}
+        self.extra: Dict[str, List[np.ndarray]] = {}
         self.closed = False
+        self.final_obs = None  # off-policy mode: module-space obs after the last step
+        self.terminated = False
 
 
 def _pad_stack(cols: List[List[np.ndarray]], T: int, fill_like) -> np.ndarray:
@@ -108,6 +120,11 @@ class MultiAgentEnvRunner:
             self.spaces[mid] = (self.e2m[mid].recompute_output_observation_space(o, a), a)
         self.module = config["multi_module_factory"](self.spaces)
         self.module.eval()
+        self.need_next = bool(config.get("need_next_obs", False))
+        self.stateful = {mid: bool(getattr(self.module[mid], "is_stateful", lambda: False)())
+                         for mid in self.module_ids}
+        self.seq_len = int(config.get("max_seq_len") or 1) if any(self.stateful.values()) else 1
+        self.rstate: List[Dict[Any, Dict[str, np.ndarray]]] = [{} for _ in range(n)]
         smooth = config.get("metrics_num_episodes_for_smoothing", 100)
         self.done_returns: deque = deque(maxlen=smooth)
         self.done_lens: deque = deque(maxlen=smooth)
@@ -142,6 +159,8 @@ class MultiAgentEnvRunner:
             ep.agent(a, self._module_for(ep, a)).add_reset(o, (infos or {}).get(a))
         self.pending[i] = dict(obs)
         self.segments[i] = {}
+        if hasattr(self, "rstate"):
+            self.rstate[i] = {}  # recurrent state restarts with the episode
         if self._has_cb:
             kw = dict(episode=ep, env_runner=self, metrics_logger=self.metrics, env=self.envs[i], env_index=i,
                       rl_module=self.module)
@@ -155,12 +174,28 @@ class MultiAgentEnvRunner:
         return p(rl_module=self.module[mid], batch={"obs": raw}, episodes=eps, shared_data={"peek": peek},
                  metrics=self.metrics)["obs"]
 
-    def _value(self, mid, ep: SingleAgentEpisode, raw_obs) -> float:
+    def _state(self, i, a, mid) -> Dict[str, np.ndarray]:
+        st = self.rstate[i].get(a)
+        if st is None:
+            st = {k: v.detach().cpu().numpy().astype(np.float32)
+                  for k, v in self.module[mid].get_initial_state().items()}
+            self.rstate[i][a] = st
+        return st
+
+    def _value(self, mid, ep: SingleAgentEpisode, raw_obs, state=None) -> float:
         m = self.module[mid]
         if not hasattr(m, "compute_values"):
             return 0.0
         o = self._to_module(mid, np.asarray(raw_obs)[None], [ep], peek=True)
-        return float(m.compute_values({"obs": torch.from_numpy(np.ascontiguousarray(o))})[0])
+        b = {"obs": torch.from_numpy(np.ascontiguousarray(o))}
+        if state:
+            b["state_in"] = {k: torch.from_numpy(v[None]) for k, v in state.items()}
+        return float(m.compute_values(b)[0])
+
+    def _final(self, seg: _Segment, ep: SingleAgentEpisode, raw_obs):
+        """Off-policy mode: the module-space observation after the segment's last step."""
+        if raw_obs is not None:
+            seg.final_obs = self._to_module(seg.mid, np.asarray(raw_obs)[None], [ep], peek=True)[0]
 
     def _close(self, seg: _Segment, out: Dict[str, list]):
         if seg.obs and not seg.closed:
@@ -214,9 +249,19 @@ class MultiAgentEnvRunner:
                 b = {"obs": torch.from_numpy(np.ascontiguousarray(mobs))}
                 b.update(self.explore_extra)
                 m = self.module[mid]
+                sts = None
+                if self.stateful[mid]:
+                    sts = [self._state(i, a, mid) for i, a in rows]
+                    b["state_in"] = {k: torch.from_numpy(np.stack([st[k] for st in sts])) for k in sts[0]}
                 out = m.forward_exploration(b) if explore else m.forward_inference(b)
                 acts = out["actions"].cpu().numpy()
                 extra = {k: out[k].cpu().numpy() for k in _KEYS if k in out}
+                if sts is not None:
+                    for k in sts[0]:
+                        extra[f"state_in_{k}"] = np.stack([st[k] for st in sts])
+                    new = {k: v.detach().cpu().numpy() for k, v in out["state_out"].items()}
+                    for r, (i, a) in enumerate(rows):
+                        self.rstate[i][a] = {k: new[k][r] for k in new}
                 env_acts = acts
                 if len(self.m2e[mid]):
                     mb = dict(extra, actions=acts)
@@ -242,7 +287,7 @@ class MultiAgentEnvRunner:
                     seg.actions.append(act)
                     seg.rewards.append(float(rew.get(a, 0.0)))
                     for k, v in ex.items():
-                        seg.extra[k].append(v)
+                        seg.extra.setdefault(k, []).append(v)
                     agent_steps += 1
                     ae = ep.agent(a, mid)
                     ae.add_step(obs.get(a), act, rew.get(a, 0.0), (infos or {}).get(a), te.get(a, False),
@@ -263,12 +308,18 @@ class MultiAgentEnvRunner:
                         continue
                     a_te, a_tr = te.get(a, False), tr.get(a, False)
                     if a_te or (all_done and not a_tr and te.get("__all__", False)):
+                        seg.terminated = True
                         self._close(seg, done_segs)
                     elif a_tr or all_done:  # truncated: bootstrap from the final observation
                         fo = obs.get(a)
-                        if fo is not None:
-                            seg.rewards[-1] += gamma * self._value(seg.mid, ep.agent(a), fo)
+                        if self.need_next:
+                            self._final(seg, ep.agent(a), fo)
+                        elif fo is not None:
+                            seg.rewards[-1] += gamma * self._value(seg.mid, ep.agent(a), fo,
+                                                                   self.rstate[i].get(a))
                         self._close(seg, done_segs)
+                    if a_te or a_tr:
+                        self.rstate[i].pop(a, None)
                 self.pending[i] = {a: o for a, o in obs.items() if not (te.get(a) or tr.get(a))}
                 if all_done:
                     self._finish_episode(i)
@@ -284,8 +335,10 @@ class MultiAgentEnvRunner:
                 if seg.closed or not seg.obs:
                     continue
                 po = self.pending[i].get(a)
-                if po is not None:
-                    seg.rewards[-1] += gamma * self._value(seg.mid, ep.agent(a), po)
+                if self.need_next:
+                    self._final(seg, ep.agent(a), po)
+                elif po is not None:
+                    seg.rewards[-1] += gamma * self._value(seg.mid, ep.agent(a), po, self.rstate[i].get(a))
                 self._close(seg, done_segs)
             self.segments[i] = {}
         self.total_steps += T * len(self.envs)
@@ -313,18 +366,31 @@ class MultiAgentEnvRunner:
 
     def _pack(self, segs: List[_Segment]) -> Dict[str, np.ndarray]:
         Tm = max(len(s.obs) for s in segs)
+        L = self.seq_len
+        Tm = ((Tm + L - 1) // L) * L  # recurrent: whole max_seq_len sequences per column
         S = len(segs)
         f = {"obs": _pad_stack([s.obs for s in segs], Tm, segs[0].obs[0]),
              "actions": _pad_stack([s.actions for s in segs], Tm, np.asarray(segs[0].actions[0])),
              "rewards": _pad_stack([[np.float32(r) for r in s.rewards] for s in segs], Tm, np.float32(0))}
-        for k in _KEYS:
-            if segs[0].extra[k]:
-                f[k] = _pad_stack([s.extra[k] for s in segs], Tm, segs[0].extra[k][0]).astype(np.float32)
+        for k in segs[0].extra:
+            f[k] = _pad_stack([s.extra.get(k, []) for s in segs], Tm, segs[0].extra[k][0]).astype(np.float32)
         mask = np.zeros((Tm, S), bool)
         term = np.zeros((Tm, S), bool)
-        for j, s in enumerate(segs):
-            mask[:len(s.obs), j] = True
-            term[len(s.obs) - 1:, j] = True  # every column ends terminal (done or cut) and stays so
+        if self.need_next:  # transitions: next_obs within the segment, then its final obs
+            nxt = np.zeros_like(f["obs"])
+            for j, s in enumerate(segs):
+                n = len(s.obs)
+                mask[:n, j] = True
+                if n > 1:
+                    nxt[:n - 1, j] = np.stack(s.obs[1:])
+                if s.final_obs is not None:
+                    nxt[n - 1, j] = s.final_obs
+                term[n - 1, j] = s.terminated or s.final_obs is None
+            f["next_obs"] = nxt
+        else:
+            for j, s in enumerate(segs):
+                mask[:len(s.obs), j] = True
+                term[len(s.obs) - 1:, j] = True  # every column ends terminal (done or cut) and stays so
         f["mask"] = mask
         f["terminateds"] = term
         f["truncateds"] = np.zeros((Tm, S), bool)

@@ -140,7 +140,8 @@ class PrioritizedReplayBuffer(ReplayBuffer):
 def fragments_to_transitions(frag: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
     """Time-major fragment [T, N, ...] (with next_obs) -> flat transitions."""
     T, N = frag["rewards"].shape
-    f = lambda x: x.reshape((T * N,) + x.shape[2:])
+    keep = frag["mask"].reshape(-1) if "mask" in frag else slice(None)  # multi-agent padding
+    f = lambda x: x.reshape((T * N,) + x.shape[2:])[keep]
     return {"obs": f(frag["obs"]), "actions": f(frag["actions"]), "rewards": f(frag["rewards"]),
             "next_obs": f(frag["next_obs"]),
             "terminateds": f(frag["terminateds"] & ~frag["truncateds"]).astype(np.float32)}
