@@ -105,6 +105,9 @@ class LLMEngine:
         self.max_num_batched_tokens = max_num_batched_tokens
         self.eos = eos_token_id
         per_block = 2 * cfg.n_layer * cfg.n_kv_head * block_size * cfg.head_dim * 2  # bytes, K+V bf16
+        # decode-GEMM weight copies (fused SwiGLU, packed streams) before the cache takes the rest of HBM
+        self.decode_gemm = bool(self.device.type == "cuda" and hasattr(model, "prepare_decode")
+                                and model.prepare_decode())
         if num_blocks is None:
             if self.device.type == "cuda":
                 free, total = torch.cuda.mem_get_info(self.device)

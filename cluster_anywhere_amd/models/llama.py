@@ -89,6 +89,7 @@ class Llama(nn.Module):
         self.final_norm = nn.Parameter(torch.ones(cfg.d_model))
         self.lm_head = None if cfg.tie_embeddings else nn.Parameter(torch.empty(cfg.vocab_size, cfg.d_model))
         self._cos_sin = None
+        self._dec = None  # decode-GEMM weight copies (prepare_decode)
 
     @torch.no_grad()
     def init_weights(self, std: float = 0.02, seed: int = 0):
@@ -112,6 +113,35 @@ class Llama(nn.Module):
     def _head(self, x):
         w = self.embed if self.lm_head is None else self.lm_head
         return F.linear(x, w)
+
+    @torch.no_grad()
+    def prepare_decode(self) -> bool:
+        """Decode-side copies of the weight-streaming GEMMs for ``decode_gemm.hip``
+        (batch <= 128): ``w_gate_up`` with gate/up rows interleaved in 64-row blocks
+        (SwiGLU fused into the GEMM epilogue, no [B, 2F] intermediate) and
+        ``w_down`` / the vocabulary projection, all prepacked in the kernel's
+        streaming order. qkv and o stay on hipBLASLt, which measured faster at
+        those widths (``tools/bench_decode_gemm3.py``). Costs one extra copy of
+        those weights in HBM (about 11.5 GB for Llama-3-8B), taken before the KV
+        cache is sized. Returns whether the decode path uses them."""
+        import os
+
+        if os.environ.get("CAAMD_DECODE_GEMM", "1") == "0" or not self.embed.is_cuda \
+                or self.embed.dtype != torch.bfloat16 or not L.decode_gemm_available():
+            self._dec = None
+            return False
+        cfg = self.cfg
+        if cfg.ffn_dim % 64 or cfg.d_model % 128 or cfg.d_model % 64 or cfg.ffn_dim % 64:
+            self._dec = None
+            return False
+        head = self.embed if self.lm_head is None else self.lm_head
+        layers = [(L.pack_decode_weight(L.interleave_gate_up(l.w_gate_up)), L.pack_decode_weight(l.w_down))
+                  for l in self.layers]
+        self._dec = {"layers": layers,
+                     "head": L.pack_decode_weight(head) if head.shape[0] % 128 == 0 else None}
+        shapes = [(l.w_down.shape[0], l.w_down.shape[1]) for l in self.layers[:1]]
+        L.decode_gemm_reserve(self.embed.device, shapes)
+        return True
 
     # -------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -157,6 +187,7 @@ class Llama(nn.Module):
         x = F.embedding(tokens, self.embed)  # [B, d]
         res = None
         pos = positions.to(torch.int32)
+        dec = self._dec if (self._dec is not None and tokens.shape[0] <= 128) else None
         for i, layer in enumerate(self.layers):
             h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
             if res is None:
@@ -167,8 +198,14 @@ class Llama(nn.Module):
             o = L.paged_decode_attention(qkv, k_caches[i], v_caches[i], block_tables, ctx_lens, max_ctx, H)
             x = L.decode_linear(o, layer.w_o)
             h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
-            x = L.decode_linear(L.silu_mul(L.decode_linear(h, layer.w_gate_up)), layer.w_down)
+            if dec is not None:  # SwiGLU in the gate/up GEMM epilogue, packed weight streams
+                gu, dn = dec["layers"][i]
+                x = L.decode_gemm(L.decode_gemm(h, gu, 2, packed=True), dn, 0, packed=True)
+            else:
+                x = L.decode_linear(L.silu_mul(L.decode_linear(h, layer.w_gate_up)), layer.w_down)
         h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
+        if dec is not None and dec["head"] is not None:
+            return L.decode_gemm(h, dec["head"], 0, packed=True)
         w = self.embed if self.lm_head is None else self.lm_head
         return L.decode_linear(h, w)
 

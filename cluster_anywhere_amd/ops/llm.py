@@ -93,6 +93,110 @@ def skinny_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# ---------------------------------------------------- decode GEMM v3 (decode_gemm.hip)
+_DG_WS: dict = {}
+
+
+def decode_gemm_splits(N: int, K: int, cus: int = 256) -> int:
+    """Split-K so the (N/128) x splits workgroups cover the CUs, >= 4 K-steps each."""
+    slabs = N // 128
+    s = max(1, min(cus // max(1, slabs), K // 256))
+    while s > 1 and K % (64 * s):
+        s -= 1
+    return s
+
+
+def _dg_ws(dev, floats: int, tickets: int):
+    ws = _DG_WS.get(dev.index)
+    if ws is None or ws[0].numel() < floats or ws[1].numel() < tickets:
+        ws = (torch.empty(max(floats, 1), device=dev, dtype=torch.float32),
+              torch.zeros(max(tickets, 1024), device=dev, dtype=torch.int32))
+        _DG_WS[dev.index] = ws
+    return ws
+
+
+def decode_gemm_available() -> bool:
+    """The decode GEMM is compiled into the extension (raises on a GPU box when the
+    extension itself is missing: no silent fallback there)."""
+    return hasattr(kernels(), "decode_gemm")
+
+
+def decode_gemm_reserve(dev, shapes) -> None:
+    """Allocate the split-K workspace for every (N, K) decode shape up front, so no
+    allocation happens inside a HIP-graph capture (graphs keep raw pointers)."""
+    cus = _cus(dev)
+    need = max([(n // 128) * decode_gemm_splits(n, k, cus) * 16384 for n, k in shapes] + [1])
+    _dg_ws(dev, need, 1024)
+
+
+def decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    return (x.dim() == 2 and 1 <= x.shape[0] <= 128 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and w.is_contiguous() and x.stride(-1) == 1 and w.shape[0] % 128 == 0 and x.shape[1] % 64 == 0
+            and w.shape[1] == x.shape[1])
+
+
+def decode_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, residual: Optional[torch.Tensor] = None,
+                splits: Optional[int] = None, packed: bool = False) -> torch.Tensor:
+    """``x @ w.T`` (epi 0), ``+ residual`` (epi 1) or SwiGLU over a 64-row-interleaved
+    gate/up weight (epi 2, see :func:`interleave_gate_up`) on the decode GEMM v3.
+    ``packed``: ``w`` is in :func:`pack_decode_weight` order."""
+    M, K = x.shape
+    N = w.shape[0]
+    s = splits or decode_gemm_splits(N, K, _cus(x.device))
+    y = torch.empty(M, N // 2 if epi == 2 else N, device=x.device, dtype=torch.bfloat16)
+    part, tick = _dg_ws(x.device, (N // 128) * s * 16384 if s > 1 else 1, N // 128)
+    kernels().decode_gemm(x, w, y, residual, part, tick, epi, s, packed)
+    return y
+
+
+_CUS: dict = {}
+
+
+def _cus(dev) -> int:
+    n = _CUS.get(dev.index)
+    if n is None:
+        n = _CUS[dev.index] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return n
+
+
+def _swz_cols(device) -> torch.Tensor:
+    """[128 rows, 8 positions] -> source 16-byte chunk (decode_gemm.hip ``swz``)."""
+    row = torch.arange(128, device=device).view(128, 1)
+    pos = torch.arange(8, device=device).view(1, 8)
+    x = (row >> 1) & 7
+    return pos ^ (x ^ ((x & 1) << 2))
+
+
+def pack_decode_weight(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] -> the decode kernel's streaming order (same shape and numel): for
+    every 128-row slab and 64-wide k step, the 16 KiB swizzled LDS image
+    contiguously (``dma_packed`` in decode_gemm.hip). Done once at load time."""
+    N, K = w.shape
+    assert N % 128 == 0 and K % 64 == 0
+    v = w.reshape(N // 128, 128, K // 64, 8, 8).permute(0, 2, 1, 3, 4)  # [slab, kstep, row, chunk, 8]
+    idx = _swz_cols(w.device).view(1, 1, 128, 8, 1).expand(N // 128, K // 64, 128, 8, 8)
+    return torch.gather(v, 3, idx).contiguous().view(N, K)
+
+
+def unpack_decode_weight(wp: torch.Tensor) -> torch.Tensor:
+    """Inverse of :func:`pack_decode_weight` (tests, checkpoint export)."""
+    N, K = wp.shape
+    v = wp.reshape(N // 128, K // 64, 128, 8, 8)
+    idx = _swz_cols(wp.device).view(1, 1, 128, 8, 1).expand_as(v)
+    out = torch.empty_like(v)
+    out.scatter_(3, idx, v)
+    return out.permute(0, 2, 1, 3, 4).contiguous().view(N, K)
+
+
+def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
+    """[gate; up] ([2F, d]) -> 64-row blocks [gate_b; up_b] for the SwiGLU epilogue."""
+    two_f, d = w.shape
+    f = two_f // 2
+    assert f % 64 == 0
+    g, u = w[:f].reshape(f // 64, 64, d), w[f:].reshape(f // 64, 64, d)
+    return torch.stack([g, u], dim=1).reshape(two_f, d).contiguous()
+
+
 def decode_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``x @ w.T`` for decode-sized batches: the skinny MFMA kernel when enabled
     (``CAAMD_SKINNY_GEMM=1``) and the shapes fit, else torch / hipBLASLt."""

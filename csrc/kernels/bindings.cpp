@@ -39,6 +39,9 @@ void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* ful
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
+hipError_t decode_gemm_launch(int epi, const bf16* X, const bf16* W, bf16* Y, const bf16* R, float* part,
+                              unsigned* tick, int M, int N, int K, int ldx, int ldy, int splits, bool packed,
+                              hipStream_t st);
 void gemm2_plan(int M, int N, int K, int slots, int max_split, int* full, int* S, int* grid,
                 long long* ws_floats, int* tickets);
 hipError_t gemm2_launch(int layout, int epi, const bf16* A, const bf16* B, bf16* C, const bf16* bias,
@@ -843,6 +846,45 @@ static void gemm2_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi
   TORCH_CHECK(e == hipSuccess, "gemm2 launch failed: ", hipGetErrorString(e));
 }
 
+// ---- decode GEMM v3 (decode_gemm.hip): y = x . w^T for M <= 128, weight-streaming --------
+// epi 0: y = acc · 1: y = acc + residual · 2: SwiGLU over 64-row-interleaved gate/up weights
+// (y has N/2 columns)
+static void decode_gemm(const Tensor& x, const Tensor& w, Tensor& y, c10::optional<Tensor> residual,
+                        Tensor& part, Tensor& tick, int64_t epi, int64_t splits, bool packed) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && y.dim() == 2, "decode_gemm: 2-D operands");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(w.size(1) == K && w.is_contiguous(), "decode_gemm: w must be a contiguous [N, K]");
+  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) >= K, "decode_gemm: x rows must be dense");
+  TORCH_CHECK(M >= 1 && M <= 128, "decode_gemm: 1 <= M <= 128");
+  TORCH_CHECK(N % 128 == 0 && K % 64 == 0, "decode_gemm: N % 128 == 0, K % 64 == 0");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "decode_gemm: epi 0, 1 or 2");
+  const int64_t NY = epi == 2 ? N / 2 : N;
+  TORCH_CHECK(y.size(0) == M && y.size(1) == NY && y.stride(1) == 1, "decode_gemm: y shape");
+  TORCH_CHECK(splits >= 1 && K % (64 * splits) == 0, "decode_gemm: K % (64 * splits) == 0");
+  const caamd::bf16* rp = nullptr;
+  if (epi == 1) {
+    TORCH_CHECK(residual.has_value(), "decode_gemm: residual epilogue needs a residual");
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->sizes() == y.sizes() && residual->stride(0) == y.stride(0) && residual->stride(1) == 1,
+                "decode_gemm: residual must match y");
+    rp = (const caamd::bf16*)residual->data_ptr();
+  }
+  if (splits > 1) {
+    TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= (N / 128) * splits * 16384,
+                "decode_gemm: partial workspace too small");
+    TORCH_CHECK(tick.is_cuda() && tick.scalar_type() == at::kInt && tick.numel() >= N / 128,
+                "decode_gemm: tickets too small");
+  }
+  hipError_t e = caamd::decode_gemm_launch((int)epi, (const caamd::bf16*)x.data_ptr(), (const caamd::bf16*)w.data_ptr(),
+                                           (caamd::bf16*)y.data_ptr(), rp, part.data_ptr<float>(),
+                                           reinterpret_cast<unsigned*>(tick.data_ptr<int>()), (int)M, (int)N, (int)K,
+                                           (int)x.stride(0), (int)y.stride(0), (int)splits, packed, cur_stream());
+  TORCH_CHECK(e == hipSuccess, "decode_gemm launch failed: ", hipGetErrorString(e));
+}
+
 static Tensor transpose_bf16(const Tensor& x) {
   CHECK_BF16(x);
   TORCH_CHECK(x.dim() == 2 && x.size(0) % 64 == 0 && x.size(1) % 64 == 0, "transpose: [R,C] with R,C % 64 == 0");
@@ -1014,6 +1056,7 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("gemm2_plan", &gemm2_plan_);
   m.def("gemm2_bf16", &gemm2_bf16);
+  m.def("decode_gemm", &decode_gemm);
   m.def("transpose_bf16", &transpose_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

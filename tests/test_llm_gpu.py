@@ -152,3 +152,51 @@ def test_skinny_decode_gemm(C, M, N, K):
         y = skinny_linear(x, w)
         assert _rel(y, ref) < 1e-2, (_rel(y, ref), skinny_splits(N, K))
     assert int(skinny_workspace(x.device)[1].abs().sum()) == 0  # counters left zeroed
+
+
+@pytest.mark.parametrize("M", [1, 7, 100, 128])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 14336), (1024, 2816), (256, 512)])
+@pytest.mark.parametrize("packed", [False, True])
+def test_decode_gemm_v3_epilogues(M, N, K, packed):
+    """decode_gemm.hip vs fp32 torch: plain store, residual add and the SwiGLU
+    epilogue (64-row interleaved gate/up weight), plain and prepacked weight
+    streams, at the split count the wrapper picks; launched twice (tickets re-arm)."""
+    import torch.nn.functional as F
+
+    torch.manual_seed(M * 7 + N)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    wi = L.interleave_gate_up(w)
+    wp, wip = (L.pack_decode_weight(w), L.pack_decode_weight(wi)) if packed else (w, wi)
+    for _ in range(2):
+        assert _rel(L.decode_gemm(x, wp, 0, packed=packed), ref) < 1e-2
+        assert _rel(L.decode_gemm(x, wp, 1, residual=r, packed=packed), ref + r.float()) < 1e-2
+        g, u = ref[:, : N // 2], ref[:, N // 2:]
+        assert _rel(L.decode_gemm(x, wip, 2, packed=packed), F.silu(g) * u) < 1e-2
+    assert torch.equal(L.unpack_decode_weight(L.pack_decode_weight(w)), w)
+
+
+def test_llama_decode_gemm_weights():
+    """The model's decode copies (interleaved + packed gate/up, packed down/head)
+    compute the same MLP block and head as the fp32 math on the original weights."""
+    import torch.nn.functional as F
+
+    from cluster_anywhere_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(0)
+    m = Llama(LlamaConfig.named("llama-small")).to("cuda", torch.bfloat16).init_weights(std=0.02)
+    assert m.prepare_decode()
+    lay = m.layers[1]
+    gu, dn = m._dec["layers"][1]
+    h = torch.randn(64, m.cfg.d_model, device="cuda", dtype=torch.bfloat16)
+    a = L.decode_gemm(h, gu, 2, packed=True)
+    gate_up = h.float() @ lay.w_gate_up.float().t()
+    f = m.cfg.ffn_dim
+    a_ref = F.silu(gate_up[:, :f]) * gate_up[:, f:]
+    assert _rel(a, a_ref) < 1e-2
+    y = L.decode_gemm(a, dn, 0, packed=True)
+    assert _rel(y, a.float() @ lay.w_down.float().t()) < 1e-2
+    logits = L.decode_gemm(h, m._dec["head"], 0, packed=True)
+    assert _rel(logits, h.float() @ m.lm_head.float().t()) < 1e-2
