@@ -7,19 +7,7 @@
 
 namespace caamd {
 
-__device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
-  return 0.5f * x * (1.f + t);
-}
-
-__device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  const float t = 1.f - 2.f / (__expf(2.f * u) + 1.f);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x * x);
-}
+// gelu_tanh / gelu_tanh_grad: common.h
 
 __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const bf16* __restrict__ h,
                                                             const bf16* __restrict__ b,

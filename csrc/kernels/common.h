@@ -62,4 +62,28 @@ inline int ew_grid(int64_t work_items, int block) {
   return (int)g;
 }
 
+// GELU(tanh) in sigmoid form: 0.5 (1 + tanh(u)) = sigmoid(2u), so
+//   gelu(z)  = z * s,                    s = 1 / (1 + 2^(-2u log2 e)), u = k0 (z + k1 z^3)
+//   gelu'(z) = s + z * s * (1 - s) * 2 k0 (1 + 3 k1 z^2)
+// on one v_exp_f32 and one v_rcp_f32 (the fused epilogues run after the MFMA loop,
+// so their VALU count is exposed; __fdividef compiled to the full IEEE division
+// sequence, ~10 VALU per element). Saturates through exp overflow / underflow:
+// rcp(inf) = 0 gives gelu = 0 and gelu' = 0 for very negative z.
+constexpr float GELU_K0 = 0.7978845608028654f, GELU_K1 = 0.044715f;
+constexpr float GELU_C0 = -2.f * GELU_K0 * 1.4426950408889634f;  // -2 k0 log2(e)
+constexpr float GELU_C1 = GELU_C0 * GELU_K1;
+__device__ __forceinline__ float gelu_sig(float z, float z2) {
+  const float t = z * __builtin_fmaf(GELU_C1, z2, GELU_C0);  // -2u log2 e
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(t));
+}
+__device__ __forceinline__ float gelu_tanh(float z) {
+  return z * gelu_sig(z, z * z);
+}
+__device__ __forceinline__ float gelu_tanh_grad(float z) {
+  const float z2 = z * z;
+  const float s = gelu_sig(z, z2);
+  const float dv = __builtin_fmaf(6.f * GELU_K0 * GELU_K1, z2, 2.f * GELU_K0);  // d(2u)/dz
+  return __builtin_fmaf(z * s * (1.f - s), dv, s);
+}
+
 }  // namespace caamd

@@ -292,7 +292,7 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
           if (m < p.M) {
             const float g = acc[mt][i];
             const float u = upv[((wave * 4 + mt) * 16 + i) * 64 + lane];
-            const float s = g / (1.f + __expf(-g));
+            const float s = g * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * g));
             p.Y[(size_t)m * p.ldy + col] = (bf16)(s * u);
           }
         }

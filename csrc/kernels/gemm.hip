@@ -52,23 +52,7 @@ enum Epi : int {
   EPI_DGELU = 4,      // C = acc * gelu'(Z[m,n]) ; dbias[n] += colsum(C) (f32 atomics)
 };
 
-// tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp + one v_rcp instead of the library
-// tanhf (the fused epilogues run after the MFMA loop, so their VALU count is
-// exposed); saturates to +-1 through exp overflow / underflow.
-__device__ __forceinline__ float fast_tanh(float u) {
-  return 1.f - __fdividef(2.f, __expf(2.f * u) + 1.f);
-}
-__device__ __forceinline__ float gelu_tanh(float z) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float t = fast_tanh(k0 * (z + k1 * z * z * z));
-  return 0.5f * z * (1.f + t);
-}
-__device__ __forceinline__ float gelu_tanh_grad(float z) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float z2 = z * z;
-  const float t = fast_tanh(k0 * (z + k1 * z2 * z));
-  return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k0 * (1.f + 3.f * k1 * z2);
-}
+// gelu_tanh / gelu_tanh_grad: common.h (sigmoid form on v_exp_f32 + v_rcp_f32).
 
 // K-major swizzle: 16-B chunk c of row r lives at chunk position c ^ ((r >> 1) & 7).
 __device__ __forceinline__ int kswz(int row) { return (row >> 1) & 7; }

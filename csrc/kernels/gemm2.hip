@@ -75,17 +75,7 @@ enum Epi : int {
   EPI_DGELU = 4,      // C = acc * gelu'(Z) ; dbias[n] += colsum(C)
 };
 
-__device__ __forceinline__ float fast_tanh(float u) { return 1.f - __fdividef(2.f, __expf(2.f * u) + 1.f); }
-__device__ __forceinline__ float gelu_tanh(float z) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * z * (1.f + fast_tanh(k0 * (z + k1 * z * z * z)));
-}
-__device__ __forceinline__ float gelu_tanh_grad(float z) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float z2 = z * z;
-  const float t = fast_tanh(k0 * (z + k1 * z2 * z));
-  return 0.5f * (1.f + t) + 0.5f * z * (1.f - t * t) * k0 * (1.f + 3.f * k1 * z2);
-}
+// gelu_tanh / gelu_tanh_grad: common.h
 
 struct Args {
   const bf16* A;
