@@ -109,7 +109,7 @@ def run2(a, b, c, layout, epi, bias=None, z=None, zout=None, dbias=None, max_spl
 def tail_plan(M: int, N: int, K: int, bm: int, bn: int, dev: torch.device, algo: int = None):
     """(full tiles, tail split) of a ping-pong launch; split 1 = no tail split."""
     algo = ALGO if algo is None else algo
-    if not TAIL or not (1 <= algo % 10 <= 3) or K < 4096:
+    if not TAIL or not (1 <= algo % 10 <= 3 or algo % 10 == 7) or K < 4096:
         # K = 1600: the split slices and slab round trip cost more than the half-empty
         # last round (which the chip runs at a higher clock); profiles/gemm_tail_split.jsonl
         return (0, 1)

@@ -16,6 +16,7 @@ void ln_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, const fl
                    bf16*, float*, bf16*, bf16*, int, int, hipStream_t);
 int ln_nv_for(int D);
 int ln_bwd_num_blocks(int rows);
+int ln_bwd_partial_rows(int rows, int D);
 void ln_bwd_config(int variant, int max_blocks);
 void bias_gelu_fwd_launch(const bf16*, const bf16*, bf16*, int64_t, int, hipStream_t);
 void bias_gelu_bwd_launch(const bf16*, const bf16*, const bf16*, bf16*, float*, bf16*, int, int,
@@ -141,7 +142,7 @@ std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tenso
   auto dx = at::empty_like(x);
   auto dg = at::empty_like(g);
   auto db = at::empty_like(g);
-  const int nblk = caamd::ln_bwd_num_blocks(rows);
+  const int nblk = caamd::ln_bwd_partial_rows(rows, D);
   auto partial = at::empty({nblk, 2, D}, x.options().dtype(at::kFloat));
   if (rows > 0) {
     caamd::ln_bwd_launch(bp(dy), bp(x), bp(g), mean.data_ptr<float>(), rstd.data_ptr<float>(),
@@ -747,7 +748,8 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   } else if (tail_split > 1) {
     const int64_t tiles = (M / bm) * (N / bn);
     TORCH_CHECK(ek != 2 && splitk == 1, "gemm: split tail is for the bf16 epilogues");
-    TORCH_CHECK(algo % 10 >= 1 && algo % 10 <= 3, "gemm: split tail needs a ping-pong algo (1-3)");
+    TORCH_CHECK((algo % 10 >= 1 && algo % 10 <= 3) || algo % 10 == 7,
+                "gemm: split tail needs a ping-pong algo (1-3, 7)");
     TORCH_CHECK(tail_full >= 0 && tail_full < tiles && tail_full % 8 == 0 &&
                     ((tiles - tail_full) * tail_split) % 8 == 0, "gemm: bad tail plan");
     TORCH_CHECK(tail_ws.has_value() && tail_cnt.has_value(), "gemm: split tail needs ws and tickets");
@@ -1061,7 +1063,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("ln_bwd_config", [](int variant, int max_blocks) {
-    TORCH_CHECK(variant == 0 || variant == 1, "ln_bwd_config: variant must be 0 or 1");
+    TORCH_CHECK(variant >= 0 && variant <= 3, "ln_bwd_config: variant must be 0-3");
     TORCH_CHECK(max_blocks >= 0 && max_blocks <= 65536, "ln_bwd_config: bad max_blocks");
     caamd::ln_bwd_config(variant, max_blocks);
   });

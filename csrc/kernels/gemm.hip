@@ -575,9 +575,21 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL = 0, int PH = 2, int DIST = 2>
+// DMA_IN_M (algo 7, one phase, distance 3): K-step t+3's DMA pieces are issued one at
+// a time between the MFMA groups of the M segment of step t instead of at the head of
+// the R segment. Barriers B1, B2, ... with the lagging row one behind: row 0 runs
+// R(t) in [B(2t+1), B(2t+2)] and M(t) in [B(2t+2), B(2t+3)], row 1 one barrier later;
+// stage t+1 is first read after B(2t+3), which closes row 0's M(t) (it waits there,
+// t+2 and t+3 in flight) and row 1's R(t) (it waits there, t+2 in flight); slot t-1,
+// overwritten during M(t), was last read in R(t-1), which both rows finished by B(2t+2). PMC (profiles/gemm_pp_pmc_r3_instep.txt): MFMA busy 58%, LDS stalls 6% --
+// the R segment (4-5 pieces at 100-185 issue cycles each beside 18 LDS reads,
+// MI355X_MICROARCH.md "LDS-DMA piece issue cost") outlasted the partner's 640-cycle
+// M segment; among bare MFMAs a piece costs about 60.
+template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL = 0, int PH = 2, int DIST = 2, bool DMA_IN_M = false>
 __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
   static_assert(DIST == 2 || (DIST == 3 && PH == 1), "prefetch distance 3 is WAR-safe only with one phase");
+  static_assert(!DMA_IN_M || (PH == 1 && DIST == 3), "DMA in the M segment: one phase, distance 3 "
+                "(slot t-1 is free in both wave rows by M(t); see the barrier schedule above)");
   constexpr int WM = 2, WN = 4;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int TMH = TM / PH;  // m-tiles per phase (PH phases per K-step)
@@ -649,6 +661,21 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
     dma_step32<BM, AK>(p.A, p.lda, m0, k0, base, wid, lane);
     dma_step32<BN, BK_>(p.B, p.ldb, n0, k0, base + A_ST, wid, lane);
   };
+  // piece q of step t's DMA for this wave, in dma()'s order (A rounds, then B rounds,
+  // then B's partial round on the waves that carry it)
+  constexpr int A_FULL = (BM * 32 * 2) / (NTHR * 16), B_FULL = (BN * 32 * 2) / (NTHR * 16);
+  constexpr int B_REM = BN * 32 * 2 - B_FULL * NTHR * 16;
+  auto dma_piece = [&](int t, int q) {
+    lds_char* base = smem + (t & (NST - 1)) * ST;
+    const int k0 = (s0 + t) * KS;
+    if (q < A_FULL) {
+      if constexpr (AK) dma_kmaj32_one<BM>(p.A, p.lda, m0, k0, base, q, wid, lane);
+      else dma_mmaj32_one<BM>(p.A, p.lda, m0, k0, base, q, wid, lane);
+    } else if (q < A_FULL + B_FULL || (B_REM > 0 && wid * 1024 < B_REM)) {
+      if constexpr (BK_) dma_kmaj32_one<BN>(p.B, p.ldb, n0, k0, base + A_ST, q - A_FULL, wid, lane);
+      else dma_mmaj32_one<BN>(p.B, p.ldb, n0, k0, base + A_ST, q - A_FULL, wid, lane);
+    }
+  };
   // per-step DMA count of this wave: the two wave rows differ when a stage is not a
   // whole number of 8 KiB rounds (BN = 320)
   const bool lo_grp = wr == 0;
@@ -686,7 +713,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
       for (int mh = 0; mh < PH; ++mh) {
         // ---- R segment
         if (mh == 0) {
-          if (!(ABL & 1) && t + DIST < nk) dma(t + DIST);
+          if (!DMA_IN_M && !(ABL & 1) && t + DIST < nk) dma(t + DIST);
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const int rr = wc * (TN * 16) + j * 16;
@@ -702,20 +729,40 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
           else if constexpr (AK) af[i] = frag_kmaj64(As, rr, lane);
           else af[i] = frag_mmaj<BM>(As, rr, 0, lane);
         }
-        if (mh == PH - 1 && !(ABL & 32)) wait_ahead(min(nk - 1, t + DIST) - (t + 1));
+        if constexpr (DMA_IN_M) {
+          // step t+1 must have landed by the barrier that closes this segment for the
+          // lagging row (the leading row waits at the end of its M segment instead);
+          // step t+2 was issued in the previous M segment and stays in flight
+          if (!lo_grp) wait_ahead(min(nk - 1, t + DIST - 1) - (t + 1));
+        } else if (mh == PH - 1 && !(ABL & 32)) {
+          wait_ahead(min(nk - 1, t + DIST) - (t + 1));
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
         // ---- M segment
         __builtin_amdgcn_s_setprio(1);
+        const bool dm = DMA_IN_M && t + DIST < nk;
 #pragma unroll
-        for (int i = 0; i < TMH; ++i)
+        for (int i = 0; i < TMH; ++i) {
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             if constexpr (ABL & 4) asm volatile("" :: "v"(bf[j]), "v"(af[i]));
             else acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[mh * TMH + i][j], 0, 0, 0);
+          if constexpr (DMA_IN_M) {
+            if (i < A_FULL + B_FULL + (B_REM > 0 ? 1 : 0) && dm) {
+              __builtin_amdgcn_sched_barrier(0);
+              dma_piece(t + DIST, i);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
         __builtin_amdgcn_s_setprio(0);
+        // leading row: step t+1 landed before the barrier after which it reads it
+        if constexpr (DMA_IN_M) {
+          if (lo_grp) wait_ahead(min(nk - 1, t + DIST) - (t + 1));
+        }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -1177,7 +1224,8 @@ static hipError_t launch_abl(const Args& a, hipStream_t st) {
   using C_ = Cfg<BM, BN, AK, BK_>;
   const int T = a.tiles_m * a.tiles_n;
   const int grid = a.tS > 1 ? a.tfull + (T - a.tfull) * a.tS : T * a.splitk;
-  if (a.tS > 1 && !(a.algo % 10 >= 1 && a.algo % 10 <= 3) && a.algo != 5) return hipErrorInvalidValue;
+  if (a.tS > 1 && !((a.algo % 10 >= 1 && a.algo % 10 <= 3) || a.algo % 10 == 7) && a.algo != 5)
+    return hipErrorInvalidValue;
   if (a.algo == 5) {  // stream-K: the weight-gradient layout (TN) on 256 x 320 tiles only
     if constexpr ((EPI == EPI_BF16 || EPI == EPI_BF16_ACC) && BM == 256 && BN == 320 && !AK && !BK_) {
       auto k = gemm_sk_kernel<BM, BN, AK, BK_, EPI>;
@@ -1194,9 +1242,10 @@ static hipError_t launch_abl(const Args& a, hipStream_t st) {
     ensure_lds((const void*)k, lds);
     const int tiles = a.tiles_m * a.tiles_n;
     hipLaunchKernelGGL(k, dim3(tiles < 256 ? tiles : 256), dim3(NTHR), lds, st, a);
-  } else if (a.algo % 10 >= 1 && a.algo % 10 <= 3) {
+  } else if ((a.algo % 10 >= 1 && a.algo % 10 <= 3) || a.algo % 10 == 7) {
     auto k = (a.algo % 10 == 1) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 2, 2>
              : (a.algo % 10 == 2) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 2>
+             : (a.algo % 10 == 7) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 3, true>
                                   : gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 3>;
     constexpr int lds = 4 * (BM + BN) * 32 * 2;
     ensure_lds((const void*)k, lds);

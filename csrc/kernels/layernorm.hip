@@ -14,8 +14,10 @@
 
 namespace caamd {
 
-// backward kernel selection (ln_bwd_config): 0 = one row at a time, 1 = prefetching
-static int g_ln_bwd_variant = 0;
+// backward kernel selection (ln_bwd_config): 0 = one row per wave, 1 = prefetching,
+// 2 = column-split, 4 rows per iteration; 3 = column-split, 2 rows (default where it
+// applies: D <= 2048; 97.9 vs 142.5 us at 32k x 1600, tools/bench_ln_bwd.py)
+static int g_ln_bwd_variant = 3;
 static int g_ln_bwd_blocks = 0;  // 0 = default grid cap
 
 template <int NV, bool HAS_RES>
@@ -303,6 +305,119 @@ __global__ __launch_bounds__(256) void ln_bwd_pf_kernel(
   for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) out[i] = red[i];
 }
 
+// Column-split backward (variant 2, the default for D <= 2048): the 4 waves of a block
+// share each row, wave w owning the column chunks [w*CPW, (w+1)*CPW) (CPW <= 64), so a
+// lane holds ONE 16-byte chunk of x / dy / dres per row and 16 fp32 dgamma / dbeta
+// accumulators (the one-row-per-wave kernels above hold 4 chunks and 64 accumulators:
+// 168 VGPRs, 3 waves per SIMD, 2.9 TB/s). RB rows per iteration keep RB x 3 loads in
+// flight per lane; the per-row sums of gd and gd*xhat are combined across the 4 waves
+// through LDS (parity double-buffered: one barrier per RB rows). Waves own disjoint
+// columns, so each block writes its dgamma / dbeta partial row without atomics.
+template <int RB, bool HAS_DRES>
+__global__ __launch_bounds__(256) void ln_bwd_cs_kernel(
+    const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ g,
+    const float* __restrict__ mean, const float* __restrict__ rstd,
+    const bf16* __restrict__ dres, bf16* __restrict__ dx, float* __restrict__ partial,
+    int rows, int D) {
+  __shared__ float red[2][RB][4][2];  // [parity][row][wave][s1 | s2]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nchunk = D >> 3;
+  const int cpw = (nchunk + 3) >> 2;
+  const int ch = wave * cpw + lane;
+  const bool act = lane < cpw && ch < nchunk;
+  float gv[8], dg[8], db[8];
+  {
+    bf16x8 t = act ? *reinterpret_cast<const bf16x8*>(g + ch * 8) : bf16x8{};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      gv[j] = (float)t[j];
+      dg[j] = db[j] = 0.f;
+    }
+  }
+  const float inv_d = 1.f / (float)D;
+  const int ngroups = (rows + RB - 1) / RB;
+  int parity = 0;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x, parity ^= 1) {
+    const int r0 = grp * RB;
+    bf16x8 xv[RB], dv[RB], rv[RB];
+    float mu[RB], rs[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = r0 + i;
+      const bool ok = act && r < rows;
+      const size_t off = (size_t)r * D + ch * 8;
+      xv[i] = ok ? *reinterpret_cast<const bf16x8*>(x + off) : bf16x8{};
+      dv[i] = ok ? *reinterpret_cast<const bf16x8*>(dy + off) : bf16x8{};
+      if (HAS_DRES) rv[i] = ok ? *reinterpret_cast<const bf16x8*>(dres + off) : bf16x8{};
+      mu[i] = r < rows ? mean[r] : 0.f;
+      rs[i] = r < rows ? rstd[r] : 0.f;
+    }
+    float s1[RB], s2[RB];
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)dv[i][j], xh = ((float)xv[i][j] - mu[i]) * rs[i];
+        const float gd = d * gv[j];
+        a += gd;
+        b += gd * xh;
+        dg[j] += d * xh;
+        db[j] += d;
+      }
+      s1[i] = a;
+      s2[i] = b;
+    }
+    // packed bf16 stays live across the reduction; the fp32 unpacks are redone in the
+    // dx pass (keeps the wave near 100 VGPRs instead of holding 3 x RB x 8 floats)
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      opt_barrier(xv[i], dv[i]);
+      if (HAS_DRES) asm volatile("" : "+v"(rv[i]));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        s1[i] += __shfl_xor(s1[i], o, 64);
+        s2[i] += __shfl_xor(s2[i], o, 64);
+      }
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < RB; ++i) {
+        red[parity][i][wave][0] = s1[i];
+        red[parity][i][wave][1] = s2[i];
+      }
+    }
+    __syncthreads();  // the other parity's slots are free again for the next group
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const float m1 = (red[parity][i][0][0] + red[parity][i][1][0] + red[parity][i][2][0] + red[parity][i][3][0]) * inv_d;
+      const float m2 = (red[parity][i][0][1] + red[parity][i][1][1] + red[parity][i][2][1] + red[parity][i][3][1]) * inv_d;
+      const int r = r0 + i;
+      if (act && r < rows) {
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float xh = ((float)xv[i][j] - mu[i]) * rs[i];
+          float v = rs[i] * ((float)dv[i][j] * gv[j] - m1 - xh * m2);
+          if (HAS_DRES) v += (float)rv[i][j];
+          o[j] = (bf16)v;
+        }
+        *reinterpret_cast<bf16x8*>(dx + (size_t)r * D + ch * 8) = o;
+      }
+    }
+  }
+  if (act) {
+    float* out = partial + (size_t)blockIdx.x * 2 * D + ch * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      out[j] = dg[j];
+      out[D + j] = db[j];
+    }
+  }
+}
+
 // Column sum of an fp32 [nrow, ncol] slab -> bf16, split at column `split`
 // (columns < split -> o0[c], the rest -> o1[c - split]). One block = 64 columns
 // x 16 waves; wave w sums rows w, w+16, ... with 8 loads in flight; LDS merge.
@@ -410,9 +525,45 @@ void ln_fwd_launch(const bf16* x, const bf16* r, bf16* s, const bf16* g, const b
   }
 }
 
+constexpr int LN_CS_RB = 4;
+
+int ln_bwd_cs_blocks(int rows) {
+  const int cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : 2048;
+  const int ng = (rows + LN_CS_RB - 1) / LN_CS_RB;
+  return ng < cap ? ng : cap;
+}
+
+static bool ln_bwd_cs_ok(int D) { return (g_ln_bwd_variant == 2 || g_ln_bwd_variant == 3) && D <= 2048 && D % 8 == 0; }
+
+// partial slab rows the backward writes (the caller sizes `partial` as [rows][2D])
+int ln_bwd_partial_rows(int rows, int D) {
+  return ln_bwd_cs_ok(D) ? ln_bwd_cs_blocks(rows) : ln_bwd_num_blocks(rows);
+}
+
 void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* mean,
                    const float* rstd, const bf16* dres, bf16* dx, float* partial, bf16* dg,
                    bf16* db, int rows, int D, hipStream_t st) {
+  if (ln_bwd_cs_ok(D)) {
+    const int nb = ln_bwd_cs_blocks(rows);
+    if (g_ln_bwd_variant == 3) {  // two rows per iteration (fewer VGPRs, more waves)
+      if (dres)
+        hipLaunchKernelGGL((ln_bwd_cs_kernel<2, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd, dres,
+                           dx, partial, rows, D);
+      else
+        hipLaunchKernelGGL((ln_bwd_cs_kernel<2, false>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd, dres,
+                           dx, partial, rows, D);
+      colsum_bf16_launch(partial, nb, 2 * D, D, dg, db, st, 0);
+      return;
+    }
+    if (dres)
+      hipLaunchKernelGGL((ln_bwd_cs_kernel<LN_CS_RB, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd,
+                         dres, dx, partial, rows, D);
+    else
+      hipLaunchKernelGGL((ln_bwd_cs_kernel<LN_CS_RB, false>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd,
+                         dres, dx, partial, rows, D);
+    colsum_bf16_launch(partial, nb, 2 * D, D, dg, db, st, 0);
+    return;
+  }
   const int nblk = ln_bwd_num_blocks(rows);
   switch (ln_nv_for(D)) {
     case 1: ln_bwd_dispatch<1>(dy, x, g, mean, rstd, dres, dx, partial, nblk, rows, D, st); break;

@@ -19,7 +19,20 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("D", [64, 768, 1600, 2048, 4096])
 @pytest.mark.parametrize("with_res", [False, True])
-def test_layernorm_fwd_bwd(C, D, with_res):
+@pytest.mark.parametrize("variant", [0, 2, 3])
+def test_layernorm_fwd_bwd(C, D, with_res, variant):
+    """Backward variants: 0 one row per wave, 2 / 3 column-split (4 / 2 rows per
+    iteration; D <= 2048, larger D falls back to 0); 148 rows exercise partial row groups."""
+    from cluster_anywhere_amd.ops import add_layer_norm, layer_norm
+
+    C.ln_bwd_config(variant, 0)
+    try:
+        _ln_check(D, with_res)
+    finally:
+        C.ln_bwd_config(3, 0)
+
+
+def _ln_check(D, with_res):
     from cluster_anywhere_amd.ops import add_layer_norm, layer_norm
 
     torch.manual_seed(0)
