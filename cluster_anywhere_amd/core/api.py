@@ -492,7 +492,10 @@ def get_gpu_ids():
     if ctx is not None and ctx.gpu_ids is not None:
         return list(range(len(ctx.gpu_ids))) if os.environ.get("ROCR_VISIBLE_DEVICES") else ctx.gpu_ids
     env = os.environ.get("CAAMD_GPU_IDS", "")
-    return [int(x) for x in env.split(",") if x]
+    ids = [int(x) for x in env.split(",") if x]
+    # a leased GPU worker (core/lease.py) runs with its lease's GPUs visible: same
+    # numbering as the head path (device indices when ROCR_VISIBLE_DEVICES is set)
+    return list(range(len(ids))) if os.environ.get("ROCR_VISIBLE_DEVICES") else ids
 
 
 def _timeline_events(ev):

@@ -124,7 +124,7 @@ class ObjEntry:
 class WorkerInfo:
     __slots__ = ("worker_id", "conn", "pid", "node", "gpu_key", "idle", "actor_id", "task",
                  "proc", "fns", "alive", "kind", "started", "tasks_inflight", "env_key", "client_id",
-                 "oom_killed", "direct_addr", "lease", "lease_blocked")
+                 "oom_killed", "direct_addr", "lease", "lease_blocked", "lease_gpus")
 
     def __init__(self, **kw):
         for s in self.__slots__:
@@ -1002,8 +1002,10 @@ class Head:
             self._schedule()
 
     def _demand(self, spec):
-        d = dict(spec.resources)
-        st = spec.strategy
+        return self._demand_for(spec.resources, spec.strategy)
+
+    def _demand_for(self, resources, st):
+        d = dict(resources)
         if st and st[0] == "pg":
             _, pg_id, bidx = st[:3]
             pg_hex = pg_id.hex()
@@ -1663,10 +1665,18 @@ class Head:
     # backlog of normal tasks leases workers of its own node for one resource shape
     # and pushes tasks straight to them (core/lease.py); the head only grants,
     # parks (FIFO) and takes back leases.
-    def _grant_leases(self, c, node, demand, want):
+    def _grant_leases(self, c, node, demand, want, gamt=0.0, env=None):
+        """Grant up to ``want`` workers of ``node`` for one scheduling key: the
+        resource demand (placement-group bundle resources for PG tasks), whole or
+        fractional GPUs pinned to the lease (the worker was spawned with those GPU
+        ids visible), and the runtime env's worker pool."""
         out = []
-        key = (node, (), None)
+        ek = _env_key(env)
         while len(out) < want:
+            gpu_ids = self._pick_gpus(node, gamt)
+            if gpu_ids is None:
+                break
+            key = (node, gpu_ids, ek)
             if not self.sched.acquire(node, demand):
                 break
             idle = self.idle.get(key)
@@ -1678,42 +1688,59 @@ class Head:
                     break
             if w is None:
                 self.sched.release(node, demand)
-                if self.starting[key] < max(1, int(self.cpu_count)) and self._num_workers(node) < self.max_workers:
-                    self._spawn_worker(node, ())
+                if self.starting[key] < max(1, int(self.cpu_count)):
+                    if self._num_workers(node) >= self.max_workers and ek is not None:
+                        self._evict_idle(node, key)
+                    if self._num_workers(node) < self.max_workers:
+                        self._spawn_worker(node, gpu_ids, env=env)
                 break
+            self._take_gpus(node, gpu_ids, gamt)
             w.idle = False
             w.task = None
             w.lease = (c, demand, time.time())
             w.lease_blocked = None
+            w.lease_gpus = (gpu_ids, gamt) if gpu_ids else None
             out.append((w.worker_id, w.direct_addr))
         return out
 
-    def _h_lease(self, c, req, resources, want):
+    def _h_lease(self, c, req, resources, want, opts=None):
         node = self.clients.get(c, {}).get("node") or self.head_hex
-        demand = {k: float(v) for k, v in resources.items() if v}
+        strategy = (opts or {}).get("strategy")
+        env = (opts or {}).get("env") or None
+        if strategy is not None and (strategy[0] != "pg" or strategy[1] not in self.pgs):
+            self._reply(c, req, "never")  # removed group / other strategy: the head path decides
+            return
+        ek = _env_key(env)
+        if ek is not None and ek in self.env_failures:
+            self._reply(c, req, "never")  # the head path fails the tasks with RuntimeEnvSetupError
+            return
+        gamt = float(resources.get("GPU", 0) or 0)
+        demand = {k: float(v) for k, v in self._demand_for(
+            {k: v for k, v in resources.items() if v}, strategy).items() if v}
         if node not in self.node_resources and node != self.head_hex:
             self._reply(c, req, "never")
             return
         if self.sched.pick_node(demand, 2, node, False, self.node_id.hex(), [], []) == "!":
-            self._reply(c, req, "never")  # the owner's node can never run this shape
+            self._reply(c, req, "never")  # the owner's node can never run this shape (or bundle)
             return
-        got = self._grant_leases(c, node, demand, max(1, int(want)))
+        got = self._grant_leases(c, node, demand, max(1, int(want)), gamt, env)
         if got:
             self._reply(c, req, got)
             return
-        other = self.sched.pick_node(demand, 0, "", False, self.node_id.hex(), [], [])
-        if other not in ("", "!") and other != node:
-            self._reply(c, req, "spill")  # another node has room now: send through the head
-            return
-        self.lease_waiters.append((c, req, node, demand, max(1, int(want))))
+        if strategy is None:
+            other = self.sched.pick_node(demand, 0, "", False, self.node_id.hex(), [], [])
+            if other not in ("", "!") and other != node:
+                self._reply(c, req, "spill")  # another node has room now: send through the head
+                return
+        self.lease_waiters.append((c, req, node, demand, max(1, int(want)), gamt, env))
 
     def _serve_lease_waiters(self):
         still = []
         for ent in self.lease_waiters:
-            c, req, node, demand, want = ent
+            c, req, node, demand, want, gamt, env = ent
             if c.closed:
                 continue
-            got = self._grant_leases(c, node, demand, want)
+            got = self._grant_leases(c, node, demand, want, gamt, env)
             if got:
                 self._reply(c, req, got)
             else:
@@ -1726,8 +1753,11 @@ class Head:
         for k, v in (w.lease_blocked or {}).items():
             rel[k] = rel.get(k, 0.0) - v  # lent back while blocked in get()
         self.sched.release(w.node, rel)
+        if getattr(w, "lease_gpus", None):
+            self._give_gpus(w.node, *w.lease_gpus)
         w.lease = None
         w.lease_blocked = None
+        w.lease_gpus = None
         self._retry_pending_pgs()
         self._retry_infeasible()
 
@@ -2150,11 +2180,24 @@ class Head:
                 self.reattach_stats["objects"] += 1
 
     def _reattach_leases(self, c, leases):
-        for (wid, res) in leases:
+        for ent in leases:
+            wid, res = ent[0], ent[1]
+            opts = ent[2] if len(ent) > 2 else None
             w = self.workers.get(wid)
             if w is None or w.lease is not None:
                 continue
-            demand = {k: float(v) for k, v in (res or {}).items() if v}
+            strategy = (opts or {}).get("strategy")
+            if strategy is not None and strategy[1] not in self.pgs:
+                strategy = None
+            demand = {k: float(v) for k, v in self._demand_for(
+                {k: v for k, v in (res or {}).items() if v}, strategy).items() if v}
+            gamt = float((res or {}).get("GPU", 0) or 0)
+            if gamt and w.gpu_key:
+                try:
+                    self._take_gpus(w.node, tuple(w.gpu_key), gamt)
+                    w.lease_gpus = (tuple(w.gpu_key), gamt)
+                except ValueError:
+                    w.lease_gpus = None
             if w.idle:
                 w.idle = False
                 lst = self.idle.get((w.node, w.gpu_key, w.env_key))
@@ -2233,7 +2276,7 @@ class Head:
         if spec is None:
             w = self.conn_worker.get(c)
             if w is not None and w.lease is not None and not w.lease_blocked:
-                cpu = {k: v for k, v in w.lease[1].items() if k == "CPU"}
+                cpu = {k: v for k, v in w.lease[1].items() if k == "CPU" or k.startswith("CPU_group_")}
                 if cpu:  # a leased worker's task blocked: lend its CPUs back
                     self.sched.release(w.node, cpu)
                     w.lease_blocked = cpu

@@ -6,9 +6,11 @@ Reference roles: ``src/ray/core_worker/transport/direct_task_transport.cc``
 lease reuse, ReturnWorker) and the raylet's ``HandleRequestWorkerLease``.
 Design for one MI355X node:
 
-* a scheduling key is the resource shape of a task (no placement group, node
-  affinity, runtime env or GPU: those keep the head path, which knows about
-  bundles, GPU ids and per-env worker pools);
+* a scheduling key is (resource shape, placement-group bundle, runtime env) — the
+  reference's SchedulingKey; GPU tasks lease GPU-pinned workers (the GPU ids stay
+  with the lease until it is returned), placement-group tasks lease against their
+  bundle's resources on the owner's node, runtime-env tasks lease workers of that
+  env's pool (node-affinity / SPREAD / label strategies keep the head path);
 * the FIRST task of a key goes through the head as before (a synchronous
   ``get(f.remote())`` loop never pays for a lease); once the owner has tasks in
   flight, further tasks of that key queue locally and the owner asks the head for
@@ -64,11 +66,25 @@ def enabled() -> bool:
 
 
 def eligible(spec) -> bool:
-    if spec.kind != NORMAL or spec.generator is not None or spec.runtime_env:
+    if spec.kind != NORMAL or spec.generator is not None:
         return False
-    if spec.strategy is not None and spec.strategy[0] != "default":
-        return False
-    return not float(spec.resources.get("GPU", 0) or 0)
+    return spec.strategy is None or spec.strategy[0] in ("default", "pg")
+
+
+def _env_sig(renv):
+    if not renv:
+        return None
+    try:
+        import json
+
+        return json.dumps(renv, sort_keys=True, default=str)
+    except (TypeError, ValueError):
+        return repr(sorted(renv.items()))
+
+
+def scheduling_key(spec):
+    st = spec.strategy if (spec.strategy is not None and spec.strategy[0] == "pg") else None
+    return (tuple(sorted(spec.resources.items())), st, _env_sig(spec.runtime_env))
 
 
 def _frame(msg) -> bytes:
@@ -77,10 +93,12 @@ def _frame(msg) -> bytes:
 
 
 class _Key:
-    __slots__ = ("resources", "queue", "leases", "requesting", "mode", "retry_at", "active")
+    __slots__ = ("resources", "strategy", "env", "queue", "leases", "requesting", "mode", "retry_at", "active")
 
-    def __init__(self, resources):
+    def __init__(self, resources, strategy=None, env=None):
         self.resources = dict(resources)
+        self.strategy = strategy  # ("pg", pg_id, bundle, ...) or None
+        self.env = env  # runtime env dict or None
         self.queue: collections.deque = collections.deque()  # (spec, keep, resolved)
         self.leases: List["_Lease"] = []
         self.requesting = False
@@ -145,10 +163,10 @@ class LeaseManager:
 
     def submit(self, spec, keep, resolved, busy: bool) -> bool:
         """Queue ``spec`` for a leased worker; False = use the head path."""
-        key = tuple(sorted(spec.resources.items()))
+        key = scheduling_key(spec)
         st = self.keys.get(key)
         if st is None:
-            st = self.keys.setdefault(key, _Key(spec.resources))
+            st = self.keys.setdefault(key, _Key(spec.resources, key[1], spec.runtime_env or None))
         if st.mode == "never":
             return False
         if not st.active and not busy:
@@ -333,7 +351,8 @@ class LeaseManager:
             if need > 0:
                 st.requesting = True
                 want = min(MAX_WANT, (need + DEPTH - 1) // DEPTH)
-                self.w.request_cb(lambda r: ("lease", r, st.resources, want),
+                opts = {"strategy": st.strategy, "env": st.env} if (st.strategy or st.env) else None
+                self.w.request_cb(lambda r: ("lease", r, st.resources, want, opts),
                                   lambda res, st=st: self._granted_cb(st, res))
         st.active = bool(st.leases or st.queue or st.requesting)
 

@@ -485,8 +485,8 @@ class CoreWorker:
                     inline[oid] = (blob, is_err)
         st["refs"], st["inline"] = refs, inline
         if self.leases is not None:
-            st["leases"] = [(lc.worker_id, dict(k.resources)) for k in list(self.leases.keys.values())
-                            for lc in list(k.leases) if lc.alive]
+            st["leases"] = [(lc.worker_id, dict(k.resources), {"strategy": k.strategy, "env": k.env})
+                            for k in list(self.leases.keys.values()) for lc in list(k.leases) if lc.alive]
         return st
 
     def _track_head_spec(self, spec):
