@@ -192,10 +192,17 @@ class Learner:
                 losses, _ = self.compute_loss(static_in)
                 with accumulate_into_grad():
                     losses[name].backward()
+                # drop the warm-up graph: a live graph keeps the parameters' AccumulateGrad
+                # nodes (bound to the stream they were created on) for the capture to reuse,
+                # and autograd then warns of a stream mismatch that can break the capture
+                del losses
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        import gc
+
+        gc.collect()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+        with torch.cuda.graph(graph, stream=side):
             flat.grad_buffer.zero_()
             losses, stats = self.compute_loss(static_in)
             with accumulate_into_grad():

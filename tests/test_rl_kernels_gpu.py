@@ -19,7 +19,7 @@ DEV = torch.device("cuda")
 
 
 def _rel(a, b):
-    return float((a.float() - b.float()).norm() / (b.float().norm() + 1e-12))
+    return float((a.detach().float() - b.detach().float()).norm() / (b.detach().float().norm() + 1e-12))
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 32, 256), (333, 64, 576), (500, 512, 3136), (64, 40, 96)])

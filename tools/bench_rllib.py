@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--minibatch", type=int, default=500)
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--seconds", type=float, default=0.0,
+                    help="run timed iterations until at least this many seconds passed (>= --iters)")
     args = ap.parse_args()
     import torch
 
@@ -46,10 +48,19 @@ def main():
     t0 = time.perf_counter()
     s0 = algo.env_steps_sampled
     samp = learn = 0.0
-    for _ in range(args.iters):
+    it = 0
+    last = t0
+    while it < args.iters or time.perf_counter() - t0 < args.seconds:
         r = algo.train()
+        it += 1
         samp += r.get("timers", {}).get("sample_s", 0.0)
         learn += r.get("timers", {}).get("learn_s", 0.0)
+        if time.perf_counter() - last > 10:
+            last = time.perf_counter()
+            print(json.dumps({"progress_s": round(last - t0, 1), "iters": it,
+                              "env_steps_per_s": round((algo.env_steps_sampled - s0) / (last - t0), 1),
+                              "episode_return_mean": r["env_runners"].get("episode_return_mean")}), flush=True)
+    args.iters = it
     dt = time.perf_counter() - t0
     steps = algo.env_steps_sampled - s0
     print(json.dumps({
