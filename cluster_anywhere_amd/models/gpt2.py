@@ -3,11 +3,13 @@
 Pre-LN transformer. The residual stream is carried as (h, pending_delta) so every
 ``h = h + delta; a = LN(h)`` pair is ONE fused ``add_layer_norm`` kernel. MLP
 bias+GELU is one fused kernel (dbias fused in backward); the LM head is tied to
-the token embedding, the vocab is padded to a multiple of 64 for the GEMMs and
-the fused cross-entropy masks the padding. The projection GEMMs (forward and
-input-gradient) are the hand-written MFMA kernels of ``ops/gemm.py`` with bias /
-bias+GELU / GELU' fused into their epilogues (weight gradients and the LM head on
-hipBLASLt); attention goes through :func:`ops.attention`.
+the token embedding, the vocab is padded to a multiple of 256 for the GEMM tiles
+and the cross-entropy masks the padding. The projection GEMMs (forward and
+input-gradient, and the weight gradients where they win) are the hand-written
+MFMA kernels of ``ops/gemm.py`` with bias / bias+GELU / GELU' fused into their
+epilogues; the LM head + loss is :func:`ops.loss.linear_cross_entropy` (chunked,
+logits never materialised, all three GEMMs on gemm.hip); attention goes through
+:func:`ops.attention`.
 
 This is the model behind the headline benchmark (Ray Train
 TorchTrainer DDP GPT-2-XL tokens/s).
@@ -21,8 +23,9 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops import add_layer_norm, attention, bias_gelu, cross_entropy, layer_norm
+from ..ops import add_layer_norm, attention, layer_norm
 from ..ops.linear import linear, mlp
+from ..ops.loss import linear_cross_entropy
 
 
 @dataclass
@@ -33,7 +36,7 @@ class GPT2Config:
     n_head: int = 25
     n_embd: int = 1600
     ln_eps: float = 1e-5
-    pad_vocab_to: int = 64
+    pad_vocab_to: int = 256
 
     @property
     def padded_vocab(self) -> int:
@@ -117,16 +120,15 @@ class GPT2(nn.Module):
     def forward(self, idx, targets=None):
         hf = self.hidden(idx)
         B, T, D = hf.shape
+        if targets is not None:
+            return linear_cross_entropy(hf.reshape(B * T, D), self.wte, targets, self.cfg.vocab_size)
         logits = F.linear(hf.reshape(B * T, D), self.wte)  # [B*T, Vpad]
-        if targets is None:
-            return logits.view(B, T, -1)[..., : self.cfg.vocab_size]
-        losses = cross_entropy(logits, targets.reshape(-1), self.cfg.vocab_size)
-        valid = (targets.reshape(-1) >= 0).sum().clamp(min=1)
-        return losses.sum() / valid
+        return logits.view(B, T, -1)[..., : self.cfg.vocab_size]
 
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs/token (fwd+bwd = 3x fwd), PaLM-style accounting incl. attention."""
         c = self.cfg
         n = sum(p.numel() for n_, p in self.named_parameters() if n_ != "wpe")
+        n -= (c.padded_vocab - c.vocab_size) * c.n_embd  # padded vocab rows are not model FLOPs
         attn = 12 * c.n_layer * c.n_embd * seq_len / 2  # causal: half the score matrix
         return 6 * n + attn

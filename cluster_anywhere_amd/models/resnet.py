@@ -15,6 +15,14 @@ Training form is an ordinary ``nn.Module`` (BatchNorm, fp32 or bf16).
 * input is uint8 NHWC straight from the object-store block, normalised by one
   HIP kernel (``ops.image_normalize``) into bf16 channels_last.
 
+On an MI355X the default (``CAAMD_OWN_CONV=1``) is the framework's own conv path
+instead: every convolution is the implicit-GEMM NHWC MFMA kernel of
+``csrc/kernels/conv.hip`` (no im2col buffer, no MIOpen) with the folded-BN bias,
+the bottleneck's residual join and ReLU in its epilogue, the stem input
+normalised and padded to 8 channels by one kernel, and the 3x3/2 max pool on a
+HIP kernel — so the conv outputs are written once and never re-read by a
+separate bias / add / ReLU pass.
+
 :class:`ResNetPredictor` wraps that in a fixed-batch HIP-graph replay (the whole
 forward is one graph launch; partial batches are padded), which is what the
 Data GPU actors run.
@@ -31,7 +39,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.vision import IMAGENET_MEAN, IMAGENET_STD, bias_act_, image_normalize
+from ..ops.vision import (IMAGENET_MEAN, IMAGENET_STD, bias_act_, conv2d_nhwc, conv_weight_nhwc, image_normalize,
+                          maxpool3s2_nhwc, normalize_pad8)
+
+OWN_CONV = os.environ.get("CAAMD_OWN_CONV", "1") == "1"
 
 
 def _conv(cin, cout, k, stride=1):
@@ -123,8 +134,8 @@ class ResNet(nn.Module):
         return _analytic_flops(self, hw)
 
     @torch.no_grad()
-    def fuse_for_inference(self, dtype=torch.bfloat16, device=None) -> "FusedResNet":
-        return FusedResNet(self, dtype, device)
+    def fuse_for_inference(self, dtype=torch.bfloat16, device=None, own_conv=None) -> "FusedResNet":
+        return FusedResNet(self, dtype, device, own_conv)
 
 
 def _analytic_flops(net: ResNet, hw: int) -> float:
@@ -154,30 +165,46 @@ def _fold(conv: nn.Conv2d, bn: nn.BatchNorm2d, dtype, device):
 
 
 class _FConv:
-    __slots__ = ("w", "b", "stride", "pad", "relu")
+    __slots__ = ("w", "b", "stride", "pad", "relu", "w2d", "ks")
 
-    def __init__(self, conv, bn, relu, dtype, device):
+    def __init__(self, conv, bn, relu, dtype, device, own=False, cin_pad=0):
         self.w, self.b = _fold(conv, bn, dtype, device)
         self.stride, self.pad, self.relu = conv.stride, conv.padding, relu
+        self.ks = conv.kernel_size[0]
+        # own-kernel form: [Cout, Kp] (k = (kh*KS + kw)*Cin + ci), Cin padded for the stem
+        self.w2d = conv_weight_nhwc(self.w.float(), cin_pad).to(dtype) if own else None
 
     def __call__(self, x, residual=None):
         # bias-free MIOpen conv + ONE fused epilogue kernel (bias, residual, ReLU)
         y = F.conv2d(x, self.w, None, self.stride, self.pad)
         return bias_act_(y, self.b, residual, self.relu or residual is not None)
 
+    def own(self, x, residual=None):
+        """x: NHWC [N, H, W, C] -> act(conv + bias (+ residual)) on conv.hip."""
+        return conv2d_nhwc(x, self.w2d, self.b, self.ks, self.stride[0], self.pad[0],
+                           self.relu or residual is not None, residual)
+
 
 class FusedResNet(nn.Module):
     """BN-folded bf16 channels_last inference form of a :class:`ResNet`."""
 
-    def __init__(self, net: ResNet, dtype, device):
+    def __init__(self, net: ResNet, dtype, device, own_conv: Optional[bool] = None):
         super().__init__()
         device = device or next(net.parameters()).device
         self.dtype, self.device = dtype, torch.device(device)
-        self.stem = _FConv(net.conv1, net.bn1, True, dtype, device)
+        if own_conv is None:
+            own_conv = OWN_CONV
+        self.own = bool(own_conv and self.device.type == "cuda" and dtype == torch.bfloat16)
+        if self.own:
+            from ..ops import kernels
+
+            kernels()  # fail loudly if the HIP extension is missing
+        o = self.own
+        self.stem = _FConv(net.conv1, net.bn1, True, dtype, device, own=o, cin_pad=8)
         self.blocks: List[tuple] = []
         for b in net.blocks:
-            convs = [_FConv(c, bn, r, dtype, device) for c, bn, r in b.convs()]
-            down = _FConv(b.down[0], b.down[1], False, dtype, device) if b.down is not None else None
+            convs = [_FConv(c, bn, r, dtype, device, own=o) for c, bn, r in b.convs()]
+            down = _FConv(b.down[0], b.down[1], False, dtype, device, own=o) if b.down is not None else None
             self.blocks.append((convs, down))
         self.fc_w = net.fc.weight.detach().to(device=device, dtype=dtype)
         self.fc_b = net.fc.bias.detach().to(device=device, dtype=dtype)
@@ -196,8 +223,24 @@ class FusedResNet(nn.Module):
         return F.linear(x, self.fc_w, self.fc_b)
 
     @torch.no_grad()
+    def forward_own(self, x8):
+        """x8: normalised NHWC bf16 [N, H, W, 8] (RGB + zero channels) -> logits, every
+        conv on conv.hip with its epilogue fused."""
+        x = maxpool3s2_nhwc(self.stem.own(x8))
+        for convs, down in self.blocks:
+            idt = x if down is None else down.own(x)
+            y = x
+            for c in convs[:-1]:
+                y = c.own(y)
+            x = convs[-1].own(y, residual=idt)
+        x = x.mean(dim=(1, 2))
+        return F.linear(x, self.fc_w, self.fc_b)
+
+    @torch.no_grad()
     def predict_uint8(self, images: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD):
         """uint8 NHWC on this device -> logits."""
+        if self.own:
+            return self.forward_own(normalize_pad8(images, mean, std))
         x = image_normalize(images, mean, std)
         if x.dtype != self.dtype:
             x = x.to(self.dtype)

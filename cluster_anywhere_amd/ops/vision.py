@@ -49,3 +49,74 @@ def bias_act_(y: torch.Tensor, b: torch.Tensor, residual=None, relu: bool = True
     if residual is not None:
         y.add_(residual)
     return y.relu_() if relu else y
+
+
+# ---- implicit-GEMM NHWC convolution (csrc/kernels/conv.hip) ------------------------
+# The Data ResNet path runs every convolution on its own MFMA kernel with the folded
+# BN bias, the residual join and ReLU in the epilogue (no MIOpen conv, no separate
+# bias / add / ReLU pass). Activations are plain contiguous NHWC [N, H, W, C].
+
+_ZERO: dict = {}
+
+
+def _zero_page(dev: torch.device) -> torch.Tensor:
+    z = _ZERO.get(dev)
+    if z is None:
+        z = _ZERO[dev] = torch.zeros(64, dtype=torch.bfloat16, device=dev)
+    return z
+
+
+def conv_weight_nhwc(w: torch.Tensor, cin_pad: int = 0) -> torch.Tensor:
+    """[Cout, Cin, KH, KW] -> [Cout, Kp]: k = (kh * KW + kw) * Cin' + ci, Cin padded
+    with zero channels to ``cin_pad`` and K zero-padded to a multiple of 32."""
+    cout, cin, kh, kw = w.shape
+    w = w.permute(0, 2, 3, 1)
+    if cin_pad > cin:
+        w = torch.nn.functional.pad(w, (0, cin_pad - cin))
+    w = w.reshape(cout, -1)
+    k = w.shape[1]
+    kp = (k + 31) // 32 * 32
+    if kp > k:
+        w = torch.nn.functional.pad(w, (0, kp - k))
+    return w.contiguous()
+
+
+def conv_tile(m: int, cout: int, cus: int = 256) -> int:
+    """0 = 256x128, 1 = 256x64 (Cout 64), 2 = 128x128 (fills the chip when the
+    256x128 grid is under two workgroups per CU)."""
+    if cout % 128:
+        return 1
+    if -(-m // 256) * (cout // 128) < 2 * cus:
+        return 2
+    return 0
+
+
+def conv2d_nhwc(x: torch.Tensor, w2d: torch.Tensor, bias: torch.Tensor, ks: int, stride: int, pad: int,
+                relu: bool, residual=None, tile=None) -> torch.Tensor:
+    """y = act(conv(x, w) + bias (+ residual)) on NHWC bf16 (GPU kernel only)."""
+    n, h, wd, _ = x.shape
+    ho = (h + 2 * pad - ks) // stride + 1
+    wo = (wd + 2 * pad - ks) // stride + 1
+    if tile is None:
+        tile = conv_tile(n * ho * wo, w2d.shape[0])
+    return kernels().conv2d_nhwc(x, w2d, bias, residual, ks, stride, pad, relu, tile, _zero_page(x.device))
+
+
+def conv2d_nhwc_ref(x: torch.Tensor, w4: torch.Tensor, bias: torch.Tensor, stride: int, pad: int, relu: bool,
+                    residual=None) -> torch.Tensor:
+    """fp32 reference of :func:`conv2d_nhwc` with the 4-D [Cout, Cin, KH, KW] weight."""
+    y = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2).float(), w4.float(), bias.float(), stride, pad)
+    y = y.permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual.float()
+    return y.relu() if relu else y
+
+
+def normalize_pad8(x: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN,
+                   std: Sequence[float] = IMAGENET_STD) -> torch.Tensor:
+    """uint8 [N, H, W, 3] -> bf16 [N, H, W, 8]: normalised RGB + 5 zero channels."""
+    return kernels().normalize_pad8(x.contiguous(), list(mean), list(std))
+
+
+def maxpool3s2_nhwc(x: torch.Tensor) -> torch.Tensor:
+    return kernels().maxpool3s2_nhwc(x)

@@ -24,6 +24,13 @@ void bias_gelu_bwd_launch(const bf16*, const bf16*, const bf16*, bf16*, float*, 
 int bias_gelu_bwd_slabs(int rows);
 void xent_fwd_launch(const bf16*, const int64_t*, float*, float*, int, int, int, hipStream_t);
 void xent_bwd_launch(bf16*, const int64_t*, const float*, const float*, int, int, int, hipStream_t);
+hipError_t conv2d_launch(const bf16* X, const bf16* Wt, const bf16* bias, const bf16* R, bf16* Y, const bf16* zero,
+                         int N, int H, int W, int lcin, int Ho, int Wo, int KS, int stride, int pad, int Cout, int Kp,
+                         bool relu, int tile, hipStream_t st);
+void normalize_pad8_launch(const uint8_t* in, bf16* out, int64_t npix, const float* sc, const float* bi,
+                           hipStream_t st);
+void maxpool3s2_launch(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
+bool xent_fused_launch(bf16*, const int64_t*, float*, float*, const float*, int, int, int, hipStream_t);
 void grad_sumsq_launch(const void*, bool, int64_t, float*, hipStream_t);
 void adamw_launch(float*, float*, float*, const void*, bool, bf16*, int64_t, float, float, float,
                   float, float, float, float, float, float, const float*, const uint8_t*,
@@ -256,6 +263,31 @@ void xent_bwd_(Tensor& logits, const Tensor& target, const Tensor& lse, const Te
     caamd::xent_bwd_launch(bp(logits), target.data_ptr<int64_t>(), lse.data_ptr<float>(),
                            dl.data_ptr<float>(), rows, (int)V, stride, cur_stream());
     LAUNCH_CHECK();
+}
+
+// Fused forward + backward, in place: logits <- scale * (softmax - onehot); returns
+// {loss, lse} per row. scale: 1-element fp32 device tensor (no host sync).
+std::vector<Tensor> xent_fused_(Tensor& logits, const Tensor& target, const Tensor& scale, int64_t V) {
+  CHECK_BF16(logits);
+  CHECK_GPU(target);
+  CHECK_CONTIG(target);
+  CHECK_DT(target, at::kLong);
+  CHECK_F32(scale);
+  TORCH_CHECK(logits.dim() == 2, "xent_fused: logits must be 2-D");
+  const int rows = (int)logits.size(0), stride = (int)logits.size(1);
+  TORCH_CHECK(stride % 8 == 0 && V > 0 && V <= stride, "xent_fused: bad stride/V");
+  TORCH_CHECK(target.numel() == rows && scale.numel() == 1, "xent_fused: size mismatch");
+  TORCH_CHECK(((uintptr_t)logits.data_ptr()) % 16 == 0, "xent_fused: 16-byte alignment");
+  auto loss = at::empty({rows}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({rows}, logits.options().dtype(at::kFloat));
+  if (rows > 0) {
+    TORCH_CHECK(caamd::xent_fused_launch(bp(logits), target.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                                         lse.data_ptr<float>(), scale.data_ptr<float>(), rows, (int)V, stride,
+                                         cur_stream()),
+                "xent_fused: row too wide for the register-resident kernel");
+    LAUNCH_CHECK();
+  }
+  return {loss, lse};
 }
 
 // ---- optimizer ---------------------------------------------------------------
@@ -645,6 +677,81 @@ Tensor image_normalize(const Tensor& x, std::vector<double> mean, std::vector<do
     caamd::image_normalize_launch(x.data_ptr<uint8_t>(), bp(out), x.numel(), sc, bi, cur_stream());
   LAUNCH_CHECK();
   return out;
+}
+
+// ---- implicit-GEMM NHWC convolution (conv.hip) ----------------------------------
+// x [N, H, W, Cin] (plain contiguous NHWC), w [Cout, Kp] with k = (kh*KS + kw)*Cin + ci
+// (zero-padded to Kp % 32 == 0), bias [Cout]; residual [N, Ho, Wo, Cout] or None.
+// y = act(conv(x, w) + bias (+ residual)); tile 0 = 256x128, 1 = 256x64, 2 = 128x128.
+Tensor conv2d_nhwc(const Tensor& x, const Tensor& w, const Tensor& bias, c10::optional<Tensor> residual,
+                   int64_t ks, int64_t stride, int64_t pad, bool relu, int64_t tile, const Tensor& zero) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(bias);
+  CHECK_BF16(zero);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv2d_nhwc: x [N,H,W,C], w [Cout,Kp]");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  const int64_t Cout = w.size(0), Kp = w.size(1);
+  TORCH_CHECK(Cin >= 8 && (Cin & (Cin - 1)) == 0, "conv2d_nhwc: Cin must be a power of two >= 8");
+  TORCH_CHECK(ks == 1 || ks == 3 || ks == 7, "conv2d_nhwc: kernel size 1, 3 or 7");
+  TORCH_CHECK(stride >= 1 && pad >= 0, "conv2d_nhwc: stride / pad");
+  TORCH_CHECK(Kp % 32 == 0 && Kp >= ks * ks * Cin, "conv2d_nhwc: Kp must cover KS*KS*Cin, multiple of 32");
+  TORCH_CHECK(bias.numel() == Cout && zero.numel() >= 8, "conv2d_nhwc: bias / zero page");
+  const int64_t bn = tile == 1 ? 64 : 128;
+  TORCH_CHECK(tile >= 0 && tile <= 2 && Cout % bn == 0, "conv2d_nhwc: Cout must be a multiple of the tile width");
+  const int64_t Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "conv2d_nhwc: empty output");
+  TORCH_CHECK(N * H * W * Cin < (1LL << 31) && N * Ho * Wo < (1LL << 31), "conv2d_nhwc: size");
+  for (const Tensor* t : {&x, &w, &zero})
+    TORCH_CHECK(((uintptr_t)t->data_ptr()) % 16 == 0, "conv2d_nhwc: 16-byte alignment");
+  auto y = at::empty({N, Ho, Wo, Cout}, x.options());
+  const caamd::bf16* rp = nullptr;
+  if (residual.has_value()) {
+    CHECK_BF16(*residual);
+    TORCH_CHECK(residual->sizes() == y.sizes(), "conv2d_nhwc: residual shape");
+    TORCH_CHECK(((uintptr_t)residual->data_ptr()) % 16 == 0, "conv2d_nhwc: residual alignment");
+    rp = bp(*residual);
+  }
+  int lcin = 0;
+  while ((1LL << lcin) < Cin) ++lcin;
+  if (N * Ho * Wo > 0) {
+    const hipError_t e = caamd::conv2d_launch(bp(x), bp(w), bp(bias), rp, bp(y), bp(zero), (int)N, (int)H, (int)W,
+                                              lcin, (int)Ho, (int)Wo, (int)ks, (int)stride, (int)pad, (int)Cout,
+                                              (int)Kp, relu, (int)tile, cur_stream());
+    TORCH_CHECK(e == hipSuccess, "conv2d_nhwc: launch failed: ", hipGetErrorString(e));
+  }
+  return y;
+}
+
+// uint8 [N, H, W, 3] -> bf16 [N, H, W, 8] (normalised, channels 3..7 zero)
+Tensor normalize_pad8(const Tensor& x, std::vector<double> mean, std::vector<double> std) {
+  CHECK_GPU(x);
+  CHECK_CONTIG(x);
+  CHECK_DT(x, at::kByte);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 3 && mean.size() == 3 && std.size() == 3, "normalize_pad8: NHWC C=3");
+  TORCH_CHECK(((uintptr_t)x.data_ptr()) % 16 == 0, "normalize_pad8: 16-byte alignment");
+  auto out = at::empty({x.size(0), x.size(1), x.size(2), 8}, x.options().dtype(at::kBFloat16));
+  float sc[3], bi[3];
+  for (int c = 0; c < 3; ++c) {
+    sc[c] = (float)(1.0 / (255.0 * std[c]));
+    bi[c] = (float)(-mean[c] / std[c]);
+  }
+  const int64_t npix = x.size(0) * x.size(1) * x.size(2);
+  if (npix) caamd::normalize_pad8_launch(x.data_ptr<uint8_t>(), bp(out), npix, sc, bi, cur_stream());
+  LAUNCH_CHECK();
+  return out;
+}
+
+// 3x3 / stride 2 / pad 1 max pool on bf16 [N, H, W, C] (C % 8 == 0)
+Tensor maxpool3s2_nhwc(const Tensor& x) {
+  CHECK_BF16(x);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "maxpool3s2: [N,H,W,C], C % 8");
+  const int64_t N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int64_t Ho = (H + 2 - 3) / 2 + 1, Wo = (W + 2 - 3) / 2 + 1;
+  auto y = at::empty({N, Ho, Wo, C}, x.options());
+  if (y.numel()) caamd::maxpool3s2_launch(bp(x), bp(y), (int)N, (int)H, (int)W, (int)C, (int)Ho, (int)Wo, cur_stream());
+  LAUNCH_CHECK();
+  return y;
 }
 
 void add_relu_(Tensor& y, const Tensor& r) {
@@ -1072,6 +1179,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bias_grad_", &bias_grad_);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd_", &xent_bwd_);
+  m.def("xent_fused_", &xent_fused_);
   m.def("grad_sumsq", &grad_sumsq);
   m.def("adamw_step", &adamw_step);
   m.def("gae", &gae);
@@ -1089,6 +1197,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("flash_attn_gqa", &flash_attn_gqa);
   m.def("image_normalize", &image_normalize);
   m.def("add_relu_", &add_relu_);
+  m.def("conv2d_nhwc", &conv2d_nhwc);
+  m.def("normalize_pad8", &normalize_pad8);
+  m.def("maxpool3s2_nhwc", &maxpool3s2_nhwc);
   m.def("bias_act_", &bias_act_);
   m.def("rl_gemm", &rl_gemm_);
   m.def("rl_im2col", &rl_im2col_);

@@ -90,6 +90,122 @@ __global__ __launch_bounds__(kXentThreads) void xent_bwd_kernel(
   }
 }
 
+// ---- fused forward + backward (the chunked LM head, ops/loss.py) ---------------
+// One 1024-thread block per row; the whole row is held in registers (NCH 16-byte
+// chunks per lane: a 50,432-wide GPT-2 row is 6,304 chunks = 7 per lane), so the
+// logits are read from HBM once and the gradient written once:
+//   max -> sum exp -> lse -> loss[row], then dlogits = scale * (softmax - onehot)
+// in place. `scale` is a device scalar (1 / #valid targets for a mean loss), so no
+// host sync is needed to know the loss normaliser.
+constexpr int kXentFusedThreads = 1024;
+
+template <int NCH>
+__global__ __launch_bounds__(kXentFusedThreads) void xent_fused_kernel(
+    bf16* __restrict__ logits, const int64_t* __restrict__ target, float* __restrict__ loss,
+    float* __restrict__ lse_out, const float* __restrict__ scale, int V, int stride) {
+  __shared__ float red[kXentFusedThreads / 64];
+  __shared__ float bcast;
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bf16* x = logits + (size_t)row * stride;
+  const int nvec = stride >> 3;
+  bf16x8 r[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = tid + j * kXentFusedThreads;
+    if (c < nvec) r[j] = *reinterpret_cast<const bf16x8*>(x + c * 8);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = tid + j * kXentFusedThreads;
+    if (c < nvec) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c * 8 + e < V) m = fmaxf(m, (float)r[j][e]);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) red[w] = m;
+  __syncthreads();
+  if (tid < 64) {
+    float v = tid < kXentFusedThreads / 64 ? red[tid] : -INFINITY;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    if (tid == 0) bcast = v;
+  }
+  __syncthreads();
+  const float M = bcast;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = tid + j * kXentFusedThreads;
+    if (c < nvec) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c * 8 + e < V) s += __expf((float)r[j][e] - M);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  __syncthreads();  // everyone has read bcast / red before they are reused
+  if (lane == 0) red[w] = s;
+  __syncthreads();
+  if (tid < 64) {
+    float v = tid < kXentFusedThreads / 64 ? red[tid] : 0.f;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (tid == 0) bcast = v;
+  }
+  __syncthreads();
+  const float L = M + __logf(bcast);
+  const int64_t t = target[row];
+  const bool valid = t >= 0 && t < V;
+  const float g = t >= 0 ? scale[0] : 0.f;
+  if (tid == 0) {
+    lse_out[row] = L;
+    if (!valid) loss[row] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = tid + j * kXentFusedThreads;
+    if (c < nvec) {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = c * 8 + e;
+        const float v = (float)r[j][e];
+        float p = col < V ? __expf(v - L) : 0.f;
+        if (col == t) {
+          loss[row] = L - v;
+          p -= 1.f;
+        }
+        o[e] = (bf16)(g * p);
+      }
+      *reinterpret_cast<bf16x8*>(x + c * 8) = o;
+    }
+  }
+}
+
+bool xent_fused_launch(bf16* logits, const int64_t* target, float* loss, float* lse, const float* scale,
+                       int rows, int V, int stride, hipStream_t st) {
+  const int nvec = stride >> 3;
+  const int nch = (nvec + kXentFusedThreads - 1) / kXentFusedThreads;
+#define XENT_FUSED(N)                                                                                 \
+  hipLaunchKernelGGL(xent_fused_kernel<N>, dim3(rows), dim3(kXentFusedThreads), 0, st, logits, target, \
+                     loss, lse, scale, V, stride)
+  if (nch <= 1) XENT_FUSED(1);
+  else if (nch <= 2) XENT_FUSED(2);
+  else if (nch <= 4) XENT_FUSED(4);
+  else if (nch <= 7) XENT_FUSED(7);
+  else if (nch <= 8) XENT_FUSED(8);
+  else if (nch <= 16) XENT_FUSED(16);
+  else return false;
+#undef XENT_FUSED
+  return true;
+}
+
 void xent_fwd_launch(const bf16* logits, const int64_t* target, float* loss, float* lse, int rows,
                      int V, int stride, hipStream_t st) {
   hipLaunchKernelGGL(xent_fwd_kernel, dim3(rows), dim3(kXentThreads), 0, st, logits, target, loss,
