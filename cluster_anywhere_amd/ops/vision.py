@@ -81,12 +81,15 @@ def conv_weight_nhwc(w: torch.Tensor, cin_pad: int = 0) -> torch.Tensor:
     return w.contiguous()
 
 
-def conv_tile(m: int, cout: int, cus: int = 256) -> int:
-    """0 = 256x128, 1 = 256x64 (Cout 64), 2 = 128x128 (fills the chip when the
-    256x128 grid is under two workgroups per CU)."""
+def conv_tile(m: int, cout: int, k: int = 1 << 30, residual: bool = False) -> int:
+    """0 = 256x128, 1 = 256x64 (Cout 64), 2 = 128x128. Per-shape timings over every
+    ResNet-50 conv at batch 512 (tools/bench_conv.py, profiles/conv_shapes_r3.jsonl):
+    the 128x128 tile wins where the epilogue dominates (a residual join, or a short
+    reduction K = Cin*KS*KS < 256: more workgroups per CU overlap one's epilogue
+    with another's main loop), the 256x128 tile everywhere else."""
     if cout % 128:
         return 1
-    if -(-m // 256) * (cout // 128) < 2 * cus:
+    if residual or k < 256:
         return 2
     return 0
 
@@ -98,7 +101,7 @@ def conv2d_nhwc(x: torch.Tensor, w2d: torch.Tensor, bias: torch.Tensor, ks: int,
     ho = (h + 2 * pad - ks) // stride + 1
     wo = (wd + 2 * pad - ks) // stride + 1
     if tile is None:
-        tile = conv_tile(n * ho * wo, w2d.shape[0])
+        tile = conv_tile(n * ho * wo, w2d.shape[0], x.shape[3] * ks * ks, residual is not None)
     return kernels().conv2d_nhwc(x, w2d, bias, residual, ks, stride, pad, relu, tile, _zero_page(x.device))
 
 

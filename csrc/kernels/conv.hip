@@ -179,7 +179,19 @@ __global__ __launch_bounds__(NTHR, 2) void conv_kernel(Args p) {
   }
 
   // ---- epilogue: acc + bias -> bf16 LDS image -> (+R) -> ReLU -> 16-byte stores ------
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // The residual rows this thread will add are loaded first (all of them, into the
+  // registers the accumulators free up), so their latency overlaps the LDS staging.
+  constexpr int CPR = BN / 8, RPP = NTHR / CPR, NIT = BM / RPP;
+  const int cc = tid % CPR, rr0 = tid / CPR;
+  bf16x8 rv[RES ? NIT : 1];
+  if constexpr (RES) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m0 + rr0 + it * RPP;
+      if (m < p.M) rv[it] = *reinterpret_cast<const bf16x8*>(p.R + (size_t)m * p.Cout + n0 + cc * 8);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -198,26 +210,23 @@ __global__ __launch_bounds__(NTHR, 2) void conv_kernel(Args p) {
     }
   }
   __syncthreads();
-  constexpr int CPR = BN / 8, RPP = NTHR / CPR;
-  const int cc = tid % CPR, rr0 = tid / CPR;
-#pragma unroll 4
-  for (int row = rr0; row < BM; row += RPP) {
-    const int m = m0 + row;
-    if (m >= p.M) break;
-    bf16x8 v = *(lds_cbf16x8*)(smem + row * ROWB + cc * 16);
-    const size_t off = (size_t)m * p.Cout + n0 + cc * 8;
-    if constexpr (RES || RELU) {
-      bf16x8 rv;
-      if constexpr (RES) rv = *reinterpret_cast<const bf16x8*>(p.R + off);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float f = (float)v[e];
-        if constexpr (RES) f += (float)rv[e];
-        if constexpr (RELU) f = fmaxf(f, 0.f);
-        v[e] = (bf16)f;
+  for (int it = 0; it < NIT; ++it) {
+    const int row = rr0 + it * RPP;
+    const int m = m0 + row;
+    if (m < p.M) {
+      bf16x8 v = *(lds_cbf16x8*)(smem + row * ROWB + cc * 16);
+      if constexpr (RES || RELU) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float f = (float)v[e];
+          if constexpr (RES) f += (float)rv[it][e];
+          if constexpr (RELU) f = fmaxf(f, 0.f);
+          v[e] = (bf16)f;
+        }
       }
+      *reinterpret_cast<bf16x8*>(p.Y + (size_t)m * p.Cout + n0 + cc * 8) = v;
     }
-    *reinterpret_cast<bf16x8*>(p.Y + off) = v;
   }
 }
 

@@ -18,6 +18,8 @@ def family(name: str) -> str:
                      ("ln_bwd", "LayerNorm bwd (ours)"), ("colsum", "column reduce (ours)"),
                      ("bias_gelu", "bias+GELU (ours)"), ("xent", "cross-entropy (ours)"),
                      ("adamw", "fused AdamW (ours)"), ("sumsq", "grad-norm (ours)"),
+                     ("conv_kernel", "conv MFMA (ours)"), ("maxpool3s2", "vision (ours)"),
+                     ("normalize_pad8", "vision (ours)"), ("igemm_fwd", "conv (MIOpen)"), ("bias_act", "bias/act (ours)"),
                      ("nccl", "RCCL"), ("rccl", "RCCL"), ("reduce_kernel", "torch reduce"),
                      ("elementwise", "torch elementwise"), ("Cat", "torch cat"),
                      ("copyBuffer", "memcpy"), ("fillBuffer", "memset")]:
