@@ -7,6 +7,7 @@ from .schedulers import (PB2, AsyncHyperBandScheduler, ASHAScheduler, Distribute
                          HyperBandForBOHB, HyperBandScheduler, MedianStoppingRule, PopulationBasedTraining,
                          ResourceChangingScheduler, TrialScheduler)
 from .search.bohb import TuneBOHB
+from .search.model_based import BayesOptSearch, HyperOptSearch, OptunaSearch
 from .search import (BasicVariantGenerator, ConcurrencyLimiter, RandomLocalSearch, Repeater, Searcher,
                      choice, grid_search, lograndint, loguniform, qlograndint, qloguniform, qrandint, qrandn,
                      quniform, randint, randn, sample_from, uniform)

@@ -89,9 +89,11 @@ def create_searcher(search_alg: str, **kwargs):
     from . import search as S
 
     from .search.bohb import TuneBOHB
+    from .search.model_based import BayesOptSearch, HyperOptSearch, OptunaSearch
 
     table = {"variant_generator": S.BasicVariantGenerator, "random": S.BasicVariantGenerator,
-             "random_local": S.RandomLocalSearch, "bohb": TuneBOHB}
+             "random_local": S.RandomLocalSearch, "bohb": TuneBOHB, "optuna": OptunaSearch,
+             "hyperopt": HyperOptSearch, "bayesopt": BayesOptSearch}
     if search_alg not in table:
         raise ValueError(f"unknown searcher {search_alg!r}; available here: {sorted(table)} "
                          "(external optimisation libraries are not installed in this image)")
