@@ -17,7 +17,11 @@ class ScalingConfig:
     accelerator_type: Optional[str] = None
 
     def __post_init__(self):
-        if self.num_workers is not None and self.num_workers < 1:
+        nw = self.num_workers
+        if isinstance(nw, (tuple, list)):  # elastic (min, max): the v2 controller's ElasticScalingPolicy
+            if len(nw) != 2 or not 1 <= int(nw[0]) <= int(nw[1]):
+                raise ValueError("elastic num_workers must be (min, max) with 1 <= min <= max")
+        elif nw is not None and nw < 1:
             raise ValueError("num_workers must be >= 1")
         if self.resources_per_worker:
             if "GPU" in self.resources_per_worker and not self.use_gpu and self.resources_per_worker["GPU"] > 0:
@@ -25,7 +29,10 @@ class ScalingConfig:
 
     @property
     def total_workers(self) -> int:
-        return self.num_workers or 1
+        nw = self.num_workers
+        if isinstance(nw, (tuple, list)):
+            return int(nw[1])
+        return nw or 1
 
     @property
     def _resources_per_worker_not_none(self) -> Dict[str, float]:

@@ -257,6 +257,11 @@ class DataParallelTrainer:
     def fit(self) -> Result:
         if self._spmd_env():
             return self._fit_spmd()
+        if os.environ.get("RAY_TRAIN_V2_ENABLED", "0") == "1" or isinstance(self.scaling_config.num_workers,
+                                                                            (tuple, list)):
+            from .v2 import TrainController
+
+            return TrainController(self).run()
         core._ensure_init()
         run_dir = self._run_dir()
         fc: FailureConfig = self.run_config.failure_config
@@ -328,107 +333,154 @@ class DataParallelTrainer:
         return kept
 
     def _run_attempt(self, run_dir, ckpt, ckpt_index):
+        wg = _WorkerGroup(self, run_dir, ckpt, ckpt_index)
+        try:
+            wg.start()
+            while True:
+                finished, err = wg.poll()
+                if err is not None:
+                    raise _AttemptFailed(err, wg.history, wg.ckpts, wg.ckpt_index)
+                if finished:
+                    break
+            wg.finish()
+            return wg.history, wg.ckpts, wg.ckpt_index
+        except _AttemptFailed:
+            raise
+        except Exception as e:
+            from ..exceptions import RayActorError
+
+            if isinstance(e, RayActorError):
+                raise _AttemptFailed(e, wg.history, wg.ckpts, wg.ckpt_index)
+            raise
+        finally:
+            wg.shutdown()
+
+
+class _WorkerGroup:
+    """One run attempt's worker group: placement group + one ``_TrainWorker`` actor
+    per bundle, backend setup, the training function started on every rank, and a
+    non-blocking ``poll()`` that streams reports / checkpoints back (used by the
+    v1 ``fit()`` loop and by the v2 ``TrainController`` state machine)."""
+
+    def __init__(self, trainer: "DataParallelTrainer", run_dir: str, ckpt, ckpt_index: int,
+                 num_workers: Optional[int] = None):
+        self.trainer = trainer
+        self.run_dir, self.ckpt, self.ckpt_index = run_dir, ckpt, ckpt_index
+        self.n = num_workers or trainer.scaling_config.total_workers
+        self.workers: List[Any] = []
+        self.pg = None
+        self.history: List[dict] = []
+        self.ckpts: List[tuple] = []
+        self.done: List[bool] = []
+        self.started_at = None
+
+    def start(self):
         from ..core.actor import ActorClass
-        from ..exceptions import RayActorError
         from ..util.placement_group import placement_group, remove_placement_group
         from ..util.scheduling_strategies import PlacementGroupSchedulingStrategy
 
-        sc = self.scaling_config
-        n = sc.total_workers
-        bundles = sc.as_placement_group_bundles()
-        pg = placement_group(bundles, strategy=sc.placement_strategy)
+        sc = self.trainer.scaling_config
+        n = self.n
+        res = sc._resources_per_worker_not_none
+        bundles = [dict(res) for _ in range(n)]
+        self.pg = pg = placement_group(bundles, strategy=sc.placement_strategy)
         ready, _ = core.wait([pg.ready()], timeout=float(os.environ.get("CAAMD_TRAIN_PG_TIMEOUT", "600")))
         if not ready:
             remove_placement_group(pg)
+            self.pg = None
             raise RuntimeError(f"could not reserve {n} training workers with {bundles[0]} each "
                                f"(cluster: {core.available_resources()})")
-        res = sc._resources_per_worker_not_none
         Worker = ActorClass(_TrainWorker, {})
-        workers = []
         for i in range(n):
             opts = dict(num_cpus=res.get("CPU", 1), num_gpus=res.get("GPU", 0),
                         resources={k: v for k, v in res.items() if k not in ("CPU", "GPU")},
                         scheduling_strategy=PlacementGroupSchedulingStrategy(pg, i),
                         runtime_env={"env_vars": {"CAAMD_NOSET_ROCR_VISIBLE_DEVICES": "1",
                                                   "HSA_ENABLE_IPC_MODE_LEGACY": "0"}})
-            workers.append(Worker.options(**opts).remote())
-        history, ckpts = [], []
-        try:
-            infos = core.get([w.node_info.remote() for w in workers], timeout=600)
-            # ranks: group workers by node (node_rank order of first appearance)
-            nodes = []
-            for inf in infos:
-                if inf["node_id"] not in nodes:
-                    nodes.append(inf["node_id"])
-            local_counts = {nd: 0 for nd in nodes}
-            local_world = {nd: sum(1 for x in infos if x["node_id"] == nd) for nd in nodes}
-            master = infos[0]
-            setups = []
-            ranks = []
-            for rank, (w, inf) in enumerate(zip(workers, infos)):
-                nd = inf["node_id"]
-                lr = local_counts[nd]
-                local_counts[nd] += 1
-                dev = inf["gpu_ids"][0] if inf["gpu_ids"] else None
-                ranks.append((rank, lr, local_world[nd], nodes.index(nd)))
-                setups.append(w.setup.remote(self.backend, rank, n, lr, local_world[nd], nodes.index(nd),
-                                             master["addr"], master["port"], dev))
-            core.get(setups, timeout=900)
-            shards = self._split_datasets(n)
-            runs = []
-            for (rank, lr, lw, nr), w in zip(ranks, workers):
-                ctx = dict(world_size=n, world_rank=rank, local_rank=lr, local_world_size=lw,
-                           node_rank=nr, experiment_name=self.run_config.name,
-                           trial_name=self.run_config.name, trial_id=uuid.uuid4().hex[:8],
-                           storage_path=self.run_config.storage_path, metadata=self.metadata,
-                           trial_dir=run_dir)
-                runs.append(w.run.remote(self.train_loop_per_worker, self.train_loop_config,
-                                         ckpt.path if ckpt else None, shards[rank], ctx, run_dir,
-                                         ckpt_index))
-            core.get(runs, timeout=600)
-            done = [False] * n
-            callbacks = self.run_config.callbacks or []
-            while not all(done):
-                polls = core.get([w.poll.remote(0.5) for w in workers])
-                err = None
-                round_reports = {}
-                for i, (reports, d, e) in enumerate(polls):
-                    done[i] = d
-                    if e is not None and err is None:
-                        err = e
-                    for (rank, m, p) in reports:
-                        round_reports.setdefault(rank, []).append((m, p))
-                # rank 0 metrics define the result; a checkpoint reported by any rank counts
-                all_paths = {}
-                for rank, items in round_reports.items():
-                    for k, (m, p) in enumerate(items):
-                        if p:
-                            all_paths.setdefault(k, p)
-                for k, (m, p) in enumerate(round_reports.get(0, [])):
-                    path = p or all_paths.get(k)
-                    history.append(m)
-                    if path:
-                        ckpts.append((m, path))
-                        ckpt_index += 1
-                    for cb in callbacks:
-                        if hasattr(cb, "on_report_with_checkpoint"):
-                            cb.on_report_with_checkpoint(m, path)
-                        elif hasattr(cb, "on_report"):
-                            cb.on_report(m)
-                if err is not None:
-                    raise _AttemptFailed(err, history, ckpts, ckpt_index)
-            core.get([w.shutdown.remote() for w in workers], timeout=60)
-            return history, ckpts, ckpt_index
-        except RayActorError as e:
-            raise _AttemptFailed(e, history, ckpts, ckpt_index)
-        finally:
-            for w in workers:
-                try:
-                    core.kill(w)
-                except Exception:
-                    pass
-            remove_placement_group(pg)
-            time.sleep(0.05)
+            self.workers.append(Worker.options(**opts).remote())
+        workers, tr = self.workers, self.trainer
+        infos = core.get([w.node_info.remote() for w in workers], timeout=600)
+        # ranks: group workers by node (node_rank order of first appearance)
+        nodes = []
+        for inf in infos:
+            if inf["node_id"] not in nodes:
+                nodes.append(inf["node_id"])
+        local_counts = {nd: 0 for nd in nodes}
+        local_world = {nd: sum(1 for x in infos if x["node_id"] == nd) for nd in nodes}
+        master = infos[0]
+        setups = []
+        ranks = []
+        for rank, (w, inf) in enumerate(zip(workers, infos)):
+            nd = inf["node_id"]
+            lr = local_counts[nd]
+            local_counts[nd] += 1
+            dev = inf["gpu_ids"][0] if inf["gpu_ids"] else None
+            ranks.append((rank, lr, local_world[nd], nodes.index(nd)))
+            setups.append(w.setup.remote(tr.backend, rank, n, lr, local_world[nd], nodes.index(nd),
+                                         master["addr"], master["port"], dev))
+        core.get(setups, timeout=900)
+        shards = tr._split_datasets(n)
+        runs = []
+        for (rank, lr, lw, nr), w in zip(ranks, workers):
+            ctx = dict(world_size=n, world_rank=rank, local_rank=lr, local_world_size=lw,
+                       node_rank=nr, experiment_name=tr.run_config.name,
+                       trial_name=tr.run_config.name, trial_id=uuid.uuid4().hex[:8],
+                       storage_path=tr.run_config.storage_path, metadata=tr.metadata,
+                       trial_dir=self.run_dir)
+            runs.append(w.run.remote(tr.train_loop_per_worker, tr.train_loop_config,
+                                     self.ckpt.path if self.ckpt else None, shards[rank], ctx, self.run_dir,
+                                     self.ckpt_index))
+        core.get(runs, timeout=600)
+        self.done = [False] * n
+        self.started_at = time.time()
+
+    def poll(self, timeout: float = 0.5):
+        """One poll round over every rank: (all finished, first error or None)."""
+        polls = core.get([w.poll.remote(timeout) for w in self.workers])
+        err = None
+        round_reports = {}
+        for i, (reports, d, e) in enumerate(polls):
+            self.done[i] = d
+            if e is not None and err is None:
+                err = e
+            for (rank, m, p) in reports:
+                round_reports.setdefault(rank, []).append((m, p))
+        # rank 0 metrics define the result; a checkpoint reported by any rank counts
+        all_paths = {}
+        for rank, items in round_reports.items():
+            for k, (m, p) in enumerate(items):
+                if p:
+                    all_paths.setdefault(k, p)
+        callbacks = self.trainer.run_config.callbacks or []
+        for k, (m, p) in enumerate(round_reports.get(0, [])):
+            path = p or all_paths.get(k)
+            self.history.append(m)
+            if path:
+                self.ckpts.append((m, path))
+                self.ckpt_index += 1
+            for cb in callbacks:
+                if hasattr(cb, "on_report_with_checkpoint"):
+                    cb.on_report_with_checkpoint(m, path)
+                elif hasattr(cb, "on_report"):
+                    cb.on_report(m)
+        return all(self.done), err
+
+    def finish(self):
+        core.get([w.shutdown.remote() for w in self.workers], timeout=60)
+
+    def shutdown(self):
+        from ..util.placement_group import remove_placement_group
+
+        for w in self.workers:
+            try:
+                core.kill(w)
+            except Exception:
+                pass
+        self.workers = []
+        if self.pg is not None:
+            remove_placement_group(self.pg)
+            self.pg = None
+        time.sleep(0.05)
 
 
 class _AttemptFailed(Exception):

@@ -251,8 +251,15 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
     }
     __syncthreads();
     if (!*flag) return;
+    // sum every split (own included, re-read from its slab) in split order, so the
+    // result does not depend on which split arrived last (bitwise reproducible)
+    if (consumer) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mt][e] = 0.f;
+    }
     for (int s = 0; s < p.splits && consumer; ++s) {
-      if (s == split) continue;
       const float* other = base + (size_t)s * (BN * 128);
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)

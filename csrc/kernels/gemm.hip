@@ -801,8 +801,12 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
       __syncthreads();
       const int last = *flag;
       if (!last) return;
+      // all slices (own included, re-read) in slice order: reproducible sums
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int s = 0; s < p.tS; ++s) {
-        if (s == slice) continue;
         const float* other = p.tws + ((size_t)tt * p.tS + s) * SLAB;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -1143,8 +1147,12 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
       __syncthreads();
       const int last = *flag;
       if (!last) continue;
+      // every contributor (own included, re-read) in run order: reproducible sums
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int gg = c0; gg <= c1; ++gg) {
-        if (gg == g) continue;
         const float* other = p.tws + (size_t)slot_of(gg) * SLAB;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
