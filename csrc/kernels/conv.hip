@@ -31,6 +31,8 @@
 //    ids with n fastest, so the n-tiles of one gathered A panel share an L2.
 #include "common.h"
 
+#include <algorithm>
+
 namespace caamd {
 namespace conv {
 
@@ -233,37 +235,35 @@ __global__ __launch_bounds__(NTHR, 2) void conv_kernel(Args p) {
 // ---- stem input: uint8 NHWC (C = 3) -> bf16 NHWC padded to 8 channels -------------
 // (x / 255 - mean) / std on the 3 real channels, zeros in 3..7, one 16-byte store
 // per pixel: the layout the implicit-GEMM gather takes (16-byte chunk = one tap).
+// A block takes 4,096 pixels: 12 KB of input in by 16-byte loads into LDS, then
+// thread t converts pixels t, t + 256, ... so a wave's stores are 1 KB contiguous.
+constexpr int NP_PIX = 4096;
 __global__ __launch_bounds__(256) void normalize_pad8_kernel(const uint8_t* __restrict__ in, bf16* __restrict__ out,
                                                              int64_t npix, float s0, float s1, float s2, float b0,
                                                              float b1, float b2) {
-  for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q * 16 < npix;
-       q += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t p0 = q * 16;
-    if (p0 + 16 <= npix) {
-      const uint4* src = reinterpret_cast<const uint4*>(in + p0 * 3);  // 48 bytes, 16-B aligned
-      uint4 raw[3] = {src[0], src[1], src[2]};
-      const uint8_t* b = reinterpret_cast<const uint8_t*>(raw);
+  __shared__ __attribute__((aligned(16))) uint8_t buf[NP_PIX * 3];
+  const int t = threadIdx.x;
+  for (int64_t p0 = (int64_t)blockIdx.x * NP_PIX; p0 < npix; p0 += (int64_t)gridDim.x * NP_PIX) {
+    const int n = (int)min((int64_t)NP_PIX, npix - p0);
+    const uint8_t* src = in + p0 * 3;
+    if (n == NP_PIX) {
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        bf16x8 o;
-        o[0] = (bf16)__builtin_fmaf((float)b[3 * i], s0, b0);
-        o[1] = (bf16)__builtin_fmaf((float)b[3 * i + 1], s1, b1);
-        o[2] = (bf16)__builtin_fmaf((float)b[3 * i + 2], s2, b2);
-#pragma unroll
-        for (int e = 3; e < 8; ++e) o[e] = (bf16)0.f;
-        reinterpret_cast<bf16x8*>(out)[p0 + i] = o;
-      }
+      for (int j = 0; j < 3; ++j)
+        reinterpret_cast<uint4*>(buf)[j * 256 + t] = reinterpret_cast<const uint4*>(src)[j * 256 + t];
     } else {
-      for (int64_t px = p0; px < npix; ++px) {
-        bf16x8 o;
-        o[0] = (bf16)__builtin_fmaf((float)in[px * 3], s0, b0);
-        o[1] = (bf16)__builtin_fmaf((float)in[px * 3 + 1], s1, b1);
-        o[2] = (bf16)__builtin_fmaf((float)in[px * 3 + 2], s2, b2);
-#pragma unroll
-        for (int e = 3; e < 8; ++e) o[e] = (bf16)0.f;
-        reinterpret_cast<bf16x8*>(out)[px] = o;
-      }
+      for (int i = t; i < n * 3; i += 256) buf[i] = src[i];
     }
+    __syncthreads();
+    for (int i = t; i < n; i += 256) {
+      bf16x8 o;
+      o[0] = (bf16)__builtin_fmaf((float)buf[3 * i], s0, b0);
+      o[1] = (bf16)__builtin_fmaf((float)buf[3 * i + 1], s1, b1);
+      o[2] = (bf16)__builtin_fmaf((float)buf[3 * i + 2], s2, b2);
+#pragma unroll
+      for (int e = 3; e < 8; ++e) o[e] = (bf16)0.f;
+      reinterpret_cast<bf16x8*>(out)[p0 + i] = o;
+    }
+    __syncthreads();
   }
 }
 
@@ -349,8 +349,9 @@ hipError_t conv2d_launch(const bf16* X, const bf16* Wt, const bf16* bias, const 
 
 void normalize_pad8_launch(const uint8_t* in, bf16* out, int64_t npix, const float* sc, const float* bi,
                            hipStream_t st) {
-  const int64_t items = (npix + 15) / 16;
-  hipLaunchKernelGGL(conv::normalize_pad8_kernel, dim3(ew_grid(items, 256)), dim3(256), 0, st, in, out, npix, sc[0],
+  const int64_t blocks = (npix + conv::NP_PIX - 1) / conv::NP_PIX;
+  hipLaunchKernelGGL(conv::normalize_pad8_kernel, dim3((unsigned)std::min<int64_t>(blocks, 2048)), dim3(256), 0, st, in,
+                     out, npix, sc[0],
                      sc[1], sc[2], bi[0], bi[1], bi[2]);
 }
 

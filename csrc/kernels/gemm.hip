@@ -952,6 +952,259 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persist_kernel(Args p) {
 
 
 // ================================================================================
+// Persistent ping-pong kernel with an ASYNCHRONOUS staged epilogue (algo 8; NT
+// layout, 256 x 320 tiles, bf16 (+bias) and bias+GELU epilogues). One 512-thread
+// workgroup per CU walks its XCD's contiguous tile range; the 4-stage LDS ring of
+// 32-deep K-steps runs continuously across tiles (the next tile's first two steps
+// are in flight while a tile's last steps compute), with the R / M segments,
+// counted vmcnt and wave-row stagger of gemm_pp_kernel (one phase per step).
+//
+// What the non-persistent kernels cannot hide (profiles/gemm_ablations_r3.jsonl:
+// "no epilogue stores" 486 vs 622 us at 32768 x 6400 x 1600): every CU stores its
+// 164-328 KB tile in the same chip-wide burst and only then starts the next tile.
+// Here the tile is staged through LDS (into the two ring slots of the tile's last
+// two K-steps plus the 16 KB of LDS past the ring, which are free at that point)
+// and streamed out with coalesced 16-byte stores, and the wave goes straight on to
+// the next tile: the stores are YOUNGER than the next tile's first two DMA steps,
+// so the first K-step's wait leaves them in flight (vmcnt(NS + CNT)), and they only
+// have to have drained one K-step later, when the next DMA step is retired.
+// Every wave issues exactly NS = 20 (bf16) / 40 (GELU: z and u) store instructions
+// per tile (10 / 20 per m-half: 128 rows x 40 chunks over 512 threads), so the
+// counted wait is exact. The staging image is accessed with inline-asm ds_read /
+// ds_write (the compiler would otherwise drain the in-flight LDS-DMA before them).
+// ================================================================================
+__device__ __forceinline__ void lds_write_b64(unsigned addr, bf16x4 v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+__device__ __forceinline__ bf16x8_t lds_read_b128(unsigned addr) {
+  bf16x8_t v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+// workgroup barrier for LDS hand-offs only: unlike __syncthreads() (whose
+// workgroup-scope fence waits vmcnt(0)) it leaves global stores and LDS-DMA in flight
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NTHR, 2) void gemm_pst_kernel(Args p) {
+  constexpr int BM = 256, BN = 320, WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16, TMH = TM / 2;
+  constexpr int KS = 32, NST = 4, DIST = 2;
+  constexpr int A_ST = BM * KS * 2, B_ST = BN * KS * 2, ST = A_ST + B_ST;
+  constexpr int ROWB = BN * 2 + 16;          // staging image row (bytes)
+  constexpr int RPS = ST / ROWB;             // image rows per ring slot (56)
+  constexpr int SPARE = NST * ST;            // 16 KB past the ring
+  constexpr int HR = BM / 2, CPR = BN / 8;   // 128 image rows x 40 chunks per m-half
+  constexpr int ITS = HR * CPR / NTHR;       // 10 chunks per thread per half
+  static_assert(HR * CPR == ITS * NTHR, "uniform store count per wave");
+  static_assert(2 * RPS + (160 * 1024 - SPARE) / ROWB >= HR, "staging image must fit");
+  constexpr int NS = (EPI == EPI_BIAS_GELU ? 4 : 2) * ITS;  // store instructions per tile per wave
+  constexpr int BIAS_OFF = SPARE + 12288;    // 640 B bias row, past the staging rows
+  static_assert(BIAS_OFF - SPARE >= (HR - 2 * RPS) * ROWB && BIAS_OFF + BN * 2 <= 160 * 1024, "bias slot");
+  constexpr int HB = 5;                      // output chunks per batch
+  static_assert(EPI == EPI_BF16 || EPI == EPI_BIAS_GELU, "pst: bf16 / bias+GELU epilogues");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const bool lo_grp = wr == 0;
+
+  const int T = p.tiles_m * p.tiles_n;
+  const int bid = blockIdx.x, G = gridDim.x;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q8 = T >> 3, r8 = T & 7;
+  const int start = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int size = q8 + (xcd < r8 ? 1 : 0);
+  const int nbx = (G >> 3) + (xcd < (G & 7) ? 1 : 0);
+  const int my_tiles = loc < size ? (size - loc + nbx - 1) / nbx : 0;
+  constexpr int GROUP_M = 8;
+  auto tile_origin = [&](int i, int& m0, int& n0) {
+    const int tile = start + loc + i * nbx;
+    const int group_sz = GROUP_M * p.tiles_n;
+    const int g = tile / group_sz;
+    const int first_m = g * GROUP_M;
+    const int gm = min(p.tiles_m - first_m, GROUP_M);
+    const int tin = tile - g * group_sz;
+    m0 = (first_m + tin % gm) * BM;
+    n0 = (tin / gm) * BN;
+  };
+  const int nk = p.K / KS;
+  const int total = my_tiles * nk;
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // DMA cursor (wave-uniform, kept in SGPRs): tile / k-step / origin of the next step
+  // to load, advanced one step per dma() call
+  int d_ti = 0, d_ks = 0, d_m0 = 0, d_n0 = 0;
+  if (my_tiles > 0) tile_origin(0, d_m0, d_n0);
+  auto dma = [&](int gs) {
+    lds_char* base = smem + (gs & (NST - 1)) * ST;
+    const int m0 = __builtin_amdgcn_readfirstlane(d_m0), n0 = __builtin_amdgcn_readfirstlane(d_n0);
+    const int k0 = __builtin_amdgcn_readfirstlane(d_ks * KS);
+    dma_step32<BM, true>(p.A, p.lda, m0, k0, base, wid, lane);
+    dma_step32<BN, true>(p.B, p.ldb, n0, k0, base + A_ST, wid, lane);
+    if (++d_ks == nk) {
+      d_ks = 0;
+      if (++d_ti < my_tiles) tile_origin(d_ti, d_m0, d_n0);
+    }
+  };
+  constexpr int CNT_LO = dma_count32<BM>(0) + dma_count32<BN>(0);
+  constexpr int CNT_HI = dma_count32<BM>(4) + dma_count32<BN>(4);
+  static_assert(dma_count32<BM>(3) == dma_count32<BM>(0) && dma_count32<BN>(3) == dma_count32<BN>(0), "");
+  static_assert(dma_count32<BM>(7) == dma_count32<BM>(4) && dma_count32<BN>(7) == dma_count32<BN>(4), "");
+  // retire DMA step gs+1: `newer` DMA steps and (first step of a tile) the previous
+  // tile's NS stores are younger and stay in flight
+  auto wait_ahead = [&](int newer, bool stores) {
+    if (stores) {
+      if (newer >= 1) { if (lo_grp) wait_vm<NS + CNT_LO>(); else wait_vm<NS + CNT_HI>(); }
+      else wait_vm<NS>();
+    } else if (newer >= 1) {
+      if (lo_grp) wait_vm<CNT_LO>(); else wait_vm<CNT_HI>();
+    } else {
+      wait_vm<0>();
+    }
+  };
+
+  if (total > 0) {
+    dma(0);
+    if (total > 1) dma(1);
+    wait_ahead(min(total, DIST) - 1, false);
+    __builtin_amdgcn_s_barrier();
+    if (!lo_grp) __builtin_amdgcn_s_barrier();
+    int ti = 0, ks = 0;
+    int c_m0, c_n0;  // origin of the tile being computed
+    tile_origin(0, c_m0, c_n0);
+    bf16x8_t bf[TN];
+    bf16x8_t af[TM];
+    for (int gs = 0; gs < total; ++gs) {
+      const lds_char* As = smem + (gs & (NST - 1)) * ST;
+      const lds_char* Bs = As + A_ST;
+      // ---- R segment
+      if (gs + DIST < total) dma(gs + DIST);
+      if (ks == 0 && p.bias && wid == 0 && lane < CPR) {
+        // this tile's bias row -> LDS (landed by the end of step ks = 1's wait; the
+        // epilogue reads it); one extra, older-than-counted op for wave 0: its
+        // counted waits then over-wait by one piece, never under-wait
+        __builtin_amdgcn_global_load_lds((const void*)(p.bias + c_n0 + lane * 8),
+                                         (void __attribute__((address_space(3)))*)(smem + BIAS_OFF), 16, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = frag_kmaj64(Bs, wc * (TN * 16) + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = frag_kmaj64(As, wr * (TM * 16) + i * 16, lane);
+      wait_ahead(min(total - 1, gs + DIST) - (gs + 1), ks == 0 && ti > 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (++ks < nk) continue;
+
+      // ---- tile done: staged epilogue into the free ring slots of steps gs-1, gs
+      if (lo_grp) __builtin_amdgcn_s_barrier();  // row 1 finishes its M(gs): rows aligned
+      const int m0 = c_m0, n0 = c_n0;
+      const unsigned sbase = (unsigned)(size_t)smem;
+      const unsigned slotA = sbase + (unsigned)(((gs + NST - 1) & (NST - 1)) * ST);
+      const unsigned slotB = sbase + (unsigned)((gs & (NST - 1)) * ST);
+      auto row_addr = [&](int r) -> unsigned {
+        return r < RPS ? slotA + r * ROWB : r < 2 * RPS ? slotB + (r - RPS) * ROWB
+                                                        : sbase + SPARE + (r - 2 * RPS) * ROWB;
+      };
+      const bool has_bias = p.bias != nullptr;
+      // opaque copies of the lane ids: keeps the compiler from hoisting the
+      // epilogue's per-lane address math out of the K loop (it would hold ~40
+      // VGPRs across the main loop and spill)
+      int tid_e, lane_e;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(tid_e) : "v"(tid));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(lane_e) : "v"(lane));
+      const int mrow = lane_e & 15, ncol = 4 * (lane_e >> 4);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h) lds_barrier();  // image reads of half 0 done
+#pragma unroll
+        for (int i = 0; i < TMH; ++i) {
+          const int ir = wr * (TMH * 16) + i * 16 + mrow;
+          const unsigned ra = row_addr(ir);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int nc = wc * (TN * 16) + j * 16 + ncol;
+            bf16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[h * TMH + i][j][r];
+            lds_write_b64(ra + nc * 2, o);
+          }
+        }
+        lds_barrier();
+        static_assert(ITS % HB == 0, "batches");
+#pragma unroll
+        for (int b = 0; b < ITS / HB; ++b) {
+          bf16x8_t v[HB], bb[HB];
+#pragma unroll
+          for (int u = 0; u < HB; ++u) {
+            const int qq = (b * HB + u) * NTHR + tid_e, ir = qq / CPR, c = qq - (qq / CPR) * CPR;
+            v[u] = lds_read_b128(row_addr(ir) + c * 16);
+            bb[u] = lds_read_b128(sbase + BIAS_OFF + c * 16);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int u = 0; u < HB; ++u) {
+            const int qq = (b * HB + u) * NTHR + tid_e, ir = qq / CPR, c = qq - (qq / CPR) * CPR;
+            const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
+            const int m = m0 + wr_ * (TM * 16) + h * (TMH * 16) + rem;
+            const size_t off = (size_t)m * p.ldc + n0 + c * 8;
+            bf16x8_t o;
+            if constexpr (EPI == EPI_BIAS_GELU) {
+              bf16x8_t z;
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                z[r] = (bf16)((float)v[u][r] + (has_bias ? (float)bb[u][r] : 0.f));
+                o[r] = (bf16)gelu_tanh((float)z[r]);
+              }
+              *reinterpret_cast<bf16x8_t*>(p.Zout + off) = z;
+            } else {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) o[r] = (bf16)((float)v[u][r] + (has_bias ? (float)bb[u][r] : 0.f));
+            }
+            *reinterpret_cast<bf16x8_t*>((bf16*)p.C + off) = o;
+          }
+        }
+      }
+      lds_barrier();  // staging reads done before step gs+1's R issues DMA into slot A
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ks = 0;
+      if (++ti < my_tiles) tile_origin(ti, c_m0, c_n0);
+      if (!lo_grp && ti < my_tiles) __builtin_amdgcn_s_barrier();  // re-stagger the second wave row
+    }
+  }
+}
+
+// ================================================================================
 // Stream-K ping-pong kernel (weight gradients: K = tokens = 32768, only 95-280
 // output tiles of 256 x 320 for 256 CUs). Grid = the CUs (one 147 KB workgroup
 // each); the tiles x K-steps iteration space is cut into gridDim.x equal runs, so
@@ -1240,6 +1493,17 @@ static hipError_t launch_abl(const Args& a, hipStream_t st) {
       constexpr int lds = 4 * (BM + BN) * 32 * 2;
       ensure_lds((const void*)k, lds);
       hipLaunchKernelGGL(k, dim3(a.tS), dim3(NTHR), lds, st, a);  // tS = number of runs
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
+  if (a.algo == 8 && a.splitk == 1) {
+    if constexpr (BM == 256 && BN == 320 && AK && BK_ && (EPI == EPI_BF16 || EPI == EPI_BIAS_GELU)) {
+      auto k = gemm_pst_kernel<EPI>;
+      constexpr int lds = 160 * 1024;
+      ensure_lds((const void*)k, lds);
+      const int tiles = a.tiles_m * a.tiles_n;
+      hipLaunchKernelGGL(k, dim3(tiles < 256 ? tiles : 256), dim3(NTHR), lds, st, a);
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
