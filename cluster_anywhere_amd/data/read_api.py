@@ -440,13 +440,64 @@ def _unavailable(name: str, lib: str):
     return fn
 
 
-for _n, _lib in (("from_dask", "dask"), ("from_spark", "pyspark"), ("from_modin", "modin"),
-                 ("from_mars", "mars"), ("from_tf", "tensorflow"), ("read_bigquery", "google-cloud-bigquery"),
-                 ("read_mongo", "pymongo"), ("read_lance", "lance"),
-                 ("read_delta_sharing_tables", "delta-sharing"),
-                 ("read_databricks_tables", "databricks-sql-connector"), ("read_clickhouse", "clickhouse-connect"),
-                 ("read_videos", "decord")):
+for _n, _lib in (("read_mongo", "pymongo"), ("read_lance", "lance"), ("read_videos", "decord")):
     globals()[_n] = _unavailable(_n, _lib)
+
+
+# ---- other dataframe / dataset libraries: duck-typed over their public export
+# methods, so a user who has the library gets blocks without this package
+# importing it (reference: read_api.py from_dask :2542, from_modin :2616,
+# from_mars :2591, from_spark :2968, from_tf :3157).
+def from_dask(df) -> Dataset:
+    """One block per Dask partition (``df.to_delayed()`` computed lazily per read task)."""
+    parts = df.to_delayed() if hasattr(df, "to_delayed") else [df]
+
+    def rd(p):
+        out = p.compute() if hasattr(p, "compute") else p
+        return B.from_batch(out)
+
+    return Dataset(("read", [(lambda p=p: rd(p)) for p in parts]))
+
+
+def from_modin(df) -> Dataset:
+    """Modin frame -> pandas partitions (``_to_pandas`` / ``to_pandas``)."""
+    pdf = df._to_pandas() if hasattr(df, "_to_pandas") else df.to_pandas()
+    return from_pandas(pdf)
+
+
+def from_mars(df) -> Dataset:
+    pdf = df.to_pandas() if hasattr(df, "to_pandas") else df.execute().fetch()
+    return from_pandas(pdf)
+
+
+def from_spark(df, *, parallelism: Optional[int] = None, override_num_blocks: Optional[int] = None) -> Dataset:
+    """Spark DataFrame -> Arrow (``toArrow`` on Spark >= 4, else ``toPandas``),
+    split into ``override_num_blocks`` blocks."""
+    t = df.toArrow() if hasattr(df, "toArrow") else df.toPandas()
+    n = len(t)
+    k = max(1, min(n, override_num_blocks or parallelism or 1)) if n else 1
+    if k == 1:
+        return from_blocks([B.from_batch(t)])
+    return from_blocks([B.from_batch(t.slice(s, e - s) if hasattr(t, "slice") else t.iloc[s:e])
+                        for s, e in _chunks(n, k)])
+
+
+def from_tf(dataset) -> Dataset:
+    """A ``tf.data.Dataset`` of dict / tuple / tensor elements, materialised
+    through ``as_numpy_iterator()`` (the reference does the same)."""
+    it = dataset.as_numpy_iterator() if hasattr(dataset, "as_numpy_iterator") else iter(dataset)
+    rows = []
+    for el in it:
+        if isinstance(el, dict):
+            rows.append(dict(el))
+        elif isinstance(el, tuple):
+            rows.append({f"item_{i}" if len(el) > 2 else ("features", "label")[i]: v for i, v in enumerate(el)})
+        else:
+            rows.append({"item": el})
+    return from_items(rows)
+
+# spoken over their HTTP protocols, no client library needed (data/connectors.py)
+from .connectors import read_bigquery, read_clickhouse, read_databricks_tables, read_delta_sharing_tables  # noqa: E402
 
 
 def read_datasource(datasource, *, parallelism: int = -1, **kw) -> Dataset:
