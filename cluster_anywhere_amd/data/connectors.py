@@ -13,6 +13,8 @@ databricks-sql-connector or google-cloud-bigquery is in the image):
   (``POST /api/2.0/sql/statements`` with ``ARROW_STREAM`` + ``EXTERNAL_LINKS``,
   polling while PENDING / RUNNING), one read task per result chunk.
   Reference: datasource/databricks_uc_datasource.py.
+* :func:`read_mongo` - pymongo (in the image; pymongoarrow is not), ``_id``-range
+  partitions, documents -> Arrow. Reference: datasource/mongo_datasource.py.
 * :func:`read_bigquery` - BigQuery REST (``tables.get`` for the schema,
   ``tabledata.list`` pages, or ``jobs.query`` for a query), rows typed from the
   schema. Reference: datasource/bigquery_datasource.py (which uses the storage
@@ -289,4 +291,72 @@ def read_bigquery(project_id: str, dataset: Optional[str] = None, query: Optiona
     return _read_ds([(lambda ld=ld: task(ld)) for ld in loaders])
 
 
-__all__ = ["read_clickhouse", "read_delta_sharing_tables", "read_databricks_tables", "read_bigquery"]
+
+
+# --------------------------------------------------------------------- MongoDB
+def _docs_to_block(docs, schema=None):
+    import pyarrow as pa
+
+    if not docs:
+        return B.from_batch(pa.table({}))
+    cols: Dict[str, list] = {}
+    keys = list(schema) if schema else []
+    for d in docs:
+        for k in d:
+            if k not in cols and (not schema or k in schema):
+                cols[k] = []
+                if not schema:
+                    keys.append(k)
+    out = {}
+    for k in keys:
+        vals = [d.get(k) for d in docs]
+        if vals and all(type(v).__name__ == "ObjectId" or v is None for v in vals):
+            vals = [str(v) if v is not None else None for v in vals]
+        out[k] = vals
+    if schema:
+        return B.from_batch(pa.table({k: pa.array(out[k], type=schema[k]) for k in keys}))
+    return B.from_batch(pa.table(out))
+
+
+def read_mongo(uri: str, database: str, collection: str, *, pipeline: Optional[List[Dict]] = None,
+               schema: Optional[Dict[str, Any]] = None, parallelism: int = -1, ray_remote_args=None,
+               concurrency: Optional[int] = None, override_num_blocks: Optional[int] = None,
+               **mongo_args) -> Dataset:
+    """Reads ``collection`` (through ``pipeline`` when given) with pymongo. The
+    collection is cut into ``_id`` ranges (boundaries from a sorted ``_id``
+    projection sampled every N documents) and each read task runs
+    ``[{$match: {_id: range}}] + pipeline``; ObjectIds become strings. ``schema``:
+    optional ``{column: pyarrow type}`` (pymongoarrow is not in the image)."""
+    import pymongo
+
+    pipeline = list(pipeline or [])
+
+    def client():
+        return pymongo.MongoClient(uri, **mongo_args)
+
+    with client() as c:
+        coll = c[database][collection]
+        n = coll.estimated_document_count()
+        k = max(1, min(n, override_num_blocks or (parallelism if parallelism > 0 else max(1, math.ceil(n / 100_000)))))
+        bounds = []
+        if k > 1:
+            step = max(1, n // k)
+            ids = [d["_id"] for d in coll.find({}, {"_id": 1}).sort("_id", 1)]
+            bounds = [ids[i] for i in range(step, len(ids), step)][: k - 1]
+    edges = [None] + bounds + [None]
+
+    def task(lo, hi):
+        m: Dict[str, Any] = {}
+        if lo is not None:
+            m["$gte"] = lo
+        if hi is not None:
+            m["$lt"] = hi
+        stages = ([{"$match": {"_id": m}}] if m else []) + [{"$sort": {"_id": 1}}] + pipeline
+        with client() as c:
+            docs = list(c[database][collection].aggregate(stages))
+        return _docs_to_block(docs, schema)
+
+    return _read_ds([(lambda lo=lo, hi=hi: task(lo, hi)) for lo, hi in zip(edges[:-1], edges[1:])])
+
+
+__all__ = ["read_clickhouse", "read_delta_sharing_tables", "read_databricks_tables", "read_bigquery", "read_mongo"]

@@ -440,7 +440,7 @@ def _unavailable(name: str, lib: str):
     return fn
 
 
-for _n, _lib in (("read_mongo", "pymongo"), ("read_lance", "lance"), ("read_videos", "decord")):
+for _n, _lib in (("read_lance", "lance"), ("read_videos", "decord")):
     globals()[_n] = _unavailable(_n, _lib)
 
 
@@ -497,7 +497,8 @@ def from_tf(dataset) -> Dataset:
     return from_items(rows)
 
 # spoken over their HTTP protocols, no client library needed (data/connectors.py)
-from .connectors import read_bigquery, read_clickhouse, read_databricks_tables, read_delta_sharing_tables  # noqa: E402
+from .connectors import (read_bigquery, read_clickhouse, read_databricks_tables,  # noqa: E402
+                         read_delta_sharing_tables, read_mongo)
 
 
 def read_datasource(datasource, *, parallelism: int = -1, **kw) -> Dataset:

@@ -219,3 +219,119 @@ def test_from_other_frameworks_duck_typed(server):
     sp = data.from_spark(SparkLike(), override_num_blocks=3)
     assert [r["b"] for r in sp.take_all()] == list("abcdef")
     assert [float(r["x"]) for r in data.from_tf(TfLike()).take_all()] == [0.0, 1.0, 2.0, 3.0]
+
+
+# ---- MongoDB: a minimal OP_MSG server (hello / ping / count / find / aggregate) ----
+class _MiniMongo:
+    """Speaks enough of the MongoDB wire protocol (OP_MSG, plus legacy OP_QUERY
+    hello) for pymongo: handshake, count, find with projection + sort, aggregate
+    with $match on an _id range, $sort on _id, $project of fields."""
+
+    def __init__(self, docs):
+        import socket
+
+        self.docs = docs
+        self.sock = socket.socket()
+        self.sock.bind(("127.0.0.1", 0))
+        self.sock.listen(16)
+        self.port = self.sock.getsockname()[1]
+        threading.Thread(target=self._accept, daemon=True).start()
+
+    def _accept(self):
+        while True:
+            try:
+                conn, _ = self.sock.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._serve, args=(conn,), daemon=True).start()
+
+    @staticmethod
+    def _recv(conn, n):
+        buf = b""
+        while len(buf) < n:
+            c = conn.recv(n - len(buf))
+            if not c:
+                raise EOFError
+            buf += c
+        return buf
+
+    def _reply(self, conn, req_id, doc, legacy):
+        import struct
+
+        import bson
+
+        body = bson.encode(doc)
+        if legacy:  # OP_REPLY
+            payload = struct.pack("<iqii", 0, 0, 0, 1) + body
+            op = 1
+        else:
+            payload = struct.pack("<I", 0) + b"\x00" + body
+            op = 2013
+        conn.sendall(struct.pack("<iiii", 16 + len(payload), 0, req_id, op) + payload)
+
+    def _run(self, cmd):
+        import datetime
+
+        name = next(iter(cmd)).lower()
+        if name in ("hello", "ismaster"):
+            return {"ok": 1.0, "isWritablePrimary": True, "ismaster": True, "helloOk": True, "maxWireVersion": 17,
+                    "minWireVersion": 0, "maxBsonObjectSize": 16 * 1024 * 1024, "maxMessageSizeBytes": 48000000,
+                    "maxWriteBatchSize": 100000, "localTime": datetime.datetime.now(datetime.timezone.utc),
+                    "logicalSessionTimeoutMinutes": 30, "connectionId": 1}
+        if name in ("ping", "endsessions", "killcursors"):
+            return {"ok": 1.0}
+        if name == "count":
+            return {"ok": 1.0, "n": len(self.docs)}
+        ns = f"{cmd.get('$db', 'db')}.{cmd[next(iter(cmd))]}"
+        if name == "find":
+            out = sorted(self.docs, key=lambda d: d["_id"])
+            proj = cmd.get("projection") or {}
+            if proj:
+                out = [{k: d[k] for k in d if k in proj or k == "_id"} for d in out]
+            return {"ok": 1.0, "cursor": {"firstBatch": out, "id": 0, "ns": ns}}
+        if name == "aggregate":
+            out = list(self.docs)
+            for st in cmd["pipeline"]:
+                if "$match" in st:
+                    rng = st["$match"].get("_id", {})
+                    out = [d for d in out if ("$gte" not in rng or d["_id"] >= rng["$gte"])
+                           and ("$lt" not in rng or d["_id"] < rng["$lt"])]
+                elif "$sort" in st:
+                    out.sort(key=lambda d: d["_id"])
+                elif "$project" in st:
+                    keep = st["$project"]
+                    out = [{k: d[k] for k in d if keep.get(k) or k == "_id"} for d in out]
+            return {"ok": 1.0, "cursor": {"firstBatch": out, "id": 0, "ns": ns}}
+        return {"ok": 0.0, "errmsg": f"unsupported {name}", "code": 59}
+
+    def _serve(self, conn):
+        import struct
+
+        import bson
+
+        try:
+            while True:
+                ln, req_id, _, op = struct.unpack("<iiii", self._recv(conn, 16))
+                body = self._recv(conn, ln - 16)
+                if op == 2013:
+                    doc = bson.decode(body[5:5 + struct.unpack("<i", body[5:9])[0]])
+                    self._reply(conn, req_id, self._run(doc), False)
+                elif op == 2004:  # legacy OP_QUERY handshake
+                    i = 4 + body[4:].index(b"\x00") + 1 + 8
+                    doc = bson.decode(body[i:i + struct.unpack("<i", body[i:i + 4])[0]])
+                    self._reply(conn, req_id, self._run(doc), True)
+                else:
+                    return
+        except (EOFError, OSError):
+            conn.close()
+
+
+def test_read_mongo(server):
+    docs = [{"_id": i, "name": f"n{i}", "v": i * 2} for i in range(20)]
+    srv = _MiniMongo(docs)
+    uri = f"mongodb://127.0.0.1:{srv.port}/?directConnection=true&serverSelectionTimeoutMS=3000"
+    ds = data.read_mongo(uri, "db", "c", override_num_blocks=4)
+    rows = ds.take_all()
+    assert [r["_id"] for r in rows] == list(range(20)) and rows[3]["v"] == 6
+    proj = data.read_mongo(uri, "db", "c", pipeline=[{"$project": {"name": 1}}]).take_all()
+    assert set(proj[0]) == {"_id", "name"} and len(proj) == 20
