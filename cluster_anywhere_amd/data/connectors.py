@@ -359,4 +359,126 @@ def read_mongo(uri: str, database: str, collection: str, *, pipeline: Optional[L
     return _read_ds([(lambda lo=lo, hi=hi: task(lo, hi)) for lo, hi in zip(edges[:-1], edges[1:])])
 
 
-__all__ = ["read_clickhouse", "read_delta_sharing_tables", "read_databricks_tables", "read_bigquery", "read_mongo"]
+
+
+# ---------------------------------------------------------------------- videos
+def _y4m_frames(raw: bytes):
+    import numpy as np
+
+    nl = raw.index(b"\n")
+    hdr = raw[:nl].split()
+    if hdr[0] != b"YUV4MPEG2":
+        raise ValueError("not a YUV4MPEG2 stream")
+    w = h = None
+    cs = b"420"
+    for t in hdr[1:]:
+        if t[:1] == b"W":
+            w = int(t[1:])
+        elif t[:1] == b"H":
+            h = int(t[1:])
+        elif t[:1] == b"C":
+            cs = t[1:]
+    sub = 1 if cs.startswith(b"444") else 2
+    cw, ch = -(-w // sub), -(-h // sub)
+    fsize = w * h + 2 * cw * ch
+    pos = nl + 1
+    while pos < len(raw):
+        e = raw.index(b"\n", pos)
+        if not raw[pos:e].startswith(b"FRAME"):
+            raise ValueError("bad Y4M frame header")
+        buf = np.frombuffer(raw, np.uint8, fsize, e + 1)
+        pos = e + 1 + fsize
+        y = buf[: w * h].reshape(h, w).astype(np.float32)
+        u = buf[w * h: w * h + cw * ch].reshape(ch, cw).astype(np.float32)
+        v = buf[w * h + cw * ch:].reshape(ch, cw).astype(np.float32)
+        if sub == 2:
+            u = u.repeat(2, 0).repeat(2, 1)[:h, :w]
+            v = v.repeat(2, 0).repeat(2, 1)[:h, :w]
+        c, d, e_ = y - 16.0, u - 128.0, v - 128.0  # BT.601 limited range
+        rgb = np.stack([1.164 * c + 1.596 * e_, 1.164 * c - 0.392 * d - 0.813 * e_, 1.164 * c + 2.017 * d], -1)
+        yield np.clip(rgb + 0.5, 0, 255).astype(np.uint8)
+
+
+def _avi_frames(raw: bytes):
+    """RIFF AVI with Motion-JPEG ('00dc' JPEG chunks) or uncompressed 24-bit DIB frames."""
+    import struct
+
+    import numpy as np
+    from PIL import Image
+
+    if raw[:4] != b"RIFF" or raw[8:12] != b"AVI ":
+        raise ValueError("not an AVI file")
+    w = h = 0
+    i = raw.find(b"strf")
+    if i >= 0:
+        w, h = struct.unpack("<ii", raw[i + 12:i + 20])
+    m = raw.find(b"movi")
+    if m < 0:
+        raise ValueError("AVI without a movi list")
+    pos = m + 4
+    while pos + 8 <= len(raw):
+        cid, size = raw[pos:pos + 4], struct.unpack("<I", raw[pos + 4:pos + 8])[0]
+        data = raw[pos + 8:pos + 8 + size]
+        if cid == b"LIST":
+            pos += 12
+            continue
+        if cid == b"idx1":
+            break
+        if cid[2:] in (b"dc", b"db") and size:
+            if data[:2] == b"\xff\xd8":
+                yield np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
+            else:
+                stride = (w * 3 + 3) & ~3
+                img = np.frombuffer(data, np.uint8, stride * abs(h)).reshape(abs(h), stride)[:, : w * 3]
+                img = img.reshape(abs(h), w, 3)[:, :, ::-1]
+                yield np.ascontiguousarray(img[::-1] if h > 0 else img)
+        pos += 8 + size + (size & 1)
+
+
+def _pil_frames(raw: bytes):
+    import numpy as np
+    from PIL import Image, ImageSequence
+
+    for fr in ImageSequence.Iterator(Image.open(io.BytesIO(raw))):
+        yield np.asarray(fr.convert("RGB"))
+
+
+_VIDEO_DECODERS = {".y4m": _y4m_frames, ".avi": _avi_frames, ".gif": _pil_frames, ".webp": _pil_frames,
+                   ".png": _pil_frames, ".apng": _pil_frames}
+
+
+def read_videos(paths, *, include_paths: bool = False, file_extensions: Optional[List[str]] = None,
+                override_num_blocks: Optional[int] = None, concurrency: Optional[int] = None,
+                ray_remote_args=None, **kw) -> Dataset:
+    """One row per frame: ``{"frame": uint8 [H, W, 3], "frame_index": int}`` (+ ``path``).
+    Decoded here without a codec library: YUV4MPEG2 (``.y4m``), AVI with
+    Motion-JPEG or uncompressed frames, and animated GIF / WebP / PNG. Codec-
+    compressed containers (H.264 / HEVC / VP9 in .mp4 / .mkv / .webm) need a video
+    decoder, which this image does not have: they raise NotImplementedError."""
+    from .read_api import _expand, _file_ds
+
+    exts = file_extensions or list(_VIDEO_DECODERS) + [".mp4", ".mkv", ".mov", ".webm"]
+    files = _expand(paths, exts)
+
+    def rd(f):
+        import numpy as np
+
+        ext = os.path.splitext(f)[1].lower()
+        dec = _VIDEO_DECODERS.get(ext)
+        if dec is None:
+            raise NotImplementedError(f"{f}: decoding {ext} needs a video codec library (not in this image); "
+                                      f"supported here: {sorted(_VIDEO_DECODERS)}")
+        with open(f, "rb") as fh:
+            raw = fh.read()
+        frames = list(dec(raw))
+        out = {"frame": np.stack(frames) if frames else np.zeros((0, 0, 0, 3), np.uint8),
+               "frame_index": np.arange(len(frames), dtype=np.int64)}
+        if include_paths:
+            out["path"] = np.array([f] * len(frames), dtype=object)
+        return out
+
+    return _file_ds(files, rd)
+
+
+__all__ = ["read_clickhouse", "read_delta_sharing_tables", "read_databricks_tables", "read_bigquery", "read_mongo",
+           "read_videos"]

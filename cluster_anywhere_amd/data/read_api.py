@@ -440,7 +440,7 @@ def _unavailable(name: str, lib: str):
     return fn
 
 
-for _n, _lib in (("read_lance", "lance"), ("read_videos", "decord")):
+for _n, _lib in (("read_lance", "lance"),):
     globals()[_n] = _unavailable(_n, _lib)
 
 
@@ -498,7 +498,7 @@ def from_tf(dataset) -> Dataset:
 
 # spoken over their HTTP protocols, no client library needed (data/connectors.py)
 from .connectors import (read_bigquery, read_clickhouse, read_databricks_tables,  # noqa: E402
-                         read_delta_sharing_tables, read_mongo)
+                         read_delta_sharing_tables, read_mongo, read_videos)
 
 
 def read_datasource(datasource, *, parallelism: int = -1, **kw) -> Dataset:

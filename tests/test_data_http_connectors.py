@@ -6,6 +6,7 @@ BigQuery REST (tables.get + tabledata.list pages, jobs.query). Reference tests:
 python/ray/data/tests/test_clickhouse.py, test_delta_sharing.py,
 test_databricks_uc_datasource.py, test_bigquery.py (mocked clients there)."""
 import io
+import os
 import json
 import re
 import threading
@@ -335,3 +336,47 @@ def test_read_mongo(server):
     assert [r["_id"] for r in rows] == list(range(20)) and rows[3]["v"] == 6
     proj = data.read_mongo(uri, "db", "c", pipeline=[{"$project": {"name": 1}}]).take_all()
     assert set(proj[0]) == {"_id", "name"} and len(proj) == 20
+
+
+def test_read_videos_native_containers(server, tmp_path):
+    """Y4M (raw YUV 4:2:0), Motion-JPEG AVI (hand-built RIFF) and animated GIF."""
+    import struct
+
+    import numpy as np
+    from PIL import Image
+
+    w, h, n = 16, 8, 3
+    # Y4M: mid-grey luma, neutral chroma -> RGB ~ (1.164 * (y - 16)) on every channel
+    with open(tmp_path / "a.y4m", "wb") as f:
+        f.write(f"YUV4MPEG2 W{w} H{h} F25:1 Ip A1:1 C420jpeg\n".encode())
+        for i in range(n):
+            f.write(b"FRAME\n" + bytes([100 + i * 10]) * (w * h) + bytes([128]) * (2 * (w // 2) * (h // 2)))
+    # MJPEG AVI: three solid-colour JPEG frames
+    frames = []
+    for c in [(255, 0, 0), (0, 255, 0), (0, 0, 255)]:
+        b = io.BytesIO()
+        Image.new("RGB", (w, h), c).save(b, format="JPEG", quality=95)
+        frames.append(b.getvalue())
+    chunks = b"".join(b"00dc" + struct.pack("<I", len(fr)) + fr + (b"\x00" if len(fr) & 1 else b"") for fr in frames)
+    movi = b"LIST" + struct.pack("<I", 4 + len(chunks)) + b"movi" + chunks
+    strf = b"strf" + struct.pack("<I", 40) + struct.pack("<iiiHH", 40, w, h, 1, 24) + b"MJPG" + b"\x00" * 20
+    hdrl = b"LIST" + struct.pack("<I", 4 + len(strf)) + b"hdrl" + strf
+    body = b"AVI " + hdrl + movi
+    (tmp_path / "b.avi").write_bytes(b"RIFF" + struct.pack("<I", len(body)) + body)
+    # animated GIF
+    ims = [Image.new("RGB", (w, h), (i * 80, 0, 0)) for i in range(n)]
+    ims[0].save(tmp_path / "c.gif", save_all=True, append_images=ims[1:], duration=40)
+
+    rows = data.read_videos(str(tmp_path), include_paths=True).take_all()
+    by = {}
+    for r in rows:
+        by.setdefault(os.path.basename(r["path"]), []).append(r)
+    assert [r["frame_index"] for r in by["a.y4m"]] == [0, 1, 2]
+    y = by["a.y4m"][1]["frame"]
+    assert y.shape == (h, w, 3) and abs(int(y[0, 0, 0]) - round(1.164 * (110 - 16))) <= 1
+    av = by["b.avi"]
+    assert len(av) == 3 and av[0]["frame"][..., 0].mean() > 200 and av[2]["frame"][..., 2].mean() > 200
+    assert len(by["c.gif"]) == 3
+    (tmp_path / "d.mp4").write_bytes(b"\x00" * 16)
+    with pytest.raises(Exception):
+        data.read_videos(str(tmp_path / "d.mp4")).take_all()
