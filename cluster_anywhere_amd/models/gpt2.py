@@ -17,6 +17,7 @@ TorchTrainer DDP GPT-2-XL tokens/s).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -24,8 +25,19 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import add_layer_norm, attention, layer_norm
+from ..ops.attention import flash_path
+from ..ops.norm import ln_bias_fusion_ok
 from ..ops.linear import linear, mlp
 from ..ops.loss import linear_cross_entropy
+
+
+# qkv bias gradient from the flash-attention backward's registers: opt-in
+# (CAAMD_FUSED_QKV_BGRAD=1) -- it measured 88.4-88.5k vs 91.0k tok/s in alternating
+# same-box runs (the backward kernels' epilogue reduction costs more than the 52 us
+# column-sum pass it replaces; profiles/step_ab_r3_bias_fusion.txt)
+_FUSED_QKV_BGRAD = os.environ.get("CAAMD_FUSED_QKV_BGRAD", "0") == "1"
+# proj / fc2 bias gradients from the LayerNorm backward (CAAMD_NO_FUSED_LN_BGRAD=1: own passes)
+_FUSED_LN_BGRAD = os.environ.get("CAAMD_NO_FUSED_LN_BGRAD", "0") != "1"
 
 
 @dataclass
@@ -79,16 +91,29 @@ class Block(nn.Module):
         nn.init.normal_(self.proj_w, std=std / math.sqrt(2 * cfg.n_layer))
         nn.init.normal_(self.fc2_w, std=std / math.sqrt(2 * cfg.n_layer))
 
-    def forward(self, h, delta):
+    def forward(self, h, delta, delta_bias=None):
+        """-> (h, mlp output, fc2 bias whose gradient the NEXT LayerNorm backward takes or None)."""
         if delta is None:
             a = layer_norm(h, self.ln1_w, self.ln1_b, self.eps)
         else:
-            h, a = add_layer_norm(h, delta, self.ln1_w, self.ln1_b, self.eps)
-        qkv = linear(a, self.attn_w, self.attn_b)
-        y = attention(qkv, self.n_head, causal=True)
-        attn_out = linear(y, self.proj_w, self.proj_b)
-        h, m = add_layer_norm(h, attn_out, self.ln2_w, self.ln2_b, self.eps)
-        return h, mlp(m, self.fc_w, self.fc_b, self.fc2_w, self.fc2_b)
+            h, a = add_layer_norm(h, delta, self.ln1_w, self.ln1_b, self.eps, res_bias=delta_bias)
+        # on the flash path the attention backward also takes the qkv bias gradient
+        # (column sums of dqkv from its registers); only with main-grad buffers,
+        # where the linear below then skips its own pass over dqkv
+        fused_b = (_FUSED_QKV_BGRAD and flash_path(a, a.shape[-1], self.n_head)
+                   and getattr(self.attn_w, "main_grad", None) is not None and a.requires_grad)
+        qkv = linear(a, self.attn_w, self.attn_b, bias_grad=not fused_b)
+        y = attention(qkv, self.n_head, causal=True, qkv_bias=self.attn_b if fused_b else None)
+        # proj / fc2 bias gradients = column sums of the residual-stream gradient,
+        # taken by the following LayerNorm backward (no separate pass over it)
+        fuse_ln = (_FUSED_LN_BGRAD and getattr(self.proj_b, "main_grad", None) is not None
+                   and getattr(self.fc2_b, "main_grad", None) is not None and h.requires_grad
+                   and ln_bias_fusion_ok(h))
+        attn_out = linear(y, self.proj_w, self.proj_b, bias_grad=not fuse_ln)
+        h, m = add_layer_norm(h, attn_out, self.ln2_w, self.ln2_b, self.eps,
+                              res_bias=self.proj_b if fuse_ln else None)
+        out = mlp(m, self.fc_w, self.fc_b, self.fc2_w, self.fc2_b, b2_grad=not fuse_ln)
+        return h, out, (self.fc2_b if fuse_ln else None)
 
 
 class GPT2(nn.Module):
@@ -111,10 +136,10 @@ class GPT2(nn.Module):
     def hidden(self, idx):
         B, T = idx.shape
         h = F.embedding(idx, self.wte) + self.wpe[:T]
-        delta = None
+        delta = dbias = None
         for blk in self.blocks:
-            h, delta = blk(h, delta)
-        _, hf = add_layer_norm(h, delta, self.lnf_w, self.lnf_b, self.cfg.ln_eps)
+            h, delta, dbias = blk(h, delta, dbias)
+        _, hf = add_layer_norm(h, delta, self.lnf_w, self.lnf_b, self.cfg.ln_eps, res_bias=dbias)
         return hf
 
     def forward(self, idx, targets=None):

@@ -38,14 +38,24 @@ def _have_flash(dh: int) -> bool:
         return False
 
 
-def attention(qkv: torch.Tensor, n_head: int, causal: bool = True) -> torch.Tensor:
+def flash_path(x: torch.Tensor, d_model: int, n_head: int) -> bool:
+    """Whether :func:`attention` on a qkv projection of ``x`` takes the flash kernels
+    (then it can also produce the projection's bias gradient, ``qkv_bias``)."""
+    return use_gpu_kernel(x) and x.dtype == torch.bfloat16 and _have_flash(d_model // n_head)
+
+
+def attention(qkv: torch.Tensor, n_head: int, causal: bool = True, qkv_bias=None) -> torch.Tensor:
+    """``qkv_bias`` (flash path only, see :func:`flash_path`): the bias of the qkv
+    projection, whose gradient the attention backward then computes."""
     B, T, three_d = qkv.shape
     D = three_d // 3
     dh = D // n_head
     if use_gpu_kernel(qkv) and qkv.dtype == torch.bfloat16 and _have_flash(dh):
         from .flash import flash_attention_qkv
 
-        return flash_attention_qkv(qkv, n_head, causal)
+        return flash_attention_qkv(qkv, n_head, causal, qkv_bias)
+    if qkv_bias is not None:
+        raise ValueError("qkv_bias is only taken on the flash path (check flash_path first)")
     q, k, v = qkv.view(B, T, 3, n_head, dh).permute(2, 0, 3, 1, 4).unbind(0)
     o = F.scaled_dot_product_attention(q, k, v, is_causal=causal)
     return o.transpose(1, 2).reshape(B, T, D)

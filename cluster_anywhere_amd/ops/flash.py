@@ -13,22 +13,38 @@ from ._lib import kernels
 
 class _FlashQKV(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, n_head, causal):
+    def forward(ctx, qkv, n_head, causal, qkv_bias):
         qkv = qkv.contiguous()
         out, lse = kernels().flash_attn_fwd(qkv, n_head, causal)
         ctx.save_for_backward(qkv, out, lse)
         ctx.n_head, ctx.causal = n_head, causal
+        ctx.qkv_bias = qkv_bias
         return out
 
     @staticmethod
     def backward(ctx, dout):
         qkv, out, lse = ctx.saved_tensors
-        dqkv = kernels().flash_attn_bwd(qkv, out, dout.contiguous(), lse, ctx.n_head, ctx.causal)
-        return dqkv, None, None
+        b = ctx.qkv_bias
+        if b is None:
+            return kernels().flash_attn_bwd(qkv, out, dout.contiguous(), lse, ctx.n_head, ctx.causal), None, None, None
+        # the qkv projection's bias gradient = column sums of dqkv, taken from the
+        # backward kernels' registers (fp32 atomics) instead of a re-read of dqkv
+        db = torch.zeros(qkv.shape[-1], device=qkv.device, dtype=torch.float32)
+        dqkv = kernels().flash_attn_bwd(qkv, out, dout.contiguous(), lse, ctx.n_head, ctx.causal, db)
+        mg = getattr(b, "main_grad", None)
+        if mg is not None:
+            from .linear import _ready
+
+            mg.add_(db)
+            _ready(b)
+            return dqkv, None, None, None
+        return dqkv, None, None, (db.to(b.dtype) if ctx.needs_input_grad[3] else None)
 
 
-def flash_attention_qkv(qkv: torch.Tensor, n_head: int, causal: bool = True) -> torch.Tensor:
-    return _FlashQKV.apply(qkv, n_head, causal)
+def flash_attention_qkv(qkv: torch.Tensor, n_head: int, causal: bool = True, qkv_bias=None) -> torch.Tensor:
+    """``qkv_bias``: the projection bias that produced ``qkv``; its gradient is then
+    computed here (the caller's linear must skip its own bias gradient)."""
+    return _FlashQKV.apply(qkv, n_head, causal, qkv_bias)
 
 
 def flash_attention_lse(qkv: torch.Tensor, n_head: int, causal: bool = True):

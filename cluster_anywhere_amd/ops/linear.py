@@ -71,9 +71,9 @@ def _dgrad(dy2, w, mfma):
 
 class _MainGradLinear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, bias_grad=True):
         ctx.save_for_backward(x, weight)
-        ctx.bias = bias
+        ctx.bias = bias if bias_grad else None  # else a later op computes it (fused)
         x2 = x.reshape(-1, x.shape[-1])
         ctx.mfma = _g.supported(x2, weight)
         if ctx.mfma:
@@ -91,19 +91,19 @@ class _MainGradLinear(torch.autograd.Function):
             dx = _dgrad(dy2, w, ctx.mfma).view(*dy.shape[:-1], w.shape[1])
         gw = _wgrad(w, dy2, x2, ctx.needs_input_grad[1])
         gb = _bgrad(b, dy2, ctx.needs_input_grad[2])
-        return dx, gw, gb
+        return dx, gw, gb, None
 
 
 class _MainGradMLP(torch.autograd.Function):
     """y = gelu(x W1^T + b1) W2^T + b2 with the GELU fused into both GEMM epilogues."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, b2_grad=True):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         u, z = _g.linear_gelu(x2, w1, b1)
         y = _g.linear_nt(u, w2, b2)
         ctx.save_for_backward(x2, w1, w2, u, z)
-        ctx.b = (b1, b2)
+        ctx.b = (b1, b2 if b2_grad else None)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w2.shape[0])
 
@@ -127,12 +127,14 @@ class _MainGradMLP(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _g.dgrad(dz, _g.transpose(w1)).view(ctx.xshape)
-        return dx, gw1, gb1, gw2, gb2
+        return dx, gw1, gb1, gw2, gb2, None
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, bias_grad: bool = True) -> torch.Tensor:
+    """``bias_grad=False``: the bias gradient is produced by a later fused op (the
+    flash-attention backward for the qkv projection); only on the main-grad path."""
     if use_gpu_kernel(x, weight) and getattr(weight, "main_grad", None) is not None and x.requires_grad:
-        return _MainGradLinear.apply(x, weight, bias)
+        return _MainGradLinear.apply(x, weight, bias, bias_grad)
     if use_gpu_kernel(x, weight) and _g.supported(x.reshape(-1, x.shape[-1]), weight):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         if not torch.is_grad_enabled() or not (x.requires_grad or weight.requires_grad):
@@ -148,8 +150,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
 _FUSED_MLP = os.environ.get("CAAMD_FUSED_MLP", "1") == "1"
 
 
-def mlp(x, w1, b1, w2, b2):
-    """GPT-2 MLP ``fc2(gelu_tanh(fc(x)))`` (fused path when the shapes tile)."""
+def mlp(x, w1, b1, w2, b2, b2_grad: bool = True):
+    """GPT-2 MLP ``fc2(gelu_tanh(fc(x)))`` (fused path when the shapes tile).
+    ``b2_grad=False``: fc2's bias gradient comes from a later fused op."""
     from .activation import bias_gelu
 
     x2 = x.reshape(-1, x.shape[-1])
@@ -157,5 +160,5 @@ def mlp(x, w1, b1, w2, b2):
             and getattr(w2, "main_grad", None) is not None and x.requires_grad
             and _g.supported(x2, w1) and _g.tile_for(x2.shape[0], w2.shape[0], w2.shape[1]) is not None
             and _g.tile_for(x2.shape[0], w2.shape[1], w2.shape[0]) is not None):
-        return _MainGradMLP.apply(x, w1, b1, w2, b2)
-    return linear(bias_gelu(linear(x, w1), b1), w2, b2)
+        return _MainGradMLP.apply(x, w1, b1, w2, b2, b2_grad)
+    return linear(bias_gelu(linear(x, w1), b1), w2, b2, bias_grad=b2_grad)

@@ -13,9 +13,16 @@ def layer_norm_ref(x, g, b, eps=1e-5):
     return F.layer_norm(x.float(), (x.shape[-1],), g.float(), b.float(), eps).to(x.dtype)
 
 
+def ln_bias_fusion_ok(x: torch.Tensor) -> bool:
+    """Whether the LayerNorm backward can also produce the column sums of its input
+    gradient (the bias gradient of the layer that produced the residual branch)."""
+    return use_gpu_kernel(x) and x.dtype == torch.bfloat16 and bool(kernels().ln_bwd_dxsum_ok(x.shape[-1]))
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, g, b, eps):
+    def forward(ctx, x, res, g, b, eps, res_bias=None):
+        ctx.res_bias = res_bias
         C = kernels()
         x = x.contiguous()
         if res is not None:
@@ -40,10 +47,18 @@ class _LayerNormFn(torch.autograd.Function):
             dres = None
         if dy is None:
             dy = torch.zeros_like(saved)
-        dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres)
+        rb = ctx.res_bias
+        if rb is not None:
+            # bias gradient of the residual branch's producer (its main-grad view)
+            dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres, rb.main_grad)
+            from .linear import _ready
+
+            _ready(rb)
+        else:
+            dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres)
         if ctx.has_res:
-            return dx, dx, dg, db, None
-        return dx, None, dg, db, None
+            return dx, dx, dg, db, None, None
+        return dx, None, dg, db, None, None
 
 
 def layer_norm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e-5):
@@ -53,10 +68,14 @@ def layer_norm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1
 
 
 def add_layer_norm(
-    x: torch.Tensor, res: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e-5
+    x: torch.Tensor, res: torch.Tensor, g: torch.Tensor, b: torch.Tensor, eps: float = 1e-5, res_bias=None
 ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Return ``(s, LN(s))`` with ``s = x + res`` in one HBM pass."""
+    """Return ``(s, LN(s))`` with ``s = x + res`` in one HBM pass. ``res_bias``: the
+    bias (with a ``main_grad``) of the layer that produced ``res``; its gradient is
+    then accumulated by this backward (see :func:`ln_bias_fusion_ok`)."""
     if use_gpu_kernel(x, res, g, b) and x.dtype == torch.bfloat16:
-        return _LayerNormFn.apply(x, res, g, b, eps)
+        return _LayerNormFn.apply(x, res, g, b, eps, res_bias)
+    if res_bias is not None:
+        raise ValueError("res_bias needs the fused LayerNorm path")
     s = x + res
     return s, F.layer_norm(s, (s.shape[-1],), g, b, eps)

@@ -11,6 +11,7 @@ Reference parity: ``python/ray/train/torch/train_loop_utils.py:299``
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -39,6 +40,9 @@ class FusedAdamW:
         self.exp_avg_sq = torch.zeros_like(self.exp_avg)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=flat.master.device)
         self.step_count = 0
+        v = os.environ.get("CAAMD_ADAM_VARIANT")  # kernel variant override (A/B timing)
+        if v is not None and flat.master.is_cuda:
+            kernels().adamw_config(int(v))
 
     def state_dict(self):
         return {

@@ -13,7 +13,8 @@ typedef __bf16 bf16;
 void ln_fwd_launch(const bf16*, const bf16*, bf16*, const bf16*, const bf16*, bf16*, float*, float*,
                    int, int, float, hipStream_t);
 void ln_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, const float*, const bf16*,
-                   bf16*, float*, bf16*, bf16*, int, int, hipStream_t);
+                   bf16*, float*, bf16*, bf16*, int, int, hipStream_t, bf16*);
+bool ln_bwd_dxsum_ok(int D);
 int ln_nv_for(int D);
 int ln_bwd_num_blocks(int rows);
 int ln_bwd_partial_rows(int rows, int D);
@@ -32,6 +33,7 @@ void normalize_pad8_launch(const uint8_t* in, bf16* out, int64_t npix, const flo
 void maxpool3s2_launch(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
 bool xent_fused_launch(bf16*, const int64_t*, float*, float*, const float*, int, int, int, hipStream_t);
 void grad_sumsq_launch(const void*, bool, int64_t, float*, hipStream_t);
+void adamw_config(int variant);
 void adamw_launch(float*, float*, float*, const void*, bool, bf16*, int64_t, float, float, float,
                   float, float, float, float, float, float, const float*, const uint8_t*,
                   hipStream_t);
@@ -130,9 +132,12 @@ std::vector<Tensor> layernorm_fwd(const Tensor& x, const c10::optional<Tensor>& 
 }
 
 // returns (dx, dg, db); dx += dres when dres given
+// dxsum (optional bf16 [D], only where ln_bwd_dxsum_ok(D)): += column sums of dx,
+// i.e. the bias gradient of the layer that produced the residual branch.
 std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& g,
                                   const Tensor& mean, const Tensor& rstd,
-                                  const c10::optional<Tensor>& dres) {
+                                  const c10::optional<Tensor>& dres,
+                                  const c10::optional<Tensor>& dxsum) {
   CHECK_BF16(dy);
   CHECK_BF16(x);
   CHECK_BF16(g);
@@ -149,12 +154,18 @@ std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tenso
   auto dx = at::empty_like(x);
   auto dg = at::empty_like(g);
   auto db = at::empty_like(g);
+  caamd::bf16* dxs = nullptr;
+  if (dxsum.has_value() && dxsum->defined()) {
+    CHECK_BF16(*dxsum);
+    TORCH_CHECK(dxsum->numel() == D && caamd::ln_bwd_dxsum_ok(D), "layernorm_bwd: dxsum needs [D] and the cs path");
+    dxs = bp(*dxsum);
+  }
   const int nblk = caamd::ln_bwd_partial_rows(rows, D);
-  auto partial = at::empty({nblk, 2, D}, x.options().dtype(at::kFloat));
+  auto partial = at::empty({nblk, dxs ? 3 : 2, D}, x.options().dtype(at::kFloat));
   if (rows > 0) {
     caamd::ln_bwd_launch(bp(dy), bp(x), bp(g), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                          bp_opt(dres), bp(dx), partial.data_ptr<float>(), bp(dg), bp(db), rows, D,
-                         cur_stream());
+                         cur_stream(), dxs);
     LAUNCH_CHECK();
   } else {
     dg.zero_();
@@ -392,8 +403,8 @@ std::vector<Tensor> vtrace(const Tensor& log_rhos, const Tensor& discounts, cons
 // ---- flash attention (packed qkv [B, T, 3*H*D]) ---------------------------------
 namespace caamd {
 void fa_fwd_launch(const bf16*, bf16*, float*, int, int, int, int, int, hipStream_t);
-void fa_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, float*, bf16*, int, int,
-                   int, int, int, hipStream_t);
+bool fa_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse, float* delta, bf16* dqkv,
+                   int B, int T, int H, int D, int causal, hipStream_t st, float* dbias);
 }
 
 static void fa_check_qkv(const Tensor& qkv, int64_t H, int& B, int& T, int& D) {
@@ -418,8 +429,10 @@ std::vector<Tensor> flash_attn_fwd(const Tensor& qkv, int64_t H, bool causal) {
   return {out, lse};
 }
 
+// dbias (optional fp32 [3*H*D]): += column sums of dqkv over the tokens (the qkv
+// projection's bias gradient), from the kernels' registers where they support it.
 Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, const Tensor& lse,
-                      int64_t H, bool causal) {
+                      int64_t H, bool causal, const c10::optional<Tensor>& dbias) {
   int B, T, D;
   fa_check_qkv(qkv, H, B, T, D);
   CHECK_BF16(out);
@@ -432,11 +445,22 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, 
   auto dqkv = at::empty_like(qkv);
   // workspace: Delta = rowsum(dO * O) and lse * log2(e), [2, B, H, T]
   auto delta = at::empty({2, (int64_t)B * H * T}, lse.options());
-  if (B > 0 && T > 0)
-    caamd::fa_bwd_launch(bp(qkv), bp(out), bp(dout), lse.data_ptr<float>(),
-                         delta.data_ptr<float>(), bp(dqkv), B, T, (int)H, D, causal ? 1 : 0,
-                         cur_stream());
+  float* dbp = nullptr;
+  if (dbias.has_value()) {
+    CHECK_F32(*dbias);
+    TORCH_CHECK(dbias->numel() == 3 * H * D, "flash_attn_bwd: dbias must have 3*H*D elements");
+    dbp = dbias->data_ptr<float>();
+  }
+  if (B > 0 && T > 0) {
+    const bool done = caamd::fa_bwd_launch(bp(qkv), bp(out), bp(dout), lse.data_ptr<float>(),
+                                           delta.data_ptr<float>(), bp(dqkv), B, T, (int)H, D, causal ? 1 : 0,
+                                           cur_stream(), dbp);
     LAUNCH_CHECK();
+    if (!done) {
+      Tensor d = dbias.value();
+      d.add_(dqkv.reshape({-1, 3 * H * D}).sum(0, false, at::kFloat));
+    }
+  }
   return dqkv;
 }
 
@@ -1168,7 +1192,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("decode_gemm", &decode_gemm);
   m.def("transpose_bf16", &transpose_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("g"),
+        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("dres"), pybind11::arg("dxsum") = pybind11::none());
+  m.def("ln_bwd_dxsum_ok", [](int64_t D) { return caamd::ln_bwd_dxsum_ok((int)D); });
   m.def("ln_bwd_config", [](int variant, int max_blocks) {
     TORCH_CHECK(variant >= 0 && variant <= 3, "ln_bwd_config: variant must be 0-3");
     TORCH_CHECK(max_blocks >= 0 && max_blocks <= 65536, "ln_bwd_config: bad max_blocks");
@@ -1181,11 +1207,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_bwd_", &xent_bwd_);
   m.def("xent_fused_", &xent_fused_);
   m.def("grad_sumsq", &grad_sumsq);
+  m.def("adamw_config", [](int64_t variant) { caamd::adamw_config((int)variant); });
   m.def("adamw_step", &adamw_step);
   m.def("gae", &gae);
   m.def("vtrace", &vtrace);
   m.def("flash_attn_fwd", &flash_attn_fwd);
-  m.def("flash_attn_bwd", &flash_attn_bwd);
+  m.def("flash_attn_bwd", &flash_attn_bwd, pybind11::arg("qkv"), pybind11::arg("out"), pybind11::arg("dout"),
+        pybind11::arg("lse"), pybind11::arg("H"), pybind11::arg("causal"), pybind11::arg("dbias") = pybind11::none());
   m.def("rmsnorm", &rmsnorm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("eps"),
         pybind11::arg("residual") = pybind11::none());
   m.def("silu_mul", &silu_mul);

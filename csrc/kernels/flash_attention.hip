@@ -32,7 +32,7 @@ namespace caamd {
 void fa64_fwd_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
                      hipStream_t);
 void fa64_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, float*, bf16*, int, int, int, int,
-                     hipStream_t);
+                     hipStream_t, float*);
 static bool fa_v1() {
   static const bool v = [] {
     const char* e = std::getenv("CAAMD_FA_V1");
@@ -667,12 +667,15 @@ void fa_fwd_launch(const bf16* qkv, bf16* out, float* lse, int B, int T, int H, 
                     B, T, H, D, causal, st);
 }
 
-void fa_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse,
+// dbias (optional, fp32 [3*H*D], accumulated): column sums of dqkv over the tokens,
+// taken in the second-generation D = 64 kernels' epilogues; returns false when the
+// path taken does not produce them (the caller sums dqkv itself).
+bool fa_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse,
                    float* delta, bf16* dqkv, int B, int T, int H, int D, int causal,
-                   hipStream_t st) {
+                   hipStream_t st, float* dbias) {
   if (D == 64 && !fa_v1()) {  // delta: 2 * B * H * T floats
-    fa64_bwd_launch(qkv, out, dout, lse, delta, dqkv, B, T, H, causal, st);
-    return;
+    fa64_bwd_launch(qkv, out, dout, lse, delta, dqkv, B, T, H, causal, st, dbias);
+    return true;
   }
   const int qblk = D == 64 ? qblk_for<64>() : qblk_for<128>();
   const int nqb = (T + qblk - 1) / qblk;
@@ -692,6 +695,7 @@ void fa_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const flo
     hipLaunchKernelGGL(fa_bwd_dkdv_kernel<128>, gk, block, dkdv_lds<128>(), st, qkv, dout, lse,
                        delta, dqkv, T, H, nkb, scale_log2, scale, causal);
   }
+  return dbias == nullptr;
 }
 
 }  // namespace caamd

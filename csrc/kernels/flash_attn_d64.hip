@@ -443,6 +443,31 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
 }
 
 // ----------------------------------------------------------------------------
+// Column sums of the block's 32-row output fragments (lane row = lane & 31, columns
+// d*32 + 8g + 4h + j for value 4g + j of acc[d], h = lane >> 5), added to out[col]:
+// the projection-bias gradient (colsum over tokens of dQ / dK / dV) taken from
+// registers, so no separate pass re-reads the 3-wide dqkv tensor. Reduced across the
+// 32 rows of a wave by shuffles, across the 4 waves in LDS, then ONE 64-lane atomic
+// instruction per block (f32 atomics cost a memory op per wave instruction whatever
+// the lane count: 64 one-lane atomics per wave made the backward 5 % slower).
+// Every thread of the block must call it (barriers inside).
+__device__ __forceinline__ void colsum_atomic(const f32x16 (&a)[2], float mul, float* __restrict__ out,
+                                              float* __restrict__ red /* LDS [4][64] */) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, h = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float v = a[d][i];
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+      if ((lane & 31) == 0) red[wave * 64 + d * 32 + 8 * (i >> 2) + 4 * h + (i & 3)] = v;
+    }
+  __syncthreads();
+  if (wave == 0) atomicAdd(out + lane, mul * (red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]));
+  __syncthreads();
+}
+
 // backward dQ (+ Delta = rowsum(dO * O), lse2 = lse * log2 e for the dK/dV
 // kernel): 4 waves x 64 queries per block, 64-key tiles {K image, V image}.
 // ----------------------------------------------------------------------------
@@ -451,7 +476,8 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                         float* __restrict__ delta, float* __restrict__ lse2o,
                                                         bf16* __restrict__ dqkv, int T, int H, int nqb,
-                                                        float scale_log2, float scale, int causal) {
+                                                        float scale_log2, float scale, int causal,
+                                                        float* __restrict__ dbias) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_t* smem = (lds_t*)smem_raw;
   constexpr int STAGE = 2 * IMG;
@@ -591,6 +617,18 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
     wait_next<4>(ahead);
     barrier_keep_dma();
   }
+  if (dbias) {  // q-bias gradient: rows past T hold zeros (never-computed tiles)
+    f32x16 sum[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      sum[d] = zero16();
+#pragma unroll
+      for (int qs = 0; qs < QS; ++qs)
+        if (q0w + qs * 32 + r < T) sum[d] += dq[qs][d];
+    }
+    __shared__ float red[256];
+    colsum_atomic(sum, scale, dbias + (size_t)hh * D, red);
+  }
 #pragma unroll
   for (int qs = 0; qs < QS; ++qs) {
     const int q = q0w + qs * 32 + r;
@@ -619,7 +657,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
                                                           const float* __restrict__ lse2g,
                                                           const float* __restrict__ delta,
                                                           bf16* __restrict__ dqkv, int T, int H, int nkb,
-                                                          float scale_log2, float scale, int causal) {
+                                                          float scale_log2, float scale, int causal,
+                                                          float* __restrict__ dbias) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_t* smem = (lds_t*)smem_raw;
   constexpr int STAGE = 2 * IMG + 512;
@@ -750,6 +789,17 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
     else wait_next<4>(ahead);
     barrier_keep_dma();
   }
+  if (dbias) {  // k / v bias gradients (block-uniform; keys past T contribute zeros)
+    __shared__ float red[256];
+    f32x16 k2[2], v2[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      k2[d] = kv ? dk[d] : zero16();
+      v2[d] = kv ? dv[d] : zero16();
+    }
+    colsum_atomic(k2, scale, dbias + (size_t)(H + hh) * D, red);
+    colsum_atomic(v2, 1.f, dbias + (size_t)(2 * H + hh) * D, red);
+  }
   if (kv) {
     bf16* krow = dqkv + ((size_t)b * T + key) * rs + (size_t)(H + hh) * D;
     bf16* vrow = krow + (size_t)H * D;
@@ -819,7 +869,7 @@ void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int 
 
 // ws: 2 * B * H * T floats (delta, then lse * log2 e)
 void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse, float* ws, bf16* dqkv,
-                     int B, int T, int H, int causal, hipStream_t st) {
+                     int B, int T, int H, int causal, hipStream_t st, float* dbias) {
   const int nkb = (T + 127) / 128;
   const float scale = 0.125f;
   const float scale_log2 = 1.44269504089f * scale;
@@ -832,14 +882,14 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
   if (qs == 2) {
     const int nqb = (T + 255) / 256;
     hipLaunchKernelGGL(fa64::bwd_dq_kernel<2>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout,
-                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal);
+                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
   } else {
     const int nqb = (T + 127) / 128;
     hipLaunchKernelGGL(fa64::bwd_dq_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout,
-                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal);
+                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
   }
   hipLaunchKernelGGL(fa64::bwd_dkdv_kernel, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
-                     lse2, delta, dqkv, T, H, nkb, scale_log2, scale, causal);
+                     lse2, delta, dqkv, T, H, nkb, scale_log2, scale, causal, dbias);
 }
 
 }  // namespace caamd

@@ -313,7 +313,9 @@ __global__ __launch_bounds__(256) void ln_bwd_pf_kernel(
 // flight per lane; the per-row sums of gd and gd*xhat are combined across the 4 waves
 // through LDS (parity double-buffered: one barrier per RB rows). Waves own disjoint
 // columns, so each block writes its dgamma / dbeta partial row without atomics.
-template <int RB, bool HAS_DRES>
+// DXS: also the column sums of dx (the bias gradient of the layer whose output was
+// the residual branch), as a third partial row section [2D, 3D).
+template <int RB, bool HAS_DRES, bool DXS = false>
 __global__ __launch_bounds__(256) void ln_bwd_cs_kernel(
     const bf16* __restrict__ dy, const bf16* __restrict__ x, const bf16* __restrict__ g,
     const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -325,13 +327,13 @@ __global__ __launch_bounds__(256) void ln_bwd_cs_kernel(
   const int cpw = (nchunk + 3) >> 2;
   const int ch = wave * cpw + lane;
   const bool act = lane < cpw && ch < nchunk;
-  float gv[8], dg[8], db[8];
+  float gv[8], dg[8], db[8], dxs[8];
   {
     bf16x8 t = act ? *reinterpret_cast<const bf16x8*>(g + ch * 8) : bf16x8{};
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       gv[j] = (float)t[j];
-      dg[j] = db[j] = 0.f;
+      dg[j] = db[j] = dxs[j] = 0.f;
     }
   }
   const float inv_d = 1.f / (float)D;
@@ -403,17 +405,19 @@ __global__ __launch_bounds__(256) void ln_bwd_cs_kernel(
           float v = rs[i] * ((float)dv[i][j] * gv[j] - m1 - xh * m2);
           if (HAS_DRES) v += (float)rv[i][j];
           o[j] = (bf16)v;
+          if (DXS) dxs[j] += (float)o[j];
         }
         *reinterpret_cast<bf16x8*>(dx + (size_t)r * D + ch * 8) = o;
       }
     }
   }
   if (act) {
-    float* out = partial + (size_t)blockIdx.x * 2 * D + ch * 8;
+    float* out = partial + (size_t)blockIdx.x * (DXS ? 3 : 2) * D + ch * 8;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       out[j] = dg[j];
       out[D + j] = db[j];
+      if (DXS) out[2 * D + j] = dxs[j];
     }
   }
 }
@@ -422,7 +426,7 @@ __global__ __launch_bounds__(256) void ln_bwd_cs_kernel(
 // (columns < split -> o0[c], the rest -> o1[c - split]). One block = 64 columns
 // x 16 waves; wave w sums rows w, w+16, ... with 8 loads in flight; LDS merge.
 __global__ __launch_bounds__(1024) void colsum_bf16_kernel(const float* __restrict__ partial,
-                                                           int nrow, int ncol, int split,
+                                                           int nrow, int ncol, int ld, int split,
                                                            bf16* __restrict__ o0,
                                                            bf16* __restrict__ o1, int accumulate) {
   __shared__ float red[16][64];
@@ -434,11 +438,11 @@ __global__ __launch_bounds__(1024) void colsum_bf16_kernel(const float* __restri
     for (; r + 7 * 16 < nrow; r += 8 * 16) {
       float t[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) t[u] = partial[(size_t)(r + u * 16) * ncol + c];
+      for (int u = 0; u < 8; ++u) t[u] = partial[(size_t)(r + u * 16) * ld + c];
 #pragma unroll
       for (int u = 0; u < 8; ++u) acc += t[u];
     }
-    for (; r < nrow; r += 16) acc += partial[(size_t)r * ncol + c];
+    for (; r < nrow; r += 16) acc += partial[(size_t)r * ld + c];
   }
   red[wave][lane] = acc;
   __syncthreads();
@@ -452,10 +456,15 @@ __global__ __launch_bounds__(1024) void colsum_bf16_kernel(const float* __restri
   }
 }
 
+void colsum_bf16_launch_ld(const float* partial, int nrow, int ncol, int ld, int split, bf16* o0, bf16* o1,
+                           hipStream_t st, int accumulate) {
+  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((ncol + 63) / 64), dim3(1024), 0, st, partial, nrow,
+                     ncol, ld, split, o0, o1, accumulate);
+}
+
 void colsum_bf16_launch(const float* partial, int nrow, int ncol, int split, bf16* o0, bf16* o1,
                         hipStream_t st, int accumulate) {
-  hipLaunchKernelGGL(colsum_bf16_kernel, dim3((ncol + 63) / 64), dim3(1024), 0, st, partial, nrow,
-                     ncol, split, o0, o1, accumulate);
+  colsum_bf16_launch_ld(partial, nrow, ncol, ncol, split, o0, o1, st, accumulate);
 }
 
 template <int NV>
@@ -540,9 +549,25 @@ int ln_bwd_partial_rows(int rows, int D) {
   return ln_bwd_cs_ok(D) ? ln_bwd_cs_blocks(rows) : ln_bwd_num_blocks(rows);
 }
 
+bool ln_bwd_dxsum_ok(int D) { return ln_bwd_cs_ok(D); }
+
+// dxsum (optional, cs path only; partial sized [rows][3D] then): bf16 vector += the
+// column sums of dx (accumulated into an existing main gradient).
 void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* mean,
                    const float* rstd, const bf16* dres, bf16* dx, float* partial, bf16* dg,
-                   bf16* db, int rows, int D, hipStream_t st) {
+                   bf16* db, int rows, int D, hipStream_t st, bf16* dxsum) {
+  if (dxsum && ln_bwd_cs_ok(D)) {
+    const int nb = ln_bwd_cs_blocks(rows);
+    if (dres)
+      hipLaunchKernelGGL((ln_bwd_cs_kernel<2, true, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd, dres,
+                         dx, partial, rows, D);
+    else
+      hipLaunchKernelGGL((ln_bwd_cs_kernel<2, false, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd,
+                         dres, dx, partial, rows, D);
+    colsum_bf16_launch_ld(partial, nb, 2 * D, 3 * D, D, dg, db, st, 0);
+    colsum_bf16_launch_ld(partial + 2 * D, nb, D, 3 * D, D, dxsum, dxsum, st, 1);
+    return;
+  }
   if (ln_bwd_cs_ok(D)) {
     const int nb = ln_bwd_cs_blocks(rows);
     if (g_ln_bwd_variant == 3) {  // two rows per iteration (fewer VGPRs, more waves)

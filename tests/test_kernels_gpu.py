@@ -113,7 +113,17 @@ def test_cross_entropy(C, rows, V, stride):
     assert lg.grad[0].abs().max().item() == 0
 
 
-def test_adamw_matches_reference(C):
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_adamw_matches_reference(C, variant):
+    """variant: bit 0 non-temporal loads/stores, bit 1 two vectors per thread."""
+    C.adamw_config(variant)
+    try:
+        _adamw_check()
+    finally:
+        C.adamw_config(0)
+
+
+def _adamw_check():
     from cluster_anywhere_amd.ops.optim import FusedAdamW
 
     torch.manual_seed(3)
@@ -268,3 +278,67 @@ def test_flash_attention_d64_spiky(C, B, T, H, causal, amp):
     g, gr = qkv.grad.view(B, T, 3, H, D), qf.grad.view(B, T, 3, H, D)
     for i, name in enumerate("qkv"):
         assert _rel(g[:, :, i], gr[:, :, i]) < 4e-2, (name, _rel(g[:, :, i], gr[:, :, i]))
+
+
+@pytest.mark.parametrize("T,causal", [(1024, True), (200, True), (333, False)])
+def test_flash_bwd_qkv_bias_grad(C, T, causal):
+    """The D = 64 backward's bias-gradient epilogue equals the column sums of the
+    dqkv it writes (fp32 reference: sum of the stored bf16 gradient)."""
+    torch.manual_seed(7)
+    B, H, D = 2, 5, 64
+    qkv = (torch.randn(B, T, 3 * H * D, device="cuda") * 0.5).bfloat16()
+    out, lse = C.flash_attn_fwd(qkv, H, causal)
+    dout = torch.randn_like(out)
+    db = torch.zeros(3 * H * D, device="cuda")
+    dqkv = C.flash_attn_bwd(qkv, out, dout, lse, H, causal, db)
+    ref = dqkv.float().reshape(-1, 3 * H * D).sum(0)
+    assert _rel(db, ref) < 1e-2
+    dqkv2 = C.flash_attn_bwd(qkv, out, dout, lse, H, causal)
+    assert torch.equal(dqkv, dqkv2)
+
+
+def test_gpt2_fused_qkv_bias_grad_matches(monkeypatch):
+    """GPT-2 block grads in the flat main-grad buffer: qkv bias gradient from the
+    attention backward and proj / fc2 bias gradients from the LayerNorm backward ==
+    the linears' own column-sum passes."""
+    import cluster_anywhere_amd.models.gpt2 as G
+    from cluster_anywhere_amd.parallel.flat import FlatParamSpace
+
+    torch.manual_seed(3)
+    cfg = G.GPT2Config(n_layer=2, n_head=5, n_embd=320, n_positions=256, vocab_size=1000)
+    x = torch.randint(0, cfg.vocab_size, (4, 257), device="cuda")
+    grads = []
+    for fused in (True, False):
+        torch.manual_seed(3)
+        m = G.GPT2(cfg).cuda()
+        flat = FlatParamSpace(m, dtype=torch.bfloat16)
+        monkeypatch.setattr(G, "_FUSED_QKV_BGRAD", True)  # the opt-in qkv path too
+        if not fused:
+            monkeypatch.setattr(G, "flash_path", lambda *a: False)
+            monkeypatch.setattr(G, "ln_bias_fusion_ok", lambda *a: False)
+        flat.zero_grad()
+        m(x[:, :-1], x[:, 1:]).backward()
+        grads.append({n: p.main_grad.float().clone() for n, p in m.named_parameters()})
+    for n in grads[0]:
+        assert _rel(grads[0][n], grads[1][n]) < 2e-2, n
+
+
+@pytest.mark.parametrize("with_res", [False, True])
+def test_layernorm_bwd_dxsum(C, with_res):
+    """The LayerNorm backward's extra output: column sums of dx accumulated into a
+    bf16 vector (the residual-branch producer's bias gradient)."""
+    torch.manual_seed(8)
+    rows, D = 777, 1600
+    x = torch.randn(rows, D, device="cuda").bfloat16()
+    g = (1 + 0.1 * torch.randn(D, device="cuda")).bfloat16()
+    b = torch.zeros(D, device="cuda").bfloat16()
+    y, mean, rstd, s = C.layernorm_fwd(x, None, g, b, 1e-5)
+    dy = torch.randn_like(x)
+    dres = torch.randn_like(x) if with_res else None
+    assert C.ln_bwd_dxsum_ok(D)
+    acc = torch.full((D,), 0.5, device="cuda").bfloat16()
+    dx, dg, db = C.layernorm_bwd(dy, x, g, mean, rstd, dres, acc)
+    dx2, dg2, db2 = C.layernorm_bwd(dy, x, g, mean, rstd, dres)
+    assert torch.equal(dx, dx2) and torch.equal(dg, dg2) and torch.equal(db, db2)
+    ref = dx.float().sum(0) + 0.5
+    assert _rel(acc, ref) < 1e-2
