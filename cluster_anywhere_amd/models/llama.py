@@ -119,10 +119,12 @@ class Llama(nn.Module):
         """Decode-side copies of the weight-streaming GEMMs for ``decode_gemm.hip``
         (batch <= 128): ``w_gate_up`` with gate/up rows interleaved in 64-row blocks
         (SwiGLU fused into the GEMM epilogue, no [B, 2F] intermediate) and
-        ``w_down`` / the vocabulary projection, all prepacked in the kernel's
-        streaming order. qkv and o stay on hipBLASLt, which measured faster at
-        those widths (``tools/bench_decode_gemm3.py``). Costs one extra copy of
-        those weights in HBM (about 11.5 GB for Llama-3-8B), taken before the KV
+        ``w_down`` / ``w_qkv`` / ``w_o`` / the vocabulary projection, all prepacked
+        in the kernel's streaming order. With the split-K partials combined by a
+        separate reduce launch the kernel also beats hipBLASLt at the qkv / o
+        widths (``tools/bench_decode_gemm3.py --sweep``,
+        ``profiles/decode_gemm_ext_reduce_r3.jsonl``). Costs one extra copy of
+        those weights in HBM (about 14 GB for Llama-3-8B), taken before the KV
         cache is sized. Returns whether the decode path uses them."""
         import os
 
@@ -135,11 +137,25 @@ class Llama(nn.Module):
             self._dec = None
             return False
         head = self.embed if self.lm_head is None else self.lm_head
-        layers = [(L.pack_decode_weight(L.interleave_gate_up(l.w_gate_up)), L.pack_decode_weight(l.w_down))
-                  for l in self.layers]
-        self._dec = {"layers": layers,
-                     "head": L.pack_decode_weight(head) if head.shape[0] % 128 == 0 else None}
-        shapes = [(l.w_down.shape[0], l.w_down.shape[1]) for l in self.layers[:1]]
+        attn_ok = os.environ.get("CAAMD_DECODE_ATTN_GEMM", "1") == "1" and all(
+            l.w_qkv.shape[0] % 128 == 0 and l.w_o.shape[0] % 128 == 0 for l in self.layers)
+        # CAAMD_DECODE_NORM_FUSED=1: RMSNorms folded into the GEMMs that consume them
+        # (norm weights in the weight columns, row statistics taken by the producer
+        # waves while x streams through, residual adds in the o / down epilogues: no
+        # rmsnorm launches in the layer). Measured level with the separate rmsnorm
+        # launches (TPOT 6.89 vs 6.88 ms, profiles/llm_decode_norm_fold_r3.txt: the
+        # statistics cost gate/up 5 us of its 50), so opt-in.
+        norm = attn_ok and os.environ.get("CAAMD_DECODE_NORM_FUSED", "0") == "1"
+        fold = (lambda w, g: L.fold_norm(w, g)) if norm else (lambda w, g: w)
+        layers = [(L.pack_decode_weight(fold(L.interleave_gate_up(l.w_gate_up), l.mlp_norm)),
+                   L.pack_decode_weight(l.w_down)) for l in self.layers]
+        attn = None
+        if attn_ok:
+            attn = [(L.pack_decode_weight(fold(l.w_qkv, l.attn_norm)), L.pack_decode_weight(l.w_o))
+                    for l in self.layers]
+        self._dec = {"layers": layers, "attn": attn, "norm": norm,
+                     "head": L.pack_decode_weight(fold(head, self.final_norm)) if head.shape[0] % 128 == 0 else None}
+        shapes = [tuple(w.shape) for l in self.layers[:1] for w in (l.w_down, l.w_qkv, l.w_o)]
         L.decode_gemm_reserve(self.embed.device, shapes)
         return True
 
@@ -188,15 +204,21 @@ class Llama(nn.Module):
         res = None
         pos = positions.to(torch.int32)
         dec = self._dec if (self._dec is not None and tokens.shape[0] <= 128) else None
+        if dec is not None and dec["norm"]:
+            return self._decode_folded(x, dec, cs, pos, slots, k_caches, v_caches, block_tables, ctx_lens, max_ctx)
         for i, layer in enumerate(self.layers):
             h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
             if res is None:
                 res = x
             # decode GEMMs stream the weights once: the skinny MFMA kernel (<= 128 rows)
-            qkv = L.decode_linear(h, layer.w_qkv)  # [B, (H+2KVH)*hd]
-            L.rope_cache_(qkv, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
+            att = dec["attn"][i] if (dec is not None and dec["attn"] is not None) else None
+            qkv = L.decode_gemm_qkv_rope(h, att[0], cs, pos, slots, k_caches[i], v_caches[i], H, KVH) \
+                if att else None
+            if qkv is None:
+                qkv = L.decode_gemm(h, att[0], 0, packed=True) if att else L.decode_linear(h, layer.w_qkv)
+                L.rope_cache_(qkv, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
             o = L.paged_decode_attention(qkv, k_caches[i], v_caches[i], block_tables, ctx_lens, max_ctx, H)
-            x = L.decode_linear(o, layer.w_o)
+            x = L.decode_gemm(o, att[1], 0, packed=True) if att else L.decode_linear(o, layer.w_o)
             h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
             if dec is not None:  # SwiGLU in the gate/up GEMM epilogue, packed weight streams
                 gu, dn = dec["layers"][i]
@@ -208,6 +230,28 @@ class Llama(nn.Module):
             return L.decode_gemm(h, dec["head"], 0, packed=True)
         w = self.embed if self.lm_head is None else self.lm_head
         return L.decode_linear(h, w)
+
+    def _decode_folded(self, x, dec, cs, pos, slots, k_caches, v_caches, block_tables, ctx_lens, max_ctx):
+        """Decode layers with every RMSNorm folded into the GEMM that consumes it:
+        per layer qkv(+RoPE +cache append) -> paged attention -> o (+residual) ->
+        gate/up (SwiGLU) -> down (+residual); ``u`` is the residual stream."""
+        cfg = self.cfg
+        H, KVH, eps = cfg.n_head, cfg.n_kv_head, cfg.norm_eps
+        u = x
+        for i in range(len(self.layers)):
+            wq, wo = dec["attn"][i]
+            gu, dn = dec["layers"][i]
+            qkv = L.decode_gemm_qkv_rope(u, wq, cs, pos, slots, k_caches[i], v_caches[i], H, KVH, norm_eps=eps)
+            if qkv is None:
+                qkv = L.decode_gemm(u, wq, 0, packed=True, norm_eps=eps)
+                L.rope_cache_(qkv, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
+            o = L.paged_decode_attention(qkv, k_caches[i], v_caches[i], block_tables, ctx_lens, max_ctx, H)
+            u = L.decode_gemm(o, wo, 1, residual=u, packed=True)
+            u = L.decode_gemm(L.decode_gemm(u, gu, 2, packed=True, norm_eps=eps), dn, 1, residual=u, packed=True)
+        if dec["head"] is not None:
+            return L.decode_gemm(u, dec["head"], 0, packed=True, norm_eps=eps)
+        h, _ = L.rms_norm(u, self.final_norm, eps)
+        return L.decode_linear(h, self.embed if self.lm_head is None else self.lm_head)
 
     # ------------------------------------------------ reference full forward
     @torch.no_grad()

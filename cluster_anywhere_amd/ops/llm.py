@@ -107,10 +107,13 @@ def decode_gemm_splits(N: int, K: int, cus: int = 256) -> int:
 
 
 def _dg_ws(dev, floats: int, tickets: int):
+    """(partials, tickets, row statistics) of the decode GEMM; the row-statistics
+    buffer holds [slabs][splits][128] sums of squares for the folded RMSNorm."""
     ws = _DG_WS.get(dev.index)
     if ws is None or ws[0].numel() < floats or ws[1].numel() < tickets:
         ws = (torch.empty(max(floats, 1), device=dev, dtype=torch.float32),
-              torch.zeros(max(tickets, 1024), device=dev, dtype=torch.int32))
+              torch.zeros(max(tickets, 1024), device=dev, dtype=torch.int32),
+              torch.empty(max(floats // 128, 1024 * 128), device=dev, dtype=torch.float32))
         _DG_WS[dev.index] = ws
     return ws
 
@@ -136,16 +139,52 @@ def decode_gemm_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def decode_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, residual: Optional[torch.Tensor] = None,
-                splits: Optional[int] = None, packed: bool = False) -> torch.Tensor:
+                splits: Optional[int] = None, packed: bool = False, norm_eps: Optional[float] = None) -> torch.Tensor:
     """``x @ w.T`` (epi 0), ``+ residual`` (epi 1) or SwiGLU over a 64-row-interleaved
     gate/up weight (epi 2, see :func:`interleave_gate_up`) on the decode GEMM v3.
-    ``packed``: ``w`` is in :func:`pack_decode_weight` order."""
+    ``packed``: ``w`` is in :func:`pack_decode_weight` order. ``norm_eps``: RMSNorm
+    folded in — ``rmsnorm(x) @ w.T`` with the norm weight already multiplied into
+    ``w``'s columns (:func:`fold_norm`); the row statistics are gathered while x
+    streams through the GEMM, so no separate normalisation pass runs."""
     M, K = x.shape
     N = w.shape[0]
     s = splits or decode_gemm_splits(N, K, _cus(x.device))
     y = torch.empty(M, N // 2 if epi == 2 else N, device=x.device, dtype=torch.bfloat16)
-    part, tick = _dg_ws(x.device, (N // 128) * s * 16384 if s > 1 else 1, N // 128)
-    kernels().decode_gemm(x, w, y, residual, part, tick, epi, s, packed)
+    part, tick, ssp = _dg_ws(x.device, (N // 128) * s * 16384 if s > 1 else 1, N // 128)
+    kernels().decode_gemm(x, w, y, residual, part, tick, epi, s, packed,
+                          ssp if norm_eps is not None else None, float(norm_eps or 0.0))
+    return y
+
+
+def fold_norm(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """``w [N, K]`` with the RMSNorm weight ``g [K]`` multiplied into its columns
+    (``rmsnorm(x) @ w.T == rsqrt-scaled x @ fold_norm(w, g).T``), in fp32 then
+    rounded once."""
+    return (w.float() * g.float()[None, :]).to(w.dtype)
+
+
+def decode_gemm_qkv_rope(x: torch.Tensor, w: torch.Tensor, cos_sin: torch.Tensor, positions: torch.Tensor,
+                         slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, H: int,
+                         KVH: int, norm_eps: Optional[float] = None) -> Optional[torch.Tensor]:
+    """qkv projection on the decode GEMM (``w`` prepacked) with RoPE and the paged
+    cache append fused into its split-K reduce launch: the same result as
+    ``decode_gemm`` + :func:`rope_cache_` with one launch and one pass over qkv
+    fewer. Returns None where it does not apply (head_dim != 128, one split, or
+    int64 positions / slots): the caller then runs the two steps."""
+    M, K = x.shape
+    N = w.shape[0]
+    if (k_cache is None or k_cache.shape[-1] != 128 or N != (H + 2 * KVH) * 128 or not decode_gemm_ok(x, w)
+            or positions.dtype != torch.int32 or slots.dtype != torch.int32
+            or _os.environ.get("CAAMD_DECODE_ROPE_FUSED", "1") == "0"):
+        return None
+    s = decode_gemm_splits(N, K, _cus(x.device))
+    if s < 2:
+        return None
+    y = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
+    part, _, ssp = _dg_ws(x.device, (N // 128) * s * 16384, N // 128)
+    kernels().decode_gemm_qkv_rope(x, w, y, part, s, cos_sin, positions.contiguous(), slots.contiguous(),
+                                   k_cache, v_cache, H, KVH, ssp if norm_eps is not None else None,
+                                   float(norm_eps or 0.0))
     return y
 
 

@@ -49,9 +49,14 @@ void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* ful
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
+void decode_gemm_config(int ext);
+hipError_t decode_gemm_qkv_rope_launch(const bf16* X, const bf16* W, bf16* Y, float* part, int M, int N, int K,
+                                       int ldx, int ldy, int splits, const float* cs, const int* pos,
+                                       const int* slot, bf16* kc, bf16* vc, int H, int KVH, int BS,
+                                       float* ssp, float eps, hipStream_t st);
 hipError_t decode_gemm_launch(int epi, const bf16* X, const bf16* W, bf16* Y, const bf16* R, float* part,
                               unsigned* tick, int M, int N, int K, int ldx, int ldy, int splits, bool packed,
-                              hipStream_t st);
+                              float* ssp, float eps, hipStream_t st);
 void gemm2_plan(int M, int N, int K, int slots, int max_split, int* full, int* S, int* grid,
                 long long* ws_floats, int* tickets);
 hipError_t gemm2_launch(int layout, int epi, const bf16* A, const bf16* B, bf16* C, const bf16* bias,
@@ -982,8 +987,19 @@ static void gemm2_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi
 // ---- decode GEMM v3 (decode_gemm.hip): y = x . w^T for M <= 128, weight-streaming --------
 // epi 0: y = acc · 1: y = acc + residual · 2: SwiGLU over 64-row-interleaved gate/up weights
 // (y has N/2 columns)
+// ssp (optional): RMSNorm folded in — per-row sums of squares workspace
+// (>= (N/128) * splits * 128 floats); rows of x are scaled by rsqrt(mean(x^2) + eps),
+// the norm weight is expected folded into w's columns.
+static float* ssp_ptr(const c10::optional<Tensor>& ssp, int64_t need) {
+  if (!ssp.has_value()) return nullptr;
+  TORCH_CHECK(ssp->is_cuda() && ssp->scalar_type() == at::kFloat && ssp->numel() >= need,
+              "decode_gemm: row-statistics workspace too small");
+  return ssp->data_ptr<float>();
+}
+
 static void decode_gemm(const Tensor& x, const Tensor& w, Tensor& y, c10::optional<Tensor> residual,
-                        Tensor& part, Tensor& tick, int64_t epi, int64_t splits, bool packed) {
+                        Tensor& part, Tensor& tick, int64_t epi, int64_t splits, bool packed,
+                        c10::optional<Tensor> ssp, double eps) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_BF16(y);
@@ -1014,8 +1030,47 @@ static void decode_gemm(const Tensor& x, const Tensor& w, Tensor& y, c10::option
   hipError_t e = caamd::decode_gemm_launch((int)epi, (const caamd::bf16*)x.data_ptr(), (const caamd::bf16*)w.data_ptr(),
                                            (caamd::bf16*)y.data_ptr(), rp, part.data_ptr<float>(),
                                            reinterpret_cast<unsigned*>(tick.data_ptr<int>()), (int)M, (int)N, (int)K,
-                                           (int)x.stride(0), (int)y.stride(0), (int)splits, packed, cur_stream());
+                                           (int)x.stride(0), (int)y.stride(0), (int)splits, packed,
+                                           ssp_ptr(ssp, (N / 128) * splits * 128), (float)eps, cur_stream());
   TORCH_CHECK(e == hipSuccess, "decode_gemm launch failed: ", hipGetErrorString(e));
+}
+
+// qkv projection on the decode GEMM (w prepacked, head_dim 128, splits > 1) with
+// RoPE and the paged-cache append fused into the split-K reduce launch:
+// y = rope(x . w^T); k / v rows of y also written to their cache slots.
+static void decode_gemm_qkv_rope(const Tensor& x, const Tensor& w, Tensor& y, Tensor& part, int64_t splits,
+                                 const Tensor& cos_sin, const Tensor& positions, const Tensor& slots,
+                                 const Tensor& k_cache, const Tensor& v_cache, int64_t H, int64_t KVH,
+                                 c10::optional<Tensor> ssp, double eps) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(y);
+  CHECK_F32(cos_sin);
+  CHECK_BF16(k_cache);
+  CHECK_BF16(v_cache);
+  for (const Tensor* t : {&positions, &slots}) {
+    CHECK_GPU(*t);
+    CHECK_CONTIG(*t);
+    CHECK_DT(*t, at::kInt);
+  }
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.size(1) == K && w.is_contiguous(), "decode_gemm_qkv_rope: x, w");
+  TORCH_CHECK(M >= 1 && M <= 128 && K % 64 == 0 && N == (H + 2 * KVH) * 128, "decode_gemm_qkv_rope: shapes");
+  TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == N && y.stride(1) == 1, "decode_gemm_qkv_rope: y");
+  TORCH_CHECK(splits >= 2 && K % (64 * splits) == 0, "decode_gemm_qkv_rope: 2 <= splits, K % (64 * splits) == 0");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= (N / 128) * splits * 16384,
+              "decode_gemm_qkv_rope: partial workspace too small");
+  TORCH_CHECK(cos_sin.dim() == 3 && cos_sin.size(1) == 64 && cos_sin.size(2) == 2, "decode_gemm_qkv_rope: cos_sin");
+  TORCH_CHECK(positions.numel() == M && slots.numel() == M, "decode_gemm_qkv_rope: positions / slots");
+  TORCH_CHECK(k_cache.dim() == 4 && k_cache.size(1) == KVH && k_cache.size(3) == 128 &&
+                  v_cache.sizes() == k_cache.sizes() && k_cache.is_contiguous() && v_cache.is_contiguous(),
+              "decode_gemm_qkv_rope: cache must be [num_blocks, KVH, BS, 128]");
+  hipError_t e = caamd::decode_gemm_qkv_rope_launch(
+      (const caamd::bf16*)x.data_ptr(), (const caamd::bf16*)w.data_ptr(), (caamd::bf16*)y.data_ptr(),
+      part.data_ptr<float>(), (int)M, (int)N, (int)K, (int)x.stride(0), (int)y.stride(0), (int)splits,
+      cos_sin.data_ptr<float>(), positions.data_ptr<int>(), slots.data_ptr<int>(), bp(k_cache), bp(v_cache), (int)H,
+      (int)KVH, (int)k_cache.size(2), ssp_ptr(ssp, (N / 128) * splits * 128), (float)eps, cur_stream());
+  TORCH_CHECK(e == hipSuccess, "decode_gemm_qkv_rope launch failed: ", hipGetErrorString(e));
 }
 
 static Tensor transpose_bf16(const Tensor& x) {
@@ -1190,6 +1245,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm2_plan", &gemm2_plan_);
   m.def("gemm2_bf16", &gemm2_bf16);
   m.def("decode_gemm", &decode_gemm);
+  m.def("decode_gemm_qkv_rope", &decode_gemm_qkv_rope);
+  m.def("decode_gemm_config", [](int64_t ext) { caamd::decode_gemm_config((int)ext); });
   m.def("transpose_bf16", &transpose_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("g"),

@@ -112,7 +112,22 @@ struct Args {
   float* part;       // split-K partials: [slabs][splits][BN*128] floats
   unsigned* tick;    // split-K tickets: [slabs], zero between launches
   int M, N, K, ldx, ldy, splits, kchunk;
+  int ext;           // 1: split-K partials only; dg_reduce_kernel combines (own launch)
+  float* ssp;        // RMSNorm folded in: per-row sums of squares of X, [slabs][splits][128]
+                     // (nullptr: plain GEMM); the norm weight is folded into W's columns
+  float eps;
 };
+
+// sum of squares of a lane's 8 X values (the RMSNorm statistic, accumulated while
+// the X tiles stream through for the MFMAs)
+__device__ __forceinline__ float sumsq8(const bf16x8& v, float acc) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const bf16x2 p2 = {v[2 * e], v[2 * e + 1]};
+    acc = __builtin_amdgcn_fdot2_f32_bf16(p2, p2, acc, false);  // v_dot2_f32_bf16
+  }
+  return acc;
+}
 
 // W prepacked (ops/llm.py pack_decode_weight): per 128-row slab and 64-k step the
 // 16 KiB LDS image (swizzle included) is stored contiguously, so a stage is one
@@ -172,6 +187,8 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
   for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[mt][i] = 0.f;
+  float ssq = 0.f;  // producer wave pi = wave - 4, lane l: row 32 pi + (l & 31), half l >> 5
+  const bool rn = p.ssp != nullptr;
 
   if (wprod)
     for (int t = 0; t < min(nsteps, DW); ++t) issue_w(t);
@@ -187,6 +204,19 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
     __builtin_amdgcn_sched_barrier(0);
     if (wprod && t + DW < nsteps) issue_w(t + DW);
     if (xprod && t + DX < nsteps) issue_x(t + DX);
+    if (rn && !consumer) {
+      // the RMSNorm statistic, off the MFMA waves and spread over the four producer
+      // waves (one per SIMD): lane l of producer wave pi sums the squares of half
+      // l >> 5 of row 32 pi + (l & 31) of step t's X image (4 of its 8 16-byte chunks;
+      // the swizzle only permutes chunks within the row); slot t stays valid until
+      // barrier t + 1
+      const lds_t* xr = xring + (t % NXS) * IMG + (32 * (wave - 4) + (lane & 31)) * 128 + (lane >> 5) * 64;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bf16x8 v = *(const __attribute__((address_space(3))) bf16x8*)(xr + c * 16);
+        ssq = sumsq8(v, ssq);
+      }
+    }
     if (consumer) {
       const lds_t* ws = wring + (t % NWS) * IMG;
       const lds_t* xs = xring + (t % NXS) * IMG;
@@ -219,11 +249,16 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
     }
   }
 
+  if (rn && !consumer) ssq += __shfl_xor(ssq, 32, 64);  // both halves: row 32 (wave - 4) + (lane & 31)
+  const int srow = 32 * (wave - 4) + lane;               // valid for producer lanes < 32
+  typedef __attribute__((address_space(3))) float lds_float;
+  lds_float* rsl = (lds_float*)(smem + 32 * 1024);  // row scales [128], past the SwiGLU hand-off
   if (p.splits > 1) {
     // ---- split-K: publish this split; the last arriver combines (release / ticket /
     // acquire: cdna_hip_programming.md §5 "Projection GEMM" item 2)
     float* base = p.part + (size_t)slab * p.splits * (BN * 128);
     float* mine = base + (size_t)split * (BN * 128);
+    if (rn && !consumer && lane < 32) p.ssp[((size_t)slab * p.splits + split) * 128 + srow] = ssq;
     if (consumer) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -233,6 +268,7 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
           *reinterpret_cast<f32x4*>(mine + ((size_t)((wave * 4 + mt) * 4 + q) * 64 + lane) * 4) = v;
         }
     }
+    if (p.ext) return;  // combined by dg_reduce_kernel
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     typedef __attribute__((address_space(3))) int lds_int;
@@ -272,6 +308,25 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
           acc[mt][4 * q + 3] += v[3];
         }
     }
+    if (rn) {
+      if (tid < 128) {
+        float t = 0.f;
+        for (int s2 = 0; s2 < p.splits; ++s2) t += p.ssp[((size_t)slab * p.splits + s2) * 128 + tid];
+        rsl[tid] = __builtin_amdgcn_rsqf(t / (float)p.K + p.eps);
+      }
+      __syncthreads();
+    }
+  } else if (rn) {
+    __syncthreads();  // every wave is past its last ring read
+    if (!consumer && lane < 32) rsl[srow] = __builtin_amdgcn_rsqf(ssq / (float)p.K + p.eps);
+    __syncthreads();
+  }
+  if (rn && consumer) {
+    const int h = lane >> 5;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[mt][i] *= rsl[32 * mt + (i & 3) + 8 * (i >> 2) + 4 * h];
   }
 
   // ---- epilogue: lane (r, h) of wave w holds column n0 + 32w + r, rows
@@ -279,7 +334,6 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
   if constexpr (EPI == EPI_SWIGLU) {
     // waves 0,1: gate columns [32w, 32w+32) of the block; waves 2,3: the matching up
     // columns. Up values go through LDS (the ring is idle now).
-    typedef __attribute__((address_space(3))) float lds_float;
     lds_float* upv = (lds_float*)smem;  // [2 waves][4 mt][16 i][64 lanes]
     __syncthreads();
     if (consumer && wave >= 2) {
@@ -320,6 +374,111 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
   }
 }
 
+// Split-K combine as a launch of its own (decode_gemm_config(1), the default): the GEMM's splits
+// only publish their partial tiles, so no workgroup serially re-reads every split's
+// 64 KiB tile after the stream (the last-arriver combine costs the whole launch one
+// CU's read of splits x 64 KiB; Llama-3-8B batch 128, cold weights: down 41.9 -> 33.9 us,
+// o 22.1 -> 15.8, qkv 25.4 -> 20.3 incl. the reduce launch, profiles/decode_gemm_ext_reduce_r3.jsonl).
+// Thread t of a slab owns one f32x4 of the
+// fragment-ordered tile (4 consecutive rows of one column) and sums the splits in
+// split order: the same bits as the in-kernel combine.
+// RMSNorm row scale from the splits' partial sums of squares (decode_gemm_kernel ssp)
+__device__ __forceinline__ float row_scale(const float* __restrict__ ssp, int slab, int splits, int m, int K,
+                                           float eps) {
+  float t = 0.f;
+  for (int s = 0; s < splits; ++s) t += ssp[((size_t)slab * splits + s) * 128 + m];
+  return __builtin_amdgcn_rsqf(t / (float)K + eps);
+}
+
+template <bool RES>
+__global__ __launch_bounds__(256) void dg_reduce_kernel(const float* __restrict__ part, const bf16* __restrict__ R,
+                                                        bf16* __restrict__ Y, int M, int ldy, int splits,
+                                                        const float* __restrict__ ssp, int K, float eps) {
+  const int slab = blockIdx.x;
+  const int idx = blockIdx.y * 256 + threadIdx.x;  // [0, 4096)
+  const float* base = part + (size_t)slab * splits * (BN * 128) + (size_t)idx * 4;
+  __shared__ float rs[128];
+  if (ssp && threadIdx.x < 128) rs[threadIdx.x] = row_scale(ssp, slab, splits, threadIdx.x, K, eps);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int k = 0; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(base + (size_t)k * (BN * 128));
+  if (ssp) __syncthreads();
+  const int lane = idx & 63, t = idx >> 6;
+  const int q = t & 3, mt = (t >> 2) & 3, wave = t >> 4;
+  const int col = slab * BN + 32 * wave + (lane & 31);
+  const int m0 = 32 * mt + 8 * q + 4 * (lane >> 5);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + j;
+    if (m < M) {
+      float v = s[j];
+      if (ssp) v *= rs[m];
+      if constexpr (RES) v += (float)R[(size_t)m * ldy + col];
+      Y[(size_t)m * ldy + col] = (bf16)v;
+    }
+  }
+}
+
+// The qkv projection's reduce launch with RoPE + paged-cache append fused
+// (llm.hip rope_cache_kernel's math on the fp32 sums): head_dim 128 = one 128-column
+// slab = one head, so rotary pair (d, d + 64) is f32x4 idx and idx + 2048 of the
+// slab's fragment-ordered tile (waves w and w + 2). cs: [max_pos, 64, 2] fp32
+// (cos, sin); pos / slot: [M]; cache pages [blocks, KVH, BS, 128].
+__global__ __launch_bounds__(256) void dg_reduce_rope_kernel(const float* __restrict__ part, bf16* __restrict__ Y,
+                                                             int M, int ldy, int splits, const float* __restrict__ cs,
+                                                             const int* __restrict__ pos, const int* __restrict__ slot,
+                                                             bf16* __restrict__ kc, bf16* __restrict__ vc, int H,
+                                                             int KVH, int BS, const float* __restrict__ ssp, int K,
+                                                             float eps) {
+  const int head = blockIdx.x;
+  const int idx = blockIdx.y * 256 + threadIdx.x;  // [0, 2048): waves 0, 1
+  const float* base = part + (size_t)head * splits * (BN * 128) + (size_t)idx * 4;
+  __shared__ float rs[128];
+  if (ssp && threadIdx.x < 128) rs[threadIdx.x] = row_scale(ssp, head, splits, threadIdx.x, K, eps);
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+  for (int k = 0; k < splits; ++k) {
+    a += *reinterpret_cast<const f32x4*>(base + (size_t)k * (BN * 128));
+    b += *reinterpret_cast<const f32x4*>(base + (size_t)k * (BN * 128) + 2048 * 4);
+  }
+  if (ssp) __syncthreads();
+  const int lane = idx & 63, t = idx >> 6;
+  const int q = t & 3, mt = (t >> 2) & 3, wave = t >> 4;
+  const int d = 32 * wave + (lane & 31);  // rotary pair (d, d + 64)
+  const int m0 = 32 * mt + 8 * q + 4 * (lane >> 5);
+  const bool rot = head < H + KVH, cache = head >= H && kc != nullptr;
+  const int kvh = head < H + KVH ? head - H : head - H - KVH;
+  bf16* cbase = head < H + KVH ? kc : vc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + j;
+    if (m >= M) continue;
+    float lo = a[j], hi = b[j];
+    if (ssp) {
+      lo *= rs[m];
+      hi *= rs[m];
+    }
+    if (rot) {
+      const float2 c = *reinterpret_cast<const float2*>(cs + ((size_t)pos[m] * 64 + d) * 2);
+      const float l0 = lo;
+      lo = l0 * c.x - hi * c.y;
+      hi = hi * c.x + l0 * c.y;
+    }
+    const bf16 blo = (bf16)lo, bhi = (bf16)hi;
+    bf16* row = Y + (size_t)m * ldy + head * BN;
+    row[d] = blo;
+    row[d + 64] = bhi;
+    if (cache) {
+      const int sl = slot[m];
+      if (sl >= 0) {
+        bf16* dst = cbase + (((size_t)(sl / BS) * KVH + kvh) * BS + sl % BS) * BN;
+        dst[d] = blo;
+        dst[d + 64] = bhi;
+      }
+    }
+  }
+}
+
 static void ensure_lds(const void* k, int bytes) {
   static std::mutex mu;
   static std::unordered_set<const void*> done;
@@ -351,11 +510,20 @@ static void launch_one(const dg::Args& a, dim3 grid, hipStream_t st) {
   else launch_cfg<EPI, PK, 6, 3>(a, grid, st);
 }
 
+static int g_dg_ext = [] {
+  const char* e = getenv("CAAMD_DG_EXT");
+  return e ? atoi(e) : 1;
+}();
+
+// 0: last-arriver combine inside the GEMM; 1: separate dg_reduce_kernel launch
+void decode_gemm_config(int ext) { g_dg_ext = ext; }
+
 hipError_t decode_gemm_launch(int epi, const bf16* X, const bf16* W, bf16* Y, const bf16* R, float* part,
                               unsigned* tick, int M, int N, int K, int ldx, int ldy, int splits, bool packed,
-                              hipStream_t st) {
+                              float* ssp, float eps, hipStream_t st) {
   if (M < 1 || M > 128 || N % dg::BN || splits < 1 || K % (dg::KS * splits)) return hipErrorInvalidValue;
-  dg::Args a{X, W, Y, R, part, tick, M, N, K, ldx, ldy, splits, K / splits};
+  const int ext = (splits > 1 && epi != dg::EPI_SWIGLU && g_dg_ext) ? 1 : 0;
+  dg::Args a{X, W, Y, R, part, tick, M, N, K, ldx, ldy, splits, K / splits, ext, ssp, eps};
   dim3 grid(N / dg::BN, splits);
   switch (epi * 2 + (packed ? 1 : 0)) {
     case 0: launch_one<dg::EPI_STORE, false>(a, grid, st); break;
@@ -366,6 +534,29 @@ hipError_t decode_gemm_launch(int epi, const bf16* X, const bf16* W, bf16* Y, co
     case 5: launch_one<dg::EPI_SWIGLU, true>(a, grid, st); break;
     default: return hipErrorInvalidValue;
   }
+  if (ext) {
+    if (epi == dg::EPI_RESID)
+      hipLaunchKernelGGL(dg::dg_reduce_kernel<true>, dim3(N / dg::BN, 16), dim3(256), 0, st, part, R, Y, M, ldy,
+                         splits, (const float*)ssp, K, eps);
+    else
+      hipLaunchKernelGGL(dg::dg_reduce_kernel<false>, dim3(N / dg::BN, 16), dim3(256), 0, st, part, R, Y, M, ldy,
+                         splits, (const float*)ssp, K, eps);
+  }
+  return hipGetLastError();
+}
+
+// qkv projection + RoPE + cache append (head_dim 128, splits > 1, W prepacked):
+// the GEMM's splits publish partials, dg_reduce_rope_kernel combines and rotates.
+hipError_t decode_gemm_qkv_rope_launch(const bf16* X, const bf16* W, bf16* Y, float* part, int M, int N, int K,
+                                       int ldx, int ldy, int splits, const float* cs, const int* pos,
+                                       const int* slot, bf16* kc, bf16* vc, int H, int KVH, int BS,
+                                       float* ssp, float eps, hipStream_t st) {
+  if (M < 1 || M > 128 || N % dg::BN || splits < 2 || K % (dg::KS * splits) || N != (H + 2 * KVH) * dg::BN)
+    return hipErrorInvalidValue;
+  dg::Args a{X, W, Y, nullptr, part, nullptr, M, N, K, ldx, ldy, splits, K / splits, 1, ssp, eps};
+  launch_one<dg::EPI_STORE, true>(a, dim3(N / dg::BN, splits), st);
+  hipLaunchKernelGGL(dg::dg_reduce_rope_kernel, dim3(N / dg::BN, 8), dim3(256), 0, st, part, Y, M, ldy, splits, cs,
+                     pos, slot, kc, vc, H, KVH, BS, (const float*)ssp, K, eps);
   return hipGetLastError();
 }
 

@@ -178,25 +178,121 @@ def test_decode_gemm_v3_epilogues(M, N, K, packed):
     assert torch.equal(L.unpack_decode_weight(L.pack_decode_weight(w)), w)
 
 
-def test_llama_decode_gemm_weights():
-    """The model's decode copies (interleaved + packed gate/up, packed down/head)
-    compute the same MLP block and head as the fp32 math on the original weights."""
+@pytest.mark.parametrize("N,K,splits", [(6144, 4096, 4), (4096, 4096, 8), (4096, 14336, 8), (256, 512, 2)])
+def test_decode_gemm_reduce_launch_matches(N, K, splits):
+    """Split-K combined by the separate reduce launch (decode_gemm_config(1)) gives
+    the same bits as the in-kernel last-arriver combine, store and residual epilogues."""
+    torch.manual_seed(N + K)
+    x = torch.randn(128, K, device="cuda", dtype=torch.bfloat16)
+    w = L.pack_decode_weight(torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05)
+    r = torch.randn(128, N, device="cuda", dtype=torch.bfloat16)
+    out = {}
+    try:
+        for ext in (0, 1):
+            L.kernels().decode_gemm_config(ext)
+            out[ext] = (L.decode_gemm(x, w, 0, splits=splits, packed=True),
+                        L.decode_gemm(x, w, 1, residual=r, splits=splits, packed=True))
+    finally:
+        L.kernels().decode_gemm_config(1)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    ref = x.float() @ L.unpack_decode_weight(w).float().t()
+    assert _rel(out[1][0], ref) < 1e-2 and _rel(out[1][1], ref + r.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,H,KVH,K", [(128, 32, 8, 4096), (37, 8, 2, 1024)])
+def test_decode_gemm_qkv_rope(M, H, KVH, K):
+    """qkv GEMM + RoPE + cache append in the split-K reduce launch vs the fp32 GEMM
+    followed by the reference rotation / cache append."""
+    torch.manual_seed(M + H)
+    D, BS, NB = 128, 16, 64
+    N = (H + 2 * KVH) * D
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    cs = L.rope_cos_sin(D, 4096, 500000.0, None, "cuda")
+    pos = torch.randint(0, 4096, (M,), device="cuda", dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device="cuda")[:M].int()
+    slots[min(3, M - 1)] = -1
+    kc = torch.zeros(NB, KVH, BS, D, device="cuda", dtype=torch.bfloat16)
+    vc, kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(kc), torch.zeros_like(kc)
+    y = L.decode_gemm_qkv_rope(x, L.pack_decode_weight(w), cs, pos, slots, kc, vc, H, KVH)
+    assert y is not None
+    ref = (x.float() @ w.float().t())
+    L.rope_cache_ref(ref, cs, pos, slots, kc2.float(), vc2.float(), H, KVH)  # fp32 rotation in place
+    kr, vr = torch.zeros_like(kc, dtype=torch.float32), torch.zeros_like(vc, dtype=torch.float32)
+    L.rope_cache_ref(ref.clone(), cs, torch.zeros_like(pos), slots, kr, vr, H, KVH)  # cos 1 / sin 0: plain append
+    assert _rel(y, ref) < 1e-2
+    assert _rel(kc, kr) < 1e-2 and _rel(vc, vr) < 1e-2
+    assert int((kc != 0).any(-1).sum()) == (M - 1) * KVH  # slot -1 skipped
+
+
+def test_llama_decode_gemm_weights(monkeypatch):
+    """The model's decode copies (interleaved + packed gate/up, packed qkv / o / down /
+    head, RMSNorm weights folded into qkv, gate/up and head) compute the same norm +
+    projections as the fp32 math on the original weights."""
     import torch.nn.functional as F
 
     from cluster_anywhere_amd.models.llama import Llama, LlamaConfig
 
     torch.manual_seed(0)
     m = Llama(LlamaConfig.named("llama-small")).to("cuda", torch.bfloat16).init_weights(std=0.02)
-    assert m.prepare_decode()
+    for lay in m.layers:
+        for g in (lay.attn_norm, lay.mlp_norm):
+            g.data = (1 + 0.2 * torch.randn_like(g.float())).bfloat16()
+    m.final_norm.data = (1 + 0.2 * torch.randn_like(m.final_norm.float())).bfloat16()
+    monkeypatch.setenv("CAAMD_DECODE_NORM_FUSED", "1")
+    assert m.prepare_decode() and m._dec["norm"]
+    eps = m.cfg.norm_eps
     lay = m.layers[1]
     gu, dn = m._dec["layers"][1]
     h = torch.randn(64, m.cfg.d_model, device="cuda", dtype=torch.bfloat16)
-    a = L.decode_gemm(h, gu, 2, packed=True)
-    gate_up = h.float() @ lay.w_gate_up.float().t()
+
+    def normed(g):
+        return L.rms_norm_ref(h, g, eps)[0].float()
+
+    a = L.decode_gemm(h, gu, 2, packed=True, norm_eps=eps)
+    gate_up = normed(lay.mlp_norm) @ lay.w_gate_up.float().t()
     f = m.cfg.ffn_dim
-    a_ref = F.silu(gate_up[:, :f]) * gate_up[:, f:]
-    assert _rel(a, a_ref) < 1e-2
-    y = L.decode_gemm(a, dn, 0, packed=True)
-    assert _rel(y, a.float() @ lay.w_down.float().t()) < 1e-2
-    logits = L.decode_gemm(h, m._dec["head"], 0, packed=True)
-    assert _rel(logits, h.float() @ m.lm_head.float().t()) < 1e-2
+    assert _rel(a, F.silu(gate_up[:, :f]) * gate_up[:, f:]) < 1e-2
+    r = torch.randn(64, m.cfg.d_model, device="cuda", dtype=torch.bfloat16)
+    y = L.decode_gemm(a, dn, 1, residual=r, packed=True)
+    assert _rel(y, a.float() @ lay.w_down.float().t() + r.float()) < 1e-2
+    logits = L.decode_gemm(h, m._dec["head"], 0, packed=True, norm_eps=eps)
+    assert _rel(logits, normed(m.final_norm) @ m.lm_head.float().t()) < 1e-2
+    qkv_w, o_w = m._dec["attn"][1]
+    assert _rel(L.decode_gemm(h, qkv_w, 0, packed=True, norm_eps=eps),
+                normed(lay.attn_norm) @ lay.w_qkv.float().t()) < 1e-2
+    o_in = torch.randn(64, o_w.shape[1], device="cuda", dtype=torch.bfloat16)
+    assert _rel(L.decode_gemm(o_in, o_w, 0, packed=True), o_in.float() @ lay.w_o.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("M", [128, 37])
+def test_llama_decode_folded_norms_match(M, monkeypatch):
+    """One decode step with the RMSNorms folded into the GEMMs (default) vs the
+    unfused decode path (rmsnorm launches, hipBLASLt qkv / o): same logits."""
+    from cluster_anywhere_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(1)
+    m = Llama(LlamaConfig.named("llama-small")).to("cuda", torch.bfloat16).init_weights(std=0.02)
+    for lay in m.layers:
+        for g in (lay.attn_norm, lay.mlp_norm):
+            g.data = (1 + 0.2 * torch.randn_like(g.float())).bfloat16()
+    cfg, BS = m.cfg, 16
+    nb = M * 4 + 4
+    kc = [torch.randn(nb, cfg.n_kv_head, BS, cfg.head_dim, device="cuda", dtype=torch.bfloat16)
+          for _ in range(cfg.n_layer)]
+    vc = [torch.randn_like(t) for t in kc]
+    bt = torch.randperm(nb, device="cuda").int()[: M * 4].view(M, 4).contiguous()
+    ctx = torch.randint(1, 4 * BS + 1, (M,), device="cuda", dtype=torch.int32)
+    pos = (ctx - 1).int()
+    slots = (bt.gather(1, (pos // BS).long()[:, None]).squeeze(1) * BS + pos % BS).int()
+    tok = torch.randint(0, cfg.vocab_size, (M,), device="cuda")
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CAAMD_DECODE_NORM_FUSED", fused)
+        monkeypatch.setenv("CAAMD_DECODE_ATTN_GEMM", fused)
+        assert m.prepare_decode()
+        k2, v2 = [t.clone() for t in kc], [t.clone() for t in vc]
+        out[fused] = (m.decode(tok, pos, slots, k2, v2, bt, ctx, 4 * BS).float(), k2, v2)
+    assert m._dec["norm"] is False
+    assert _rel(out["1"][0], out["0"][0]) < 2e-2
+    assert _rel(torch.stack(out["1"][1]), torch.stack(out["0"][1])) < 1e-2

@@ -134,6 +134,10 @@ def bench():
 if __name__ == "__main__":
     torch.manual_seed(0)
     nbad = check()
+    if "--ext" in sys.argv:  # the same checks with the separate reduce launch
+        L.kernels().decode_gemm_config(1)
+        nbad += check()
+        L.kernels().decode_gemm_config(0)
     if nbad:
         print(f"{nbad} numerics failures", flush=True)
         sys.exit(1)
@@ -145,15 +149,19 @@ if __name__ == "__main__":
             w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
             nw = max(2, -(-(1 << 30) // (N * K * 2)))
             wps = [L.pack_decode_weight(w)] + [L.pack_decode_weight(w) for _ in range(nw - 1)]
-            out = {"sweep": name}
-            for sp in (1, 2, 3, 4, 6, 8, 16):
-                if K % (64 * sp) or (N // 128) * sp > 1024:
-                    continue
-                it = [0]
+            for ext in (0, 1):
+                # ext 1: split-K partials combined by a separate reduce launch
+                L.kernels().decode_gemm_config(ext)
+                out = {"sweep": name, "ext_reduce": ext}
+                for sp in (1, 2, 3, 4, 6, 8, 16):
+                    if K % (64 * sp) or (N // 128) * sp > 1024:
+                        continue
+                    it = [0]
 
-                def nx():
-                    it[0] = (it[0] + 1) % nw
-                    return wps[it[0]]
-                out[sp] = round(timeit(lambda: L.decode_gemm(x, nx(), splits=sp, packed=True)), 1)
-            print(json.dumps(out), flush=True)
+                    def nx():
+                        it[0] = (it[0] + 1) % nw
+                        return wps[it[0]]
+                    out[sp] = round(timeit(lambda: L.decode_gemm(x, nx(), splits=sp, packed=True)), 1)
+                print(json.dumps(out), flush=True)
+            L.kernels().decode_gemm_config(0)
             del wps
