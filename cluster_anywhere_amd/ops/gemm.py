@@ -159,6 +159,11 @@ WGRAD_SK = os.environ.get("CAAMD_WGRAD_SK", "1") == "1"
 # tokens (profiles/wgrad_stream_k.jsonl): GPT-2-XL fc (6400 x 1600, lockstep split-K
 # 2) and attention proj (1600 x 1600, 245 runs). qkv and fc2 stay on hipBLASLt.
 WGRAD_WINNERS = {(6400, 1600): 250, (1600, 1600): 245}
+# extra entries for A/B runs: CAAMD_WGRAD_EXTRA="1600x6400:420,4800x1600:190"
+for _e in filter(None, os.environ.get("CAAMD_WGRAD_EXTRA", "").split(",")):
+    _shape, _runs = _e.split(":")
+    _m, _n = _shape.split("x")
+    WGRAD_WINNERS[(int(_m), int(_n))] = int(_runs)
 
 
 def wgrad_runs(M: int, N: int, K: int) -> Optional[int]:
