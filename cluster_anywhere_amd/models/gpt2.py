@@ -36,6 +36,12 @@ from ..ops.loss import linear_cross_entropy
 # same-box runs (the backward kernels' epilogue reduction costs more than the 52 us
 # column-sum pass it replaces; profiles/step_ab_r3_bias_fusion.txt)
 _FUSED_QKV_BGRAD = os.environ.get("CAAMD_FUSED_QKV_BGRAD", "0") == "1"
+# fc2 weight stored transposed ([4d, d] in memory, the shape stays [d, 4d]): its weight
+# gradient dW^T = u^T dy is then the fc-shaped 6400 x 1600 problem whose 125 tiles x 2
+# splits fill the CUs on gemm.hip, instead of 1600 x 6400 (140 ragged tiles) on
+# hipBLASLt; the dgrad reads the stored layout directly and the forward transposes it
+# once (CAAMD_FC2_T=0: plain layout)
+_FC2_T = os.environ.get("CAAMD_FC2_T", "1") == "1"
 # proj / fc2 bias gradients from the LayerNorm backward (CAAMD_NO_FUSED_LN_BGRAD=1: own passes)
 _FUSED_LN_BGRAD = os.environ.get("CAAMD_NO_FUSED_LN_BGRAD", "0") != "1"
 
@@ -83,7 +89,7 @@ class Block(nn.Module):
         self.ln2_b = nn.Parameter(torch.zeros(d))
         self.fc_w = nn.Parameter(torch.empty(4 * d, d))
         self.fc_b = nn.Parameter(torch.zeros(4 * d))
-        self.fc2_w = nn.Parameter(torch.empty(d, 4 * d))
+        self.fc2_w = nn.Parameter(torch.empty(4 * d, d).t() if _FC2_T else torch.empty(d, 4 * d))
         self.fc2_b = nn.Parameter(torch.zeros(d))
         std = 0.02
         nn.init.normal_(self.attn_w, std=std)

@@ -40,16 +40,29 @@ def _ready(p):
 def _wgrad(w, dy2, x2, needs):
     mg = getattr(w, "main_grad", None)
     if mg is not None:
+        a, b, c = dy2, x2, mg
+        if mg.dim() == 2 and not mg.is_contiguous() and mg.t().is_contiguous():
+            a, b, c = x2, dy2, mg.t()  # transposed storage: dW^T += X^T dY
         runs = None
-        if mg.is_cuda and mg.dtype == torch.bfloat16 and _g._ok(dy2, x2, mg):
-            runs = _g.wgrad_runs(mg.shape[0], mg.shape[1], dy2.shape[0])
+        if c.is_cuda and c.dtype == torch.bfloat16 and _g._ok(a, b, c):
+            runs = _g.wgrad_runs(c.shape[0], c.shape[1], a.shape[0])
         if runs is not None:
-            _g.run_sk(dy2, x2, mg, 2, True, runs=runs)  # dW += dY^T X (gemm.hip, split-K / stream-K)
+            _g.run_sk(a, b, c, 2, True, runs=runs)  # c += a^T b (gemm.hip, split-K / stream-K)
         else:
-            mg.addmm_(dy2.t(), x2)
+            c.addmm_(a.t(), b)
         _ready(w)
         return None
     return dy2.t() @ x2 if needs else None
+
+
+def _wt(w):
+    """W^T as a contiguous [K_in, N_out] (free for a transposed-storage weight)."""
+    return w.t() if (not w.is_contiguous() and w.t().is_contiguous()) else _g.transpose(w)
+
+
+def _wn(w):
+    """W as a contiguous [N_out, K_in] (one transpose for a transposed-storage weight)."""
+    return _g.transpose(w.t()) if (not w.is_contiguous() and w.t().is_contiguous()) else w
 
 
 def _bgrad(b, dy2, needs):
@@ -101,7 +114,7 @@ class _MainGradMLP(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, b2_grad=True):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         u, z = _g.linear_gelu(x2, w1, b1)
-        y = _g.linear_nt(u, w2, b2)
+        y = _g.linear_nt(u, _wn(w2), b2)
         ctx.save_for_backward(x2, w1, w2, u, z)
         ctx.b = (b1, b2 if b2_grad else None)
         ctx.xshape = x.shape
@@ -115,7 +128,7 @@ class _MainGradMLP(torch.autograd.Function):
         gw2 = _wgrad(w2, dy2, u, ctx.needs_input_grad[3])
         gb2 = _bgrad(b2, dy2, ctx.needs_input_grad[4])
         db1 = torch.zeros(w1.shape[0], device=dy2.device, dtype=torch.float32)
-        dz = _g.dgrad_dgelu(dy2, _g.transpose(w2), z, db1)
+        dz = _g.dgrad_dgelu(dy2, _wt(w2), z, db1)
         gb1 = None
         bmg = getattr(b1, "main_grad", None)
         if bmg is not None:
@@ -158,7 +171,8 @@ def mlp(x, w1, b1, w2, b2, b2_grad: bool = True):
     x2 = x.reshape(-1, x.shape[-1])
     if (_FUSED_MLP and use_gpu_kernel(x, w1, w2) and b1 is not None and getattr(w1, "main_grad", None) is not None
             and getattr(w2, "main_grad", None) is not None and x.requires_grad
-            and _g.supported(x2, w1) and _g.tile_for(x2.shape[0], w2.shape[0], w2.shape[1]) is not None
+            and _g.supported(x2, w1) and (w2.is_contiguous() or w2.t().is_contiguous())
+            and _g.tile_for(x2.shape[0], w2.shape[0], w2.shape[1]) is not None
             and _g.tile_for(x2.shape[0], w2.shape[1], w2.shape[0]) is not None):
         return _MainGradMLP.apply(x, w1, b1, w2, b2, b2_grad)
     return linear(bias_gelu(linear(x, w1), b1), w2, b2, bias_grad=b2_grad)

@@ -41,6 +41,24 @@ class ParamSlot:
     decay: bool
 
 
+def _phys(t: torch.Tensor) -> Optional[torch.Tensor]:
+    """A 2-D parameter stored transposed (``t.t()`` contiguous, e.g. GPT-2's fc2
+    weight kept as [in, out] so its weight gradient tiles the CUs): its physical
+    [in, out] view; None for a contiguous parameter."""
+    if t.dim() == 2 and not t.is_contiguous() and t.t().is_contiguous():
+        return t.t()
+    return None
+
+
+def _slot_view(buf: torch.Tensor, offset: int, like: torch.Tensor) -> torch.Tensor:
+    """``buf[offset:offset + like.numel()]`` viewed with ``like``'s shape AND memory
+    layout (so the flat order of the param, its gradient, the fp32 master and the
+    Adam moments stay elementwise aligned for transposed parameters too)."""
+    flat = buf[offset: offset + like.numel()]
+    ph = _phys(like)
+    return flat.view(ph.shape).t() if ph is not None else flat.view_as(like)
+
+
 def default_decay_rule(name: str, p: torch.Tensor) -> bool:
     """GPT-style: decay matrices/embeddings, not biases or norm gains."""
     return p.dim() >= 2
@@ -87,12 +105,13 @@ class FlatParamSpace:
         with torch.no_grad():
             for s in self.slots:
                 src = s.param.detach()
-                if master is not None:
-                    master[s.offset : s.offset + s.numel].copy_(src.reshape(-1).float())
-                view = self.param_buffer[s.offset : s.offset + s.numel].view_as(src)
+                ph = _phys(src)
+                if master is not None:  # physical (storage) order, like the views below
+                    master[s.offset : s.offset + s.numel].copy_((ph if ph is not None else src).reshape(-1).float())
+                view = _slot_view(self.param_buffer, s.offset, src)
                 view.copy_(src)
                 s.param.data = view
-                s.param.grad = self.grad_buffer[s.offset : s.offset + s.numel].view_as(src)
+                s.param.grad = _slot_view(self.grad_buffer, s.offset, src)
                 # fused layers (ops.linear) accumulate straight into this view
                 s.param.main_grad = s.param.grad
                 if s.decay:
@@ -107,7 +126,7 @@ class FlatParamSpace:
         for s in self.slots:
             g = s.param.grad
             if g is None or g.data_ptr() != self.grad_buffer[s.offset :].data_ptr():
-                s.param.grad = self.grad_buffer[s.offset : s.offset + s.numel].view_as(s.param)
+                s.param.grad = _slot_view(self.grad_buffer, s.offset, s.param)
 
     def param_index(self) -> Dict[int, ParamSlot]:
         return {id(s.param): s for s in self.slots}

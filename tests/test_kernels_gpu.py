@@ -120,7 +120,7 @@ def test_adamw_matches_reference(C, variant):
     try:
         _adamw_check()
     finally:
-        C.adamw_config(0)
+        C.adamw_config(2)  # the default (adamw.hip g_adam_variant)
 
 
 def _adamw_check():
@@ -321,6 +321,40 @@ def test_gpt2_fused_qkv_bias_grad_matches(monkeypatch):
         grads.append({n: p.main_grad.float().clone() for n, p in m.named_parameters()})
     for n in grads[0]:
         assert _rel(grads[0][n], grads[1][n]) < 2e-2, n
+
+
+@pytest.mark.parametrize("d,layers,batch", [(320, 2, 4), (1600, 1, 16)])
+def test_gpt2_fc2_transposed_storage(d, layers, batch, monkeypatch):
+    """fc2 weight stored transposed (default): same loss and gradients as the plain
+    layout; at d = 1600 with 16k tokens its weight gradient runs on gemm.hip's
+    split-K kernel (the 6400 x 1600 shape) into the transposed main-grad view."""
+    import cluster_anywhere_amd.models.gpt2 as G
+    from cluster_anywhere_amd.ops import gemm as _g
+    from cluster_anywhere_amd.parallel.flat import FlatParamSpace
+
+    cfg = G.GPT2Config(n_layer=layers, n_head=d // 64, n_embd=d, n_positions=1024, vocab_size=1000)
+    torch.manual_seed(5)
+    x = torch.randint(0, cfg.vocab_size, (batch, 1025 if d == 1600 else 257), device="cuda")
+    state, out = None, []
+    for t in (False, True):
+        monkeypatch.setattr(G, "_FC2_T", t)
+        torch.manual_seed(5)
+        m = G.GPT2(cfg).cuda()
+        assert m.blocks[0].fc2_w.is_contiguous() != t
+        if state is None:
+            state = {k: v.detach().clone() for k, v in m.state_dict().items()}
+        else:
+            m.load_state_dict(state)
+        flat = FlatParamSpace(m, dtype=torch.bfloat16)
+        flat.zero_grad()
+        loss = m(x[:, :-1], x[:, 1:])
+        loss.backward()
+        out.append((loss.item(), {n: p.main_grad.float().clone() for n, p in m.named_parameters()}))
+        if t and d == 1600:
+            assert _g.wgrad_runs(4 * d, d, batch * 1024) is not None  # the gemm.hip path ran
+    assert abs(out[0][0] - out[1][0]) < 1e-2
+    for n in out[0][1]:
+        assert _rel(out[0][1][n], out[1][1][n]) < 2e-2, n
 
 
 @pytest.mark.parametrize("with_res", [False, True])
