@@ -237,6 +237,16 @@ def dgrad_dgelu(dy2: torch.Tensor, wt: torch.Tensor, z: torch.Tensor, dbias_f32:
     return _run(dy2, wt, out, EPI_DGELU, z=z, dbias=dbias_f32)
 
 
+def linear_nn(x2: torch.Tensor, wt: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x2 @ wt (+ b)`` with ``wt = W^T`` row-major [K_in, N_out] (layout 1: the
+    B tile is read with the hardware transpose reads, no weight transpose pass)."""
+    M, K = x2.shape
+    N = wt.shape[1]
+    out = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)
+    bm, bn = tile_for(M, N, K)
+    return run_pp(x2, wt, out, 1, EPI_BF16, bm, bn, bias=b)
+
+
 def transpose(w: torch.Tensor) -> torch.Tensor:
     if w.is_cuda and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0:
         return kernels().transpose_bf16(w.contiguous())

@@ -114,7 +114,10 @@ class _MainGradMLP(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, b2_grad=True):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         u, z = _g.linear_gelu(x2, w1, b1)
-        y = _g.linear_nt(u, _wn(w2), b2)
+        if _FC2_NN and not w2.is_contiguous():
+            y = _g.linear_nn(u, w2.t(), b2)  # transposed storage read as the NN layout
+        else:
+            y = _g.linear_nt(u, _wn(w2), b2)
         ctx.save_for_backward(x2, w1, w2, u, z)
         ctx.b = (b1, b2 if b2_grad else None)
         ctx.xshape = x.shape
@@ -161,6 +164,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias=None, bias_grad: bool = T
 # fused MLP wins in the real step (86.8k / 86.6k vs 85.9k / 85.8k tok/s, alternating
 # runs on one box), so it is the default (CAAMD_FUSED_MLP=0 selects the unfused path).
 _FUSED_MLP = os.environ.get("CAAMD_FUSED_MLP", "1") == "1"
+# fc2 forward from its transposed storage on the NN layout instead of transpose + NT
+_FC2_NN = os.environ.get("CAAMD_FC2_NN", "0") == "1"
 
 
 def mlp(x, w1, b1, w2, b2, b2_grad: bool = True):
