@@ -71,7 +71,8 @@ def train_loop_per_worker(cfg):
     on_gpu = device.type == "cuda"
     torch.manual_seed(1234)
     mcfg = GPT2Config.named(cfg["model"])
-    model = GPT2(mcfg).to(device)
+    with torch.device(device):  # random init straight in HBM (no 6 GB host copy per rank)
+        model = GPT2(mcfg)
     step = DataParallelStep(model, lr=1e-4, weight_decay=0.1, max_grad_norm=1.0,
                             bucket_cap_mb=cfg["bucket_mb"], zero=bool(cfg["zero"]) and world > 1)
     B, T = cfg["micro_batch"], cfg["seq_len"]
