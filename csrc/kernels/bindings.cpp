@@ -480,7 +480,7 @@ bool paged_decode_launch(const bf16*, int, const bf16*, const bf16*, const int*,
 int paged_max_parts(int);
 int paged_mfma_max_parts(int);
 bool paged_decode_mfma_launch(const bf16*, int, const bf16*, const bf16*, const int*, int, const int*, bf16*,
-                              float*, float*, int, int, int, int, int, int, float, hipStream_t);
+                              float*, float*, int, int, int, int, int, int, float, unsigned*, hipStream_t);
 void fa_fwd_gqa_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
                        int, hipStream_t);
 }
@@ -591,7 +591,8 @@ void rope_cache_(Tensor& qkv, const Tensor& cos_sin, const Tensor& positions, co
 // impl: -1 auto (MFMA kernel for D=128 / 16-token pages / G <= 16 unless CAAMD_PAGED_MFMA=0),
 //        0 the VALU kernel, 1 the MFMA kernel
 Tensor paged_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
-                    const Tensor& ctx_lens, int64_t max_ctx, int64_t H, double scale, int64_t impl) {
+                    const Tensor& ctx_lens, int64_t max_ctx, int64_t H, double scale, int64_t impl,
+                    c10::optional<Tensor> tickets) {
   CHECK_GPU(q);
   CHECK_DT(q, at::kBFloat16);
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "paged_decode: q must be [B, >=H*D] with unit inner stride");
@@ -624,11 +625,22 @@ Tensor paged_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cach
     pml = at::empty({B, H, mp, 2}, q.options().dtype(at::kFloat));
   }
   if (B > 0) {
-    auto launch = impl == 1 ? caamd::paged_decode_mfma_launch : caamd::paged_decode_launch;
-    const bool ok = launch(
-        bp(q), (int)q.stride(0), bp(k_cache), bp(v_cache), block_tables.data_ptr<int>(), (int)block_tables.size(1),
-        ctx_lens.data_ptr<int>(), bp(out), mp > 1 ? pacc.data_ptr<float>() : nullptr,
-        mp > 1 ? pml.data_ptr<float>() : nullptr, B, (int)H, KVH, D, BS, (int)max_ctx, (float)scale, cur_stream());
+    unsigned* tk = nullptr;  // MFMA kernel: the last partition block merges (no reduce launch)
+    if (impl == 1 && tickets.has_value()) {
+      TORCH_CHECK(tickets->is_cuda() && tickets->scalar_type() == at::kInt && tickets->numel() >= B * KVH,
+                  "paged_decode: tickets must be >= B * KVH zeroed int32");
+      tk = reinterpret_cast<unsigned*>(tickets->data_ptr<int>());
+    }
+    float* pa = mp > 1 ? pacc.data_ptr<float>() : nullptr;
+    float* pm = mp > 1 ? pml.data_ptr<float>() : nullptr;
+    const bool ok = impl == 1
+        ? caamd::paged_decode_mfma_launch(bp(q), (int)q.stride(0), bp(k_cache), bp(v_cache),
+                                          block_tables.data_ptr<int>(), (int)block_tables.size(1),
+                                          ctx_lens.data_ptr<int>(), bp(out), pa, pm, B, (int)H, KVH, D, BS,
+                                          (int)max_ctx, (float)scale, tk, cur_stream())
+        : caamd::paged_decode_launch(bp(q), (int)q.stride(0), bp(k_cache), bp(v_cache), block_tables.data_ptr<int>(),
+                                     (int)block_tables.size(1), ctx_lens.data_ptr<int>(), bp(out), pa, pm, B, (int)H,
+                                     KVH, D, BS, (int)max_ctx, (float)scale, cur_stream());
     TORCH_CHECK(ok, "paged_decode: unsupported head_dim/group (D in {64,128}, H/KVH in {1,2,4,8})");
     LAUNCH_CHECK();
   }
@@ -1278,7 +1290,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_cache_", &rope_cache_);
   m.def("paged_decode", &paged_decode, pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
         pybind11::arg("block_tables"), pybind11::arg("ctx_lens"), pybind11::arg("max_ctx"), pybind11::arg("H"),
-        pybind11::arg("scale"), pybind11::arg("impl") = -1);
+        pybind11::arg("scale"), pybind11::arg("impl") = -1, pybind11::arg("tickets") = pybind11::none());
   m.def("flash_attn_gqa", &flash_attn_gqa);
   m.def("image_normalize", &image_normalize);
   m.def("add_relu_", &add_relu_);

@@ -71,8 +71,9 @@ def test_tune_registry_and_torch_predictor(tmp_path):
     tune.register_trainable("my_fn", lambda cfg: {"score": cfg["x"] * 2})
     assert tune.registry.get_trainable_cls("my_fn")({"x": 2}) == {"score": 4}
     assert isinstance(tune.create_scheduler("asha", metric="m", mode="max"), tune.ASHAScheduler)
+    assert isinstance(tune.create_searcher("hyperopt", metric="m", mode="max"), tune.HyperOptSearch)
     with pytest.raises(ValueError):
-        tune.create_searcher("hyperopt")
+        tune.create_searcher("no-such-searcher")
     m = torch.nn.Linear(3, 2)
     ck = TorchCheckpoint.from_model(m)
     p = TorchPredictor.from_checkpoint(ck, model=torch.nn.Linear(3, 2))

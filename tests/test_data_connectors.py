@@ -157,6 +157,10 @@ def test_read_hudi_cow_table(cluster, tmp_path):
     assert sorted(r["id"] for r in ds.take_all()) == [1, 2, 3, 4, 10, 11]
 
 
-def test_remaining_stubs_fail_loudly():
+def test_remaining_stubs_fail_loudly(tmp_path):
     with pytest.raises(ImportError, match="not installed"):
-        ray.data.read_videos("x.mp4")
+        ray.data.read_lance(str(tmp_path))
+    # codec-compressed video containers: a clear error when the file is decoded
+    (tmp_path / "clip.mp4").write_bytes(b"\x00\x00\x00\x18ftypmp42")
+    with pytest.raises(Exception, match="codec"):
+        ray.data.read_videos(str(tmp_path / "clip.mp4")).take_all()

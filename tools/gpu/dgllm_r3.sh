@@ -10,6 +10,9 @@ for v in ${ORDER:-new old new old}; do
   case $v in
     old) E="CAAMD_DG_EXT=0 CAAMD_DECODE_ATTN_GEMM=0" ;;
     mid) E="CAAMD_DECODE_NORM_FUSED=0" ;;
+    ring1) E="CAAMD_DG_RING=1" ;;
+    merge) E="CAAMD_PAGED_MERGE=1" ;;
+    ring2) E="CAAMD_DG_RING=2" ;;
     *) E="" ;;
   esac
   env $E timeout -k 10 300 python -u tools/bench_llm.py $A > $O/bench_$v.log 2>&1 || { echo "bench $v failed"; tail -5 $O/bench_$v.log; exit 1; }
