@@ -450,6 +450,8 @@ for _n, _lib in (("read_lance", "lance"),):
 # from_mars :2591, from_spark :2968, from_tf :3157).
 def from_dask(df) -> Dataset:
     """One block per Dask partition (``df.to_delayed()`` computed lazily per read task)."""
+    if not (hasattr(df, "to_delayed") or hasattr(df, "compute")):
+        raise TypeError(f"from_dask expects a Dask DataFrame (to_delayed / compute), got {type(df).__name__}")
     parts = df.to_delayed() if hasattr(df, "to_delayed") else [df]
 
     def rd(p):
