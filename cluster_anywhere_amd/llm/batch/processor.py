@@ -1,8 +1,8 @@
 """Batch-LLM processors: preprocess -> stages -> postprocess over a Dataset.
 
 Reference roles: ``python/ray/llm/_internal/batch/processor/base.py``
-(``ProcessorConfig`` :17, ``Processor`` :43, ``ProcessorBuilder`` registry :157)
-and ``http_request_proc.py`` (``HttpRequestProcessorConfig`` + builder). The
+(``ProcessorConfig`` :17, ``Processor`` :43, ``ProcessorBuilder`` :157) and
+``http_request_proc.py``. The
 reference's engine processor wraps vLLM; :class:`EngineProcessorConfig` builds
 the same chat-template -> tokenize -> engine -> detokenize pipeline over the
 in-tree gfx950 engine, one engine actor per GPU (``concurrency`` actors).
@@ -31,81 +31,75 @@ class ProcessorConfig(BaseModel):
 
 
 class Processor:
-    """A preprocess stage, one or more processing stages, and a postprocess
-    stage (reference: processor/base.py:43). Calling it on a Dataset returns the
-    lazily transformed Dataset."""
+    """Dataset -> Dataset pipeline: pack each row into the data column (optionally
+    through ``preprocess``), run the stages as ``map_batches`` operators in order,
+    unpack (optionally through ``postprocess``). Calling it is lazy: it returns
+    the transformed Dataset. Role reference: processor/base.py:43.
+
+    Stages are named after their class; repeats get ``_2``, ``_3`` ... suffixes."""
 
     data_column: str = "__data"
 
     def __init__(self, config: ProcessorConfig, stages: List[StatefulStage],
                  preprocess: Optional[Callable] = None, postprocess: Optional[Callable] = None):
         self.config = config
-        self.preprocess = wrap_preprocess(preprocess, self.data_column) if preprocess is not None else None
-        self.postprocess = wrap_postprocess(postprocess, self.data_column) if postprocess is not None else None
-        self.stages: "OrderedDict[str, StatefulStage]" = OrderedDict()
-        for s in stages:
-            self._append_stage(s)
+        col = self.data_column
+        self.preprocess = wrap_preprocess(preprocess, col) if preprocess is not None else None
+        self.postprocess = wrap_postprocess(postprocess, col) if postprocess is not None else None
+        self._named: List[tuple] = []
+        seen: Dict[str, int] = {}
+        for st in stages:
+            base = type(st).__name__
+            seen[base] = seen.get(base, 0) + 1
+            self._named.append((base if seen[base] == 1 else f"{base}_{seen[base]}", st))
+
+    @property
+    def stages(self) -> "OrderedDict[str, StatefulStage]":
+        return OrderedDict(self._named)
 
     def __call__(self, dataset):
-        if self.preprocess is not None:
-            dataset = dataset.map(self.preprocess)
-        else:
-            dc = self.data_column
-            dataset = dataset.map(lambda row: {dc: dict(row)})
-        for stage in self.stages.values():
-            kw = stage.get_dataset_map_batches_kwargs(batch_size=self.config.batch_size,
-                                                      data_column=self.data_column)
-            dataset = dataset.map_batches(stage.fn, **kw)
-        if self.postprocess is not None:
-            dataset = dataset.map(self.postprocess)
-        else:
-            dc = self.data_column
-            dataset = dataset.map(lambda row: dict(row[dc]))
-        return dataset
-
-    def _append_stage(self, stage: StatefulStage) -> None:
-        name = type(stage).__name__
-        if name in self.stages:
-            n = sum(1 for k in self.stages if k == name or k.startswith(name + "_"))
-            name = f"{name}_{n + 1}"
-        self.stages[name] = stage
+        col = self.data_column
+        dataset = dataset.map(self.preprocess or (lambda row: {col: dict(row)}))
+        for _, st in self._named:
+            dataset = dataset.map_batches(
+                st.fn, **st.get_dataset_map_batches_kwargs(batch_size=self.config.batch_size, data_column=col))
+        return dataset.map(self.postprocess or (lambda row: dict(row[col])))
 
     def list_stage_names(self) -> List[str]:
-        return list(self.stages)
+        return [n for n, _ in self._named]
 
     def get_stage_by_name(self, name: str) -> StatefulStage:
-        if name in self.stages:
-            return self.stages[name]
-        raise ValueError(f"Stage {name} not found")
+        for n, st in self._named:
+            if n == name:
+                return st
+        raise ValueError(f"no stage named {name!r}; stages: {self.list_stage_names()}")
 
 
 class ProcessorBuilder:
-    """Config type -> builder registry (reference: processor/base.py:157)."""
+    """Maps a config class to the function that builds its Processor. A config
+    subclass without its own builder uses the nearest registered base class's.
+    Role reference: processor/base.py:157."""
 
-    _registry: Dict[str, Callable] = {}
+    _builders: Dict[type, Callable] = {}
 
     @classmethod
     def register(cls, config_type: Type[ProcessorConfig], builder: Callable) -> None:
-        name = config_type.__name__
-        if name in cls._registry:
-            raise ValueError(f"Processor config type {name} already registered.")
-        cls._registry[name] = builder
+        if config_type in cls._builders:
+            raise ValueError(f"a builder for {config_type.__name__} is already registered")
+        cls._builders[config_type] = builder
 
     @classmethod
     def build(cls, config: ProcessorConfig, override_stage_config_fn: Optional[Callable] = None,
               **kwargs) -> Processor:
-        builder = None
-        for klass in type(config).__mro__:  # public subclasses resolve to their base's builder
-            builder = cls._registry.get(klass.__name__)
-            if builder is not None:
-                break
+        builder = next((cls._builders[k] for k in type(config).__mro__ if k in cls._builders), None)
         if builder is None:
-            raise ValueError(f"Processor config type {type(config).__name__} not registered. "
-                             f"Available types: {list(cls._registry)}")
+            known = sorted(k.__name__ for k in cls._builders)
+            raise ValueError(f"{type(config).__name__} is not registered with ProcessorBuilder "
+                             f"(registered configs: {known})")
         proc = builder(config, **kwargs)
         if override_stage_config_fn is not None:
-            for name, stage in proc.stages.items():
-                override_stage_config_fn(name, stage)
+            for name, st in proc._named:
+                override_stage_config_fn(name, st)
         return proc
 
 

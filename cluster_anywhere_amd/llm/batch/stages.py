@@ -1,18 +1,15 @@
 """Batch-LLM stages: stateful ``map_batches`` UDFs composed by a :class:`Processor`.
 
-Reference roles: ``python/ray/llm/_internal/batch/stages/base.py`` (row-wrapping
-pre/post-process, ``StatefulStageUDF`` — row-aligned async UDF over the
-processor's data column — and ``StatefulStage`` at :233), ``chat_template_stage.py``,
+Reference roles: ``python/ray/llm/_internal/batch/stages/base.py`` (the stage
+UDF / stage description pair), ``chat_template_stage.py``,
 ``tokenize_stage.py`` (tokenize + detokenize), ``http_request_stage.py`` and
 ``prepare_image_stage.py``; the reference's engine stage delegates to vLLM.
 Here the engine stage drives the in-tree paged-KV engine (:mod:`..engine`,
 gfx950 decode kernels, HIP graphs) inside a GPU actor of the data executor.
 
-Row contract (same as the reference): every stage reads the rows of the
-``data_column`` (a column of dicts), runs its UDF over the batch and merges the
-UDF's per-row outputs back into those dicts; outputs may arrive out of order
-and are matched by ``__idx_in_batch``; every input row must be produced exactly
-once.
+Row contract (public, shared with the reference): a stage reads the dicts of
+the ``data_column``, its UDF yields one output per input row tagged with the
+row's ``__idx_in_batch``, in any order, and the output is merged into the row.
 """
 from __future__ import annotations
 
@@ -43,109 +40,162 @@ def _plain(v):
     return v
 
 
+class _PackRow:
+    """Pre-processing map: the user's row function runs on the raw row and its
+    output is folded into a copy of that row, which becomes the single value of
+    the processor's data column (every stage reads and writes that column)."""
+
+    def __init__(self, fn: Callable, data_column: str):
+        self.fn, self.col = fn, data_column
+
+    def __call__(self, row: Dict[str, Any]) -> Dict[str, Any]:
+        packed = dict(row)
+        packed.update(self.fn(row))
+        return {self.col: packed}
+
+
+class _UnpackRow:
+    """Post-processing map: the user's function sees the data-column dict and
+    decides the output columns."""
+
+    def __init__(self, fn: Callable, data_column: str):
+        self.fn, self.col = fn, data_column
+
+    def __call__(self, row: Dict[str, Any]) -> Dict[str, Any]:
+        try:
+            packed = row[self.col]
+        except KeyError:
+            raise ValueError(f"postprocess: row has no {self.col!r} column (columns: {sorted(row)})") from None
+        return self.fn(packed)
+
+
 def wrap_preprocess(fn: Callable, data_column: str) -> Callable:
-    """Row -> {data_column: row + fn(row)} (reference: stages/base.py:12)."""
-
-    def _preprocess(row: Dict[str, Any]) -> Dict[str, Any]:
-        data = dict(row)
-        data.update(fn(row))
-        return {data_column: data}
-
-    return _preprocess
+    return _PackRow(fn, data_column)
 
 
 def wrap_postprocess(fn: Callable, data_column: str) -> Callable:
-    """{data_column: row} -> fn(row): the user picks the output columns."""
+    return _UnpackRow(fn, data_column)
 
-    def _postprocess(row: Dict[str, Any]) -> Dict[str, Any]:
-        if data_column not in row:
-            raise ValueError(f"[Internal] {data_column} not found in row {row}")
-        return fn(row[data_column])
 
-    return _postprocess
+class _Ledger:
+    """Which rows of one batch a stage UDF still owes. Positions are handed out
+    as the row tag; an output is accepted once per position."""
+
+    __slots__ = ("rows", "owed", "left", "stage")
+
+    def __init__(self, rows: List[Dict[str, Any]], stage: str):
+        self.rows = rows
+        self.owed = bytearray(b"\x01") * len(rows)
+        self.left = len(rows)
+        self.stage = stage
+
+    def settle(self, tag: Any, out: Dict[str, Any]) -> Dict[str, Any]:
+        if not isinstance(tag, (int, np.integer)) or not 0 <= int(tag) < len(self.rows):
+            raise ValueError(f"{self.stage}: output tag {tag!r} names no row of this batch")
+        pos = int(tag)
+        if not self.owed[pos]:
+            raise ValueError(f"{self.stage}: row {pos} was produced more than once "
+                             "(a stage UDF maps every input row to exactly one output row)")
+        self.owed[pos] = 0
+        self.left -= 1
+        merged = self.rows[pos]
+        merged.update(out)
+        return merged
+
+    def unsettled(self) -> List[int]:
+        return [i for i, o in enumerate(self.owed) if o]
 
 
 class StatefulStageUDF:
-    """Row-aligned async UDF over the processor's data column
-    (reference: stages/base.py:65)."""
+    """Base of a processor stage: a stateful, async ``map_batches`` callable.
+
+    Subclasses implement ``udf(rows)``, an async generator over the batch's
+    data-column dicts that yields one dict per input row, carrying the row's tag
+    under ``IDX_IN_BATCH_COLUMN`` (outputs may come in any order). The base class
+    tags the rows, checks the contract and merges every output into its input row
+    (output keys win), handing each finished row downstream at once so a slow row
+    does not hold back the others. Role reference: stages/base.py:65."""
 
     IDX_IN_BATCH_COLUMN: str = "__idx_in_batch"
 
     def __init__(self, data_column: str):
         self.data_column = data_column
 
-    async def __call__(self, batch: Dict[str, Any]) -> AsyncIterator[Dict[str, Any]]:
-        if not batch or self.data_column not in batch:
-            if not batch:
-                return
-            raise ValueError(f"[Internal] {self.data_column} not found in batch {list(batch)}")
+    def _rows_of(self, batch: Dict[str, Any]) -> List[Dict[str, Any]]:
+        if self.data_column not in batch:
+            raise ValueError(f"{type(self).__name__}: batch has no {self.data_column!r} column "
+                             f"(columns: {sorted(batch)})")
         col = batch[self.data_column]
-        inputs = [dict(r) for r in (col.tolist() if hasattr(col, "tolist") else col)]
-        if not inputs:
+        return [dict(r) for r in (col.tolist() if hasattr(col, "tolist") else col)]
+
+    async def __call__(self, batch: Dict[str, Any]) -> AsyncIterator[Dict[str, Any]]:
+        if not batch:
             return
-        self.validate_inputs(inputs)
-        for i, row in enumerate(inputs):
-            row[self.IDX_IN_BATCH_COLUMN] = i
-        left = set(range(len(inputs)))
-        # one row per yield: the executor coalesces them into output blocks, so a
-        # slow row never holds back the rows finished before it
-        async for out in self.udf(inputs):
-            if self.IDX_IN_BATCH_COLUMN not in out:
-                raise ValueError(f"The output of the UDF must contain the column {self.IDX_IN_BATCH_COLUMN}.")
-            i = out.pop(self.IDX_IN_BATCH_COLUMN)
-            if i not in left:
-                raise ValueError(f"The row {i} is outputed twice. This is likely due to the UDF is not one-to-one.")
-            left.remove(i)
-            row = inputs[i]
-            row.pop(self.IDX_IN_BATCH_COLUMN, None)
-            row.update(out)
-            yield {self.data_column: [row]}
-        if left:
-            raise ValueError(f"The rows {sorted(left)} are not outputed.")
+        rows = self._rows_of(batch)
+        if not rows:
+            return
+        self.validate_inputs(rows)
+        tag = self.IDX_IN_BATCH_COLUMN
+        for pos, r in enumerate(rows):
+            r[tag] = pos
+        ledger = _Ledger(rows, type(self).__name__)
+        async for out in self.udf(rows):
+            if tag not in out:
+                raise ValueError(f"{ledger.stage}: every output row must carry its input tag "
+                                 f"{tag!r} (got keys {sorted(out)})")
+            pos = out.pop(tag)
+            merged = ledger.settle(pos, out)
+            merged.pop(tag, None)
+            yield {self.data_column: [merged]}
+        if ledger.left:
+            raise ValueError(f"{ledger.stage}: generator ended with {ledger.left} row(s) never produced: "
+                             f"{ledger.unsettled()[:16]}")
 
     def validate_inputs(self, inputs: List[Dict[str, Any]]):
-        need = set(self.expected_input_keys)
-        for row in inputs:
-            keys = set(row)
-            if self.IDX_IN_BATCH_COLUMN in keys:
-                raise ValueError(f"The input column {self.IDX_IN_BATCH_COLUMN} is reserved for internal use.")
-            missing = need - keys
-            if missing:
-                raise ValueError(f"Required input keys {missing} not found at the input of "
-                                 f"{type(self).__name__}. Input keys: {keys}")
+        want = self.expected_input_keys
+        tag = self.IDX_IN_BATCH_COLUMN
+        for r in inputs:
+            if tag in r:
+                raise ValueError(f"{type(self).__name__}: input rows may not use the key {tag!r}; "
+                                 "it is reserved for the stage's row tags")
+            gaps = [k for k in want if k not in r]
+            if gaps:
+                raise ValueError(f"{type(self).__name__}: Required input keys missing: {gaps} "
+                                 f"(row has {sorted(r)})")
 
     @property
     def expected_input_keys(self) -> List[str]:
         return []
 
     async def udf(self, rows: List[Dict[str, Any]]) -> AsyncIterator[Dict[str, Any]]:
-        raise NotImplementedError("StageUDF must implement the udf method")
+        raise NotImplementedError(f"{type(self).__name__} must define udf(rows)")
         yield  # pragma: no cover
 
 
 class StatefulStage(BaseModel):
-    """One processor stage: the UDF class, its constructor kwargs and the
-    ``map_batches`` kwargs (concurrency, GPUs ...) (reference: stages/base.py:233)."""
+    """A stage description: which UDF class runs, its constructor kwargs and the
+    ``map_batches`` options it runs with (actors, CPUs / GPUs). The processor
+    owns ``batch_size`` and ``data_column``. Role reference: stages/base.py:233."""
 
     model_config = ConfigDict(arbitrary_types_allowed=True, validate_assignment=True)
 
-    fn: Type[StatefulStageUDF] = Field(description="The stateful UDF class of this stage.")
+    fn: Type[StatefulStageUDF] = Field(description="UDF class of this stage.")
     fn_constructor_kwargs: Dict[str, Any] = Field(default_factory=dict)
     map_batches_kwargs: Dict[str, Any] = Field(default_factory=lambda: dict(concurrency=1))
 
     def get_dataset_map_batches_kwargs(self, batch_size: int, data_column: str) -> Dict[str, Any]:
-        kw = dict(self.map_batches_kwargs)
-        if kw.get("batch_size", batch_size) != batch_size:
-            logger.warning("batch_size is set to %d in map_batches_kwargs, but it will be overridden by the "
-                           "batch size configured by the processor %d.", kw["batch_size"], batch_size)
-        kw["batch_size"] = batch_size
-        ctor = dict(self.fn_constructor_kwargs)
-        if "data_column" in ctor:
-            raise ValueError("'data_column' cannot be used as in fn_constructor_kwargs.")
-        ctor["data_column"] = data_column
-        kw["fn_constructor_kwargs"] = ctor
-        kw.setdefault("num_cpus", 0.25)  # light host stages; the engine stage sets its own
-        return kw
+        if "data_column" in self.fn_constructor_kwargs:
+            raise ValueError(f"{type(self).__name__}: fn_constructor_kwargs may not set 'data_column'; "
+                             "the processor passes its own")
+        user_bs = self.map_batches_kwargs.get("batch_size")
+        if user_bs not in (None, batch_size):
+            logger.warning("%s: map_batches_kwargs batch_size=%s ignored, the processor runs batches of %d",
+                           type(self).__name__, user_bs, batch_size)
+        opts = {"num_cpus": 0.25}  # host-side stages are light; the engine stage sets its own
+        opts.update(self.map_batches_kwargs)
+        opts["batch_size"] = batch_size
+        opts["fn_constructor_kwargs"] = {**self.fn_constructor_kwargs, "data_column": data_column}
+        return opts
 
 
 # ------------------------------------------------------------ text stages

@@ -896,8 +896,8 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   } else if (tail_split > 1) {
     const int64_t tiles = (M / bm) * (N / bn);
     TORCH_CHECK(ek != 2 && splitk == 1, "gemm: split tail is for the bf16 epilogues");
-    TORCH_CHECK((algo % 10 >= 1 && algo % 10 <= 3) || algo % 10 == 7,
-                "gemm: split tail needs a ping-pong algo (1-3, 7)");
+    TORCH_CHECK((algo % 10 >= 1 && algo % 10 <= 3) || algo % 10 == 7 || algo % 10 == 9,
+                "gemm: split tail needs a ping-pong algo (1-3, 7, 9)");
     TORCH_CHECK(tail_full >= 0 && tail_full < tiles && tail_full % 8 == 0 &&
                     ((tiles - tail_full) * tail_split) % 8 == 0, "gemm: bad tail plan");
     TORCH_CHECK(tail_ws.has_value() && tail_cnt.has_value(), "gemm: split tail needs ws and tickets");

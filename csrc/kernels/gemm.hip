@@ -1418,6 +1418,240 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
   }
 }
 
+// ================================================================================
+// Full-line kernel (algo 9, NT layout: A[M][K], B[N][K], both K-major).
+//
+// What limited the 32-deep ping-pong kernel (profiles/gemm_ablations_r3.jsonl:
+// "DMA + barriers only" 452 of 622 us at 32768 x 6400 x 1600): a 32-deep K-major
+// slot holds 64 B of each 128-B row, so every LDS-DMA wave-instruction touched 16
+// half-used cache lines (16 rows x 64 B), twice the address / tag work per byte of
+// full lines (cdna_hip_programming.md §5 "Projection GEMM": fragment-shaped loads,
+// TA_BUSY 2x at equal traffic). Here a K-step is 64 deep: every DMA instruction
+// moves 8 whole rows x 128 B.
+//
+//  * Two LDS buffers of one 64-deep K-tile each (A 256 x 128 B + B BN x 128 B:
+//    144 KB at BN = 320), XOR-swizzled 16-B chunks (c ^ ((row >> 1) & 7)),
+//    ds_read_b128 fragments (frag_kmaj).
+//  * DMA by buffer_load ... lds: one 128-bit descriptor per operand and tile (SGPRs),
+//    one 32-bit lane offset per DMA round, the K offset in soffset -- no 64-bit
+//    address math in the loop.
+//  * Four phases per K-tile, (k-sub, m-half) = (0,0) (0,1) (1,0) (1,1): each an R
+//    segment (DMA rounds of K-tile t+1, 4 A fragments, + TN B fragments on m-half 0)
+//    and an M segment (4 x TN MFMAs), the two wave rows staggered by one barrier so
+//    that every SIMD pairs one wave's R with the other's M (as gemm_pp_kernel).
+//  * K-tile t+1's DMA rounds (9 per wave at BN = 320) are spread over the R segments
+//    of phases 0 .. DSPLIT-1 of K-tile t (DSPLIT 2: 5 + 4). Buffer (t+1)&1 last held
+//    K-tile t-1, whose last reads (phase 3) every wave retired (lgkmcnt(0)) before the
+//    barrier that opens phase 0 of t. RAW: the leading row reads t+1 after the barrier
+//    that closes its M(t,3) and the lagging row's R(t,3); both rows wait vmcnt(0) just
+//    before it (nothing newer than K-tile t+1 is ever in flight there).
+// ================================================================================
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  // wave-uniform inputs made provably uniform (cdna_hip_programming.md T20)
+  const size_t b = (size_t)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  const void* pb = (const void*)(((size_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)pb, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
+}
+
+// one 16-B-per-lane LDS-DMA round: dst = wave-uniform LDS base (+ lane * 16)
+__device__ __forceinline__ void dma_lds16(__amdgpu_buffer_rsrc_t r, lds_char* dst, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (void __attribute__((address_space(3)))*)dst, 16, voff,
+                                           __builtin_amdgcn_readfirstlane(soff), 0, 0);
+}
+
+template <int BM, int BN, int EPI, int ABL = 0, int DSPLIT = 2>
+__global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
+  constexpr int WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  constexpr int PH = 4, TMH = TM / 2;
+  constexpr int A_ST = BM * 128, B_ST = BN * 128, ST = A_ST + B_ST;
+  constexpr int NA = A_ST / (NTHR * 16), NB = B_ST / (NTHR * 16), NR = NA + NB;
+  static_assert(A_ST % (NTHR * 16) == 0 && B_ST % (NTHR * 16) == 0, "whole DMA rounds");
+  static_assert(DSPLIT >= 1 && DSPLIT <= 3, "DMA rounds go into phases 0 .. DSPLIT-1");
+  static_assert(TM % 2 == 0, "two m-halves");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const bool lo_grp = wr == 0;
+
+  // ---- tile / slice (same XCD-aware order and split-K tail as gemm_pp_kernel) ------
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  int slice, tile, nsplit;
+  bool tail = false;
+  {
+    const int xcd = bid & 7, loc = bid >> 3;
+    if (p.tS > 1) {
+      const int nfx = p.tfull >> 3, ntx = (nwg - p.tfull) >> 3;
+      if (loc < nfx) {
+        tile = xcd * nfx + loc;
+        slice = 0;
+        nsplit = 1;
+      } else {
+        const int s = xcd * ntx + (loc - nfx);
+        tile = p.tfull + s / p.tS;
+        slice = s - (s / p.tS) * p.tS;
+        nsplit = p.tS;
+        tail = true;
+      }
+    } else {
+      const int q = nwg >> 3, r = nwg & 7;
+      tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+      slice = 0;
+      nsplit = 1;
+    }
+  }
+  constexpr int GROUP_M = 8;
+  const int group_sz = GROUP_M * p.tiles_n;
+  const int g = tile / group_sz;
+  const int first_m = g * GROUP_M;
+  const int gm = min(p.tiles_m - first_m, GROUP_M);
+  const int tin = tile - g * group_sz;
+  const int m0 = (first_m + tin % gm) * BM, n0 = (tin / gm) * BN;
+
+  const int nt_total = p.K / 64;
+  const int per = (nt_total + nsplit - 1) / nsplit;
+  const int t0 = slice * per;
+  const int nk = max(0, min(nt_total, t0 + per) - t0);
+
+  // ---- DMA: descriptors per tile, one lane offset per round ------------------------
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A + (size_t)m0 * p.lda, (unsigned)(BM * p.lda * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B + (size_t)n0 * p.ldb, (unsigned)(BN * p.ldb * 2));
+  // Round j covers rows 64 j + 8 wid + (lane >> 3); the swizzle (row >> 1) & 7 does not
+  // depend on j, so a lane's offset is one VGPR per operand and the round's row offset
+  // (64 j rows) goes with the K offset into soffset.
+  const int lrow = wid * 8 + (lane >> 3);
+  const int lchunk = (lane & 7) ^ kswz(lrow);
+  const int voff_a = (lrow * p.lda + lchunk * 8) * 2, voff_b = (lrow * p.ldb + lchunk * 8) * 2;
+  // round j of K-tile t -> buffer t & 1
+#define K64_DMA_ROUND(t_, j_)                                                                          \
+  dma_lds16((j_) < NA ? ra : rb,                                                                      \
+            smem + ((t_) & 1) * ST +                                                                  \
+                ((j_) < NA ? ((j_) * NTHR + wid * 64) * 16 : A_ST + (((j_) - NA) * NTHR + wid * 64) * 16), \
+            (j_) < NA ? voff_a : voff_b,                                                              \
+            (t0 + (t_)) * 128 + ((j_) < NA ? (j_) * 64 * p.lda : ((j_) - NA) * 64 * p.ldb) * 2)
+  // rounds of phase q: [lo, hi)
+  auto rlo = [](int q) { return q >= DSPLIT ? NR : (NR * q) / DSPLIT; };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j) K64_DMA_ROUND(0, j);
+    if (nk > 1) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) K64_DMA_ROUND(1, j);
+      wait_vm<NR>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (!lo_grp) __builtin_amdgcn_s_barrier();  // stagger the second wave row by one barrier
+    bf16x8_t bf[TN];
+    bf16x8_t af[TMH];
+    for (int t = 0; t < nk; ++t) {
+      const lds_char* As = smem + (t & 1) * ST;
+      const lds_char* Bs = As + A_ST;
+      const bool pre = !(ABL & 1) && t >= 1 && t + 1 < nk;  // K-tile t+1 (t = 0: issued in the prologue)
+#pragma unroll
+      for (int q = 0; q < PH; ++q) {
+        const int ks = q >> 1, mh = q & 1;
+        // ---- R segment
+        if (pre) {
+#pragma unroll
+          for (int j = rlo(q); j < rlo(q + 1); ++j) K64_DMA_ROUND(t + 1, j);
+        }
+        if (mh == 0) {
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if constexpr (ABL & 2) { bf[j] = bf16x8_t{}; asm volatile("" : "+v"(bf[j])); }
+            else bf[j] = frag_kmaj(Bs, wc * (TN * 16) + j * 16, ks, lane);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TMH; ++i) {
+          if constexpr (ABL & 2) { af[i] = bf16x8_t{}; asm volatile("" : "+v"(af[i])); }
+          else af[i] = frag_kmaj(As, wr * (TM * 16) + (mh * TMH + i) * 16, ks, lane);
+        }
+        if (q == PH - 1 && !lo_grp) wait_vm<0>();  // lagging row: K-tile t+1 landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        // ---- M segment
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TMH; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            if constexpr (ABL & 4) asm volatile("" :: "v"(bf[j]), "v"(af[i]));
+            else acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[mh * TMH + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (q == PH - 1 && lo_grp) wait_vm<0>();  // leading row: K-tile t+1 landed
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (lo_grp) __builtin_amdgcn_s_barrier();  // equal barrier counts for both rows
+  }
+  if (tail) {
+    // ---- split-K tail: publish this slice; the last arriver combines (as gemm_pp_kernel)
+    const int tt = tile - p.tfull;
+    constexpr int SLAB = BM * BN;
+    float* mine = p.tws + ((size_t)tt * p.tS + slice) * SLAB;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    typedef __attribute__((address_space(3))) int lds_int;
+    lds_int* flag = (lds_int*)smem;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(p.tcnt + tt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == p.tS - 1;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        p.tcnt[tt] = 0;  // ready for the next launch
+      }
+      *flag = last;
+    }
+    __syncthreads();
+    const int last = *flag;
+    if (!last) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = 0; s < p.tS; ++s) {
+      const float* other = p.tws + ((size_t)tt * p.tS + s) * SLAB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] += *reinterpret_cast<const f32x4*>(other + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4);
+    }
+  }
+  epilogue_staged<BM, BN, TM, TN, EPI, (ABL & 8)>(p, acc, m0, n0, wr, wc, lane, smem, tid);
+}
+#undef K64_DMA_ROUND
+
 // Split-K combine: out(bf16) [+]= sum_s slab_s (+ bias); f32 partials [S][M][ldc].
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ part, int S,
                                                             long long slab, bf16* __restrict__ out,
@@ -1455,8 +1689,53 @@ static void ensure_lds(const void* k, int bytes) {
     (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
+// algo 9 (full-line kernel): algo = 9 + 10 * ABL + 1000 * DSPLIT (0 -> 2). Development
+// ablations only on 256 x 320 bf16 tiles at the default DMA split.
+template <int BM, int BN, int EPI, int ABL, int DS>
+static hipError_t launch_k64_v(const Args& a, hipStream_t st) {
+  auto k = gemm_k64_kernel<BM, BN, EPI, ABL, DS>;
+  constexpr int lds = 2 * (BM + BN) * 128;
+  ensure_lds((const void*)k, lds);
+  const int T = a.tiles_m * a.tiles_n;
+  const int grid = a.tS > 1 ? a.tfull + (T - a.tfull) * a.tS : T;
+  hipLaunchKernelGGL(k, dim3(grid), dim3(NTHR), lds, st, a);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int EPI>
+static hipError_t launch_k64(const Args& a, hipStream_t st) {
+  const int abl = (a.algo / 10) % 100, ds = a.algo / 1000;
+  if (a.splitk != 1) return hipErrorInvalidValue;
+  if (abl == 0) {
+    switch (ds) {
+      case 1: return launch_k64_v<BM, BN, EPI, 0, 1>(a, st);
+      case 0:
+      case 2: return launch_k64_v<BM, BN, EPI, 0, 2>(a, st);
+      case 3: return launch_k64_v<BM, BN, EPI, 0, 3>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if constexpr (BM == 256 && BN == 320 && EPI == EPI_BF16) {
+    switch (abl) {
+      case 1: return launch_k64_v<BM, BN, EPI, 1, 2>(a, st);
+      case 2: return launch_k64_v<BM, BN, EPI, 2, 2>(a, st);
+      case 3: return launch_k64_v<BM, BN, EPI, 3, 2>(a, st);
+      case 4: return launch_k64_v<BM, BN, EPI, 4, 2>(a, st);
+      case 5: return launch_k64_v<BM, BN, EPI, 5, 2>(a, st);
+      case 6: return launch_k64_v<BM, BN, EPI, 6, 2>(a, st);
+      case 8: return launch_k64_v<BM, BN, EPI, 8, 2>(a, st);
+      default: break;
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int BM, int BN, bool AK, bool BK_, int EPI>
 static hipError_t launch_t(const Args& a, hipStream_t st) {
+  if (a.algo % 10 == 9) {
+    if constexpr (AK && BK_ && EPI != EPI_F32 && BM == 256) return launch_k64<BM, BN, EPI>(a, st);
+    return hipErrorInvalidValue;
+  }
   if constexpr (BM == 256 && BN == 320 && AK && BK_ && EPI == 0) {
     if (a.algo >= 10) {
       switch (a.algo / 10) {

@@ -73,14 +73,14 @@ def test_stage_udf_errors():
             for _ in range(2):
                 yield {self.IDX_IN_BATCH_COLUMN: 0}
 
-    with pytest.raises(ValueError, match="outputed twice"):
+    with pytest.raises(ValueError, match="more than once"):
         _drain(Dup("__data"), {"__data": [{"x": 1}]})
 
     class Drop(StatefulStageUDF):
         async def udf(self, rows):
             yield {self.IDX_IN_BATCH_COLUMN: 0}
 
-    with pytest.raises(ValueError, match="not outputed"):
+    with pytest.raises(ValueError, match="never produced"):
         _drain(Drop("__data"), {"__data": [{"x": 1}, {"x": 2}]})
 
 
