@@ -305,6 +305,11 @@ class Head:
         self.env_failures: Dict[str, str] = {}  # runtime-env key -> setup error
         self.reattached_running: Dict[bytes, tuple] = {}  # task id -> (worker, node, demand) of a re-registered run
         self._held_resubmits: List[tuple] = []  # (conn, spec) replayed by owners during the re-attach grace
+        # re-attach ordering: a lease whose worker has not re-registered yet is
+        # parked under the worker id; an idle re-registered worker is held out of the idle
+        # pool until its lease holder claims it or the grace ends
+        self._parked_leases: Dict[bytes, tuple] = {}  # worker id -> (owner conn, lease entry)
+        self._reattach_hold: List[WorkerInfo] = []
         self.reattach_stats = {"workers": 0, "actors": 0, "objects": 0, "drivers": 0, "lost_objects": 0,
                                "recreated_actors": 0, "dead_actors": 0}
         if self.gcs is not None:
@@ -2114,7 +2119,7 @@ class Head:
             return
         self.reattach_stats["workers"] += 1
         w = WorkerInfo(worker_id=worker_id, pid=pid, node=node, gpu_key=tuple(extra.get("gpu_ids") or ()),
-                       kind="worker", alive=True, conn=c)
+                       kind="worker", alive=True, conn=c, env_key=_env_key(extra.get("runtime_env")))
         w.started = time.time()
         w.client_id = worker_id
         w.direct_addr = extra.get("direct")
@@ -2152,7 +2157,14 @@ class Head:
         for tid in extra.get("finishing") or ():
             self.reattached_running.setdefault(tid, (worker_id, node, {}))
         self._release_held(lambda sp: sp.task_id in self.reattached_running)
+        parked = self._parked_leases.pop(worker_id, None)
+        if parked is not None and not parked[0].closed:
+            self._apply_reattached_lease(parked[0], w, parked[1])
+            return
         if not busy:
+            if self._reattaching:
+                self._reattach_hold.append(w)  # its lease holder may still re-register
+                return
             w.idle = True
             self.idle[(node, w.gpu_key, w.env_key)].append(w)
             self._schedule()
@@ -2181,31 +2193,47 @@ class Head:
 
     def _reattach_leases(self, c, leases):
         for ent in leases:
-            wid, res = ent[0], ent[1]
-            opts = ent[2] if len(ent) > 2 else None
+            wid = ent[0]
             w = self.workers.get(wid)
-            if w is None or w.lease is not None:
+            if w is None:
+                if self._reattaching:
+                    self._parked_leases[wid] = (c, ent)  # applied when the worker re-registers
                 continue
-            strategy = (opts or {}).get("strategy")
-            if strategy is not None and strategy[1] not in self.pgs:
-                strategy = None
-            demand = {k: float(v) for k, v in self._demand_for(
-                {k: v for k, v in (res or {}).items() if v}, strategy).items() if v}
-            gamt = float((res or {}).get("GPU", 0) or 0)
-            if gamt and w.gpu_key:
-                try:
-                    self._take_gpus(w.node, tuple(w.gpu_key), gamt)
-                    w.lease_gpus = (tuple(w.gpu_key), gamt)
-                except ValueError:
-                    w.lease_gpus = None
-            if w.idle:
-                w.idle = False
-                lst = self.idle.get((w.node, w.gpu_key, w.env_key))
-                if lst and w in lst:
-                    lst.remove(w)
-            if demand:
-                self.sched.acquire(w.node, demand)
-            w.lease = (c, demand, time.time())
+            self._apply_reattached_lease(c, w, ent)
+
+    def _apply_reattached_lease(self, c, w, ent):
+        """Restore one lease an owner held before the restart: the worker leaves the
+        idle pool (or the re-attach hold) and its resources are taken back. If they
+        cannot be (the node is over-committed now), the lease ends the way a dead
+        lease ends: the worker is stopped and the owner's lease loop resubmits."""
+        if w.lease is not None or w.actor_id is not None:
+            return
+        res = ent[1]
+        opts = ent[2] if len(ent) > 2 else None
+        strategy = (opts or {}).get("strategy")
+        if strategy is not None and strategy[1] not in self.pgs:
+            strategy = None
+        demand = {k: float(v) for k, v in self._demand_for(
+            {k: v for k, v in (res or {}).items() if v}, strategy).items() if v}
+        if w in self._reattach_hold:
+            self._reattach_hold.remove(w)
+        if w.idle:
+            w.idle = False
+            lst = self.idle.get((w.node, w.gpu_key, w.env_key))
+            if lst and w in lst:
+                lst.remove(w)
+        if demand and not self.sched.acquire(w.node, demand):
+            self._kill_worker(w.worker_id)
+            return
+        gamt = float((res or {}).get("GPU", 0) or 0)
+        w.lease_gpus = None
+        if gamt and w.gpu_key:
+            try:
+                self._take_gpus(w.node, tuple(w.gpu_key), gamt)
+                w.lease_gpus = (tuple(w.gpu_key), gamt)
+            except ValueError:
+                pass
+        w.lease = (c, demand, time.time())
 
     def _release_held(self, pred):
         keep, go = [], []
@@ -2223,6 +2251,12 @@ class Head:
         from ..exceptions import ObjectLostError  # noqa: F401  (clients raise it for "lost" payloads)
 
         self._reattaching = False
+        self._parked_leases.clear()  # their workers never came back: the owners see the loss
+        hold, self._reattach_hold = self._reattach_hold, []
+        for w in hold:
+            if w.alive and w.lease is None and w.actor_id is None and self.workers.get(w.worker_id) is w:
+                w.idle = True
+                self.idle[(w.node, w.gpu_key, w.env_key)].append(w)
         for a in list(self.actors.values()):
             if a.state != "RECONNECTING":
                 continue
@@ -2249,6 +2283,8 @@ class Head:
                 e.lost = True
                 self.reattach_stats["lost_objects"] += 1
                 self._seal_object(oid, None, 0, None, ())
+        if hold:
+            self._schedule()
 
     def _health_check(self):
         if self.gcs is not None and self._gcs_actors:

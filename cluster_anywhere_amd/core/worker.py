@@ -467,6 +467,11 @@ class CoreWorker:
         gpus = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
         st = {"job_id": self.job_id, "gpu_ids": gpus, "actor_id": self.actor_id,
               "direct": self.direct_server.path if self.direct_server is not None else None}
+        renv = os.environ.get("CAAMD_RUNTIME_ENV")
+        if renv:  # the head keys its idle pools by runtime env: keep this worker in its own
+            import json
+
+            st["runtime_env"] = json.loads(renv)
         st["running"] = [(tid, self._running_res.get(tid) or {}) for tid in list(self._running_res)
                          if tid in self.running_tasks]
         st["finishing"] = list(self._unsent_done)

@@ -114,7 +114,14 @@ class _LinearXentFn(torch.autograd.Function):
         return torch.cat(losses).sum() * scale[0]
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, g):
+        # dh / dw were computed in forward and are scaled in place here: a second
+        # backward through the same graph would scale them twice
+        if getattr(ctx, "consumed", False):
+            raise RuntimeError("linear_cross_entropy: backward ran twice through one forward "
+                               "(retain_graph=True is not supported by the fused LM head)")
+        ctx.consumed = True
         dh, dw = ctx.saved_tensors
         w = ctx.w
         gb = g.to(torch.bfloat16)
@@ -136,7 +143,10 @@ def linear_cross_entropy(h2: torch.Tensor, w: torch.Tensor, target: torch.Tensor
     ignored) without materialising the logits when the shapes tile, else the
     plain logits + fused cross-entropy path."""
     target = target.reshape(-1)
-    if linear_cross_entropy_ok(h2, w):
+    # the fused head computes the dgrad / wgrad GEMMs inside forward: only worth it
+    # when a backward will follow (eval and no_grad take the plain logits path)
+    wants_grad = torch.is_grad_enabled() and (h2.requires_grad or w.requires_grad)
+    if wants_grad and linear_cross_entropy_ok(h2, w):
         return _LinearXentFn.apply(h2, w, target.contiguous().long(), vocab, chunk or HEAD_CHUNK)
     logits = F.linear(h2, w)
     losses = cross_entropy(logits, target, vocab)

@@ -45,19 +45,28 @@ class FusedAdamW:
             kernels().adamw_config(int(v))
 
     def state_dict(self):
-        return {
+        sd = {
             "step": self.step_count,
             "exp_avg": self.exp_avg,
             "exp_avg_sq": self.exp_avg_sq,
             "master": self.flat.master,
             "lr": self.lr,
         }
+        if hasattr(self.flat, "layout"):
+            # the flat buffers' element order depends on which weights are stored
+            # transposed (CAAMD_FC2_T): record it so a resume can map them back
+            sd["layout"] = self.flat.layout()
+        return sd
 
     def load_state_dict(self, sd):
         self.step_count = int(sd["step"])
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         self.flat.master.copy_(sd["master"])
+        saved = sd.get("layout")
+        if saved is not None and hasattr(self.flat, "relayout_"):
+            for buf in (self.exp_avg, self.exp_avg_sq, self.flat.master):
+                self.flat.relayout_(buf, saved)
         self.lr = sd.get("lr", self.lr)
 
     def step(self, grads: Optional[torch.Tensor] = None, param_out=None, inv_world: float = 1.0,

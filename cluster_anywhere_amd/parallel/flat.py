@@ -39,6 +39,7 @@ class ParamSlot:
     offset: int
     numel: int
     decay: bool
+    transposed: bool = False  # stored in physical [in, out] order (see _phys)
 
 
 def _phys(t: torch.Tensor) -> Optional[torch.Tensor]:
@@ -92,7 +93,7 @@ class FlatParamSpace:
         off = 0
         self.slots: List[ParamSlot] = []
         for n, p in named:
-            self.slots.append(ParamSlot(n, p, off, p.numel(), decay_rule(n, p)))
+            self.slots.append(ParamSlot(n, p, off, p.numel(), decay_rule(n, p), _phys(p) is not None))
             off = _round_up(off + p.numel(), align)
         self.align = align
         self.numel = _round_up(off, max(pad_multiple, align))
@@ -127,6 +128,32 @@ class FlatParamSpace:
             g = s.param.grad
             if g is None or g.data_ptr() != self.grad_buffer[s.offset :].data_ptr():
                 s.param.grad = _slot_view(self.grad_buffer, s.offset, s.param)
+
+    def layout(self) -> List[tuple]:
+        """(name, offset, numel, logical shape, transposed) per slot: what an
+        optimizer checkpoint needs to map its flat fp32 buffers onto this space."""
+        return [(s.name, s.offset, s.numel, tuple(s.param.shape), s.transposed) for s in self.slots]
+
+    def relayout_(self, buf: torch.Tensor, saved: List[tuple]) -> torch.Tensor:
+        """Bring a flat fp32 buffer written under ``saved`` (a :meth:`layout`) into
+        this space's layout in place: slots stored transposed in one and plainly in
+        the other (e.g. GPT-2's fc2 under a different ``CAAMD_FC2_T``) are
+        transposed; any other difference is an error."""
+        mine = {s.name: s for s in self.slots}
+        if len(saved) != len(self.slots):
+            raise ValueError(f"optimizer state has {len(saved)} parameter slots, this model {len(self.slots)}")
+        with torch.no_grad():
+            for name, off, numel, shape, transposed in saved:
+                s = mine.get(name)
+                if s is None or s.offset != off or s.numel != numel or tuple(s.param.shape) != tuple(shape):
+                    raise ValueError(f"optimizer state slot {name!r} (offset {off}, {numel} elements, shape "
+                                     f"{tuple(shape)}) does not match this model's parameters")
+                if bool(transposed) != s.transposed:
+                    seg = buf[off: off + numel]
+                    r, c = shape
+                    src = seg.view(c, r) if transposed else seg.view(r, c)  # saved physical order
+                    seg.copy_(src.t().contiguous().reshape(-1))
+        return buf
 
     def param_index(self) -> Dict[int, ParamSlot]:
         return {id(s.param): s for s in self.slots}

@@ -101,3 +101,45 @@ def test_dp_matches_single_process(world, zero, bucket_mb):
     assert torch.allclose(got_g[:n], ref_g[:n], atol=1e-6, rtol=1e-4), (got_g[:n] - ref_g[:n]).abs().max()
     # Adam normalises away tiny summation-order noise only approximately; lr = 1e-2
     assert torch.allclose(got[:n], ref[:n], atol=2e-3), (got[:n] - ref[:n]).abs().max()
+
+
+def test_optimizer_state_survives_transposed_storage_change():
+    """An optimizer checkpoint saved with a weight stored transposed (GPT-2's fc2
+    under CAAMD_FC2_T=1) resumes into a plainly stored model with the master and
+    moments mapped back per element (and vice versa)."""
+    from cluster_anywhere_amd.ops.optim import FusedAdamW
+    from cluster_anywhere_amd.parallel.flat import FlatParamSpace
+
+    def model(transposed):
+        m = torch.nn.Module()
+        w = torch.arange(12, dtype=torch.float32).reshape(3, 4) / 7.0
+        m.w = torch.nn.Parameter(w.t().contiguous().t() if transposed else w.clone())
+        m.b = torch.nn.Parameter(torch.ones(5))
+        return m
+
+    torch.manual_seed(0)
+    src = model(True)
+    fs = FlatParamSpace(src, dtype=torch.float32)
+    opt = FusedAdamW(fs, lr=1e-2)
+    fs.grad_buffer.normal_()
+    opt.step()
+    sd = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in opt.state_dict().items()}
+    assert sd["layout"][0][4] is True
+
+    dst = model(False)
+    fd = FlatParamSpace(dst, dtype=torch.float32)
+    opt2 = FusedAdamW(fd, lr=1e-2)
+    opt2.load_state_dict(sd)
+    fd.sync_params_from_master()
+    assert torch.equal(dst.w.detach(), src.w.detach())
+    # moments: logical element (i, j) must agree
+    m_src = fs.slots[0]
+    m_dst = fd.slots[0]
+    from cluster_anywhere_amd.parallel.flat import _slot_view
+    a = _slot_view(opt.exp_avg, m_src.offset, src.w)
+    b = _slot_view(opt2.exp_avg, m_dst.offset, dst.w)
+    assert torch.equal(a, b)
+
+    bad = dict(sd, layout=[("w", 0, 12, (4, 3), True)] + sd["layout"][1:])
+    with pytest.raises(ValueError, match="does not match"):
+        FusedAdamW(FlatParamSpace(model(False), dtype=torch.float32)).load_state_dict(bad)

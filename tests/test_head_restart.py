@@ -166,3 +166,42 @@ def test_pubsub_actor_and_node_events(tmp_path):
                 agent.kill()
     finally:
         ray.shutdown()
+
+
+@ray.remote
+def getenv(k):
+    return os.environ.get(k)
+
+
+def test_head_restart_keeps_env_pools_and_leases(tmp_path):
+    """Workers started for a runtime env re-register into their own env's pool, and
+    leases held across the restart are restored whichever of the driver or the
+    leased worker re-registers first (ADVICE r3 on head.py:2116 / :2186)."""
+    tmp = str(tmp_path / "caamd")
+    store = str(tmp_path / "gcs" / "tables.log")
+    log = str(tmp_path / "head.log")
+    head, info = _start_head(tmp, store, log)
+    head2 = None
+    try:
+        ray.init(address=info["address"])
+        envd = getenv.options(runtime_env={"env_vars": {"CAAMD_T_FOO": "bar"}})
+        assert ray.get(envd.remote("CAAMD_T_FOO")) == "bar"
+        assert ray.get(getenv.remote("CAAMD_T_FOO")) is None
+        burst = [slow.remote(2.0, i) for i in range(6)]  # leased workers busy across the restart
+        time.sleep(0.6)
+        os.kill(head.pid, signal.SIGKILL)
+        head.wait()
+        head2, _ = _start_head(tmp, store, log)
+        assert ray.get(burst, timeout=120) == list(range(6))
+        plain = ray.get([getenv.remote("CAAMD_T_FOO") for _ in range(40)], timeout=90)
+        assert all(v is None for v in plain), plain
+        assert ray.get(envd.remote("CAAMD_T_FOO"), timeout=60) == "bar"
+    finally:
+        ray.shutdown()
+        for p in (head, head2):
+            if p is not None and p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+                try:
+                    p.wait(30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
