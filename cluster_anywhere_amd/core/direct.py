@@ -157,7 +157,8 @@ class DirectClient:
                 retryable = msg[7] if len(msg) > 7 else False
                 with self.lock:
                     rec = self.pending.pop(task_id, None)
-                    if not self.pending:
+                    drained = not self.pending
+                    if drained:
                         self.idle.notify_all()
                 if rec is None:
                     continue
@@ -165,6 +166,8 @@ class DirectClient:
                     self.sink._done(self, rec[0], results, error_kind, retryable, (t0, t1, pid))
                 else:
                     self.worker._on_direct_done(rec[0], results, (t0, t1, pid))
+                    if drained:
+                        self.worker._direct_drained(self.actor_id)
         with self.lock:
             self.alive = False
             recs = sorted(self.pending.values(), key=lambda r: r[2])
@@ -174,6 +177,7 @@ class DirectClient:
             self.sink._lost(self, [r[0] for r in recs])
         else:
             self.worker._on_direct_lost(self.actor_id, [r[0] for r in recs])
+            self.worker._direct_drained(self.actor_id)  # after the resubmits, on the same connection
 
     def wait_idle(self, timeout: float) -> bool:
         """Block until every call sent on this connection has been answered (or the

@@ -1274,8 +1274,11 @@ class Head:
                 if self.workers.get(worker_id) is not w or not self.running:
                     return
                 log = open(log_path, "ab")
-                proc = subprocess.Popen([py, "-m", "cluster_anywhere_amd.core.worker_main"], env=e, stdout=log,
+                env_dir = os.path.dirname(os.path.dirname(py))
+                proc = subprocess.Popen([py, "-m", "cluster_anywhere_amd.core.worker_main"],
+                                        env=dict(e, CAAMD_PIP_ENV_DIR=env_dir), stdout=log,
                                         stderr=subprocess.STDOUT, stdin=subprocess.DEVNULL, cwd=os.getcwd())
+                _pip.mark_in_use(env_dir, proc.pid)  # no eviction while this worker runs
                 log.close()
                 w.proc, w.pid = proc, proc.pid
 

@@ -23,7 +23,7 @@ import sys
 import threading
 import time
 import traceback
-from typing import Any, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional
 
 from . import context, serialization
 from .head import ACTOR_CREATE, ACTOR_METHOD, INLINE_MAX, NORMAL, TaskSpec
@@ -65,6 +65,19 @@ class RefCounter:
         self.local_only: Dict[bytes, tuple] = {}
         # direct results still in flight whose refs already escaped: sealed normally
         self.must_seal = set()
+        # actor handle refs whose last local handle went away while direct calls to
+        # the actor were still unanswered: their decref (which lets the head append
+        # __ray_terminate__ to the actor's queue) waits until those calls are done,
+        # since the head's terminate would otherwise overtake them (Pool race, r3)
+        self.handle_busy: Optional[Callable[[bytes], bool]] = None
+        self.held_handles = set()
+
+    def release_held_handle(self, oid: bytes):
+        """The direct calls that held back ``oid``'s decref are all answered."""
+        with self.lock:
+            if oid in self.held_handles and oid not in self.counts:
+                self.held_handles.discard(oid)
+                self.ops.append(("d", oid))
 
     def add(self, oid: bytes, announce: bool):
         with self.lock:
@@ -114,6 +127,8 @@ class RefCounter:
                 del self.local_only[oid]
             elif oid in self.direct_pending:
                 self.direct_dropped.add(oid)
+            elif self.handle_busy is not None and self.handle_busy(oid):
+                self.held_handles.add(oid)
             else:
                 self.ops.append(("d", oid))
         else:
@@ -160,6 +175,7 @@ class CoreWorker:
         self.job_id = job_id
         self.conn = connect(address)
         self.refs = RefCounter()
+        self.refs.handle_busy = self._handle_busy
         # re-entrant: pickling a message may seal an escaping owner-local ref first
         self.send_lock = threading.RLock()
         self._req = itertools.count(1)
@@ -560,6 +576,24 @@ class CoreWorker:
                 return dc
         self.actor_direct[actor_id] = ("head", now)
         return None
+
+    def _handle_busy(self, oid: bytes) -> bool:
+        """RefCounter hook (called under its lock): is ``oid`` an actor-handle ref
+        whose actor still owes this process answers to direct calls?"""
+        from .actor import HANDLE_SUFFIX
+
+        if len(oid) <= len(HANDLE_SUFFIX) or not oid.endswith(HANDLE_SUFFIX):
+            return False
+        dc = self.actor_direct.get(oid[: -len(HANDLE_SUFFIX)])
+        return dc is not None and not isinstance(dc, tuple) and bool(dc.pending)
+
+    def _direct_drained(self, actor_id: bytes):
+        """Every direct call to ``actor_id`` is answered (or resubmitted through the
+        head): a handle decref held back for them may go now."""
+        from .actor import handle_ref_id
+
+        if self.refs.held_handles:
+            self.refs.release_held_handle(handle_ref_id(actor_id))
 
     def _to_head_path(self, actor_id, drop: bool = False):
         """Route this caller's later calls to ``actor_id`` through the head. Calls
@@ -1267,6 +1301,10 @@ class CoreWorker:
         self._reply_done(spec, results, error_kind, retryable)
         context.set_current_task(None)
         if getattr(self, "_exit_actor_after", False):
+            try:  # an intentional exit: the head must not restart the actor
+                self.send(("actor_exit", self.actor_id))
+            except (ConnectionClosed, OSError):
+                pass
             self._hard_exit()
 
     def _hard_exit(self):

@@ -134,6 +134,10 @@ class URICache:
             pass
 
     def evict(self, keep: Optional[str] = None, in_use=()) -> List[str]:
+        """Remove least-recently-used envs until the cache fits. An env is skipped
+        when it is ``keep`` / in ``in_use``, when a live process registered as its
+        user (:func:`mark_in_use`; any head's workers, not only this process's), or
+        when another process holds its build lock."""
         ents = self.entries()
         sizes = {d: _dir_bytes(d) for _, d in ents}
         total = sum(sizes.values())
@@ -141,12 +145,58 @@ class URICache:
         for _, d in ents:  # oldest first
             if total <= self.max_bytes:
                 break
-            if d == keep or d in in_use:
+            if d == keep or d in in_use or live_users(d):
                 continue
-            shutil.rmtree(d, ignore_errors=True)
+            with open(d + ".lock", "w") as lk:
+                try:
+                    fcntl.flock(lk, fcntl.LOCK_EX | fcntl.LOCK_NB)
+                except OSError:
+                    continue  # being built or re-validated right now
+                try:
+                    if live_users(d):
+                        continue
+                    shutil.rmtree(d, ignore_errors=True)
+                    shutil.rmtree(d + ".users", ignore_errors=True)
+                finally:
+                    fcntl.flock(lk, fcntl.LOCK_UN)
             total -= sizes[d]
             gone.append(d)
         return gone
+
+
+def mark_in_use(env_dir: str, pid: Optional[int] = None) -> None:
+    """Register ``pid`` (default: this process) as a user of ``env_dir`` so no
+    cache eviction removes the env while it runs."""
+    users = env_dir + ".users"
+    os.makedirs(users, exist_ok=True)
+    with open(os.path.join(users, str(pid or os.getpid())), "w"):
+        pass
+
+
+def live_users(env_dir: str) -> List[int]:
+    """Pids registered as users of ``env_dir`` that are still running (stale
+    registrations are dropped)."""
+    users = env_dir + ".users"
+    try:
+        names = os.listdir(users)
+    except OSError:
+        return []
+    live = []
+    for n in names:
+        try:
+            pid = int(n)
+            os.kill(pid, 0)
+            live.append(pid)
+        except ValueError:
+            continue
+        except ProcessLookupError:
+            try:
+                os.unlink(os.path.join(users, n))
+            except OSError:
+                pass
+        except PermissionError:
+            live.append(pid)
+    return live
 
 
 def _cache() -> URICache:

@@ -7,12 +7,28 @@ list of ``(args, kwargs)`` calls and returns one list), so per-item scheduling
 cost is paid once per chunk. ``maxtasksperchild`` retires an actor after that
 many chunks and starts a fresh one (re-running the initializer). Ordered
 results for ``map``/``imap``; ``imap_unordered`` yields chunks as they finish.
+
+A chunk whose actor dies (OOM kill, node loss, a crashed initializer) is run again
+on a fresh actor, up to ``_CHUNK_ATTEMPTS`` times, so a lost pool process costs a
+re-run, not the whole map (the pool's functions are stateless, as stdlib requires).
 """
 from __future__ import annotations
 
 import threading
 from multiprocessing import TimeoutError
 from typing import Any, Callable, Dict, Iterable, List, Optional, Tuple
+
+
+_CHUNK_ATTEMPTS = 4
+
+
+class _Chunk:
+    """One submitted batch: what to re-run if its actor dies."""
+
+    __slots__ = ("ref", "func", "batch", "slot", "handle")
+
+    def __init__(self, ref, func, batch, slot, handle):
+        self.ref, self.func, self.batch, self.slot, self.handle = ref, func, batch, slot, handle
 
 
 class PoolTaskError(Exception):
@@ -42,8 +58,9 @@ class _PoolActor:
 class AsyncResult:
     """Result of ``apply_async`` / ``map_async`` (stdlib semantics)."""
 
-    def __init__(self, refs, callback=None, error_callback=None, single_result=False):
-        self._refs = refs
+    def __init__(self, pool, chunks, callback=None, error_callback=None, single_result=False):
+        self._pool = pool
+        self._chunks = chunks
         self._single = single_result
         self._callback, self._error_callback = callback, error_callback
         self._event = threading.Event()
@@ -52,10 +69,8 @@ class AsyncResult:
         threading.Thread(target=self._collect, daemon=True).start()
 
     def _collect(self):
-        from ...core.api import get
-
         try:
-            chunks = get(self._refs)
+            chunks = [self._pool._resolve(c) for c in self._chunks]
             flat = [x for c in chunks for x in c]
             err = next((x for x in flat if isinstance(x, PoolTaskError)), None)
             if err is not None:
@@ -112,6 +127,7 @@ class Pool:
         self._maxtasks = maxtasksperchild or -1
         self._remote_args = dict(ray_remote_args or {})
         self._closed = False
+        self._terminated = False
         self._lock = threading.Lock()
         self._cls = api.remote(**self._remote_args)(_PoolActor) if self._remote_args else api.remote(_PoolActor)
         self._actors: List[list] = [self._new_actor() for _ in range(processes)]
@@ -125,19 +141,40 @@ class Pool:
     def _processes(self) -> int:
         return len(self._actors)
 
-    def _submit(self, func, batch):
+    def _submit(self, func, batch, retry: bool = False) -> _Chunk:
         with self._lock:
-            if self._closed:
+            if self._closed and not retry:
                 raise ValueError("Pool not running")
+            if self._terminated:
+                raise ValueError("Pool terminated")
             i = self._next
             self._next = (self._next + 1) % len(self._actors)
             entry = self._actors[i]
-            ref = entry[0].run_batch.remote(func, batch)
+            handle = entry[0]
+            ref = handle.run_batch.remote(func, batch)
             entry[1] += 1
             if self._maxtasks > 0 and entry[1] >= self._maxtasks:
-                entry[0].__ray_terminate__.remote()  # runs after its queued batches
+                handle.__ray_terminate__.remote()  # runs after its queued batches
                 self._actors[i] = self._new_actor()
-            return ref
+            return _Chunk(ref, func, batch, i, handle)
+
+    def _resolve(self, chunk: _Chunk, timeout: Optional[float] = None) -> list:
+        """The chunk's result list; a chunk whose actor died is re-run on a fresh one."""
+        from ...core.api import get
+        from ...exceptions import ActorDiedError, ActorUnavailableError
+
+        for attempt in range(_CHUNK_ATTEMPTS):
+            try:
+                return get(chunk.ref, timeout=timeout)
+            except (ActorDiedError, ActorUnavailableError):
+                if attempt == _CHUNK_ATTEMPTS - 1 or self._terminated:
+                    raise
+                with self._lock:
+                    entry = self._actors[chunk.slot]
+                    if entry[0] is chunk.handle:  # not replaced yet (by maxtasksperchild or another chunk)
+                        self._actors[chunk.slot] = self._new_actor()
+                chunk = self._submit(chunk.func, chunk.batch, retry=True)
+        raise AssertionError("unreachable")
 
     def _chunks(self, func, iterable, chunksize, star):
         items = list(iterable)
@@ -156,37 +193,35 @@ class Pool:
         return self.apply_async(func, args, kwargs).get()
 
     def apply_async(self, func, args=None, kwargs=None, callback=None, error_callback=None) -> AsyncResult:
-        ref = self._submit(func, [(tuple(args or ()), kwargs)])
-        return AsyncResult([ref], callback, error_callback, single_result=True)
+        chunk = self._submit(func, [(tuple(args or ()), kwargs)])
+        return AsyncResult(self, [chunk], callback, error_callback, single_result=True)
 
     def map(self, func: Callable, iterable: Iterable, chunksize: Optional[int] = None) -> list:
         return self.map_async(func, iterable, chunksize).get()
 
     def map_async(self, func, iterable, chunksize=None, callback=None, error_callback=None) -> AsyncResult:
-        return AsyncResult(self._chunks(func, iterable, chunksize, False), callback, error_callback)
+        return AsyncResult(self, self._chunks(func, iterable, chunksize, False), callback, error_callback)
 
     def starmap(self, func, iterable, chunksize=None) -> list:
         return self.starmap_async(func, iterable, chunksize).get()
 
     def starmap_async(self, func, iterable, chunksize=None, callback=None, error_callback=None) -> AsyncResult:
-        return AsyncResult(self._chunks(func, iterable, chunksize, True), callback, error_callback)
+        return AsyncResult(self, self._chunks(func, iterable, chunksize, True), callback, error_callback)
 
     def imap(self, func: Callable, iterable: Iterable, chunksize: int = 1):
-        from ...core.api import get
-
-        for ref in self._chunks(func, iterable, chunksize, False):
-            for x in get(ref):
+        for chunk in self._chunks(func, iterable, chunksize, False):
+            for x in self._resolve(chunk):
                 if isinstance(x, PoolTaskError):
                     raise x.underlying
                 yield x
 
     def imap_unordered(self, func: Callable, iterable: Iterable, chunksize: int = 1):
-        from ...core.api import get, wait
+        from ...core.api import wait
 
-        pending = self._chunks(func, iterable, chunksize, False)
+        pending = {c.ref: c for c in self._chunks(func, iterable, chunksize, False)}
         while pending:
-            done, pending = wait(pending, num_returns=1)
-            for x in get(done[0]):
+            done, _ = wait(list(pending), num_returns=1)
+            for x in self._resolve(pending.pop(done[0])):
                 if isinstance(x, PoolTaskError):
                     raise x.underlying
                 yield x
@@ -198,6 +233,7 @@ class Pool:
         from ...core.api import kill
 
         self._closed = True
+        self._terminated = True
         for a, _ in self._actors:
             try:
                 kill(a)

@@ -1462,15 +1462,21 @@ __device__ __forceinline__ void dma_lds16(__amdgpu_buffer_rsrc_t r, lds_char* ds
                                            __builtin_amdgcn_readfirstlane(soff), 0, 0);
 }
 
-template <int BM, int BN, int EPI, int ABL = 0, int DSPLIT = 2>
+// PH = 4: phases (k-sub, m-half), 4 x TN MFMAs each; PH = 2: phases = m-halves with
+// both k-subs, 8 x TN MFMAs each (half the barriers, twice the fragment registers).
+// ABL (timing ablations): 1 no in-loop DMA, 2 no LDS reads, 4 no MFMA, 8 no epilogue
+// stores, 16 no vmcnt waits, 32 every K-tile re-reads the first (L2-hot).
+template <int BM, int BN, int EPI, int ABL = 0, int DSPLIT = 2, int PH = 4>
 __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
   constexpr int WM = 2, WN = 4;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
-  constexpr int PH = 4, TMH = TM / 2;
+  constexpr int TMH = TM / 2;
+  static_assert(PH == 2 || PH == 4, "phases per K-tile");
+  static_assert(PH == 4 || DSPLIT == 1, "two phases: all DMA rounds in phase 0");
   constexpr int A_ST = BM * 128, B_ST = BN * 128, ST = A_ST + B_ST;
   constexpr int NA = A_ST / (NTHR * 16), NB = B_ST / (NTHR * 16), NR = NA + NB;
   static_assert(A_ST % (NTHR * 16) == 0 && B_ST % (NTHR * 16) == 0, "whole DMA rounds");
-  static_assert(DSPLIT >= 1 && DSPLIT <= 3, "DMA rounds go into phases 0 .. DSPLIT-1");
+  static_assert(DSPLIT >= 1 && DSPLIT <= PH - 1, "DMA rounds go into phases 0 .. DSPLIT-1");
   static_assert(TM % 2 == 0, "two m-halves");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   lds_char* smem = (lds_char*)smem_raw;
@@ -1536,7 +1542,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
             smem + ((t_) & 1) * ST +                                                                  \
                 ((j_) < NA ? ((j_) * NTHR + wid * 64) * 16 : A_ST + (((j_) - NA) * NTHR + wid * 64) * 16), \
             (j_) < NA ? voff_a : voff_b,                                                              \
-            (t0 + (t_)) * 128 + ((j_) < NA ? (j_) * 64 * p.lda : ((j_) - NA) * 64 * p.ldb) * 2)
+            ((ABL & 32) ? t0 : t0 + (t_)) * 128 + ((j_) < NA ? (j_) * 64 * p.lda : ((j_) - NA) * 64 * p.ldb) * 2)
   // rounds of phase q: [lo, hi)
   auto rlo = [](int q) { return q >= DSPLIT ? NR : (NR * q) / DSPLIT; };
 
@@ -1552,39 +1558,44 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
     if (nk > 1) {
 #pragma unroll
       for (int j = 0; j < NR; ++j) K64_DMA_ROUND(1, j);
-      wait_vm<NR>();
+      if constexpr (!(ABL & 16)) wait_vm<NR>();
     } else {
       wait_vm<0>();
     }
     __builtin_amdgcn_s_barrier();
     if (!lo_grp) __builtin_amdgcn_s_barrier();  // stagger the second wave row by one barrier
-    bf16x8_t bf[TN];
-    bf16x8_t af[TMH];
+    constexpr int NKS = PH == 4 ? 1 : 2;  // k-subs per phase
+    bf16x8_t bf[NKS][TN];
+    bf16x8_t af[NKS][TMH];
     for (int t = 0; t < nk; ++t) {
       const lds_char* As = smem + (t & 1) * ST;
       const lds_char* Bs = As + A_ST;
       const bool pre = !(ABL & 1) && t >= 1 && t + 1 < nk;  // K-tile t+1 (t = 0: issued in the prologue)
 #pragma unroll
       for (int q = 0; q < PH; ++q) {
-        const int ks = q >> 1, mh = q & 1;
+        const int mh = PH == 4 ? (q & 1) : q;
         // ---- R segment
         if (pre) {
 #pragma unroll
           for (int j = rlo(q); j < rlo(q + 1); ++j) K64_DMA_ROUND(t + 1, j);
         }
-        if (mh == 0) {
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            if constexpr (ABL & 2) { bf[j] = bf16x8_t{}; asm volatile("" : "+v"(bf[j])); }
-            else bf[j] = frag_kmaj(Bs, wc * (TN * 16) + j * 16, ks, lane);
+        for (int u = 0; u < NKS; ++u) {
+          const int ks = PH == 4 ? (q >> 1) : u;
+          if (mh == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              if constexpr (ABL & 2) { bf[u][j] = bf16x8_t{}; asm volatile("" : "+v"(bf[u][j])); }
+              else bf[u][j] = frag_kmaj(Bs, wc * (TN * 16) + j * 16, ks, lane);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < TMH; ++i) {
+            if constexpr (ABL & 2) { af[u][i] = bf16x8_t{}; asm volatile("" : "+v"(af[u][i])); }
+            else af[u][i] = frag_kmaj(As, wr * (TM * 16) + (mh * TMH + i) * 16, ks, lane);
           }
         }
-#pragma unroll
-        for (int i = 0; i < TMH; ++i) {
-          if constexpr (ABL & 2) { af[i] = bf16x8_t{}; asm volatile("" : "+v"(af[i])); }
-          else af[i] = frag_kmaj(As, wr * (TM * 16) + (mh * TMH + i) * 16, ks, lane);
-        }
-        if (q == PH - 1 && !lo_grp) wait_vm<0>();  // lagging row: K-tile t+1 landed
+        if (!(ABL & 16) && q == PH - 1 && !lo_grp) wait_vm<0>();  // lagging row: K-tile t+1 landed
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -1592,13 +1603,15 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
         // ---- M segment
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < TMH; ++i)
+        for (int u = 0; u < NKS; ++u)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            if constexpr (ABL & 4) asm volatile("" :: "v"(bf[j]), "v"(af[i]));
-            else acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[mh * TMH + i][j], 0, 0, 0);
+          for (int i = 0; i < TMH; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              if constexpr (ABL & 4) asm volatile("" :: "v"(bf[u][j]), "v"(af[u][i]));
+              else acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[u][j], af[u][i], acc[mh * TMH + i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        if (q == PH - 1 && lo_grp) wait_vm<0>();  // leading row: K-tile t+1 landed
+        if (!(ABL & 16) && q == PH - 1 && lo_grp) wait_vm<0>();  // leading row: K-tile t+1 landed
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -1691,9 +1704,9 @@ static void ensure_lds(const void* k, int bytes) {
 
 // algo 9 (full-line kernel): algo = 9 + 10 * ABL + 1000 * DSPLIT (0 -> 2). Development
 // ablations only on 256 x 320 bf16 tiles at the default DMA split.
-template <int BM, int BN, int EPI, int ABL, int DS>
+template <int BM, int BN, int EPI, int ABL, int DS, int PH = 4>
 static hipError_t launch_k64_v(const Args& a, hipStream_t st) {
-  auto k = gemm_k64_kernel<BM, BN, EPI, ABL, DS>;
+  auto k = gemm_k64_kernel<BM, BN, EPI, ABL, DS, PH>;
   constexpr int lds = 2 * (BM + BN) * 128;
   ensure_lds((const void*)k, lds);
   const int T = a.tiles_m * a.tiles_n;
@@ -1702,30 +1715,32 @@ static hipError_t launch_k64_v(const Args& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// variant v = algo / 1000: 0 / 2 -> 4 phases, DMA over phases 0-1; 1 -> phase 0; 3 ->
+// phases 0-2; 4 -> 2 phases (DMA in phase 0). Ablations (abl = algo / 10 % 100) on
+// 256 x 320 bf16 tiles for variants 2 and 4.
 template <int BM, int BN, int EPI>
 static hipError_t launch_k64(const Args& a, hipStream_t st) {
-  const int abl = (a.algo / 10) % 100, ds = a.algo / 1000;
+  const int abl = (a.algo / 10) % 100, v = a.algo / 1000;
   if (a.splitk != 1) return hipErrorInvalidValue;
   if (abl == 0) {
-    switch (ds) {
+    switch (v) {
       case 1: return launch_k64_v<BM, BN, EPI, 0, 1>(a, st);
       case 0:
       case 2: return launch_k64_v<BM, BN, EPI, 0, 2>(a, st);
       case 3: return launch_k64_v<BM, BN, EPI, 0, 3>(a, st);
+      case 4: return launch_k64_v<BM, BN, EPI, 0, 1, 2>(a, st);
       default: return hipErrorInvalidValue;
     }
   }
   if constexpr (BM == 256 && BN == 320 && EPI == EPI_BF16) {
+#define K64_ABL(n)                                                   \
+  case n:                                                            \
+    return v == 4 ? launch_k64_v<BM, BN, EPI, n, 1, 2>(a, st) : launch_k64_v<BM, BN, EPI, n, 2>(a, st);
     switch (abl) {
-      case 1: return launch_k64_v<BM, BN, EPI, 1, 2>(a, st);
-      case 2: return launch_k64_v<BM, BN, EPI, 2, 2>(a, st);
-      case 3: return launch_k64_v<BM, BN, EPI, 3, 2>(a, st);
-      case 4: return launch_k64_v<BM, BN, EPI, 4, 2>(a, st);
-      case 5: return launch_k64_v<BM, BN, EPI, 5, 2>(a, st);
-      case 6: return launch_k64_v<BM, BN, EPI, 6, 2>(a, st);
-      case 8: return launch_k64_v<BM, BN, EPI, 8, 2>(a, st);
+      K64_ABL(1) K64_ABL(2) K64_ABL(3) K64_ABL(4) K64_ABL(6) K64_ABL(8) K64_ABL(22) K64_ABL(38) K64_ABL(54)
       default: break;
     }
+#undef K64_ABL
   }
   return hipErrorInvalidValue;
 }

@@ -140,4 +140,30 @@ def test_uri_cache_evicts_least_recently_used(tmp_path):
     c.touch(str(root / "a"))  # a becomes the most recently used
     gone = c.evict()
     assert gone == [str(root / "b")]
-    assert sorted(os.listdir(root)) == ["a", "c"]
+    assert sorted(n for n in os.listdir(root) if not n.endswith(".lock")) == ["a", "c"]
+
+
+def test_uri_cache_skips_envs_with_live_users(tmp_path):
+    """An env some live process registered as its user (a worker running in it,
+    possibly under another head) is never evicted; stale registrations are dropped."""
+    import subprocess
+    import sys
+
+    from cluster_anywhere_amd.runtime_env.pip import _MARKER, URICache, live_users, mark_in_use
+
+    root = tmp_path / "pip"
+    for i, name in enumerate(["a", "b", "c"]):
+        d = root / name
+        d.mkdir(parents=True)
+        (d / "blob").write_bytes(b"x" * 1000)
+        (d / _MARKER).write_text("{}")
+        os.utime(d / _MARKER, (1000 + i, 1000 + i))
+    mark_in_use(str(root / "a"))  # this process uses the oldest env
+    dead = subprocess.Popen([sys.executable, "-c", "pass"])
+    dead.wait()
+    mark_in_use(str(root / "b"), dead.pid)  # a user that has exited
+    assert live_users(str(root / "a")) == [os.getpid()]
+    c = URICache(str(root), max_bytes=2100)
+    assert c.evict() == [str(root / "b")]
+    assert live_users(str(root / "b")) == []
+    assert os.path.isdir(root / "a")

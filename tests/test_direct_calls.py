@@ -182,3 +182,26 @@ def test_calls_after_kill_do_not_reach_actor(cluster):
     assert _direct_client(a) is None
     with pytest.raises((ActorDiedError, RayActorError)):
         ray.get(a.add.remote(99), timeout=60)
+
+
+def test_dropping_last_handle_waits_for_direct_calls(cluster):
+    """Dropping the last handle of an actor terminates it only after the calls
+    already sent to it have run: the handle's decref (after which the head queues
+    __ray_terminate__) is held back until the direct calls are answered, so the
+    head-path terminate cannot overtake them (the multiprocessing.Pool
+    maxtasksperchild race of round 3)."""
+    import gc
+
+    @ray.remote
+    class Slow:
+        def work(self, t, v):
+            time.sleep(t)
+            return v
+
+    for _ in range(3):
+        a = Slow.remote()
+        assert ray.get(a.work.remote(0, -1)) == -1  # on the direct path now
+        refs = [a.work.remote(0.05, i) for i in range(8)]
+        del a
+        gc.collect()
+        assert ray.get(refs, timeout=60) == list(range(8))

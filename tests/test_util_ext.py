@@ -172,6 +172,24 @@ def test_multiprocessing_pool(cluster):
         assert p.map(_read_init, range(6), chunksize=1) == [42] * 6
 
 
+def _slow_sq(x):
+    time.sleep(0.2)
+    return x * x
+
+
+def test_pool_reruns_chunks_of_a_killed_process(cluster):
+    """A pool process that dies mid-map (OOM kill, crash) costs a re-run of its
+    chunks on a fresh actor, not the map (ActorDiedError under load, round 3)."""
+    from cluster_anywhere_amd.util.multiprocessing import Pool
+
+    with Pool(2) as p:
+        r = p.map_async(_slow_sq, range(12), chunksize=1)
+        time.sleep(0.3)
+        ray.kill(p._actors[0][0])
+        assert r.get(timeout=120) == [i * i for i in range(12)]
+        assert sorted(p.imap_unordered(_sq, range(6))) == [i * i for i in range(6)]
+
+
 @ray.remote(max_retries=0)
 def _hog(path):
     with open(path, "w") as f:
@@ -209,3 +227,4 @@ def test_oom_killer(tmp_path, monkeypatch):
         assert ray.get(_hog_then_ok.remote(str(path), str(tmp_path / "m")), timeout=30) == "retried"
     finally:
         ray.shutdown()
+
