@@ -198,7 +198,12 @@ def actor_stage(inputs: Iterator, spec: dict, op=None) -> Iterator[Tuple[Any, di
     initial = max(min_size, min(max_size, int(spec.get("initial_size") or min_size)))
     per_actor = spec.get("max_tasks_in_flight") or ctx.actor_max_tasks_in_flight
     opts = {k: v for k, v in spec["resources"].items() if v}
-    Actor = remote(**opts)(_MapWorker) if opts else remote(_MapWorker)
+    # a map actor that dies (OOM kill, node loss) is restarted, its UDF re-constructed,
+    # and the batches it owed are run again, so every row is produced exactly once
+    # (reference: actor_pool_map_operator.py:351-357); ray_remote_args may override
+    opts.setdefault("max_restarts", -1)
+    opts.setdefault("max_task_retries", -1)
+    Actor = remote(**opts)(_MapWorker)
 
     actors: List[Any] = []        # ready actors
     load: List[int] = []

@@ -94,6 +94,15 @@ class AlgorithmConfig:
         # callbacks
         self.callbacks_class = None
         self.callbacks_functions: Dict[str, Callable] = {}
+        # fault tolerance (reference: AlgorithmConfig.fault_tolerance)
+        self.restart_failed_env_runners = True
+        self.ignore_env_runner_failures = False
+        self.max_num_env_runner_restarts = 1000
+        self.delay_between_env_runner_restarts_s = 0.0
+        self.env_runner_health_probe_timeout_s = 30.0
+        # learner actors of a LearnerGroup are re-created from the last learner state
+        self.restart_failed_learners = True
+        self.max_num_learner_restarts = 100
         # misc
         self.seed = None
         self.evaluation_interval = None
@@ -239,8 +248,17 @@ class AlgorithmConfig:
     def api_stack(self, **_):
         return self
 
-    def fault_tolerance(self, **_):
-        return self
+    def fault_tolerance(self, *, restart_failed_env_runners=NotProvided, ignore_env_runner_failures=NotProvided,
+                        max_num_env_runner_restarts=NotProvided, delay_between_env_runner_restarts_s=NotProvided,
+                        env_runner_health_probe_timeout_s=NotProvided, restart_failed_learners=NotProvided,
+                        max_num_learner_restarts=NotProvided, **_):
+        return self._set(restart_failed_env_runners=restart_failed_env_runners,
+                         ignore_env_runner_failures=ignore_env_runner_failures,
+                         max_num_env_runner_restarts=max_num_env_runner_restarts,
+                         delay_between_env_runner_restarts_s=delay_between_env_runner_restarts_s,
+                         env_runner_health_probe_timeout_s=env_runner_health_probe_timeout_s,
+                         restart_failed_learners=restart_failed_learners,
+                         max_num_learner_restarts=max_num_learner_restarts)
 
     def checkpointing(self, **_):
         return self
@@ -375,8 +393,11 @@ class Algorithm(Trainable):
         self.callbacks = make_callbacks(c.callbacks_class, c.callbacks_functions)
         self.is_multi_agent = c.is_multi_agent
         runner_cls = MultiAgentEnvRunner if self.is_multi_agent else EnvRunner
-        self.env_runner_group = EnvRunnerGroup(c.runner_config(), c.num_env_runners, c.num_cpus_per_env_runner,
-                                               runner_cls=runner_cls)
+        self.env_runner_group = EnvRunnerGroup(
+            c.runner_config(), c.num_env_runners, c.num_cpus_per_env_runner, runner_cls=runner_cls,
+            restart_failed=c.restart_failed_env_runners, ignore_failures=c.ignore_env_runner_failures,
+            max_restarts=c.max_num_env_runner_restarts, restart_delay_s=c.delay_between_env_runner_restarts_s,
+            on_recreated=self._on_env_runners_recreated)
         self.obs_space, self.act_space = self.env_runner_group.spaces()
         if self.is_multi_agent:
             self.module_spaces = self.obs_space  # module id -> (obs_space, act_space)
@@ -398,6 +419,12 @@ class Algorithm(Trainable):
 
     def setup_algo(self):
         pass
+
+    def _on_env_runners_recreated(self, indices):
+        cb = getattr(self, "callbacks", None)
+        if cb is not None:
+            cb.on_env_runners_recreated(algorithm=self, env_runner_group=self.env_runner_group,
+                                        env_runner_indices=indices, is_evaluation=False)
 
     def _sync_weights(self, extra: Optional[Dict] = None):
         self.env_runner_group.sync_weights(self.learner_group.get_module_state(), extra)

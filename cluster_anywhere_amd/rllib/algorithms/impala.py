@@ -133,23 +133,23 @@ class IMPALA(Algorithm):
             return g.sample()
         from ...core import api as core
 
-        for i, r in enumerate(g.remote):
-            if i not in self._inflight:
-                self._inflight[i] = r.sample.remote()
-        refs = list(self._inflight.values())
-        ready, _ = core.wait(refs, num_returns=1)
-        ready_set = set(ready)
-        frags, done = [], []
-        for i, ref in list(self._inflight.items()):
-            if ref in ready_set:
-                frags.append(core.get(ref))
-                done.append(i)
-                del self._inflight[i]
+        frags = []
+        while not frags:
+            for i in g.healthy_indices():
+                if i not in self._inflight:
+                    self._inflight[i] = g.remote[i].sample.remote()
+            ready, _ = core.wait(list(self._inflight.values()), num_returns=1)
+            ready_set = set(ready)
+            results = g._gather({i: ref for i, ref in self._inflight.items() if ref in ready_set})
+            for i in [i for i, ref in self._inflight.items() if ref in ready_set]:
+                del self._inflight[i]  # answered, or failed (then restored / dropped)
+            frags = [results[i] for i in sorted(results)]
+            done = sorted(results)
         # only the runners that returned get fresh weights (others keep sampling)
-        st = core.put(self.learner_group.get_module_state())
-        core.get([g.remote[i].set_weights.remote(st) for i in done])
+        g.sync_weights_to(self.learner_group.get_module_state(), done)
         for i in done:
-            self._inflight[i] = g.remote[i].sample.remote()
+            if g.healthy[i]:
+                self._inflight[i] = g.remote[i].sample.remote()
         return frags
 
     def _sync_weights(self, extra=None):

@@ -351,25 +351,83 @@ def _free_port():
 
 
 class LearnerGroup:
+    """The local learner (``num_learners == 0``) or N learner actors training one
+    module data-parallel (gloo / RCCL process group).
+
+    Learner actors are restarted (``restart_failed_learners``, up to
+    ``max_num_learner_restarts``): a call that finds an actor dead tears the whole
+    group down (its process group is broken), starts a new one on a fresh
+    rendezvous port, restores the last learner state this group saw (the state of
+    the last completed update: module weights, optimizer moments, update count)
+    and runs the call again."""
+
     def __init__(self, learner_cls, config: Dict[str, Any], module_factory, obs_space, act_space):
         self.n = config.get("num_learners", 0)
         self.local = None
         self.actors = []
+        self.restart_failed = bool(config.get("restart_failed_learners", True))
+        self.max_restarts = int(config.get("max_num_learner_restarts", 100))
+        self.num_restarts = 0
+        self._last_state = None
+        self._spec = (learner_cls, config, module_factory, obs_space, act_space)
         if self.n == 0:
             self.local = learner_cls(config, module_factory, obs_space, act_space)
         else:
-            from ...core import api as core
-            from ...core.actor import ActorClass
+            self._start()
 
-            A = ActorClass(_LearnerActor, {})
-            port = _free_port()
-            gpus = config.get("num_gpus_per_learner", 1) if core.cluster_resources().get("GPU", 0) > 0 else 0
-            self.actors = [A.options(num_cpus=config.get("num_cpus_per_learner", 1), num_gpus=gpus,
-                                     runtime_env={"env_vars": {"CAAMD_NOSET_ROCR_VISIBLE_DEVICES": "1",
-                                                               "HSA_ENABLE_IPC_MODE_LEGACY": "0"}})
-                           .remote(learner_cls, config, module_factory, obs_space, act_space, i, self.n,
-                                   "127.0.0.1", port) for i in range(self.n)]
-            core.get([a.call.remote("get_module_state") for a in self.actors])
+    def _start(self):
+        from ...core import api as core
+        from ...core.actor import ActorClass
+
+        learner_cls, config, module_factory, obs_space, act_space = self._spec
+        A = ActorClass(_LearnerActor, {})
+        port = _free_port()
+        gpus = config.get("num_gpus_per_learner", 1) if core.cluster_resources().get("GPU", 0) > 0 else 0
+        self.actors = [A.options(num_cpus=config.get("num_cpus_per_learner", 1), num_gpus=gpus,
+                                 runtime_env={"env_vars": {"CAAMD_NOSET_ROCR_VISIBLE_DEVICES": "1",
+                                                           "HSA_ENABLE_IPC_MODE_LEGACY": "0"}})
+                       .remote(learner_cls, config, module_factory, obs_space, act_space, i, self.n,
+                               "127.0.0.1", port) for i in range(self.n)]
+        core.get([a.call.remote("get_module_state") for a in self.actors])
+
+    def _restart(self, err):
+        import logging
+
+        from ...core import api as core
+
+        if not self.restart_failed or self.num_restarts >= self.max_restarts:
+            raise err
+        self.num_restarts += 1
+        logging.getLogger(__name__).warning("learner actor failed (%s); restarting the learner group "
+                                            "(restart %d)", err, self.num_restarts)
+        for a in self.actors:
+            try:
+                core.kill(a)
+            except Exception:  # noqa: BLE001
+                pass
+        self._start()
+        if self._last_state is not None:
+            core.get([a.call.remote("set_state", self._last_state) for a in self.actors])
+
+    def _run(self, make_calls):
+        """``make_calls()`` -> refs, one per learner actor; their results. Restarts
+        the group and retries when an actor died."""
+        from ...core import api as core
+        from ...exceptions import RayActorError, WorkerCrashedError
+
+        while True:
+            refs = make_calls()
+            try:
+                return core.get(refs)
+            except (RayActorError, WorkerCrashedError) as e:
+                self._restart(e)
+
+    def _checkpoint(self):
+        """Remember the state to restore after a restart (rank 0's, host tensors)."""
+        if self.restart_failed and self.local is None:
+            from ...core import api as core
+
+            self._last_state = core.get(self.actors[0].call.remote("get_state"))
 
     def _shard(self, batch, i):
         return _shard_nested(batch, i, self.n)
@@ -377,20 +435,20 @@ class LearnerGroup:
     def update(self, batch, minibatch_size=None, num_epochs=1, shuffle=True):
         if self.local is not None:
             return self.local.update(batch, minibatch_size, num_epochs, shuffle)
-        from ...core import api as core
-
         mbs = None if minibatch_size is None else max(1, minibatch_size // self.n)
-        res = core.get([a.call.remote("update", self._shard(batch, i), mbs, num_epochs, shuffle)
-                        for i, a in enumerate(self.actors)])
+        res = self._run(lambda: [a.call.remote("update", self._shard(batch, i), mbs, num_epochs, shuffle)
+                                 for i, a in enumerate(self.actors)])
+        self._checkpoint()
         return _mean_nested(res)
 
     def call(self, method, *args, **kwargs):
         """Run a learner method on the local learner / all learner actors (rank 0's result)."""
         if self.local is not None:
             return getattr(self.local, method)(*args, **kwargs)
-        from ...core import api as core
-
-        return core.get([a.call.remote(method, *args, **kwargs) for a in self.actors])[0]
+        out = self._run(lambda: [a.call.remote(method, *args, **kwargs) for a in self.actors])[0]
+        if method.startswith(("learn", "update", "train")):
+            self._checkpoint()
+        return out
 
     def get_module_state(self):
         return self.call("get_module_state")
@@ -401,9 +459,9 @@ class LearnerGroup:
     def set_state(self, st):
         if self.local is not None:
             return self.local.set_state(st)
-        from ...core import api as core
-
-        core.get([a.call.remote("set_state", st) for a in self.actors])
+        self._run(lambda: [a.call.remote("set_state", st) for a in self.actors])
+        if self.restart_failed:
+            self._last_state = st
 
     def stop(self):
         from ...core import api as core

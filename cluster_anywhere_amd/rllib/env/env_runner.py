@@ -256,15 +256,39 @@ class EnvRunner:
         return True
 
 
+def _actor_failures():
+    from ...exceptions import RayActorError, WorkerCrashedError
+
+    return (RayActorError, WorkerCrashedError)
+
+
 class EnvRunnerGroup:
-    """A local runner (``num_env_runners == 0``) or N remote runner actors."""
+    """A local runner (``num_env_runners == 0``) or N remote runner actors.
+
+    Remote runners are fault tolerant (reference role: ``env_runner_group.py`` over
+    ``FaultTolerantActorManager``): every fan-out call collects its results per
+    runner, and a runner whose actor died is, by default
+    (``restart_failed_env_runners``), replaced by a fresh runner at the same index
+    that gets the last broadcast weights and connector state before it rejoins
+    (``on_recreated`` fires with the indices). With restarts off,
+    ``ignore_env_runner_failures`` keeps training on the healthy runners; otherwise
+    the failure is raised. A fan-out never waits on a dead runner's result."""
 
     def __init__(self, config: Dict[str, Any], num_env_runners: int = 0, num_cpus_per_env_runner: float = 1,
-                 runner_cls=None):
+                 runner_cls=None, *, restart_failed: bool = True, ignore_failures: bool = False,
+                 max_restarts: int = 1000, restart_delay_s: float = 0.0, on_recreated=None):
         self.config = config
         self.runner_cls = runner_cls or EnvRunner
         self.local = None
         self.remote = []
+        self.restart_failed = restart_failed
+        self.ignore_failures = ignore_failures
+        self.max_restarts = max_restarts
+        self.restart_delay_s = restart_delay_s
+        self.on_recreated = on_recreated
+        self.num_restarts = 0
+        self._weights = None  # (object ref, extra) of the last broadcast
+        self._connector_state = None
         if num_env_runners == 0:
             self.local = self.runner_cls(config, 0)
         else:
@@ -272,24 +296,109 @@ class EnvRunnerGroup:
             from ...core.actor import ActorClass
 
             Remote = ActorClass(self.runner_cls, {})
-            self.remote = [Remote.options(num_cpus=num_cpus_per_env_runner).remote(config, i + 1)
-                           for i in range(num_env_runners)]
+            self._spawn = lambda i: Remote.options(num_cpus=num_cpus_per_env_runner).remote(config, i + 1)
+            self.remote = [self._spawn(i) for i in range(num_env_runners)]
+            self.healthy = [True] * num_env_runners
             core.get([r.ping.remote() for r in self.remote])
         self._merger = None
 
-    def _all(self, method, *args):
+    # -------------------------------------------------------- fault tolerance
+    def healthy_indices(self) -> List[int]:
+        return [i for i, ok in enumerate(self.healthy) if ok] if self.remote else []
+
+    def _fanout(self, method, *args, indices=None) -> Dict[int, Any]:
+        """``method(*args)`` on the given (default: every healthy) remote runner;
+        {index: result} of the runners that answered. Failed runners are handled
+        (restored / dropped / raised) before this returns."""
         from ...core import api as core
 
+        idx = self.healthy_indices() if indices is None else list(indices)
+        calls = {i: getattr(self.remote[i], method).remote(*args) for i in idx}
+        return self._gather(calls)
+
+    def _gather(self, calls: Dict[int, Any]) -> Dict[int, Any]:
+        from ...core import api as core
+
+        out, failed = {}, []
+        for i, ref in calls.items():
+            try:
+                out[i] = core.get(ref)
+            except _actor_failures() as e:  # noqa: PERF203
+                failed.append((i, e))
+        if failed:
+            self.handle_failures(failed)
+        return out
+
+    def handle_failures(self, failed) -> None:
+        """[(index, error)] of runners whose actor died."""
+        import logging
+
+        for i, _ in failed:
+            self.healthy[i] = False
+        logging.getLogger(__name__).warning("env runner(s) %s failed: %s", [i for i, _ in failed], failed[0][1])
+        if self.restart_failed:
+            self.restore([i for i, _ in failed])
+        elif not self.ignore_failures:
+            raise failed[0][1]
+        if not self.healthy_indices():
+            raise RuntimeError("every env runner has failed and none could be restored") from failed[0][1]
+
+    def restore(self, indices: List[int]) -> List[int]:
+        """Replace the runners at ``indices`` by fresh actors brought up to date."""
+        import time as _time
+
+        from ...core import api as core
+
+        todo = list(indices)
+        for attempt in range(3):
+            if not todo:
+                break
+            if self.num_restarts + len(todo) > self.max_restarts:
+                raise RuntimeError(f"env runners {todo} failed after {self.num_restarts} restarts "
+                                   f"(max_num_env_runner_restarts={self.max_restarts})")
+            if self.restart_delay_s > 0:
+                _time.sleep(self.restart_delay_s)
+            for i in todo:
+                try:
+                    core.kill(self.remote[i])
+                except Exception:  # noqa: BLE001 - already gone
+                    pass
+                self.remote[i] = self._spawn(i)
+                self.num_restarts += 1
+            try:
+                self._catch_up(todo)
+            except _actor_failures():
+                continue  # a replacement died while starting: replace it again
+            for i in todo:
+                self.healthy[i] = True
+            if self.on_recreated is not None:
+                self.on_recreated(list(todo))
+            return list(todo)
+        raise RuntimeError(f"could not restore env runners {todo}")
+
+    def _catch_up(self, idx: List[int]) -> None:
+        from ...core import api as core
+
+        core.get([self.remote[i].ping.remote() for i in idx])
+        if self._weights is not None:
+            core.get([self.remote[i].set_weights.remote(*self._weights) for i in idx])
+        if self._connector_state is not None:
+            core.get([self.remote[i].set_connector_state.remote(self._connector_state) for i in idx])
+
+    # ----------------------------------------------------------------- calls
+    def _all(self, method, *args):
         if self.local is not None:
             return [getattr(self.local, method)(*args)]
-        return core.get([getattr(r, method).remote(*args) for r in self.remote])
+        res = self._fanout(method, *args)
+        return [res[i] for i in sorted(res)]
 
     def spaces(self):
-        from ...core import api as core
-
         if self.local is not None:
             return self.local.get_spaces()
-        return core.get(self.remote[0].get_spaces.remote())
+        while True:
+            res = self._fanout("get_spaces", indices=self.healthy_indices()[:1])
+            if res:
+                return next(iter(res.values()))
 
     def sync_weights(self, state, extra: Optional[Dict] = None):
         from ...core import api as core
@@ -297,8 +406,16 @@ class EnvRunnerGroup:
         if self.local is not None:
             self.local.set_weights(state, extra)
             return
-        ref = core.put(state)
-        core.get([r.set_weights.remote(ref, extra) for r in self.remote])
+        self._weights = (core.put(state), extra)
+        self._fanout("set_weights", *self._weights)
+
+    def sync_weights_to(self, state, indices: List[int], extra: Optional[Dict] = None):
+        """Broadcast to some runners only (async samplers refresh the ones that
+        just returned); the state also becomes what restored runners get."""
+        from ...core import api as core
+
+        self._weights = (core.put(state), extra)
+        self._fanout("set_weights", *self._weights, indices=[i for i in indices if self.healthy[i]])
 
     def sync_connector_states(self):
         """Merge the runners' connector statistics (e.g. MeanStdFilter deltas) and
@@ -312,18 +429,21 @@ class EnvRunnerGroup:
             self._merger = {k: build_pipeline(self.config.get(f"{k}_connector"))
                             for k in ("env_to_module", "module_to_env")}
         merged = {k: p.merge_states([s[k] for s in states]) for k, p in self._merger.items()}
+        self._connector_state = merged
         self._all("set_connector_state", merged)
         return merged
 
     def sample(self, num_timesteps: Optional[int] = None, explore: bool = True) -> List[Dict]:
-        from ...core import api as core
-
         if self.local is not None:
             return [self.local.sample(num_timesteps, explore)]
-        return core.get([r.sample.remote(num_timesteps, explore) for r in self.remote])
+        for _ in range(3):
+            res = self._fanout("sample", num_timesteps, explore)
+            if res:
+                return [res[i] for i in sorted(res)]
+        raise RuntimeError("no env runner returned a sample")
 
     def sample_async(self, num_timesteps: Optional[int] = None):
-        return [r.sample.remote(num_timesteps) for r in self.remote]
+        return [self.remote[i].sample.remote(num_timesteps) for i in self.healthy_indices()]
 
     def metrics(self) -> Dict[str, Any]:
         from ..utils.metrics import merge_reduced, strip_meta

@@ -171,3 +171,38 @@ def test_dataset_into_trainer(cluster, tmp_path):
                      scaling_config=ScalingConfig(num_workers=2),
                      run_config=RunConfig(name="ds", storage_path=str(tmp_path))).fit()
     assert r.metrics["rows"] > 0
+
+
+class _DiesOnce:
+    """Map UDF whose actor process SIGKILLs itself on its first batch (one actor of
+    the pool, once): the pool restarts it and re-runs the batch."""
+
+    def __init__(self, marker):
+        self.marker = marker
+
+    def __call__(self, batch):
+        import signal
+
+        try:
+            fd = os.open(self.marker, os.O_CREAT | os.O_EXCL | os.O_WRONLY)
+        except FileExistsError:
+            fd = None
+        if fd is not None:
+            os.close(fd)
+            os.kill(os.getpid(), signal.SIGKILL)
+        batch["id2"] = batch["id"] * 2
+        return batch
+
+
+def test_actor_pool_map_survives_sigkilled_actor(cluster, tmp_path):
+    """Reference: actor_pool_map_operator.py:351-357 (map actors restart, their
+    tasks retry): a SIGKILLed map actor costs a re-run, and every row comes out
+    exactly once."""
+    n = 3000
+    ds = rd.range(n, override_num_blocks=30).map_batches(
+        _DiesOnce, fn_constructor_args=(str(tmp_path / "died"),), concurrency=2, batch_size=100)
+    rows = ds.take_all()
+    assert os.path.exists(tmp_path / "died")
+    ids = sorted(r["id"] for r in rows)
+    assert ids == list(range(n))
+    assert all(r["id2"] == 2 * r["id"] for r in rows)
