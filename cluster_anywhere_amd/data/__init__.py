@@ -4,6 +4,23 @@ from .aggregate import AbsMax, AggregateFn, Count, Max, Mean, Min, Std, Sum
 from .context import DataContext
 from .dataset import ActorPoolStrategy, Dataset, GroupedData, MaterializedDataset, Schema, TaskPoolStrategy
 from .iterator import DataIterator
+from .datasource import (BlockBasedFileDatasink, BlockMetadata, Datasink, Datasource, FileShuffleConfig, ReadTask,
+                         RowBasedFileDatasink, TaskContext, WriteResult)
+from .execution_options import ExecutionOptions, ExecutionResources
+from .preprocessors import Preprocessor
+
+DatasetIterator = DataIterator  # the reference's older name of the iterator class
+DatasetContext = DataContext  # ditto for the context
+NodeIdStr = str  # node ids are hex strings
+
+
+class TFXReadOptions:
+    """``read_tfrecords(tfx_read_options=...)`` (reference: tfrecords_datasource.py):
+    accepted for parity; the own tf.train.Example codec needs no TFX batching."""
+
+    def __init__(self, batch_size: int = 2048, auto_infer_schema: bool = True):
+        self.batch_size = batch_size
+        self.auto_infer_schema = auto_infer_schema
 from .read_api import (
     from_arrow,
     from_arrow_refs,
@@ -56,6 +73,9 @@ __all__ = [
     "from_pandas", "from_arrow", "from_numpy_refs", "from_pandas_refs", "from_arrow_refs",
     "from_torch", "from_huggingface", "read_parquet", "read_csv", "read_json", "read_text",
     "read_numpy", "read_binary_files", "read_images", "read_datasource", "preprocessors",
+    "Datasource", "ReadTask", "Datasink", "BlockBasedFileDatasink", "RowBasedFileDatasink", "BlockMetadata",
+    "TaskContext", "WriteResult", "FileShuffleConfig", "ExecutionOptions", "ExecutionResources",
+    "DatasetIterator", "DatasetContext", "NodeIdStr", "Preprocessor", "TFXReadOptions",
 ] + ['read_parquet_bulk', 'read_tfrecords', 'read_webdataset', 'read_sql', 'from_dask', 'from_spark', 'from_modin', 'from_mars', 'from_tf', 'read_bigquery', 'read_mongo', 'read_lance', 'read_iceberg', 'read_hudi', 'read_delta_sharing_tables', 'read_databricks_tables', 'read_clickhouse', 'read_avro', 'read_audio', 'read_videos']
 
 

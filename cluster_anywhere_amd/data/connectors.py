@@ -482,3 +482,132 @@ def read_videos(paths, *, include_paths: bool = False, file_extensions: Optional
 
 __all__ = ["read_clickhouse", "read_delta_sharing_tables", "read_databricks_tables", "read_bigquery", "read_mongo",
            "read_videos"]
+
+
+# ------------------------------------------------------------------------ sinks
+from .datasource import Datasink as _Datasink  # noqa: E402
+
+
+def _plain_value(v):
+    import numpy as _np
+
+    if isinstance(v, _np.generic):
+        return v.item()
+    if isinstance(v, _np.ndarray):
+        return v.tolist()
+    return v
+
+
+class MongoDatasink(_Datasink):
+    """``Dataset.write_mongo``: each write task opens its own client and inserts
+    its blocks' rows (``insert_many``, unordered); returns the count inserted."""
+
+    def __init__(self, uri: str, database: str, collection: str, **mongo_args):
+        self.uri, self.database, self.collection = uri, database, collection
+        self.mongo_args = mongo_args
+
+    def write(self, blocks, ctx) -> int:
+        import pymongo
+
+        n = 0
+        client = pymongo.MongoClient(self.uri, **self.mongo_args)
+        try:
+            coll = client[self.database][self.collection]
+            for blk in blocks:
+                docs = [{k: _plain_value(v) for k, v in r.items()} for r in B.to_arrow(blk).to_pylist()]
+                if docs:
+                    n += len(coll.insert_many(docs, ordered=False).inserted_ids)
+        finally:
+            client.close()
+        return n
+
+
+_BQ_TYPES = (("bool", "BOOLEAN"), ("int", "INTEGER"), ("uint", "INTEGER"), ("float", "FLOAT"),
+             ("double", "FLOAT"), ("timestamp", "TIMESTAMP"), ("datetime", "TIMESTAMP"), ("date", "DATE"),
+             ("binary", "BYTES"), ("bytes", "BYTES"))
+
+
+def _bq_type(t: str) -> str:
+    t = str(t).lower()
+    for prefix, bq in _BQ_TYPES:
+        if t.startswith(prefix):
+            return bq
+    return "STRING"
+
+
+class BigQueryDatasink(_Datasink):
+    """``Dataset.write_bigquery`` over the REST API (the client library is not in
+    the image): ``on_write_start`` drops the table when ``overwrite_table`` and
+    creates it from the Dataset schema; write tasks stream rows with
+    ``tabledata.insertAll`` (500 rows per request, 429 / 5xx retried with backoff)."""
+
+    ROWS_PER_REQUEST = 500
+
+    def __init__(self, project_id: str, dataset: str, schema: Optional[Dict[str, str]], *,
+                 max_retry_cnt: int = 10, overwrite_table: bool = True):
+        if "." not in dataset:
+            raise ValueError('dataset must be "<dataset>.<table>"')
+        self.project_id = project_id
+        self.dataset_id, self.table = dataset.split(".", 1)
+        self.schema = dict(schema or {})
+        self.max_retry_cnt = max_retry_cnt
+        self.overwrite_table = overwrite_table
+        # resolved on the driver: the write tasks' workers need not share its environment
+        self._endpoint = os.environ.get("BIGQUERY_API_ENDPOINT", "https://bigquery.googleapis.com").rstrip("/")
+        self._token = os.environ.get("GOOGLE_OAUTH_ACCESS_TOKEN")
+        if not self._token:
+            raise ValueError("set GOOGLE_OAUTH_ACCESS_TOKEN (an OAuth2 access token for BigQuery)")
+
+    def _api(self):
+        return (f"{self._endpoint}/bigquery/v2/projects/{self.project_id}/datasets/{self.dataset_id}",
+                {"Authorization": f"Bearer {self._token}"})
+
+    def _call(self, method, url, headers, body=None, ok=()):
+        """JSON response of one REST call; 429 / 5xx retried with backoff; status
+        codes in ``ok`` (e.g. 404 on a DELETE) are not errors."""
+        import requests
+
+        for attempt in range(self.max_retry_cnt + 1):
+            r = requests.request(method, url, headers=headers, json=body, timeout=120)
+            if (r.status_code == 429 or r.status_code >= 500) and attempt < self.max_retry_cnt:
+                time.sleep(min(8.0, 0.25 * (2 ** attempt)))
+                continue
+            if r.status_code >= 400 and r.status_code not in ok:
+                raise RuntimeError(f"BigQuery {method} {url} -> HTTP {r.status_code}: {r.text[:500]}")
+            return r.json() if r.content and r.status_code < 300 else {}
+
+    def on_write_start(self) -> None:
+        base, headers = self._api()
+        if self.overwrite_table:
+            self._call("DELETE", f"{base}/tables/{self.table}", headers, ok=(404,))
+        fields = [{"name": k, "type": _bq_type(v), "mode": "NULLABLE"} for k, v in self.schema.items()]
+        self._call("POST", f"{base}/tables", headers,
+                   {"tableReference": {"projectId": self.project_id, "datasetId": self.dataset_id,
+                                       "tableId": self.table}, "schema": {"fields": fields}},
+                   ok=(409,))  # 409: it exists (overwrite_table=False) -> append
+
+    def write(self, blocks, ctx) -> int:
+        import base64
+
+        base, headers = self._api()
+        n = 0
+        for blk in blocks:
+            rows = B.to_arrow(blk).to_pylist()
+            for s in range(0, len(rows), self.ROWS_PER_REQUEST):
+                chunk = []
+                for r in rows[s:s + self.ROWS_PER_REQUEST]:
+                    row = {}
+                    for k, v in r.items():
+                        v = _plain_value(v)
+                        if isinstance(v, (bytes, bytearray)):
+                            v = base64.b64encode(bytes(v)).decode()
+                        elif hasattr(v, "isoformat"):
+                            v = v.isoformat()
+                        row[k] = v
+                    chunk.append({"json": row})
+                out = self._call("POST", f"{base}/tables/{self.table}/insertAll", headers,
+                                 {"rows": chunk, "skipInvalidRows": False, "ignoreUnknownValues": False})
+                if out.get("insertErrors"):
+                    raise RuntimeError(f"BigQuery insertAll rejected rows: {out['insertErrors'][:3]}")
+                n += len(chunk)
+        return n

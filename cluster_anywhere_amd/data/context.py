@@ -38,7 +38,21 @@ class DataContext:
 
     @property
     def execution_options(self):
-        return self
+        """The :class:`~.execution_options.ExecutionOptions` of executions started
+        from this context (``preserve_order`` is ``execution_preserve_order``)."""
+        from .execution_options import ExecutionOptions
+
+        opts = self.__dict__.get("_execution_options")
+        if opts is None:
+            opts = self.__dict__["_execution_options"] = ExecutionOptions()
+        opts.preserve_order = self.execution_preserve_order
+        return opts
+
+    @execution_options.setter
+    def execution_options(self, opts):
+        opts.validate()
+        self.__dict__["_execution_options"] = opts
+        self.execution_preserve_order = bool(opts.preserve_order)
 
     @property
     def preserve_order(self) -> bool:
@@ -47,3 +61,15 @@ class DataContext:
     @preserve_order.setter
     def preserve_order(self, v: bool):
         self.execution_preserve_order = bool(v)
+
+    def resource_limits(self):
+        """(cpu, gpu, object_store_memory) limits of an execution; None = no limit."""
+        opts = self.__dict__.get("_execution_options")
+        if opts is None:
+            return None, None, None
+        r = opts.resource_limits
+        return r.cpu, r.gpu, r.object_store_memory
+
+    def excluded_cpus(self) -> float:
+        opts = self.__dict__.get("_execution_options")
+        return float((opts.exclude_resources.cpu or 0.0) if opts is not None else 0.0)

@@ -279,6 +279,15 @@ def _slice_concat(specs):
     return out, _meta(out)
 
 
+def _datasink_write_task(sink, idx, op_name, *blocks):
+    """Remote write task of ``write_datasink``: (sink's return, rows, bytes)."""
+    from .datasource import TaskContext
+
+    blocks = [b for b in blocks]
+    ret = sink.write(iter(blocks), TaskContext(task_idx=idx, op_name=f"Write({op_name})"))
+    return ret, sum(B.num_rows(b) for b in blocks), sum(B.size_bytes(b) for b in blocks)
+
+
 def _write_block(block, path, fmt, idx, kw):
     if path:
         os.makedirs(path, exist_ok=True)
@@ -910,11 +919,80 @@ class Dataset:
     def to_mars(self, *a, **k):
         raise ImportError("to_mars needs mars, which is not installed in this image")
 
-    def write_datasink(self, datasink, **kw):
-        from ..core.api import get
+    def write_datasink(self, datasink, *, ray_remote_args: Optional[Dict[str, Any]] = None,
+                       concurrency: Optional[int] = None) -> None:
+        """Write through a :class:`~.datasource.Datasink`: ``on_write_start`` here,
+        ``write(blocks, ctx)`` in remote tasks as the blocks stream out of the
+        executor (bundled to ``min_rows_per_write`` rows when the sink sets it; at
+        most ``concurrency`` tasks in flight), then ``on_write_complete`` with the
+        collected :class:`~.datasource.WriteResult` -- or ``on_write_failed`` and a
+        raise. Reference: dataset.py:3991."""
+        from ..core.api import get, wait
+        from .datasource import WriteResult
+        from .executor import _cluster_cpus
 
-        for r, _ in self._execute():
-            datasink.write([get(r)])
+        opts = dict(ray_remote_args or {})
+        if not datasink.supports_distributed_writes:
+            from ..runtime_context import get_runtime_context
+            from ..util.scheduling_strategies import NodeAffinitySchedulingStrategy
+
+            opts["scheduling_strategy"] = NodeAffinitySchedulingStrategy(get_runtime_context().get_node_id(),
+                                                                         soft=False)
+        task = _rf(_datasink_write_task, **opts)
+        limit = max(1, int(concurrency or 2 * _cluster_cpus()))
+        min_rows = datasink.min_rows_per_write or 0
+        name = datasink.get_name()
+        datasink.on_write_start()
+        refs: List[Any] = []
+        try:
+            bundle, rows = [], 0
+            running: List[Any] = []
+
+            def submit():
+                nonlocal bundle, rows, running
+                ref = task.remote(datasink, len(refs), name, *bundle)
+                refs.append(ref)
+                running.append(ref)
+                bundle, rows = [], 0
+                if len(running) >= limit:  # bounded in flight: wait for one to finish
+                    _, running = wait(running, num_returns=1)
+
+            for r, meta in self._execute():
+                bundle.append(r)
+                rows += int(meta.get("num_rows") or 0)
+                if rows >= min_rows:
+                    submit()
+            if bundle:
+                submit()
+            outs = get(refs)
+        except Exception as e:  # noqa: BLE001 - reported to the sink, then raised
+            datasink.on_write_failed(e)
+            raise
+        result = WriteResult(num_rows=sum(o[1] for o in outs), size_bytes=sum(o[2] for o in outs),
+                             write_returns=[o[0] for o in outs])
+        datasink.on_write_complete(result)
+
+    def write_mongo(self, uri: str, database: str, collection: str, *,
+                    ray_remote_args: Optional[Dict[str, Any]] = None, concurrency: Optional[int] = None) -> None:
+        """Insert every row as a document (pymongo ``insert_many`` per block, from
+        the write tasks). Reference: dataset.py write_mongo."""
+        from .connectors import MongoDatasink
+
+        self.write_datasink(MongoDatasink(uri, database, collection), ray_remote_args=ray_remote_args,
+                            concurrency=concurrency)
+
+    def write_bigquery(self, project_id: str, dataset: str, max_retry_cnt: int = 10,
+                       overwrite_table: Optional[bool] = True, *,
+                       ray_remote_args: Optional[Dict[str, Any]] = None, concurrency: Optional[int] = None) -> None:
+        """``dataset`` = ``"<dataset>.<table>"``: the table is (re)created with the
+        Dataset's schema and filled through the BigQuery REST ``tabledata.insertAll``
+        API from the write tasks (retrying 429 / 5xx up to ``max_retry_cnt`` times)."""
+        from .connectors import BigQueryDatasink
+
+        sch = self.schema()
+        self.write_datasink(BigQueryDatasink(project_id, dataset, dict(zip(sch.names, sch.types)) if sch else None,
+                                             max_retry_cnt=max_retry_cnt, overwrite_table=overwrite_table),
+                            ray_remote_args=ray_remote_args, concurrency=concurrency)
 
     def __repr__(self):
         return f"Dataset(num_ops={len(self._ops)}, source={self._source[0]})"

@@ -110,16 +110,31 @@ class _MapWorker:
 
 # ------------------------------------------------------------------ stages
 def _cluster_cpus() -> int:
+    """CPUs an execution may use: the cluster's, minus ExecutionOptions'
+    ``exclude_resources.cpu``, capped by its ``resource_limits.cpu``."""
     from ..core import context
 
     if context.local_mode:
         return 1
+    ctx = DataContext.get_current()
     try:
         from ..core.api import cluster_resources
 
-        return max(1, int(cluster_resources().get("CPU", 1)))
+        n = float(cluster_resources().get("CPU", 1)) - ctx.excluded_cpus()
     except Exception:
-        return 4
+        n = 4.0
+    cpu_limit = ctx.resource_limits()[0]
+    if cpu_limit is not None:
+        n = min(n, float(cpu_limit))
+    return max(1, int(n))
+
+
+def _cpu_limited_inflight(default: int) -> int:
+    """Tasks in flight per operator under ExecutionOptions' CPU limit."""
+    cpu_limit = DataContext.get_current().resource_limits()[0]
+    if cpu_limit is not None and cpu_limit != float("inf"):
+        return max(1, min(default, int(cpu_limit)))
+    return default
 
 
 def _retire(inflight: collections.deque, preserve_order: bool, block: bool = True):
@@ -154,7 +169,7 @@ def task_stage(inputs: Iterator, chain: List[Callable], resources: Dict[str, Any
     from ..core.api import get
 
     ctx = DataContext.get_current()
-    max_inflight = max_inflight or ctx.max_tasks_in_flight_per_op or max(2, 2 * _cluster_cpus())
+    max_inflight = _cpu_limited_inflight(max_inflight or ctx.max_tasks_in_flight_per_op or max(2, 2 * _cluster_cpus()))
     keep_order = ctx.execution_preserve_order
     if op is not None:
         op.warmup_cap = max(2, min(max_inflight, _cluster_cpus()))
@@ -194,6 +209,10 @@ def actor_stage(inputs: Iterator, spec: dict, op=None) -> Iterator[Tuple[Any, di
     ctx = DataContext.get_current()
     keep_order = ctx.execution_preserve_order
     max_size = max(1, int(spec.get("max_size") or spec["size"]))
+    gpu_limit = ctx.resource_limits()[1]
+    per_gpu = float(spec["resources"].get("num_gpus") or 0)
+    if gpu_limit is not None and gpu_limit != float("inf") and per_gpu > 0:
+        max_size = max(1, min(max_size, int(gpu_limit / per_gpu)))  # ExecutionOptions GPU limit
     min_size = max(1, min(max_size, int(spec.get("min_size") or spec["size"])))
     initial = max(min_size, min(max_size, int(spec.get("initial_size") or min_size)))
     per_actor = spec.get("max_tasks_in_flight") or ctx.actor_max_tasks_in_flight

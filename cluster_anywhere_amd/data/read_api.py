@@ -148,8 +148,15 @@ def _file_ds(files, reader, **kw) -> Dataset:
     return ds
 
 
+def _shuffled(files, shuffle):
+    """``shuffle="files"`` / ``FileShuffleConfig(seed)``: read the files in random order."""
+    from .datasource import shuffle_paths
+
+    return shuffle_paths(files, shuffle)
+
+
 def read_parquet(paths, *, columns: Optional[List[str]] = None, filter=None, **kw) -> Dataset:
-    files = _expand(paths, [".parquet"])
+    files = _shuffled(_expand(paths, [".parquet"]), kw.pop("shuffle", None))
 
     def rd(f):
         import pyarrow.parquet as pq
@@ -160,7 +167,7 @@ def read_parquet(paths, *, columns: Optional[List[str]] = None, filter=None, **k
 
 
 def read_csv(paths, **arrow_csv_args) -> Dataset:
-    files = _expand(paths, [".csv", ".csv.gz"])
+    files = _shuffled(_expand(paths, [".csv", ".csv.gz"]), arrow_csv_args.pop("shuffle", None))
 
     def rd(f):
         import pyarrow.csv as pcsv
@@ -171,7 +178,7 @@ def read_csv(paths, **arrow_csv_args) -> Dataset:
 
 
 def read_json(paths, *, lines: bool = True, **kw) -> Dataset:
-    files = _expand(paths, [".json", ".jsonl"])
+    files = _shuffled(_expand(paths, [".json", ".jsonl"]), kw.pop("shuffle", None))
 
     def rd(f):
         import pandas as pd
@@ -185,7 +192,7 @@ def read_json(paths, *, lines: bool = True, **kw) -> Dataset:
 
 
 def read_text(paths, *, encoding: str = "utf-8", drop_empty_lines: bool = True, **kw) -> Dataset:
-    files = _expand(paths)
+    files = _shuffled(_expand(paths), kw.pop("shuffle", None))
 
     def rd(f):
         with open(f, encoding=encoding) as fh:
@@ -198,12 +205,12 @@ def read_text(paths, *, encoding: str = "utf-8", drop_empty_lines: bool = True, 
 
 
 def read_numpy(paths, **kw) -> Dataset:
-    files = _expand(paths, [".npy"])
+    files = _shuffled(_expand(paths, [".npy"]), kw.pop("shuffle", None))
     return _file_ds(files, lambda f: {"data": np.load(f, allow_pickle=False)})
 
 
 def read_binary_files(paths, *, include_paths: bool = False, **kw) -> Dataset:
-    files = _expand(paths)
+    files = _shuffled(_expand(paths), kw.pop("shuffle", None))
 
     def rd(f):
         with open(f, "rb") as fh:
@@ -217,7 +224,7 @@ def read_binary_files(paths, *, include_paths: bool = False, **kw) -> Dataset:
 
 
 def read_images(paths, *, size=None, mode=None, include_paths: bool = False, **kw) -> Dataset:
-    files = _expand(paths, [".png", ".jpg", ".jpeg", ".bmp", ".gif", ".npy"])
+    files = _shuffled(_expand(paths, [".png", ".jpg", ".jpeg", ".bmp", ".gif", ".npy"]), kw.pop("shuffle", None))
 
     def rd(f):
         if f.endswith(".npy"):
@@ -503,6 +510,30 @@ from .connectors import (read_bigquery, read_clickhouse, read_databricks_tables,
                          read_delta_sharing_tables, read_mongo, read_videos)
 
 
-def read_datasource(datasource, *, parallelism: int = -1, **kw) -> Dataset:
-    tasks = datasource.get_read_tasks(parallelism if parallelism > 0 else 8)
-    return Dataset(("read", [(lambda t=t: B.concat([B.from_batch(x) for x in t()])) for t in tasks]))
+def _run_read_task(task):
+    """One read operator input: a ReadTask (or any callable) -> one block."""
+    out = task()
+    if out is None:
+        return {}
+    if isinstance(out, dict) or B.is_arrow(out) or hasattr(out, "to_numpy") and hasattr(out, "columns"):
+        return B.from_batch(out)  # a single block, not an iterable of blocks
+    return B.concat([B.from_batch(x) for x in out])
+
+
+def read_datasource(datasource, *, parallelism: int = -1, ray_remote_args: Optional[Dict[str, Any]] = None,
+                    concurrency: Optional[int] = None, override_num_blocks: Optional[int] = None,
+                    **read_args) -> Dataset:
+    """Read a custom :class:`~.datasource.Datasource`: ``get_read_tasks`` runs here
+    once; each :class:`~.datasource.ReadTask` is one read input of the streaming
+    executor, run in a remote task. Reference: read_api.py read_datasource."""
+    import functools
+
+    from .context import DataContext
+    from .executor import _cluster_cpus
+
+    n = override_num_blocks or (parallelism if parallelism and parallelism > 0 else 0)
+    if not n:
+        n = max(DataContext.get_current().read_op_min_num_blocks, 2 * _cluster_cpus())
+    tasks = datasource.get_read_tasks(int(n), **read_args) if read_args else datasource.get_read_tasks(int(n))
+    fns = [functools.partial(_run_read_task, t) for t in tasks]
+    return Dataset(("read", fns))

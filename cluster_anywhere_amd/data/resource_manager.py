@@ -104,6 +104,9 @@ class ResourceManager:
 
         ctx = DataContext.get_current()
         cap = ctx.execution_object_store_bytes
+        limit = ctx.resource_limits()[2]
+        if limit is not None and limit != float("inf"):
+            cap = float(limit)  # ExecutionOptions(resource_limits=ExecutionResources(object_store_memory=...))
         if not cap:
             try:
                 from ..core.api import cluster_resources

@@ -40,6 +40,8 @@ def _arrow_stream(t):
 class State:
     polls = 0
     auth = []
+    bq_tables = {}
+    bq_inserts = 0
 
 
 class Handler(BaseHTTPRequestHandler):
@@ -93,12 +95,35 @@ class Handler(BaseHTTPRequestHandler):
             req = json.loads(body)
             State.dbx_req = req
             return self._send(200, {"statement_id": "s1", "status": {"state": "PENDING"}})
+        if u.path == "/bigquery/v2/projects/p1/datasets/d1/tables":
+            req = json.loads(body)
+            name = req["tableReference"]["tableId"]
+            if name in State.bq_tables:
+                return self._send(409, {"error": {"code": 409, "message": "Already Exists"}})
+            State.bq_tables[name] = {"schema": req["schema"], "rows": []}
+            return self._send(200, req)
+        m = re.match(r"^/bigquery/v2/projects/p1/datasets/d1/tables/(\w+)/insertAll$", u.path)
+        if m:
+            State.bq_inserts += 1
+            if State.bq_inserts == 1:  # the first request is throttled: the sink retries
+                return self._send(503, {"error": {"code": 503}})
+            State.bq_tables[m.group(1)]["rows"].extend(r["json"] for r in json.loads(body)["rows"])
+            return self._send(200, {"kind": "bigquery#tableDataInsertAllResponse"})
         if u.path.startswith("/bigquery/v2/projects/p1/queries"):
             return self._send(200, {"jobReference": {"jobId": "j1"}, "jobComplete": True,
                                     "schema": {"fields": [{"name": "id", "type": "INTEGER"},
                                                           {"name": "ok", "type": "BOOLEAN"}]},
                                     "rows": [{"f": [{"v": "1"}, {"v": "true"}]}], "pageToken": "t2"})
         self._send(404, "no")
+
+    def do_DELETE(self):
+        m = re.match(r"^/bigquery/v2/projects/p1/datasets/d1/tables/(\w+)$", urlparse(self.path).path)
+        if m and m.group(1) in State.bq_tables:
+            del State.bq_tables[m.group(1)]
+            self.send_response(204)
+            self.end_headers()
+            return
+        self._send(404, {"error": {"code": 404}})
 
     def do_GET(self):
         u = urlparse(self.path)
@@ -283,6 +308,9 @@ class _MiniMongo:
             return {"ok": 1.0}
         if name == "count":
             return {"ok": 1.0, "n": len(self.docs)}
+        if name == "insert":
+            self.docs.extend(cmd.get("documents") or [])
+            return {"ok": 1.0, "n": len(cmd.get("documents") or [])}
         ns = f"{cmd.get('$db', 'db')}.{cmd[next(iter(cmd))]}"
         if name == "find":
             out = sorted(self.docs, key=lambda d: d["_id"])
@@ -315,7 +343,22 @@ class _MiniMongo:
                 ln, req_id, _, op = struct.unpack("<iiii", self._recv(conn, 16))
                 body = self._recv(conn, ln - 16)
                 if op == 2013:
-                    doc = bson.decode(body[5:5 + struct.unpack("<i", body[5:9])[0]])
+                    n0 = struct.unpack("<i", body[5:9])[0]
+                    doc = bson.decode(body[5:5 + n0])
+                    i = 5 + n0
+                    while i < len(body) and body[i] == 1:  # kind-1 document sequence (insert documents)
+                        size = struct.unpack("<i", body[i + 1:i + 5])[0]
+                        end = i + 1 + size
+                        j = body.index(b"\x00", i + 5)
+                        ident = body[i + 5:j].decode()
+                        j += 1
+                        seq = []
+                        while j < end:
+                            dl = struct.unpack("<i", body[j:j + 4])[0]
+                            seq.append(bson.decode(body[j:j + dl]))
+                            j += dl
+                        doc[ident] = seq
+                        i = end
                     self._reply(conn, req_id, self._run(doc), False)
                 elif op == 2004:  # legacy OP_QUERY handshake
                     i = 4 + body[4:].index(b"\x00") + 1 + 8
@@ -380,3 +423,28 @@ def test_read_videos_native_containers(server, tmp_path):
     (tmp_path / "d.mp4").write_bytes(b"\x00" * 16)
     with pytest.raises(Exception):
         data.read_videos(str(tmp_path / "d.mp4")).take_all()
+
+
+def test_write_mongo_round_trip(server):
+    srv = _MiniMongo([])
+    uri = f"mongodb://127.0.0.1:{srv.port}/?directConnection=true&serverSelectionTimeoutMS=3000"
+    data.range(60, override_num_blocks=6).map(lambda r: {"_id": r["id"], "sq": r["id"] ** 2}).write_mongo(
+        uri, "db", "w")
+    assert sorted(d["_id"] for d in srv.docs) == list(range(60))
+    back = data.read_mongo(uri, "db", "w").take_all()
+    assert {r["_id"]: r["sq"] for r in back} == {i: i * i for i in range(60)}
+
+
+def test_write_bigquery_creates_table_and_inserts(server, monkeypatch):
+    monkeypatch.setenv("BIGQUERY_API_ENDPOINT", server)
+    monkeypatch.setenv("GOOGLE_OAUTH_ACCESS_TOKEN", "tok")
+    State.bq_tables["t2"] = {"schema": {}, "rows": [{"stale": 1}]}  # dropped by overwrite_table
+    ds = data.from_items([{"id": i, "name": f"r{i}", "x": i / 4, "ok": i % 2 == 0} for i in range(1200)])
+    ds.write_bigquery("p1", "d1.t2")
+    t = State.bq_tables["t2"]
+    types = {f["name"]: f["type"] for f in t["schema"]["fields"]}
+    assert types == {"id": "INTEGER", "name": "STRING", "x": "FLOAT", "ok": "BOOLEAN"}
+    assert sorted(r["id"] for r in t["rows"]) == list(range(1200))
+    assert State.bq_inserts >= 4  # 500-row requests, one retried after a 503
+    ds.limit(10).write_bigquery("p1", "d1.t2", overwrite_table=False)  # 409 on create -> append
+    assert len(State.bq_tables["t2"]["rows"]) == 1210
