@@ -16,6 +16,7 @@ nodes connect to over TCP.
 from __future__ import annotations
 
 import collections
+import itertools
 import os
 import selectors
 import signal
@@ -267,6 +268,10 @@ class Head:
         self.gen_stats: Dict[bytes, dict] = {}
         self.handle_objs: Dict[bytes, bytes] = {}  # handle object id -> actor id
         self.events: collections.deque = collections.deque(maxlen=200000)
+        # cluster events for the state API (reference: list_cluster_events / the
+        # dashboard's event head): node / actor / job / OOM / infeasibility records
+        self.cluster_events: collections.deque = collections.deque(maxlen=10000)
+        self._event_seq = itertools.count(1)
         self.jobs: Dict[bytes, dict] = {}
         self.metrics: Dict[str, dict] = {}
         self.max_workers = int(max(4, resources.get("CPU", 1) * 4))
@@ -303,6 +308,7 @@ class Head:
         self._reattaching = False
         self.subscribers: Dict[str, Set[Conn]] = {}  # pubsub channel -> subscriber connections
         self.env_failures: Dict[str, str] = {}  # runtime-env key -> setup error
+        self.env_specs: Dict[str, Any] = {}  # runtime-env key -> the runtime env (state API)
         self.reattached_running: Dict[bytes, tuple] = {}  # task id -> (worker, node, demand) of a re-registered run
         self._held_resubmits: List[tuple] = []  # (conn, spec) replayed by owners during the re-attach grace
         # re-attach ordering: a lease whose worker has not re-registered yet is
@@ -513,6 +519,8 @@ class Head:
             jid = extra.get("job_id", b"")
             if jid not in self.jobs:
                 self.jobs[jid] = {"start": time.time(), "pid": pid, "driver": worker_id}
+                self._cluster_event("INFO", "GCS", f"job {jid.hex() if isinstance(jid, bytes) else jid} started",
+                                    job_id=jid.hex() if isinstance(jid, bytes) else str(jid), pid=pid)
                 if self.gcs is not None:
                     self.gcs.job_put(jid, self.jobs[jid])
 
@@ -1080,6 +1088,8 @@ class Head:
             if spec not in self.infeasible:
                 self.infeasible.append(spec)
                 self.events.append(("infeasible", spec.task_id, spec.fn_name, time.time()))
+                self._cluster_event("WARNING", "RAYLET", f"task {spec.fn_name} is infeasible: no node has "
+                                    f"{self._demand(spec)}", task_id=spec.task_id.hex())
             return True  # parked
         if node == "":
             return False
@@ -1196,6 +1206,8 @@ class Head:
     def _spawn_worker(self, node, gpu_ids, worker_id=None, env=None):
         worker_id = worker_id or os.urandom(16)
         ek = _env_key(env)
+        if ek is not None:
+            self.env_specs.setdefault(ek, env)
         key = (node, tuple(gpu_ids), ek)
         self.starting[key] += 1
         if node != self.head_hex:
@@ -1579,9 +1591,21 @@ class Head:
                 continue
             self._send(sc, ("pub", channel, key, info))
 
+    def _cluster_event(self, severity: str, source: str, message: str, **fields):
+        self.cluster_events.append({"event_id": next(self._event_seq), "severity": severity,
+                                    "source_type": source, "message": message, "time": time.time(),
+                                    "custom_fields": fields})
+
     def _set_actor_state(self, a, state):
         if a.state == state:
             return
+        if state == "DEAD":
+            self._cluster_event("WARNING" if a.death_cause else "INFO", "GCS",
+                                f"actor {a.class_name} {a.actor_id.hex()[:12]} died: {a.death_cause or 'exited'}",
+                                actor_id=a.actor_id.hex(), pid=a.pid, node_id=a.node)
+        elif state == "RESTARTING":
+            self._cluster_event("WARNING", "GCS", f"actor {a.class_name} {a.actor_id.hex()[:12]} is restarting",
+                                actor_id=a.actor_id.hex())
         a.state = state
         self._publish("actor", a.actor_id, {"state": state, "name": a.name, "namespace": a.namespace,
                                             "class_name": a.class_name, "pid": a.pid, "node": a.node,
@@ -1971,6 +1995,8 @@ class Head:
                     f"threshold {self.mem_monitor.threshold:.2f}); retries exhausted.")))
             else:
                 self._fail_task(spec, ("WorkerCrashedError", "the worker died while running the task"))
+                self._cluster_event("ERROR", "RAYLET", f"worker {w.pid} died while running {spec.fn_name}",
+                                    worker_id=w.worker_id.hex(), task_id=spec.task_id.hex(), node_id=w.node)
         w.tasks_inflight.clear()
         self.workers.pop(w.worker_id, None)
         self._schedule()
@@ -2017,6 +2043,8 @@ class Head:
         self.oom_killed_ids.add(w.worker_id)
         self.mem_monitor.kills += 1
         self.events.append(("oom_kill", w.worker_id.hex(), time.time(), frac))
+        self._cluster_event("ERROR", "RAYLET", f"memory monitor killed worker {w.pid} at {frac:.0%} node memory",
+                            worker_id=w.worker_id.hex(), node_id=w.node, memory_fraction=frac)
         if w.actor_id is not None:
             a = self.actors.get(w.actor_id)
             if a is not None:
@@ -2505,9 +2533,31 @@ class Head:
                      "node_id": a.node, "num_restarts": a.num_restarts,
                      "death_cause": a.death_cause} for a in self.actors.values()]
         if what == "tasks":
-            return [{"task_id": t.task_id.hex(), "name": t.fn_name, "state": t.state,
-                     "kind": ["NORMAL_TASK", "ACTOR_CREATION_TASK", "ACTOR_TASK"][t.kind],
-                     "node_id": t.node, "attempt": t.attempt} for t in self.tasks.values()]
+            live = {t.task_id: {"task_id": t.task_id.hex(), "name": t.fn_name, "state": t.state,
+                                "kind": ["NORMAL_TASK", "ACTOR_CREATION_TASK", "ACTOR_TASK"][t.kind],
+                                "node_id": t.node, "attempt": t.attempt} for t in self.tasks.values()}
+            # tasks the head no longer tracks (finished; or run on owner leases / direct
+            # actor calls, which report only their task events): from the event buffer
+            done: Dict[bytes, Dict[str, Any]] = {}
+            for e in self.events:
+                if e[0] not in ("submit", "start", "end") or not isinstance(e[1], (bytes, bytearray)):
+                    continue
+                if e[1] in live:
+                    continue
+                r = done.get(e[1])
+                if r is None:
+                    r = done[e[1]] = {"task_id": e[1].hex(), "name": e[2], "state": "PENDING_SCHEDULING",
+                                      "kind": "NORMAL_TASK", "node_id": None, "attempt": 0}
+                if e[0] == "start":
+                    r["start_time_ms"] = int(e[3] * 1000) if e[3] else None
+                    if len(e) > 4:
+                        r["worker_pid"] = e[4]
+                    if r["state"] != "FINISHED":
+                        r["state"] = "RUNNING"
+                elif e[0] == "end":
+                    r["end_time_ms"] = int(e[3] * 1000)
+                    r["state"] = "FINISHED"
+            return list(live.values()) + list(done.values())
         if what == "objects":
             return [{"object_id": o.hex(), "state": ["PENDING", "READY", "FREED"][e.state],
                      "size": e.size, "inline": e.inline is not None, "ref_count": e.refcount,
@@ -2525,6 +2575,24 @@ class Head:
             return [{"job_id": j.hex() if isinstance(j, bytes) else str(j), **v} for j, v in self.jobs.items()]
         if what == "events":
             return list(self.events)
+        if what == "cluster_events":
+            return list(self.cluster_events)
+        if what == "runtime_envs":
+            envs: Dict[Any, Dict[str, Any]] = {}
+            for w in self.workers.values():
+                if w.env_key is None:
+                    continue
+                e = envs.setdefault(w.env_key, {"runtime_env_key": w.env_key,
+                                                "runtime_env": self.env_specs.get(w.env_key),
+                                                "nodes": set(), "num_workers": 0,
+                                                "success": w.env_key not in self.env_failures,
+                                                "error": self.env_failures.get(w.env_key)})
+                e["nodes"].add(w.node)
+                e["num_workers"] += 1
+            for k, err in self.env_failures.items():
+                envs.setdefault(k, {"runtime_env_key": k, "runtime_env": self.env_specs.get(k), "nodes": set(),
+                                    "num_workers": 0, "success": False, "error": err})
+            return [dict(e, nodes=sorted(e["nodes"])) for e in envs.values()]
         if what == "store":
             return {"capacity": self.store.capacity, "used": self.store.used,
                     "num_objects": self.store.num_objects}
@@ -2593,6 +2661,7 @@ class Head:
                                       "head_tcp": self.tcp_address, "reconnect_s": self.reconnect_s}))
         self.events.append(("node_added", node_hex, time.time()))
         self._publish("node", node_hex, {"state": "ALIVE", "address": addr, "resources": dict(res)})
+        self._cluster_event("INFO", "GCS", f"node {node_hex[:12]} ({addr}) joined", node_id=node_hex)
         self._retry_pending_pgs()
         self._retry_infeasible()
         self._schedule()
@@ -2604,6 +2673,7 @@ class Head:
             self.node_info[node_hex]["Alive"] = False
         self.events.append(("node_removed", node_hex, time.time()))
         self._publish("node", node_hex, {"state": "DEAD"})
+        self._cluster_event("ERROR", "GCS", f"node {node_hex[:12]} died", node_id=node_hex)
         # objects whose only copy lived there are lost: re-execute their lineage
         # where possible (reference: object_recovery_manager.cc RecoverObject)
         for oid, e in list(self.objects.items()):
