@@ -72,6 +72,9 @@ def _rebuild_ref(id_bytes):
     return ObjectRef(id_bytes)
 
 
+_END = object()  # end-of-stream sentinel of ObjectRefGenerator.__anext__
+
+
 class ObjectRefGenerator:
     """Iterator over the ObjectRefs a ``num_returns="streaming"`` task yields,
     in order, as soon as each is produced (reference: _raylet.pyx:ObjectRefGenerator)."""
@@ -104,12 +107,20 @@ class ObjectRefGenerator:
     def __aiter__(self):
         return self
 
+    def _next_or_end(self):
+        # StopIteration cannot cross a Future (asyncio turns it into a TypeError):
+        # the end of the stream comes back as a sentinel instead
+        try:
+            return self.__next__()
+        except StopIteration:
+            return _END
+
     async def __anext__(self):
         loop = asyncio.get_running_loop()
-        try:
-            return await loop.run_in_executor(None, self.__next__)
-        except StopIteration:
+        item = await loop.run_in_executor(None, self._next_or_end)
+        if item is _END:
             raise StopAsyncIteration
+        return item
 
     def completed(self) -> ObjectRef:
         return self._keep

@@ -97,6 +97,10 @@ class LLMServer:
             raise RuntimeError(f"engine failed: {self.engine.error}")
 
 
+def _sse(obj) -> str:
+    return "data: " + json.dumps(obj) + "\n\n"
+
+
 def _router_cls():
     from fastapi import FastAPI, Request
     from fastapi.responses import JSONResponse, StreamingResponse
@@ -126,12 +130,18 @@ def _router_cls():
             if h is None:
                 return JSONResponse({"error": f"unknown model {body.get('model')}"}, status_code=404)
             if body.get("stream"):
-                chunks = []
-                async for d in h.options(stream=True, method_name="stream").remote(body):
-                    chunks.append("data: " + json.dumps({"choices": [{"text": d["text"],
-                                                                      "finish_reason": d["finish_reason"]}]}) + "\n\n")
-                chunks.append("data: [DONE]\n\n")
-                return StreamingResponse(iter(chunks), media_type="text/event-stream")
+                cid, created = f"cmpl-{uuid.uuid4().hex[:12]}", int(time.time())
+                model = body.get("model") or next(iter(self.servers))
+
+                async def sse():
+                    # one SSE event per engine step, written as soon as the replica yields it
+                    async for d in h.options(stream=True, method_name="stream").remote(body):
+                        yield _sse({"id": cid, "object": "text_completion", "created": created, "model": model,
+                                    "choices": [{"index": 0, "text": d["text"], "token_ids": d["token_ids"],
+                                                 "finish_reason": d["finish_reason"]}]})
+                    yield "data: [DONE]\n\n"
+
+                return StreamingResponse(sse(), media_type="text/event-stream")
             return await h.generate.remote(body)
 
         @api.post("/v1/chat/completions")
@@ -140,6 +150,20 @@ def _router_cls():
             h = self._server(body)
             if h is None:
                 return JSONResponse({"error": f"unknown model {body.get('model')}"}, status_code=404)
+            if body.get("stream"):
+                cid, created = f"chatcmpl-{uuid.uuid4().hex[:12]}", int(time.time())
+                model = body.get("model") or next(iter(self.servers))
+
+                async def sse():
+                    head = {"id": cid, "object": "chat.completion.chunk", "created": created, "model": model}
+                    yield _sse(dict(head, choices=[{"index": 0, "delta": {"role": "assistant"},
+                                                    "finish_reason": None}]))
+                    async for d in h.options(stream=True, method_name="stream").remote(body):
+                        yield _sse(dict(head, choices=[{"index": 0, "delta": {"content": d["text"]},
+                                                        "finish_reason": d["finish_reason"]}]))
+                    yield "data: [DONE]\n\n"
+
+                return StreamingResponse(sse(), media_type="text/event-stream")
             r = await h.generate.remote(body)
             c = r["choices"][0]
             return {"id": r["id"].replace("cmpl", "chatcmpl"), "object": "chat.completion", "created": r["created"],
@@ -162,9 +186,35 @@ def build_llm_deployment(llm_config: LLMConfig, *, name_prefix: str = "LLMServer
     return d.options(ray_actor_options=opts, **dc).bind(llm_config)
 
 
-def build_openai_app(llm_serving_args: Union[Dict, List[LLMConfig]]) -> Application:
-    configs = llm_serving_args.get("llm_configs") if isinstance(llm_serving_args, dict) else llm_serving_args
+def build_openai_app(llm_serving_args) -> Application:
+    """``llm_serving_args``: an :class:`LLMServingArgs`, ``{"llm_configs": [...]}`` or
+    a list of configs."""
+    if isinstance(llm_serving_args, dict):
+        configs = llm_serving_args.get("llm_configs")
+    elif hasattr(llm_serving_args, "llm_configs"):
+        configs = llm_serving_args.llm_configs
+    else:
+        configs = llm_serving_args
     configs = [c if isinstance(c, LLMConfig) else LLMConfig(**c) for c in configs]
     servers = {c.model_id: build_llm_deployment(c) for c in configs}
     Router = deployment(_router_cls(), name="LLMRouter")
     return Router.bind(servers)
+
+
+# ---- reference names (python/ray/serve/llm.py:19-63) -------------------------------
+VLLMDeployment = LLMServer  # the engine deployment class (the in-tree engine, not vLLM)
+
+
+def LLMModelRouterDeployment(*args, **kwargs):
+    """The OpenAI-compatible router deployment class (FastAPI ingress), built lazily
+    so importing serve.llm does not import FastAPI."""
+    return _router_cls()(*args, **kwargs)
+
+
+@dataclass
+class LLMServingArgs:
+    llm_configs: List[Union[LLMConfig, Dict[str, Any]]] = field(default_factory=list)
+
+
+def build_vllm_deployment(llm_config: LLMConfig) -> Application:
+    return build_llm_deployment(llm_config)

@@ -4,7 +4,8 @@ proxy_router.py).
 A uvicorn server on its own thread inside an actor. Requests are matched to the
 longest ``route_prefix``; the body is read fully and shipped with method / path
 (relative to the prefix) / query / headers to the ingress deployment's
-``handle_http`` through the same power-of-two router handles use. Routes are
+``handle_http_stream`` through the same power-of-two router handles use; the
+response comes back as a stream (one item when it is complete at once). Routes are
 refreshed from the controller every 0.5 s. ``/-/healthz`` and ``/-/routes`` are
 built-in."""
 from __future__ import annotations
@@ -107,26 +108,48 @@ class HTTPProxy:
         loop = asyncio.get_event_loop()
         from ..exceptions import RayActorError
 
+        # the replica streams the response back (handle_http_stream): a complete
+        # response is one item; a streaming one (SSE, StreamingResponse) is relayed
+        # chunk by chunk as the app produces it
+        gen = first = tag = None
         try:
             for attempt in range(3):
                 tag, h, _ = await loop.run_in_executor(None, router.choose, model_id)
                 try:
-                    status, hdrs, body = await h.handle_http.remote(req)
+                    gen = h.handle_http_stream.options(num_returns="streaming").remote(req)
+                    first = await (await gen.__anext__())
                     break
                 except RayActorError:
                     # the replica went away (redeploy / downscale / crash): re-resolve and retry
+                    router.done(tag)
+                    tag = None
                     if attempt == 2:
                         raise
                     router.invalidate()
-                finally:
-                    router.done(tag)
         except Exception as e:  # noqa
+            if tag is not None:
+                router.done(tag)
             return await _respond(send, 500, f"{type(e).__name__}: {e}".encode())
-        await send({"type": "http.response.start", "status": status,
-                    "headers": [(k.encode(), v.encode()) for k, v in hdrs
-                                if k.lower() != "content-length"]
-                    + [(b"content-length", str(len(body)).encode())]})
-        await send({"type": "http.response.body", "body": body})
+        try:
+            if first[0] == "full":
+                _, status, hdrs, body = first
+                await send({"type": "http.response.start", "status": status,
+                            "headers": [(k.encode(), v.encode()) for k, v in hdrs
+                                        if k.lower() != "content-length"]
+                            + [(b"content-length", str(len(body)).encode())]})
+                await send({"type": "http.response.body", "body": body})
+                return
+            _, status, hdrs = first
+            await send({"type": "http.response.start", "status": status,
+                        "headers": [(k.encode(), v.encode()) for k, v in hdrs if k.lower() != "content-length"]})
+            try:
+                async for ref in gen:
+                    item = await ref
+                    await send({"type": "http.response.body", "body": item[1], "more_body": True})
+            finally:
+                await send({"type": "http.response.body", "body": b"", "more_body": False})
+        finally:
+            router.done(tag)
 
     def stats(self):
         return {"num_requests": self.num_requests, "port": self.port}

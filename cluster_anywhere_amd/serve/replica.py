@@ -200,6 +200,103 @@ class ServeReplica:
         else:
             yield r
 
+    async def handle_http_stream(self, req: Dict):
+        """Streaming form of :meth:`handle_http` for the proxy: yields
+        ``("full", status, headers, body)`` when the response is complete in one
+        message, else ``("start", status, headers)`` then ``("body", bytes)`` chunks
+        as the app sends them (Server-Sent Events, StreamingResponse, generator
+        results of plain ``__call__`` deployments) -- nothing is buffered to the end."""
+        self.ongoing += 1
+        self.total += 1
+        tok = _request_context.set(RequestContext(req.get("route_prefix", ""), req.get("request_id", ""),
+                                                  self.app_name, req.get("model_id", "")))
+        try:
+            if self.asgi is None:
+                from starlette.requests import Request
+
+                scope, receive = self._asgi_scope(req)
+                r = await self._invoke(self._method("__call__"), (Request(scope, receive),), {})
+                if inspect.isasyncgen(r) or inspect.isgenerator(r):
+                    yield ("start", 200, [("content-type", "text/plain; charset=utf-8")])
+                    if inspect.isasyncgen(r):
+                        async for x in r:
+                            yield ("body", x if isinstance(x, bytes) else str(x).encode())
+                    else:
+                        for x in r:
+                            yield ("body", x if isinstance(x, bytes) else str(x).encode())
+                    return
+                yield ("full",) + tuple(_to_http(r))
+                return
+            q: asyncio.Queue = asyncio.Queue()
+            scope, receive = self._asgi_scope(req)
+
+            async def send(msg):
+                await q.put(msg)
+
+            async def run_app():
+                try:
+                    await self.asgi(scope, receive, send)
+                except Exception as e:  # noqa: BLE001 - surfaced as a 500 below
+                    await q.put({"type": "caamd.error", "error": e})
+                finally:
+                    await q.put(None)
+
+            runner = asyncio.ensure_future(run_app())
+            status, headers, started = 500, [], False
+            try:
+                while True:
+                    msg = await q.get()
+                    if msg is None:
+                        break
+                    kind = msg["type"]
+                    if kind == "http.response.start":
+                        status = msg["status"]
+                        headers = [(k.decode(), v.decode()) for k, v in msg.get("headers", [])]
+                    elif kind == "http.response.body":
+                        body, more = msg.get("body", b""), msg.get("more_body", False)
+                        if not started and not more:
+                            yield ("full", status, headers, body)
+                            return
+                        if not started:
+                            started = True
+                            yield ("start", status, headers)
+                        if body:
+                            yield ("body", body)
+                        if not more:
+                            return
+                    elif kind == "caamd.error" and not started:
+                        e = msg["error"]
+                        yield ("full", 500, [("content-type", "text/plain; charset=utf-8")],
+                               f"{type(e).__name__}: {e}".encode())
+                        return
+                if not started:
+                    yield ("full", status, headers, b"")
+            finally:
+                if not runner.done():
+                    runner.cancel()
+        finally:
+            self.ongoing -= 1
+            _request_context.reset(tok)
+
+    def _asgi_scope(self, req: Dict):
+        scope = {"type": "http", "asgi": {"version": "3.0"}, "http_version": "1.1",
+                 "method": req["method"], "scheme": "http",
+                 "path": req["path"], "raw_path": req["path"].encode(),
+                 "root_path": "", "query_string": req.get("query_string", b""),
+                 "headers": [(k.encode().lower(), v.encode()) for k, v in req.get("headers", [])],
+                 "client": ("127.0.0.1", 0), "server": ("127.0.0.1", 80)}
+        body = req.get("body", b"")
+        sent = {"done": False}
+
+        async def receive():
+            if not sent["done"]:
+                sent["done"] = True
+                return {"type": "http.request", "body": body, "more_body": False}
+            await asyncio.sleep(3600)
+            return {"type": "http.disconnect"}
+
+        return scope, receive
+
     async def handle_http(self, req: Dict):
         """``req``: method, path, query_string, headers, body, route_prefix."""
         self.ongoing += 1

@@ -280,7 +280,39 @@ def test_llm_openai_app(cluster, tmp_path):
         {"model": "llama-tiny", "messages": [{"role": "user", "content": "hi"}], "max_tokens": 3}).encode(),
         headers={"content-type": "application/json"})
     assert json.loads(body)["usage"]["completion_tokens"] == 3
+    _check_sse_streams_before_done("/llm/v1/completions",
+                                   {"model": "llama-tiny", "prompt": "hello", "max_tokens": 96, "ignore_eos": True,
+                                    "stream": True}, lambda c: c["choices"][0]["text"])
+    _check_sse_streams_before_done("/llm/v1/chat/completions",
+                                   {"model": "llama-tiny", "messages": [{"role": "user", "content": "hi"}],
+                                    "max_tokens": 96, "ignore_eos": True, "stream": True},
+                                   lambda c: c["choices"][0]["delta"].get("content", ""))
     serve.delete("llm")
+
+
+def _check_sse_streams_before_done(path, req, text_of):
+    """The first SSE event reaches the client while the generation is still running
+    (not collected and sent at the end): its arrival is well before the [DONE]."""
+    port = serve.http_port()
+    r = urllib.request.Request(f"http://127.0.0.1:{port}{path}", data=json.dumps(req).encode(),
+                               headers={"content-type": "application/json"})
+    t0 = time.time()
+    events, t_first = [], None
+    with urllib.request.urlopen(r, timeout=60) as resp:
+        assert resp.headers.get("content-type", "").startswith("text/event-stream")
+        for raw in resp:
+            line = raw.decode().strip()
+            if not line.startswith("data: "):
+                continue
+            if t_first is None:
+                t_first = time.time() - t0
+            if line == "data: [DONE]":
+                break
+            events.append(json.loads(line[6:]))
+    t_done = time.time() - t0
+    assert len(events) > 10, events[:3]
+    assert t_first < 0.5 * t_done, (t_first, t_done)
+    assert sum(len(text_of(e)) for e in events) > 0
 
 
 @serve.deployment(num_replicas=2)
