@@ -3,6 +3,7 @@
 // contiguity and shape on the host BEFORE launching, so a bad call raises a
 // Python error instead of faulting the GPU.
 #include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
@@ -1240,9 +1241,62 @@ std::vector<Tensor> ppo_loss_cat_(const Tensor& logits, const Tensor& vf, const 
   return {dlogits, dvf, stats};
 }
 
+// ---- device guard for every tensor entry point -----------------------------------
+// Workers may see several GPUs (Train worker groups run with every GPU of the node
+// visible for RCCL P2P), and a tensor need not live on the current device: every
+// binding below runs under a HIP device guard set to the device of its GPU tensor
+// arguments, after checking that all of them live on ONE device (a launch on the
+// current device's stream with another device's pointers would fault or silently
+// compute on the wrong GPU). Registered through GUARDED(fn) in PYBIND11_MODULE.
+struct DeviceSel {
+  int index = -1;
+  void see_device(bool is_gpu, int idx, const char* what) {
+    if (!is_gpu) return;
+    if (index < 0) {
+      index = idx;
+    } else {
+      TORCH_CHECK(idx == index, "kernel arguments live on different GPUs (", what, " is on cuda:", idx,
+                  ", an earlier tensor on cuda:", index, ")");
+    }
+  }
+  void see(const Tensor& t) {
+    if (t.defined()) see_device(t.is_cuda(), t.is_cuda() ? (int)t.get_device() : -1, "a tensor");
+  }
+  void see(const c10::optional<Tensor>& t) {
+    if (t.has_value()) see(*t);
+  }
+  void see(const std::vector<Tensor>& ts) {
+    for (const auto& t : ts) see(t);
+  }
+  template <typename T>
+  void see(const T&) {}
+};
+
+template <auto F>
+struct GuardedCall;
+template <typename R, typename... A, R (*F)(A...)>
+struct GuardedCall<F> {
+  static R call(A... a) {
+    DeviceSel sel;
+    (sel.see(a), ...);
+    c10::hip::OptionalHIPGuard guard;
+    if (sel.index >= 0) guard.set_index((c10::DeviceIndex)sel.index);
+    return F(std::forward<A>(a)...);
+  }
+};
+#define GUARDED(f) (&GuardedCall<&f>::call)
+
+// CPU-testable form of the selection rule: [(is_gpu, index)] -> chosen index (-1: none)
+static int64_t select_device_(const std::vector<std::pair<bool, int64_t>>& devs) {
+  DeviceSel sel;
+  for (const auto& d : devs) sel.see_device(d.first, (int)d.second, "an argument");
+  return sel.index;
+}
+
 PYBIND11_MODULE(_C, m) {
+  m.def("_select_device", &select_device_);
   m.doc() = "cluster_anywhere_amd gfx950 HIP kernels";
-  m.def("gemm_bf16", &gemm_bf16, pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
+  m.def("gemm_bf16", GUARDED(gemm_bf16), pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
         pybind11::arg("layout"), pybind11::arg("epi"), pybind11::arg("bm"), pybind11::arg("bn"),
         pybind11::arg("bias"), pybind11::arg("z"), pybind11::arg("zout"), pybind11::arg("dbias"),
         pybind11::arg("splitk"), pybind11::arg("ws"), pybind11::arg("accumulate"),
@@ -1254,14 +1308,14 @@ PYBIND11_MODULE(_C, m) {
     caamd::gemm_tail_plan((int)tiles, (int)K, (int)ks, (int)slots, (int)max_split, &full, &S);
     return std::vector<int64_t>{full, S};
   });
-  m.def("gemm2_plan", &gemm2_plan_);
-  m.def("gemm2_bf16", &gemm2_bf16);
-  m.def("decode_gemm", &decode_gemm);
-  m.def("decode_gemm_qkv_rope", &decode_gemm_qkv_rope);
+  m.def("gemm2_plan", GUARDED(gemm2_plan_));
+  m.def("gemm2_bf16", GUARDED(gemm2_bf16));
+  m.def("decode_gemm", GUARDED(decode_gemm));
+  m.def("decode_gemm_qkv_rope", GUARDED(decode_gemm_qkv_rope));
   m.def("decode_gemm_config", [](int64_t ext) { caamd::decode_gemm_config((int)ext); });
-  m.def("transpose_bf16", &transpose_bf16);
-  m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("g"),
+  m.def("transpose_bf16", GUARDED(transpose_bf16));
+  m.def("layernorm_fwd", GUARDED(layernorm_fwd));
+  m.def("layernorm_bwd", GUARDED(layernorm_bwd), pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("g"),
         pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("dres"), pybind11::arg("dxsum") = pybind11::none());
   m.def("ln_bwd_dxsum_ok", [](int64_t D) { return caamd::ln_bwd_dxsum_ok((int)D); });
   m.def("ln_bwd_config", [](int variant, int max_blocks) {
@@ -1269,38 +1323,38 @@ PYBIND11_MODULE(_C, m) {
     TORCH_CHECK(max_blocks >= 0 && max_blocks <= 65536, "ln_bwd_config: bad max_blocks");
     caamd::ln_bwd_config(variant, max_blocks);
   });
-  m.def("bias_gelu_fwd", &bias_gelu_fwd);
-  m.def("bias_gelu_bwd", &bias_gelu_bwd);
-  m.def("bias_grad_", &bias_grad_);
-  m.def("xent_fwd", &xent_fwd);
-  m.def("xent_bwd_", &xent_bwd_);
-  m.def("xent_fused_", &xent_fused_);
-  m.def("grad_sumsq", &grad_sumsq);
+  m.def("bias_gelu_fwd", GUARDED(bias_gelu_fwd));
+  m.def("bias_gelu_bwd", GUARDED(bias_gelu_bwd));
+  m.def("bias_grad_", GUARDED(bias_grad_));
+  m.def("xent_fwd", GUARDED(xent_fwd));
+  m.def("xent_bwd_", GUARDED(xent_bwd_));
+  m.def("xent_fused_", GUARDED(xent_fused_));
+  m.def("grad_sumsq", GUARDED(grad_sumsq));
   m.def("adamw_config", [](int64_t variant) { caamd::adamw_config((int)variant); });
-  m.def("adamw_step", &adamw_step);
-  m.def("gae", &gae);
-  m.def("vtrace", &vtrace);
-  m.def("flash_attn_fwd", &flash_attn_fwd);
-  m.def("flash_attn_bwd", &flash_attn_bwd, pybind11::arg("qkv"), pybind11::arg("out"), pybind11::arg("dout"),
+  m.def("adamw_step", GUARDED(adamw_step));
+  m.def("gae", GUARDED(gae));
+  m.def("vtrace", GUARDED(vtrace));
+  m.def("flash_attn_fwd", GUARDED(flash_attn_fwd));
+  m.def("flash_attn_bwd", GUARDED(flash_attn_bwd), pybind11::arg("qkv"), pybind11::arg("out"), pybind11::arg("dout"),
         pybind11::arg("lse"), pybind11::arg("H"), pybind11::arg("causal"), pybind11::arg("dbias") = pybind11::none());
-  m.def("rmsnorm", &rmsnorm, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("eps"),
+  m.def("rmsnorm", GUARDED(rmsnorm), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("eps"),
         pybind11::arg("residual") = pybind11::none());
-  m.def("silu_mul", &silu_mul);
-  m.def("skinny_gemm", &skinny_gemm);
-  m.def("rope_cache_", &rope_cache_);
-  m.def("paged_decode", &paged_decode, pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
+  m.def("silu_mul", GUARDED(silu_mul));
+  m.def("skinny_gemm", GUARDED(skinny_gemm));
+  m.def("rope_cache_", GUARDED(rope_cache_));
+  m.def("paged_decode", GUARDED(paged_decode), pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
         pybind11::arg("block_tables"), pybind11::arg("ctx_lens"), pybind11::arg("max_ctx"), pybind11::arg("H"),
         pybind11::arg("scale"), pybind11::arg("impl") = -1, pybind11::arg("tickets") = pybind11::none());
-  m.def("flash_attn_gqa", &flash_attn_gqa);
-  m.def("image_normalize", &image_normalize);
-  m.def("add_relu_", &add_relu_);
-  m.def("conv2d_nhwc", &conv2d_nhwc);
-  m.def("normalize_pad8", &normalize_pad8);
-  m.def("maxpool3s2_nhwc", &maxpool3s2_nhwc);
-  m.def("bias_act_", &bias_act_);
-  m.def("rl_gemm", &rl_gemm_);
-  m.def("rl_im2col", &rl_im2col_);
-  m.def("rl_col2im", &rl_col2im_);
-  m.def("rl_colsum", &rl_colsum_);
-  m.def("ppo_loss_cat", &ppo_loss_cat_);
+  m.def("flash_attn_gqa", GUARDED(flash_attn_gqa));
+  m.def("image_normalize", GUARDED(image_normalize));
+  m.def("add_relu_", GUARDED(add_relu_));
+  m.def("conv2d_nhwc", GUARDED(conv2d_nhwc));
+  m.def("normalize_pad8", GUARDED(normalize_pad8));
+  m.def("maxpool3s2_nhwc", GUARDED(maxpool3s2_nhwc));
+  m.def("bias_act_", GUARDED(bias_act_));
+  m.def("rl_gemm", GUARDED(rl_gemm_));
+  m.def("rl_im2col", GUARDED(rl_im2col_));
+  m.def("rl_col2im", GUARDED(rl_col2im_));
+  m.def("rl_colsum", GUARDED(rl_colsum_));
+  m.def("ppo_loss_cat", GUARDED(ppo_loss_cat_));
 }
