@@ -8,5 +8,10 @@ from .core import DefaultActorCriticModule, Learner, LearnerGroup, RLModule, RLM
 from .core.multi_rl_module import MultiRLModule, MultiRLModuleSpec
 from .env import register_env
 from .env.multi_agent_env import MultiAgentEnv, make_multi_agent
+from .env import VectorEnv
+from .env.base_env import BaseEnv
+from .env.external_env import ExternalEnv
+from .evaluation import RolloutWorker
+from .policy import MultiAgentBatch, Policy, SampleBatch, TFPolicy, TorchPolicy
 
 __all__ = [n for n in dir() if not n.startswith("_")]
