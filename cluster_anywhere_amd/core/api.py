@@ -121,6 +121,11 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
          _temp_dir: Optional[str] = None, _node_ip_address: str = "127.0.0.1",
          **kwargs) -> RayContext:
     global _head
+    logging_config = kwargs.pop("logging_config", None)
+    if logging_config is not None:
+        # driver now; workers started by this process's head through the environment
+        logging_config._apply()
+        os.environ["CAAMD_LOGGING_CONFIG"] = logging_config._to_env()
     with _init_lock:
         if is_initialized():
             if ignore_reinit_error:

@@ -2575,6 +2575,16 @@ class Head:
             return [{"job_id": j.hex() if isinstance(j, bytes) else str(j), **v} for j, v in self.jobs.items()]
         if what == "events":
             return list(self.events)
+        if what == "object_locations":
+            out = {}
+            for oid in arg or ():
+                e = self.objects.get(oid)
+                if e is None or e.state != READY:
+                    continue
+                inline = e.inline is not None
+                out[oid] = {"node_ids": [] if inline else [e.node or self.head_hex], "size": e.size,
+                            "spilled": e.spilled_path is not None}
+            return out
         if what == "cluster_events":
             return list(self.cluster_events)
         if what == "runtime_envs":

@@ -52,6 +52,11 @@ def main():
                     os.environ.get("CAAMD_NODE_ID", ""),
                     extra={"gpu_ids": [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]})
     context.worker = cw
+    lc = os.environ.get("CAAMD_LOGGING_CONFIG")
+    if lc:  # init(logging_config=...) of the driver that started this cluster
+        from .._compat import LoggingConfig
+
+        LoggingConfig._from_env(lc)._apply()
     try:
         cw.run_worker_loop()
     finally:

@@ -48,7 +48,27 @@ class DAGNode:
     def experimental_compile(self, **kw):
         from .compiled import CompiledDAG
 
+        ctx = DAGContext.get_current()
+        kw.setdefault("_max_inflight_executions", ctx.max_inflight_executions)
+        if ctx.buffer_size_bytes:
+            kw.setdefault("_buffer_size_bytes", ctx.buffer_size_bytes)
         return CompiledDAG(self, **kw)
+
+    def _label(self) -> str:
+        kind = type(self).__name__
+        name = (getattr(self, "_method", None) or getattr(getattr(self, "_fn", None), "__name__", None)
+                or getattr(getattr(self, "_ac", None), "__name__", None) or "")
+        return f"{kind}\\n{name}" if name else kind
+
+    def visualize(self, filename: str = "compiled_graph", format: str = "dot", view: bool = False,
+                  return_dot: bool = False, **kwargs):
+        """Graphviz DOT text of the graph (graphviz itself is not in the image):
+        written to ``filename`` + ``.dot`` and returned with ``return_dot``."""
+        dot = to_dot(self)
+        path = filename if filename.endswith(".dot") else f"{filename}.dot"
+        with open(path, "w") as f:
+            f.write(dot)
+        return dot if return_dot else path
 
 
 class InputValue:
@@ -164,5 +184,64 @@ class MultiOutputNode(DAGNode):
         return [x._exec(cache, inp) if isinstance(x, DAGNode) else x for x in self._args]
 
 
+def to_dot(root: DAGNode) -> str:
+    """DOT digraph of the nodes reachable from ``root`` (edges: argument -> consumer)."""
+    ids: Dict[int, str] = {}
+    lines = ["digraph DAG {", "  rankdir=LR;"]
+    stack, seen = [root], set()
+    edges = []
+    while stack:
+        n = stack.pop()
+        if id(n) in seen:
+            continue
+        seen.add(id(n))
+        ids[id(n)] = f"n{len(ids)}"
+        deps = list(n._children())
+        tgt = getattr(n, "_target", None)
+        if isinstance(tgt, DAGNode):
+            deps.append(tgt)
+        for d in deps:
+            edges.append((d, n))
+            stack.append(d)
+    nodes = {}
+    stack, seen = [root], set()
+    while stack:
+        n = stack.pop()
+        if id(n) in seen:
+            continue
+        seen.add(id(n))
+        nodes[id(n)] = n
+        stack.extend(n._children())
+        tgt = getattr(n, "_target", None)
+        if isinstance(tgt, DAGNode):
+            stack.append(tgt)
+    for k, n in nodes.items():
+        lines.append(f'  {ids[k]} [label="{n._label()}"];')
+    for a, b in edges:
+        lines.append(f"  {ids[id(a)]} -> {ids[id(b)]};")
+    lines.append("}")
+    return "\n".join(lines) + "\n"
+
+
+def plot(dag: DAGNode, to_file=None) -> str:
+    """Reference: ray.dag.plot (pydot): here the DOT text, also written to ``to_file``."""
+    dot = to_dot(dag)
+    if to_file:
+        with open(str(to_file), "w") as f:
+            f.write(dot)
+    return dot
+
+
+from .context import DAGContext  # noqa: E402
+
+# node-metadata keys of the reference's DAG serialization (python/ray/dag/constants.py)
+PARENT_CLASS_NODE_KEY = "parent_class_node"
+PREV_CLASS_METHOD_CALL_KEY = "prev_class_method_call"
+BIND_INDEX_KEY = "bind_index"
+IS_CLASS_METHOD_OUTPUT_KEY = "is_class_method_output"
+COLLECTIVE_OPERATION_KEY = "collective_operation"
+DAGNODE_TYPE_KEY = "__dag_node_type__"
+
 __all__ = ["DAGNode", "InputNode", "FunctionNode", "ClassNode", "ClassMethodNode", "MultiOutputNode",
-           "CollectiveOutputNode"]
+           "CollectiveOutputNode", "DAGContext", "plot", "PARENT_CLASS_NODE_KEY", "PREV_CLASS_METHOD_CALL_KEY",
+           "BIND_INDEX_KEY", "IS_CLASS_METHOD_OUTPUT_KEY", "COLLECTIVE_OPERATION_KEY", "DAGNODE_TYPE_KEY"]

@@ -120,4 +120,21 @@ class JobSubmissionClient:
         raise TimeoutError(f"job {job_id} still running after {timeout}s")
 
 
-__all__ = ["JobSubmissionClient", "JobStatus", "JobDetails", "JobInfo"]
+class JobType(str, enum.Enum):
+    """How a job came to be: submitted through the job API, or a driver script
+    that called ``init()`` itself."""
+
+    SUBMISSION = "SUBMISSION"
+    DRIVER = "DRIVER"
+
+
+@dataclass
+class DriverInfo:
+    """The driver process of a job (reference: job_submission DriverInfo)."""
+
+    id: str
+    node_ip_address: str
+    pid: str
+
+
+__all__ = ["JobSubmissionClient", "JobStatus", "JobDetails", "JobInfo", "JobType", "DriverInfo"]

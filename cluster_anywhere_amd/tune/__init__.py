@@ -5,6 +5,7 @@ from .callback import Callback, CLIReporter, CSVLoggerCallback, JsonLoggerCallba
 from .controller import Trial
 from .schedulers import (PB2, AsyncHyperBandScheduler, ASHAScheduler, DistributeResources, FIFOScheduler,
                          HyperBandForBOHB, HyperBandScheduler, MedianStoppingRule, PopulationBasedTraining,
+                         PopulationBasedTrainingReplay,
                          ResourceChangingScheduler, TrialScheduler)
 from .search.bohb import TuneBOHB
 from .search.model_based import BayesOptSearch, HyperOptSearch, OptunaSearch

@@ -328,8 +328,10 @@ class PopulationBasedTraining(TrialScheduler):
                  perturbation_interval: float = 60.0, burn_in_period: float = 0,
                  hyperparam_mutations: Optional[Dict] = None, quantile_fraction: float = 0.25,
                  resample_probability: float = 0.25, perturbation_factors=(1.2, 0.8),
-                 custom_explore_fn: Optional[Callable] = None, seed=None, synch: bool = False):
+                 custom_explore_fn: Optional[Callable] = None, seed=None, synch: bool = False,
+                 log_config: bool = True):
         super().__init__(metric, mode)
+        self.log_config = log_config
         self.time_attr, self.interval, self.burn = time_attr, perturbation_interval, burn_in_period
         self.mutations = hyperparam_mutations or {}
         self.q, self.resample_p, self.factors = quantile_fraction, resample_probability, perturbation_factors
@@ -381,10 +383,101 @@ class PopulationBasedTraining(TrialScheduler):
         if trial.trial_id in bottom and trial not in top:
             donor = self.rng.choice(top)
             if donor.latest_checkpoint is not None:
-                trial.pending_exploit = (donor.latest_checkpoint, self._explore(donor.config))
+                new_cfg = self._explore(donor.config)
+                if self.log_config:
+                    self._log_policy(trial, donor, t, new_cfg)
+                trial.pending_exploit = (donor.latest_checkpoint, new_cfg)
                 self.num_perturbations += 1
                 return self.PAUSE
         return self.CONTINUE
+
+    def _log_policy(self, trial, donor, step, new_cfg):
+        """``<experiment>/pbt_policy_<trial_id>.txt``: the donor's schedule, then one
+        JSON row [donor_id, trial_id, donor_step, step, donor_config, new_config]
+        -- the file :class:`PopulationBasedTrainingReplay` replays."""
+        import json
+        import os
+
+        exp = os.path.dirname(trial.local_path)
+        src = os.path.join(exp, f"pbt_policy_{donor.trial_id}.txt")
+        prior = open(src).read() if os.path.exists(src) else ""
+        row = [donor.trial_id, trial.trial_id, donor.last_result.get(self.time_attr, 0), step,
+               _jsonable(donor.config), _jsonable(new_cfg)]
+        os.makedirs(exp, exist_ok=True)
+        with open(os.path.join(exp, f"pbt_policy_{trial.trial_id}.txt"), "w") as f:
+            f.write(prior + json.dumps(row) + "\n")
+
+
+def _jsonable(cfg):
+    import json
+
+    out = {}
+    for k, v in cfg.items():
+        try:
+            json.dumps(v)
+            out[k] = v
+        except TypeError:
+            out[k] = repr(v)
+    return out
+
+
+class PopulationBasedTrainingReplay(TrialScheduler):
+    """Replay the hyperparameter schedule one PBT trial ended up with (reference
+    role: pbt.py:1012): reads ``pbt_policy_<trial_id>.txt`` (written by PBT with
+    ``log_config=True``), starts the single trial with the schedule's initial
+    config and, when the trial reaches each recorded step, restarts it from its
+    own latest checkpoint with the next config."""
+
+    def __init__(self, policy_file: str):
+        import json
+        import os
+
+        path = os.path.expanduser(policy_file)
+        if not os.path.exists(path):
+            raise ValueError(f"Policy file not found: {path}")
+        rows = []
+        with open(path) as f:
+            for ln in f:
+                if ln.strip():
+                    try:
+                        rows.append(json.loads(ln))
+                    except json.JSONDecodeError:
+                        raise ValueError(f"Could not read PBT policy file: {path}") from None
+        # walk back from the last change while the chain of trial ids is unbroken
+        schedule, expect, initial = [], None, None
+        for old_tag, new_tag, _old_step, new_step, old_conf, new_conf in reversed(rows):
+            if expect is not None and new_tag != expect:
+                break
+            expect = old_tag
+            initial = old_conf
+            schedule.append((new_step, new_conf))
+        super().__init__()
+        self.policy_file = path
+        self.config = initial
+        self.schedule = list(reversed(schedule))
+        self._trial = None
+        self.num_perturbations = 0
+        self.time_attr = "training_iteration"
+
+    def on_trial_add(self, trial):
+        if self._trial is not None:
+            raise ValueError("PopulationBasedTrainingReplay trains one trial (num_samples=1)")
+        self._trial = trial
+        if self.config is not None:
+            trial.config = dict(trial.config or {}, **self.config)
+        elif not trial.config:
+            raise ValueError("the replay policy is empty and the trial has no config")
+
+    def on_trial_result(self, trial, result):
+        if not self.schedule:
+            return self.CONTINUE
+        step, cfg = self.schedule[0]
+        if result.get(self.time_attr, 0) < step or trial.latest_checkpoint is None:
+            return self.CONTINUE
+        self.schedule.pop(0)
+        trial.pending_exploit = (trial.latest_checkpoint, dict(trial.config, **cfg))
+        self.num_perturbations += 1
+        return self.PAUSE
 
 
 class PB2(PopulationBasedTraining):

@@ -235,6 +235,20 @@ def test_pbt_exploits(cluster, tmp_path):
     scores = sorted(r.metrics["score"] for r in grid)
     # the weak trial inherited the strong one's progress: both end well above 12 * 0.01
     assert scores[0] > 1.0
+    # log_config: the exploited trial's schedule is on disk and replays (reference:
+    # test_trial_scheduler_pbt.py PopulationBasedTrainingReplay)
+    exp = os.path.join(str(tmp_path), "pbt")
+    policies = [f for f in os.listdir(exp) if f.startswith("pbt_policy_")]
+    assert policies
+    rows = [json.loads(ln) for ln in open(os.path.join(exp, policies[0]))]
+    assert len(rows[-1]) == 6 and rows[-1][1] == policies[0][len("pbt_policy_"):-4]
+    replay = tune.schedulers.PopulationBasedTrainingReplay(os.path.join(exp, policies[0]))
+    assert replay.config is not None and replay.schedule
+    res = tune.Tuner(pbt_trial, tune_config=tune.TuneConfig(metric="score", mode="max", scheduler=replay),
+                     run_config=tune.RunConfig(storage_path=str(tmp_path), name="replay")).fit()
+    assert replay.num_perturbations == len(rows) and res[0].metrics["lr"] == rows[-1][5]["lr"]
+    with pytest.raises(ValueError):
+        tune.schedulers.PopulationBasedTrainingReplay(str(tmp_path / "missing.txt"))
 
 
 def slow_trial(config):
