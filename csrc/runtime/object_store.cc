@@ -57,6 +57,8 @@ ObjectStore::ObjectStore(const std::string& name, uint64_t capacity, uint64_t ta
     hdr_->used_bytes = 0;
     hdr_->num_objects = 0;
     hdr_->tick = 0;
+    hdr_->copy_threads_active = 0;
+    hdr_->copy_threads_budget = std::max(2u, std::thread::hardware_concurrency() / 2);
     pthread_mutexattr_t a;
     pthread_mutexattr_init(&a);
     pthread_mutexattr_setpshared(&a, PTHREAD_PROCESS_SHARED);
@@ -347,19 +349,39 @@ void ObjectStore::copy_in(uint64_t off, const void* src, uint64_t n, int threads
   uint8_t* dst = base_ + off;
   const uint8_t* s = (const uint8_t*)src;
   const uint64_t kMinChunk = 16ull << 20;
-  int nt = (int)std::min<uint64_t>((uint64_t)std::max(threads, 1), (n + kMinChunk - 1) / kMinChunk);
+  int want = (int)std::min<uint64_t>((uint64_t)std::max(threads, 1), (n + kMinChunk - 1) / kMinChunk);
+  if (want <= 1) {
+    memcpy(dst, s, n);
+    return;
+  }
+  // claim extra threads from the node-wide budget (the caller's own thread is free)
+  uint32_t budget = __atomic_load_n(&hdr_->copy_threads_budget, __ATOMIC_RELAXED);
+  if (budget == 0) budget = 4;
+  uint32_t cur = __atomic_load_n(&hdr_->copy_threads_active, __ATOMIC_RELAXED);
+  uint32_t take;
+  do {
+    take = cur >= budget ? 0 : std::min<uint32_t>((uint32_t)(want - 1), budget - cur);
+  } while (take && !__atomic_compare_exchange_n(&hdr_->copy_threads_active, &cur, cur + take, true,
+                                                 __ATOMIC_ACQ_REL, __ATOMIC_RELAXED));
+  const int nt = 1 + (int)take;
   if (nt <= 1) {
     memcpy(dst, s, n);
     return;
   }
+  struct Release {
+    uint32_t* a;
+    uint32_t k;
+    ~Release() { __atomic_fetch_sub(a, k, __ATOMIC_ACQ_REL); }
+  } release{&hdr_->copy_threads_active, take};
   const uint64_t chunk = ((n + nt - 1) / nt + 4095) & ~4095ull;
   std::vector<std::thread> ts;
-  for (int i = 0; i < nt; ++i) {
+  for (int i = 1; i < nt; ++i) {  // chunk 0 on the calling thread
     const uint64_t b = (uint64_t)i * chunk;
     if (b >= n) break;
     const uint64_t e = std::min(n, b + chunk);
     ts.emplace_back([=] { memcpy(dst + b, s + b, e - b); });
   }
+  memcpy(dst, s, std::min(n, chunk));
   for (auto& t : ts) t.join();
 }
 

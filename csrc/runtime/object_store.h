@@ -57,6 +57,11 @@ struct Header {
   uint64_t num_objects;
   uint64_t tick;
   pthread_mutex_t mu;
+  // copy threads currently running in copy_in() across every process of the node:
+  // concurrent large puts share one node-wide budget instead of each spawning its
+  // own full set (10 putters x 4 threads on 8 cores thrashed the memory system)
+  uint32_t copy_threads_active;
+  uint32_t copy_threads_budget;
 };
 
 class ObjectStore {
