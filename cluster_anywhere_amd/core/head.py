@@ -1185,7 +1185,11 @@ class Head:
                 self.free_gpus.setdefault(node, []).append(g)
 
     def _num_workers(self, node):
-        return sum(1 for w in self.workers.values() if w.node == node and w.alive) + sum(
+        """Pooled (task / not-yet-actor) workers on ``node``: the soft cap
+        ``max_workers`` bounds these only -- a worker that hosts an actor is
+        dedicated to it and never blocks task workers (reference: the raylet's
+        worker pool soft limit, worker_pool.cc, counts idle/task workers)."""
+        return sum(1 for w in self.workers.values() if w.node == node and w.alive and w.actor_id is None) + sum(
             v for (n, _g, _e), v in self.starting.items() if n == node)
 
     def _evict_idle(self, node, keep_key):

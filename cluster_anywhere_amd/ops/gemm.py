@@ -12,6 +12,11 @@ every GPT-2-XL projection at micro-batch x seq = 32768 tokens. Anything else
 
 Tile choice: 256 x 320 (divides 1600/4800/6400) with the ping-pong pipeline
 (``algo=2``: BK=32, 4-deep LDS ring, LDS-DMA two K-steps ahead, counted vmcnt, staggered wave rows), else 256 x 256.
+NT GEMMs with N or K >= 4096 (fc / fc2 / qkv forward and dgrad) take the full-line
+kernel instead (``algo=4009``: BK=64, one 128-byte line per row and K-tile, two LDS
+buffers, DMA of K-tile t+1 issued in the first of two MFMA phases of t): 2-4 %
+faster on those shapes, 2 % slower on the 1600 x 1600 projection
+(``profiles/gemm_k64_r4.jsonl``).
 """
 from __future__ import annotations
 
@@ -32,6 +37,14 @@ MAX_SPLIT = int(os.environ.get("CAAMD_GEMM2_MAX_SPLIT", "4"))
 # split-K tail of the ping-pong kernel: tiles past the last full round of CUs are
 # split over K-slices so that round is not half empty (N = 1600: 640 tiles = 2.5 rounds)
 TAIL = os.environ.get("CAAMD_GEMM_TAIL", "1") == "1"
+# full-line BK=64 kernel (algo 4009) on the large NT shapes (CAAMD_GEMM_K64=0: off)
+K64 = os.environ.get("CAAMD_GEMM_K64", "1") == "1"
+K64_ALGO = 4009
+
+
+def k64_ok(layout: int, epi: int, bm: int, bn: int, N: int, K: int) -> bool:
+    return (K64 and layout == 0 and (bm, bn) == (256, 320) and epi != EPI_F32 and max(N, K) >= 4096
+            and K % 64 == 0)
 MAX_TAIL_SPLIT = int(os.environ.get("CAAMD_GEMM_TAIL_SPLIT", "4"))
 
 EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_BIAS_GELU, EPI_DGELU = range(5)
@@ -109,15 +122,16 @@ def run2(a, b, c, layout, epi, bias=None, z=None, zout=None, dbias=None, max_spl
 def tail_plan(M: int, N: int, K: int, bm: int, bn: int, dev: torch.device, algo: int = None):
     """(full tiles, tail split) of a ping-pong launch; split 1 = no tail split."""
     algo = ALGO if algo is None else algo
-    if not TAIL or not (1 <= algo % 10 <= 3 or algo % 10 == 7) or K < 4096:
+    if not TAIL or not (1 <= algo % 10 <= 3 or algo % 10 in (7, 9)) or K < 4096:
         # K = 1600: the split slices and slab round trip cost more than the half-empty
         # last round (which the chip runs at a higher clock); profiles/gemm_tail_split.jsonl
         return (0, 1)
-    key = ("pp", M, N, K, bm, bn, dev.index, MAX_TAIL_SPLIT)
+    key = ("pp", M, N, K, bm, bn, dev.index, MAX_TAIL_SPLIT, algo % 10 == 9)
     p = _PLANS.get(key)
     if p is None:
         slots = torch.cuda.get_device_properties(dev).multi_processor_count
-        p = _PLANS[key] = tuple(kernels().gemm_tail_plan((M // bm) * (N // bn), K, 32, slots, MAX_TAIL_SPLIT))
+        ks = 64 if algo % 10 == 9 else 32
+        p = _PLANS[key] = tuple(kernels().gemm_tail_plan((M // bm) * (N // bn), K, ks, slots, MAX_TAIL_SPLIT))
     return p
 
 
@@ -139,6 +153,8 @@ def run_pp(a, b, c, layout, epi, bm, bn, bias=None, z=None, zout=None, dbias=Non
     persistent async-epilogue kernel where it applies and no tail split is planned."""
     M, N = c.shape
     K = a.shape[0] if layout == 2 else a.shape[1]
+    if algo is None and ALGO == 2 and k64_ok(layout, epi, bm, bn, N, K):
+        algo = K64_ALGO
     algo = ALGO if algo is None else algo
     full, S = tail_plan(M, N, K, bm, bn, c.device, algo)
     if S == 1 and algo == ALGO and pst_ok(layout, epi, bm, bn, M, N, K):

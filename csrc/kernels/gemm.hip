@@ -1466,26 +1466,10 @@ __device__ __forceinline__ void dma_lds16(__amdgpu_buffer_rsrc_t r, lds_char* ds
 // both k-subs, 8 x TN MFMAs each (half the barriers, twice the fragment registers).
 // ABL (timing ablations): 1 no in-loop DMA, 2 no LDS reads, 4 no MFMA, 8 no epilogue
 // stores, 16 no vmcnt waits, 32 every K-tile re-reads the first (L2-hot).
-// L2 prefetch: touch one dword of each of `lanes` 128-B lines (rows r0 + lane of a
-// K-major operand at byte column soff) with a plain buffer load into a dummy VGPR.
-// Inline asm: the compiler neither counts it (our waits do: it is issued after the
-// K-tile's DMA, so `vmcnt(#prefetches)` retires the DMA and leaves it in flight)
-// nor reuses `dummy` before the asm that names it after that wait.
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4_t desc_words(const void* base, unsigned bytes) {
-  const size_t b = (size_t)base;
-  i32x4_t d;
-  d[0] = (int)__builtin_amdgcn_readfirstlane((unsigned)b);
-  d[1] = (int)(__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) & 0xffffu);
-  d[2] = (int)__builtin_amdgcn_readfirstlane(bytes);
-  d[3] = 0x00020000;
-  return d;
-}
-__device__ __forceinline__ void l2_touch(i32x4_t desc, int voff, int soff, int& dummy) {
-  asm volatile("buffer_load_dword %0, %1, %2, %3 offen" : "+v"(dummy) : "v"(voff), "s"(desc), "s"(soff) : "memory");
-}
-
-template <int BM, int BN, int EPI, int ABL = 0, int DSPLIT = 2, int PH = 4, bool PF = false>
+// (An L2 prefetch of K-tile t+2 -- one plain buffer load per 128-B line, issued behind
+// K-tile t+1's DMA -- measured 4-8 % slower on every shape and was removed;
+// profiles/gemm_k64_r4.jsonl, algos 5009-7009.)
+template <int BM, int BN, int EPI, int ABL = 0, int DSPLIT = 2, int PH = 4>
 __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
   constexpr int WM = 2, WN = 4;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -1564,15 +1548,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
             ((ABL & 32) ? t0 : t0 + (t_)) * 128 + ((j_) < NA ? (j_) * 64 * p.lda : ((j_) - NA) * 64 * p.ldb) * 2)
   // rounds of phase q: [lo, hi)
   auto rlo = [](int q) { return q >= DSPLIT ? NR : (NR * q) / DSPLIT; };
-  // L2 prefetch of K-tile t+2 (PF): wave w touches A rows [w*BM/8, +BM/8) and B rows
-  // [w*BN/8, +BN/8), one line per lane (lanes past the share repeat its last row)
-  constexpr int NPF = PF ? 2 : 0;
-  const i32x4_t da = desc_words(p.A + (size_t)m0 * p.lda, (unsigned)(BM * p.lda * 2));
-  const i32x4_t db = desc_words(p.B + (size_t)n0 * p.ldb, (unsigned)(BN * p.ldb * 2));
-  const int pfa = (wid * (BM / 8) + min(lane, BM / 8 - 1)) * p.lda * 2;
-  const int pfb = (wid * (BN / 8) + min(lane, BN / 8 - 1)) * p.ldb * 2;
-  int pf_dummy = 0;
-
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -1606,11 +1581,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
 #pragma unroll
           for (int j = rlo(q); j < rlo(q + 1); ++j) K64_DMA_ROUND(t + 1, j);
         }
-        if (PF && q == (PH == 4 ? DSPLIT : 1) && t + 2 < nk) {  // behind this K-tile's DMA
-          const int so = (t0 + t + 2) * 128;
-          l2_touch(da, pfa, so, pf_dummy);
-          l2_touch(db, pfb, so, pf_dummy);
-        }
 #pragma unroll
         for (int u = 0; u < NKS; ++u) {
           const int ks = PH == 4 ? (q >> 1) : u;
@@ -1627,9 +1597,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
             else af[u][i] = frag_kmaj(As, wr * (TM * 16) + (mh * TMH + i) * 16, ks, lane);
           }
         }
-        if (!(ABL & 16) && q == PH - 1 && !lo_grp) {  // lagging row: K-tile t+1 landed
-          if (PF && t + 2 < nk) wait_vm<NPF>(); else wait_vm<0>();
-        }
+        if (!(ABL & 16) && q == PH - 1 && !lo_grp) wait_vm<0>();  // lagging row: K-tile t+1 landed
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -1645,19 +1613,13 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
               if constexpr (ABL & 4) asm volatile("" :: "v"(bf[u][j]), "v"(af[u][i]));
               else acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[u][j], af[u][i], acc[mh * TMH + i][j], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        if (!(ABL & 16) && q == PH - 1 && lo_grp) {  // leading row: K-tile t+1 landed
-          if (PF && t + 2 < nk) wait_vm<NPF>(); else wait_vm<0>();
-        }
+        if (!(ABL & 16) && q == PH - 1 && lo_grp) wait_vm<0>();  // leading row: K-tile t+1 landed
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (lo_grp) __builtin_amdgcn_s_barrier();  // equal barrier counts for both rows
-  }
-  if constexpr (PF) {
-    wait_vm<0>();
-    asm volatile("" ::"v"(pf_dummy));  // the prefetch destination stays reserved until here
   }
   if (tail) {
     // ---- split-K tail: publish this slice; the last arriver combines (as gemm_pp_kernel)
@@ -1744,9 +1706,9 @@ static void ensure_lds(const void* k, int bytes) {
 
 // algo 9 (full-line kernel): algo = 9 + 10 * ABL + 1000 * DSPLIT (0 -> 2). Development
 // ablations only on 256 x 320 bf16 tiles at the default DMA split.
-template <int BM, int BN, int EPI, int ABL, int DS, int PH = 4, bool PF = false>
+template <int BM, int BN, int EPI, int ABL, int DS, int PH = 4>
 static hipError_t launch_k64_v(const Args& a, hipStream_t st) {
-  auto k = gemm_k64_kernel<BM, BN, EPI, ABL, DS, PH, PF>;
+  auto k = gemm_k64_kernel<BM, BN, EPI, ABL, DS, PH>;
   constexpr int lds = 2 * (BM + BN) * 128;
   ensure_lds((const void*)k, lds);
   const int T = a.tiles_m * a.tiles_n;
@@ -1769,18 +1731,13 @@ static hipError_t launch_k64(const Args& a, hipStream_t st) {
       case 2: return launch_k64_v<BM, BN, EPI, 0, 2>(a, st);
       case 3: return launch_k64_v<BM, BN, EPI, 0, 3>(a, st);
       case 4: return launch_k64_v<BM, BN, EPI, 0, 1, 2>(a, st);
-      case 5: return launch_k64_v<BM, BN, EPI, 0, 2, 4, true>(a, st);
-      case 6: return launch_k64_v<BM, BN, EPI, 0, 1, 2, true>(a, st);
-      case 7: return launch_k64_v<BM, BN, EPI, 0, 1, 4, true>(a, st);
       default: return hipErrorInvalidValue;
     }
   }
   if constexpr (BM == 256 && BN == 320 && EPI == EPI_BF16) {
 #define K64_ABL(n)                                                                                     \
   case n:                                                                                              \
-    return v == 4   ? launch_k64_v<BM, BN, EPI, n, 1, 2>(a, st)                                        \
-           : v == 6 ? launch_k64_v<BM, BN, EPI, n, 1, 2, true>(a, st)                                  \
-                    : launch_k64_v<BM, BN, EPI, n, 2>(a, st);
+    return v == 4 ? launch_k64_v<BM, BN, EPI, n, 1, 2>(a, st) : launch_k64_v<BM, BN, EPI, n, 2>(a, st);
     switch (abl) {
       K64_ABL(1) K64_ABL(2) K64_ABL(3) K64_ABL(4) K64_ABL(6) K64_ABL(8) K64_ABL(22) K64_ABL(38) K64_ABL(54)
       default: break;

@@ -184,3 +184,68 @@ def test_fused_mlp_matches_unfused_reference():
     assert _rel(x.grad, xf.grad) < 3e-2
     for p, r in ((w1, w1f), (b1, b1f), (w2, w2f), (b2, b2f)):
         assert _rel(p.main_grad, r.grad) < 3e-2, (p.shape, _rel(p.main_grad, r.grad))
+
+
+@pytest.mark.parametrize("algo", [9, 1009, 3009, 4009])
+@pytest.mark.parametrize("K", [64, 128, 448, 1600])
+def test_gemm_k64_variants(algo, K):
+    """Full-line BK=64 kernel (NT only): every DMA-split / phase / L2-prefetch variant,
+    K-tile counts 1, 2, 7 (odd: the double-buffer tail) and 25, vs fp32."""
+    from cluster_anywhere_amd.ops.gemm import gemm
+
+    M, N = 512, 960
+    a, b = _mk((M, K), 21), _mk((N, K), 22)
+    c = gemm(a, b, 0, algo=algo, tile=(256, 320))
+    assert _rel(c, a.float() @ b.float().t()) < 5e-3
+
+
+def test_gemm_k64_epilogues_and_dispatch():
+    """The dispatcher sends NT GEMMs with max(N, K) >= 4096 to algo 4009; its bias,
+    bias+GELU and dGELU+bias-grad epilogues vs fp32, and the result equals an explicit
+    algo-4009 launch."""
+    from cluster_anywhere_amd.ops import gemm as G
+    from cluster_anywhere_amd.ops import kernels
+
+    assert G.k64_ok(0, G.EPI_BF16, 256, 320, 4800, 1600) and not G.k64_ok(0, G.EPI_BF16, 256, 320, 1600, 1600)
+    M, K, N = 512, 640, 4160  # N = 13 x 320 >= 4096
+    x, w = _mk((M, K), 23), _mk((N, K), 24) * 0.05
+    b = _mk((N,), 25)
+    ref = x.float() @ w.float().t() + b.float()
+    y = G.linear_nt(x, w, b)
+    assert _rel(y, ref) < 5e-3
+    c = torch.empty_like(y)
+    kernels().gemm_bf16(x, w, c, 0, G.EPI_BF16, 256, 320, b, None, None, None, 1, None, False, 4009,
+                        None, None, 0, 1)
+    assert torch.equal(c, y)
+    u, z = G.linear_gelu(x, w, b)
+    assert _rel(z, ref) < 5e-3
+    assert _rel(u, F.gelu(z.float(), approximate="tanh")) < 1e-2
+    dy = _mk((M, K), 26)
+    w2 = _mk((K, N), 27) * 0.05
+    db = torch.zeros(N, device="cuda")
+    dz = G.dgrad_dgelu(dy, G.transpose(w2), z, db)
+    zf = z.float()
+    t = torch.tanh(0.7978845608028654 * (zf + 0.044715 * zf ** 3))
+    gp = 0.5 * (1 + t) + 0.5 * zf * (1 - t * t) * 0.7978845608028654 * (1 + 3 * 0.044715 * zf * zf)
+    dzr = (dy.float() @ w2.float()) * gp
+    assert _rel(dz, dzr) < 1e-2 and _rel(db, dzr.sum(0)) < 1e-2
+
+
+def test_gemm_k64_split_tail():
+    """K >= 4096 on algo 4009: the tiles past the last full round of CUs are split
+    over K-slices (fp32 slabs + tickets), vs fp32 and vs the unsplit launch."""
+    from cluster_anywhere_amd.ops import gemm as G
+    from cluster_anywhere_amd.ops import kernels
+
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    M, N, K = 256 * 16, 320 * 20, 4800  # 320 tiles: one full round + a 64-tile tail on 256 CUs
+    full, S = G.tail_plan(M, N, K, 256, 320, torch.device("cuda"), 4009)
+    if cus == 256:
+        assert S > 1, (full, S)
+    a, b = _mk((M, K), 28), _mk((N, K), 29) * 0.05
+    c = G.linear_nt(a, b)
+    assert _rel(c, a.float() @ b.float().t()) < 5e-3
+    c1 = torch.empty_like(c)
+    kernels().gemm_bf16(a, b, c1, 0, G.EPI_BF16, 256, 320, None, None, None, None, 1, None, False, 4009,
+                        None, None, 0, 1)
+    assert _rel(c, c1) < 2e-3

@@ -37,6 +37,18 @@ def make_images(batch, hw=224):
     return {"image": img, "id": ids}
 
 
+class StubActor:
+    """``--stub``: no model, no GPU -- the actor only touches its batch (one byte
+    per image) so the run measures the read -> object store -> actor -> driver
+    plumbing that the GPU actors sit on (the host-side ceiling of the pipeline)."""
+
+    def __init__(self, **_):
+        pass
+
+    def __call__(self, batch):
+        return {"id": batch["id"], "label": batch["image"][:, 0, 0, 0].astype(np.int64)}
+
+
 class ResNet50Actor:
     def __init__(self, model="resnet50", batch_size=512, hw=224):
         from cluster_anywhere_amd.models.resnet import ResNetPredictor
@@ -59,6 +71,7 @@ def main():
     ap.add_argument("--actors-per-gpu", type=int, default=3,
                     help=">1 shares each GPU between actors (fractional num_gpus) so one's H2D "
                          "copy / host work overlaps another's graph replay")
+    ap.add_argument("--stub", action="store_true", help="GPU-less stub actors (plumbing ceiling, see StubActor)")
     ap.add_argument("--timeline", default="", help="write a chrome trace + per-function summary here")
     ap.add_argument("--preserve-order", action="store_true",
                     help="deliver blocks in input order (off by default, as in the reference's DataContext)")
@@ -71,7 +84,7 @@ def main():
     gpu = torch.cuda.is_available()
     data.DataContext.get_current().execution_preserve_order = args.preserve_order
     ncpu = args.cpus or min(os.cpu_count() or 8, 16 * max(1, args.gpus))
-    ray.init(num_cpus=ncpu, num_gpus=args.gpus if gpu else 0,
+    ray.init(num_cpus=ncpu, num_gpus=args.gpus if gpu and not args.stub else 0,
              object_store_memory=min(64 << 30, max(4 << 30, args.batch_size * args.hw * args.hw * 3 * 64)))
     # whole batches per block: a block of batch_size+1 rows would cost the actor a
     # second (padded) graph replay for its 1-row remainder
@@ -83,7 +96,10 @@ def main():
         ds = data.range(n, override_num_blocks=max(1, min(blocks, n // args.batch_size or 1)))
         ds = ds.map_batches(make_images, batch_size=args.batch_size, fn_kwargs={"hw": args.hw})
         apg = max(1, args.actors_per_gpu)
-        ds = ds.map_batches(ResNet50Actor, batch_size=args.batch_size, num_gpus=(1.0 / apg) if gpu else 0,
+        ds = ds.map_batches(StubActor if args.stub else ResNet50Actor, batch_size=args.batch_size,
+                            num_gpus=(1.0 / apg) if gpu and not args.stub else 0,
+                            **({"num_cpus": min(0.25, ncpu / (2.0 * args.gpus * max(1, args.actors_per_gpu)))}
+                               if args.stub else {}),
                             concurrency=max(1, args.gpus) * apg, zero_copy_batch=True,
                             fn_constructor_kwargs={"model": args.model, "batch_size": args.batch_size,
                                                    "hw": args.hw})
@@ -105,14 +121,15 @@ def main():
     rps = n / dt
     from cluster_anywhere_amd.models.resnet import resnet
 
-    gflop = resnet(args.model).flops_per_image(args.hw) / 1e9
+    gflop = 0.0 if args.stub else resnet(args.model).flops_per_image(args.hw) / 1e9
     stats = ds.stats()
     print(json.dumps({
         "metric": "Data GPU rows/sec (map_batches ResNet-50 inference)",
         "value": round(rps, 1), "unit": "rows/s", "n_gpus": args.gpus, "rows": n, "warmup_rows": warm,
         "seconds": round(dt, 3), "higher_is_better": True, "scaling": "strong",
         "dtype": "bf16" if gpu else "fp32", "data": "synthetic uint8 224x224x3 images, random-init weights",
-        "config": {"model": args.model, "batch_size": args.batch_size, "hw": args.hw, "read_blocks": blocks,
+        "config": {"model": "stub (no model, no GPU)" if args.stub else args.model, "batch_size": args.batch_size,
+                   "hw": args.hw, "read_blocks": blocks,
                    "actors": args.gpus * max(1, args.actors_per_gpu), "cpus": ncpu,
                    "preserve_order": args.preserve_order},
         "model_tflops_per_gpu": round(rps * gflop / 1e3 / max(1, args.gpus), 1),
