@@ -173,8 +173,12 @@ WGRAD_SK = os.environ.get("CAAMD_WGRAD_SK", "1") == "1"
 
 # (N_out, K_in) -> runs where the kernel measured faster than hipBLASLt at 32768
 # tokens (profiles/wgrad_stream_k.jsonl): GPT-2-XL fc (6400 x 1600, lockstep split-K
-# 2) and attention proj (1600 x 1600, 245 runs). qkv and fc2 stay on hipBLASLt.
+# 2) and attention proj (1600 x 1600, 245 runs = 35 tiles x 7 slices). qkv stays on
+# hipBLASLt; fc2 is stored transposed, so its weight gradient is the fc shape.
 WGRAD_WINNERS = {(6400, 1600): 250, (1600, 1600): 245}
+# slice-major lockstep order (one token window per XCD at a time) for run counts
+# that are a whole number of slices per tile (CAAMD_WGRAD_LOCKSTEP=0: stream-K order)
+WGRAD_LOCKSTEP = os.environ.get("CAAMD_WGRAD_LOCKSTEP", "1") == "1"
 # extra entries for A/B runs: CAAMD_WGRAD_EXTRA="1600x6400:420,4800x1600:190"
 for _e in filter(None, os.environ.get("CAAMD_WGRAD_EXTRA", "").split(",")):
     _shape, _runs = _e.split(":")
@@ -215,8 +219,9 @@ def run_sk(a, b, c, layout: int, accumulate: bool, runs: Optional[int] = None):
     if runs is None:
         runs = sk_runs(M, N, K, c.device)
     ws, cnt = _workspace(c.device, 2 * runs * 256 * 320, tiles)
+    slices = runs // tiles if WGRAD_LOCKSTEP and runs % tiles == 0 and runs > tiles else 0
     kernels().gemm_bf16(a, b, c, layout, EPI_BF16_ACC if accumulate else EPI_BF16, 256, 320, None, None,
-                        None, None, 1, None, accumulate, 5, ws, cnt, 0, runs)
+                        None, None, 1, None, accumulate, 5, ws, cnt, slices, runs)
     return c
 
 

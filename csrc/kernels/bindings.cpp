@@ -892,6 +892,9 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
     TORCH_CHECK(tail_ws->numel() >= 2 * runs * bm * bn, "gemm(stream-K): slab workspace too small");
     TORCH_CHECK(tail_cnt->numel() >= tiles, "gemm(stream-K): too few tickets");
     TORCH_CHECK(tiles * (K / 32) >= runs, "gemm(stream-K): fewer K-steps than runs");
+    // tail_full > 0: lockstep split-K over tail_full slices, one run per (slice, tile)
+    TORCH_CHECK(tail_full <= 0 || (runs == tiles * tail_full && K / 32 >= tail_full),
+                "gemm(stream-K lockstep): runs must be tiles x slices, slices <= K-steps");
     twp = tail_ws->data_ptr<float>();
     tcp = tail_cnt->data_ptr<int>();
   } else if (tail_split > 1) {

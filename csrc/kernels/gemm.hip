@@ -1218,6 +1218,12 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pst_kernel(Args p) {
 // Ragged M (1600 / 4800 output rows): A columns past M are clamped on load and
 // never stored. Same R / M segments, counted vmcnt and wave-row stagger as
 // gemm_pp_kernel (one phase per 32-deep K-step, DMA two steps ahead).
+// Lockstep mode (p.tfull = S > 0, G = tiles x S): run g is slice g / tiles of tile
+// g % tiles, the slices cut the K-steps evenly (+-1 when S does not divide them).
+// Runs are slice-major, so the ~32 consecutive runs an XCD holds are neighbouring
+// tiles of ONE token window at the same time and share its dY / X rows in that
+// XCD's L2 (the stream-K order gives an XCD consecutive windows of a few tiles:
+// nothing shared, HBM-bound at 1600 x 1600).
 // ================================================================================
 template <int BM, int BN, bool AK, bool BK_, int EPI>
 __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
@@ -1242,8 +1248,15 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
     g = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
   }
   const int nk_tile = p.K / KS;
-  const long long W = (long long)p.tiles_m * p.tiles_n * nk_tile;
-  const long long r0 = (long long)g * W / G, r1 = (long long)(g + 1) * W / G;
+  const int T = p.tiles_m * p.tiles_n;
+  const int LS = p.tfull;  // > 0: lockstep split-K over LS slices (G == T * LS)
+  const long long W = (long long)T * nk_tile;
+  long long r0 = (long long)g * W / G, r1 = (long long)(g + 1) * W / G;
+  if (LS > 0) {
+    const int sl = g / T, tl = g - sl * T;
+    r0 = (long long)tl * nk_tile + (long long)sl * nk_tile / LS;
+    r1 = (long long)tl * nk_tile + (long long)(sl + 1) * nk_tile / LS;
+  }
   auto run_start = [&](int gg) { return (long long)gg * W / G; };
   // first run containing global step x: largest gg with run_start(gg) <= x
   auto run_of = [&](long long x) { return (int)(((x + 1) * G + W - 1) / W - 1); };
@@ -1371,12 +1384,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
     if (nk < nk_tile) {
       // ---- shared tile: publish, and combine if this is the last contributor -----
       const long long t_first = (long long)tile * nk_tile;
-      const int c0 = run_of(t_first), c1 = run_of(tile_end - 1);
+      const int c0 = LS > 0 ? 0 : run_of(t_first), c1 = LS > 0 ? LS - 1 : run_of(tile_end - 1);
       constexpr int SLAB = BM * BN;
       auto slot_of = [&](int gg) {  // a run's first tile uses slot 2g, its last 2g+1
         return 2 * gg + ((run_start(gg) / nk_tile) == tile ? 0 : 1);
       };
-      float* mine = p.tws + (size_t)slot_of(g) * SLAB;
+      // contributor c0 + i of this tile -> its slab (lockstep: slice i's run)
+      auto slab_of = [&](int c) { return LS > 0 ? c * T + tile : slot_of(c); };
+      float* mine = p.tws + (size_t)(LS > 0 ? g : slot_of(g)) * SLAB;
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1406,7 +1421,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int gg = c0; gg <= c1; ++gg) {
-        const float* other = p.tws + (size_t)slot_of(gg) * SLAB;
+        const float* other = p.tws + (size_t)slab_of(gg) * SLAB;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll

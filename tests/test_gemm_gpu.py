@@ -249,3 +249,33 @@ def test_gemm_k64_split_tail():
     kernels().gemm_bf16(a, b, c1, 0, G.EPI_BF16, 256, 320, None, None, None, None, 1, None, False, 4009,
                         None, None, 0, 1)
     assert _rel(c, c1) < 2e-3
+
+
+@pytest.mark.parametrize("lockstep", [True, False])
+@pytest.mark.parametrize("MN,runs", [((1600, 1600), 245), ((640, 960), 18), ((1600, 640), 56)])
+def test_wgrad_stream_k_and_lockstep(lockstep, MN, runs):
+    """Weight-gradient kernel (algo 5, TN layout): dW (+)= dY^T X over 4096 tokens,
+    ragged M (1600 = 6.25 x 256), stream-K order and the slice-major lockstep order
+    (runs = tiles x slices, slices not dividing the 128 K-steps), overwrite and
+    accumulate, vs fp32."""
+    from cluster_anywhere_amd.ops import gemm as G
+
+    M, N = MN
+    K = 4096
+    dy, x = _mk((K, M), 31), _mk((K, N), 32)
+    ref = dy.float().t() @ x.float()
+    old = G.WGRAD_LOCKSTEP
+    G.WGRAD_LOCKSTEP = lockstep
+    try:
+        c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        G.run_sk(dy, x, c, 2, False, runs)
+        assert _rel(c, ref) < 5e-3
+        c0 = _mk((M, N), 33)
+        c2 = c0.clone()
+        G.run_sk(dy, x, c2, 2, True, runs)
+        assert _rel(c2, ref + c0.float()) < 5e-3
+        c3 = torch.empty_like(c)
+        G.run_sk(dy, x, c3, 2, False, runs)  # tickets were reset by the last arrivers
+        assert torch.equal(c, c3)
+    finally:
+        G.WGRAD_LOCKSTEP = old
