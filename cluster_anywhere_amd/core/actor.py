@@ -35,6 +35,21 @@ def method(*args, **kwargs):
     return deco
 
 
+class TransportResult:
+    """Return value of an actor method that picks its tensor transport per call
+    (``TransportResult(value, "ipc")``): the worker serializes ``value`` with that
+    transport instead of the method's static ``@method(tensor_transport=...)``.
+    Serve replicas use it to honour the annotation of the deployment method they
+    dispatch to (serve/replica.py)."""
+
+    __slots__ = ("value", "transport")
+
+    def __init__(self, value, transport):
+        if transport not in (None, "object_store", "ipc"):
+            raise ValueError("tensor_transport must be 'object_store' (host copy) or 'ipc'")
+        self.value, self.transport = value, transport
+
+
 def _method_meta(cls) -> Dict[str, Any]:
     meta = {}
     for name, m in inspect.getmembers(cls, predicate=lambda x: inspect.isfunction(x) or inspect.ismethod(x)):

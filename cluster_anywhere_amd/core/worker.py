@@ -1424,6 +1424,11 @@ class CoreWorker:
         tt = None
         if spec.kind == ACTOR_METHOD and self.actor_instance is not None:
             tt = getattr(getattr(type(self.actor_instance), spec.method, None), "__ray_tensor_transport__", None)
+        if n == 1 and type(result).__name__ == "TransportResult":
+            from .actor import TransportResult
+
+            if isinstance(result, TransportResult):  # the method chose its transport for this call
+                tt, result = result.transport or tt, result.value
         if n == 1:
             return [self._result_entry(spec.return_ids[0], result, tt)]
         if n == 0:

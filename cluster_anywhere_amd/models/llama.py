@@ -12,6 +12,7 @@ here the engine is ``cluster_anywhere_amd/llm/engine.py``.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -90,6 +91,7 @@ class Llama(nn.Module):
         self.lm_head = None if cfg.tie_embeddings else nn.Parameter(torch.empty(cfg.vocab_size, cfg.d_model))
         self._cos_sin = None
         self._dec = None  # decode-GEMM weight copies (prepare_decode)
+        self._shared = False  # originals released: prefill / decode / forward all read the packed copies
 
     @torch.no_grad()
     def init_weights(self, std: float = 0.02, seed: int = 0):
@@ -111,8 +113,37 @@ class Llama(nn.Module):
         return self._cos_sin
 
     def _head(self, x):
+        if self._shared and self._dec["head"] is not None:
+            return self._dg(x, self._dec["head"])
         w = self.embed if self.lm_head is None else self.lm_head
         return F.linear(x, w)
+
+    def _dg(self, x, w, epi: int = 0, residual=None):
+        """Decode GEMM on a packed weight for any row count (<= 128 rows per launch)."""
+        if x.shape[0] <= 128:
+            return L.decode_gemm(x, w, epi, residual=residual, packed=True)
+        return torch.cat([L.decode_gemm(x[i:i + 128], w, epi, packed=True,
+                                        residual=None if residual is None else residual[i:i + 128])
+                          for i in range(0, x.shape[0], 128)])
+
+    def _weight(self, i: int, name: str) -> torch.Tensor:
+        """Layer i's weight in nn.Linear layout (unpacked from the shared copy if the
+        original was released)."""
+        layer = self.layers[i]
+        if not self._shared:
+            return getattr(layer, name)
+        if name == "w_qkv":
+            return L.unpack_decode_weight(self._dec["attn"][i][0])
+        if name == "w_o":
+            return L.unpack_decode_weight(self._dec["attn"][i][1])
+        if name == "w_gate_up":
+            gu = L.unpack_decode_weight(self._dec["layers"][i][0])
+            two_f, d = gu.shape
+            blk = gu.reshape(two_f // 128, 2, 64, d)
+            return torch.cat([blk[:, 0].reshape(two_f // 2, d), blk[:, 1].reshape(two_f // 2, d)])
+        if name == "w_down":
+            return L.unpack_decode_weight(self._dec["layers"][i][1])
+        raise KeyError(name)
 
     @torch.no_grad()
     def prepare_decode(self) -> bool:
@@ -128,6 +159,7 @@ class Llama(nn.Module):
         cache is sized. Returns whether the decode path uses them."""
         import os
 
+        self._restore_originals()
         if os.environ.get("CAAMD_DECODE_GEMM", "1") == "0" or not self.embed.is_cuda \
                 or self.embed.dtype != torch.bfloat16 or not L.decode_gemm_available():
             self._dec = None
@@ -157,7 +189,42 @@ class Llama(nn.Module):
                      "head": L.pack_decode_weight(fold(head, self.final_norm)) if head.shape[0] % 128 == 0 else None}
         shapes = [tuple(w.shape) for l in self.layers[:1] for w in (l.w_down, l.w_qkv, l.w_o)]
         L.decode_gemm_reserve(self.embed.device, shapes)
+        # One weight copy: prefill runs gemm.hip straight from the packed layout
+        # (ops/gemm.py prefill_linear), so the nn.Linear-layout originals are
+        # released (about 14 GB for Llama-3-8B, +1 GB untied LM head) unless the
+        # norms are folded into the packed copies or a projection does not tile.
+        from ..ops import gemm as G
+
+        d, f = cfg.d_model, cfg.ffn_dim
+        hd = cfg.head_dim
+        tiles = all(n % 256 == 0 for n in ((cfg.n_head + 2 * cfg.n_kv_head) * hd, cfg.n_head * hd, 2 * f, d)) \
+            and d % 64 == 0 and f % 64 == 0 and (cfg.n_head * hd) % 64 == 0
+        self._dec["prefill"] = bool(attn and not norm and tiles and G.ENABLED
+                                    and os.environ.get("CAAMD_LLM_PACKED_PREFILL", "1") == "1")
+        if self._dec["prefill"] and os.environ.get("CAAMD_LLM_SHARED_WEIGHTS", "1") == "1":
+            empty = lambda p: p.data.new_empty((0,) + tuple(p.shape[1:]))  # noqa: E731
+            for l in self.layers:
+                for n in ("w_qkv", "w_o", "w_gate_up", "w_down"):
+                    getattr(l, n).data = empty(getattr(l, n))
+            if self.lm_head is not None and self._dec["head"] is not None:
+                self.lm_head.data = empty(self.lm_head)
+            self._shared = True
+            torch.cuda.empty_cache()
         return True
+
+    @torch.no_grad()
+    def _restore_originals(self):
+        """Undo the weight sharing of :meth:`prepare_decode` (re-preparation,
+        checkpoint export): the nn.Linear-layout weights rebuilt from the packed copies."""
+        if not self._shared:
+            return
+        for i, l in enumerate(self.layers):
+            for n in ("w_qkv", "w_o", "w_gate_up", "w_down"):
+                getattr(l, n).data = self._weight(i, n)
+        if self.lm_head is not None and self.lm_head.numel() == 0:
+            self.lm_head.data = L.unpack_decode_weight(self._dec["head"])
+        self._shared = False
+        self._dec = None
 
     # -------------------------------------------------------------- prefill
     @torch.no_grad()
@@ -170,6 +237,8 @@ class Llama(nn.Module):
         B, T = tokens.shape
         H, KVH, hd = cfg.n_head, cfg.n_kv_head, cfg.head_dim
         cs = self.cos_sin(tokens.device)
+        if self._dec is not None and self._dec.get("prefill"):
+            return self._prefill_packed(tokens, positions, slots, k_caches, v_caches, last_idx)
         x = F.embedding(tokens, self.embed)  # [B, T, d]
         res = None
         pos = positions.reshape(-1).to(torch.int32)
@@ -191,6 +260,43 @@ class Llama(nn.Module):
         last = h[torch.arange(B, device=h.device), last_idx.long()]
         return self._head(last)
 
+    def _prefill_packed(self, tokens, positions, slots, k_caches, v_caches, last_idx):
+        """Prefill on gemm.hip from the packed weights: the residual stream ``res``
+        ([M rounded up to 256, d]) is updated in place by the o / down GEMM epilogues
+        (``res += o W_o^T``, ``res += swiglu W_down^T``), the gate/up GEMM stores
+        silu(gate) * up directly. Rows past M are padding (zero inputs, never read)."""
+        from ..ops import gemm as G
+
+        cfg = self.cfg
+        B, T = tokens.shape
+        H, KVH, hd = cfg.n_head, cfg.n_kv_head, cfg.head_dim
+        M = B * T
+        Mp = -(-M // 256) * 256
+        cs = self.cos_sin(tokens.device)
+        pos = positions.reshape(-1).to(torch.int32)
+        res = torch.zeros(Mp, cfg.d_model, device=tokens.device, dtype=self.embed.dtype)
+        res[:M] = F.embedding(tokens.reshape(-1), self.embed)
+        o_pad = torch.zeros(Mp, H * hd, device=tokens.device, dtype=res.dtype) if Mp != M else None
+        for i in range(len(self.layers)):
+            layer = self.layers[i]
+            wq, wo = self._dec["attn"][i]
+            gu, dn = self._dec["layers"][i]
+            h, _ = L.rms_norm(res, layer.attn_norm, cfg.norm_eps)
+            qkv = G.prefill_linear(h, wq)[:M].view(B, T, -1)
+            L.rope_cache_(qkv, cs, pos, slots, k_caches[i] if k_caches is not None else None,
+                          v_caches[i] if v_caches is not None else None, H, KVH)
+            o = L.prefill_attention(qkv[..., : H * hd], qkv[..., H * hd: (H + KVH) * hd],
+                                    qkv[..., (H + KVH) * hd:], H, KVH, causal=True).reshape(M, H * hd)
+            if o_pad is not None:
+                o_pad[:M] = o
+                o = o_pad
+            G.prefill_linear(o, wo, out=res, accumulate=True)
+            h, _ = L.rms_norm(res, layer.mlp_norm, cfg.norm_eps)
+            G.prefill_linear(G.prefill_linear(h, gu, epi=G.EPI_SWIGLU), dn, out=res, accumulate=True)
+        h, _ = L.rms_norm(res[:M], self.final_norm, cfg.norm_eps)
+        last = h.view(B, T, -1)[torch.arange(B, device=h.device), last_idx.long()]
+        return self._head(last)
+
     # --------------------------------------------------------------- decode
     @torch.no_grad()
     def decode(self, tokens: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor, k_caches, v_caches,
@@ -203,7 +309,7 @@ class Llama(nn.Module):
         x = F.embedding(tokens, self.embed)  # [B, d]
         res = None
         pos = positions.to(torch.int32)
-        dec = self._dec if (self._dec is not None and tokens.shape[0] <= 128) else None
+        dec = self._dec if (self._dec is not None and (tokens.shape[0] <= 128 or self._shared)) else None
         if dec is not None and dec["norm"]:
             return self._decode_folded(x, dec, cs, pos, slots, k_caches, v_caches, block_tables, ctx_lens, max_ctx)
         for i, layer in enumerate(self.layers):
@@ -215,19 +321,19 @@ class Llama(nn.Module):
             qkv = L.decode_gemm_qkv_rope(h, att[0], cs, pos, slots, k_caches[i], v_caches[i], H, KVH) \
                 if att else None
             if qkv is None:
-                qkv = L.decode_gemm(h, att[0], 0, packed=True) if att else L.decode_linear(h, layer.w_qkv)
+                qkv = self._dg(h, att[0]) if att else L.decode_linear(h, layer.w_qkv)
                 L.rope_cache_(qkv, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
             o = L.paged_decode_attention(qkv, k_caches[i], v_caches[i], block_tables, ctx_lens, max_ctx, H)
-            x = L.decode_gemm(o, att[1], 0, packed=True) if att else L.decode_linear(o, layer.w_o)
+            x = self._dg(o, att[1]) if att else L.decode_linear(o, layer.w_o)
             h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
             if dec is not None:  # SwiGLU in the gate/up GEMM epilogue, packed weight streams
                 gu, dn = dec["layers"][i]
-                x = L.decode_gemm(L.decode_gemm(h, gu, 2, packed=True), dn, 0, packed=True)
+                x = self._dg(self._dg(h, gu, 2), dn)
             else:
                 x = L.decode_linear(L.silu_mul(L.decode_linear(h, layer.w_gate_up)), layer.w_down)
         h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
         if dec is not None and dec["head"] is not None:
-            return L.decode_gemm(h, dec["head"], 0, packed=True)
+            return self._dg(h, dec["head"])
         w = self.embed if self.lm_head is None else self.lm_head
         return L.decode_linear(h, w)
 
@@ -264,16 +370,18 @@ class Llama(nn.Module):
         cs = self.cos_sin(tokens.device)
         x = F.embedding(tokens, self.embed)
         res = None
-        for layer in self.layers:
+        for i, layer in enumerate(self.layers):
             h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
             if res is None:
                 res = x
-            qkv = F.linear(h, layer.w_qkv)
+            qkv = F.linear(h, self._weight(i, "w_qkv"))
             L.rope_cache_(qkv, cs, pos.reshape(-1).to(torch.int32), None, None, None, H, KVH)
             o = L.prefill_attention(qkv[..., : H * hd], qkv[..., H * hd: (H + KVH) * hd],
                                     qkv[..., (H + KVH) * hd:], H, KVH, causal=True)
-            x = F.linear(o, layer.w_o)
+            x = F.linear(o, self._weight(i, "w_o"))
             h, res = L.rms_norm(x, layer.mlp_norm, cfg.norm_eps, res)
-            x = F.linear(L.silu_mul(F.linear(h, layer.w_gate_up)), layer.w_down)
+            x = F.linear(L.silu_mul(F.linear(h, self._weight(i, "w_gate_up"))), self._weight(i, "w_down"))
         h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
+        if self._shared and self._dec["head"] is not None:
+            return F.linear(h, L.unpack_decode_weight(self._dec["head"]))
         return self._head(h)

@@ -47,7 +47,7 @@ def k64_ok(layout: int, epi: int, bm: int, bn: int, N: int, K: int) -> bool:
             and K % 64 == 0)
 MAX_TAIL_SPLIT = int(os.environ.get("CAAMD_GEMM_TAIL_SPLIT", "4"))
 
-EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_BIAS_GELU, EPI_DGELU = range(5)
+EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_BIAS_GELU, EPI_DGELU, EPI_SWIGLU = range(6)
 
 
 def tile_for(M: int, N: int, K: int) -> Optional[Tuple[int, int]]:
@@ -285,3 +285,38 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: int = 0, *, algo: Optional[in
         raise ValueError(f"no MFMA tile for M={M} N={N} K={K}")
     c = torch.empty(M, N, device=a.device, dtype=torch.bfloat16)
     return run_pp(a, b, c, layout, EPI_BF16, bm, bn, algo=algo)
+
+
+# ---------------------------------------------------------------- serving prefill
+# Llama prefill projections on the full-line kernel straight from the decode GEMM's
+# packed weight copy (ops/llm.py pack_decode_weight): 256 x 256 tiles (every packed
+# N is a multiple of 128, the slabs of a tile are contiguous), the SwiGLU of the
+# 64-row-interleaved gate/up weight and the residual adds of o / down in the
+# epilogues, so prefill keeps no second copy of the weights and no [M, 2F]
+# intermediate.
+PREFILL_ALGO = int(os.environ.get("CAAMD_PREFILL_ALGO", "4009"))
+
+
+def prefill_ok(M: int, N: int, K: int) -> bool:
+    return ENABLED and M % 256 == 0 and N % 256 == 0 and K % 64 == 0 and M > 0
+
+
+def prefill_linear(x2: torch.Tensor, wp: torch.Tensor, *, epi: int = EPI_BF16, out: Optional[torch.Tensor] = None,
+                   accumulate: bool = False) -> torch.Tensor:
+    """``x2 [M, K] @ W^T`` with ``wp`` = W [N, K] in packed order: ``epi`` 0 -> [M, N]
+    (``accumulate``: ``out += ...``, the residual add), ``EPI_SWIGLU`` -> [M, N/2] =
+    silu(gate) * up for a gate/up weight interleaved in 64-row blocks."""
+    M, K = x2.shape
+    N = wp.shape[0]
+    if not prefill_ok(M, N, K):
+        raise ValueError(f"prefill_linear: M % 256, N % 256, K % 64 must be 0 (M={M} N={N} K={K})")
+    if out is None:
+        out = torch.empty(M, N // 2 if epi == EPI_SWIGLU else N, device=x2.device, dtype=torch.bfloat16)
+    algo = PREFILL_ALGO
+    full, S = tail_plan(M, N, K, 256, 256, x2.device, algo)
+    ws = cnt = None
+    if S > 1:
+        ws, cnt = _workspace(x2.device, ((M // 256) * (N // 256) - full) * S * 256 * 256, (M // 256) * (N // 256) - full)
+    kernels().gemm_bf16(x2, wp, out, 0, epi, 256, 256, None, None, None, None, 1, None, accumulate, algo,
+                        ws, cnt, full, S, True)
+    return out

@@ -131,13 +131,20 @@ class ServeReplica:
                 from .grpc_proxy import decode_request
 
                 args = (decode_request(grpc_t, args[0]),) + tuple(args[1:])
-            r = await self._invoke(self._method(meta.get("method", "__call__")), args, kwargs)
+            m = self._method(meta.get("method", "__call__"))
+            r = await self._invoke(m, args, kwargs)
             if inspect.isgenerator(r) or inspect.isasyncgen(r):
                 raise TypeError("method returned a generator: call it with handle.options(stream=True)")
             if grpc_t:
                 from .grpc_proxy import encode_response
 
                 return encode_response(r)
+            if getattr(m, "__ray_tensor_transport__", None) == "ipc":
+                # @ray.method(tensor_transport="ipc") on the deployment method: GPU
+                # tensors in the result go to the caller as HIP IPC handles (no host copy)
+                from ..core.actor import TransportResult
+
+                return TransportResult(r, "ipc")
             return r
         finally:
             _request_context.reset(tok)

@@ -36,7 +36,9 @@ class DataParallelStep:
         bucket_cap_mb = bucket_cap_mb or DEFAULT_BUCKET_MB
         world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.world = world
-        self.zero = bool(zero and world > 1)
+        # ZeRO-1 only pays with more than one rank; zero="always" runs the sharded
+        # path on any initialised group (world-1 RCCL test of the ZeRO machinery)
+        self.zero = bool(zero and (world > 1 or (zero == "always" and dist.is_initialized())))
         p0 = next(model.parameters())
         if p0.is_cuda:
             from ..ops.gemm_tuning import use_tuned_gemms

@@ -45,7 +45,7 @@ void vtrace_launch(const float*, const float*, const float*, const float*, const
 hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
                        const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
                        int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
-                       int tfull, int tS, float* tws, int* tcnt);
+                       int tfull, int tS, float* tws, int* tcnt, int bpack);
 void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
@@ -814,12 +814,14 @@ void add_relu_(Tensor& y, const Tensor& r) {
 // layout 0: a[M,K] b[N,K] (y = x W^T) · 1: a[M,K] b[K,N] (dx = dy W) · 2: a[K,M] b[K,N] (dW = dy^T x)
 // epi 0: c = acc(+bias) · 1: c += acc(+bias) · 2: ws[s] = partial (split-K; then reduced into c)
 //     3: zout = acc+bias, c = gelu(zout) (layout 0) · 4: c = acc*gelu'(z), dbias += colsum(c) (layout 0)
+//     5: b = [gate; up] in 64-row blocks, c [M, N/2] = silu(gate) * up (layout 0)
+// bpack: b is in the decode GEMM's packed order (algo 9, layout 0, BN % 128 == 0)
 static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi, int64_t bm,
                       int64_t bn, c10::optional<Tensor> bias, c10::optional<Tensor> z,
                       c10::optional<Tensor> zout, c10::optional<Tensor> dbias, int64_t splitk,
                       c10::optional<Tensor> ws, bool accumulate, int64_t algo,
                       c10::optional<Tensor> tail_ws, c10::optional<Tensor> tail_cnt, int64_t tail_full,
-                      int64_t tail_split) {
+                      int64_t tail_split, bool bpack) {
   CHECK_BF16(a);
   CHECK_BF16(b);
   CHECK_BF16(c);
@@ -830,7 +832,10 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   const int64_t N = layout == 0 ? b.size(0) : b.size(1);
   const int64_t Kb = layout == 0 ? b.size(1) : b.size(0);
   TORCH_CHECK(Kb == K, "gemm: K mismatch");
-  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm: output shape mismatch");
+  TORCH_CHECK(c.size(0) == M && c.size(1) == (epi == 5 ? N / 2 : N), "gemm: output shape mismatch");
+  if (bpack)
+    TORCH_CHECK(algo % 10 == 9 && layout == 0 && bn % 128 == 0 && N % 128 == 0,
+                "gemm: packed B needs algo 9, layout 0 and 128-row-aligned tiles");
   TORCH_CHECK((bm == 256 && (bn == 256 || bn == 320)) || (bm == 128 && bn == 320), "gemm: tile");
   if (algo == 5) {  // stream-K: ragged M allowed (8-aligned), bf16 / accumulate epilogues
     TORCH_CHECK(M % 8 == 0 && N % bn == 0 && K % 64 == 0, "gemm(stream-K): M%8, N%BN, K%64 must be 0");
@@ -866,6 +871,9 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
     TORCH_CHECK(z->sizes() == c.sizes() && dbias->numel() == N, "gemm: z / dbias shape");
     zp = (const bf16*)z->data_ptr();
     dbp = dbias->data_ptr<float>();
+  } else if (epi == 5) {
+    TORCH_CHECK(layout == 0 && bn % 128 == 0 && N % 128 == 0 && bp == nullptr && splitk == 1,
+                "gemm: SwiGLU needs layout 0, BN % 128 == 0, no bias, no split-K");
   } else if (epi == 2 || splitk > 1) {
     TORCH_CHECK(ws.has_value(), "gemm: split-K needs a workspace");
     CHECK_F32(*ws);
@@ -878,7 +886,7 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
     ek = accumulate ? 1 : 0;
   }
   TORCH_CHECK(splitk == 1 || ek == 2, "gemm: split-K only with the f32 partial epilogue");
-  const int lda = (int)a.size(1), ldb = (int)b.size(1), ldc = (int)N;
+  const int lda = (int)a.size(1), ldb = (int)b.size(1), ldc = (int)(epi == 5 ? N / 2 : N);
   float* twp = nullptr;
   int* tcp = nullptr;
   if (algo == 5) {
@@ -917,7 +925,8 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   hipError_t e = caamd::gemm_launch((int)layout, ek, (int)bm, (int)bn, (const bf16*)a.data_ptr(),
                                     (const bf16*)b.data_ptr(), cp, bp, zp, zop, dbp, (int)M, (int)N,
                                     (int)K, lda, ldb, ldc, (int)splitk, (int)algo, cur_stream(),
-                                    (int)tail_full, (tail_split > 1 || algo == 5) ? (int)tail_split : 1, twp, tcp);
+                                    (int)tail_full, (tail_split > 1 || algo == 5) ? (int)tail_split : 1, twp, tcp,
+                                    bpack ? 1 : 0);
   TORCH_CHECK(e == hipSuccess, "gemm launch failed: ", hipGetErrorString(e));
   if (ek == 2) {
     caamd::gemm_splitk_reduce(ws->data_ptr<float>(), (int)splitk, M * N, (bf16*)c.data_ptr(),
@@ -1305,7 +1314,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("splitk"), pybind11::arg("ws"), pybind11::arg("accumulate"),
         pybind11::arg("algo") = 1, pybind11::arg("tail_ws") = pybind11::none(),
         pybind11::arg("tail_cnt") = pybind11::none(), pybind11::arg("tail_full") = -1,
-        pybind11::arg("tail_split") = 1);
+        pybind11::arg("tail_split") = 1, pybind11::arg("bpack") = false);
   m.def("gemm_tail_plan", [](int64_t tiles, int64_t K, int64_t ks, int64_t slots, int64_t max_split) {
     int full, S;
     caamd::gemm_tail_plan((int)tiles, (int)K, (int)ks, (int)slots, (int)max_split, &full, &S);

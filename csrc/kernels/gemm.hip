@@ -50,6 +50,7 @@ enum Epi : int {
   EPI_F32 = 2,        // Cf32[slice] = acc          (split-K partial slab)
   EPI_BIAS_GELU = 3,  // Z = acc + bias ; C = gelu(Z)
   EPI_DGELU = 4,      // C = acc * gelu'(Z[m,n]) ; dbias[n] += colsum(C) (f32 atomics)
+  EPI_SWIGLU = 5,     // B rows = [gate; up] in 64-row blocks: C[m, n/2] = silu(g) * u (ldc = N/2)
 };
 
 // gelu_tanh / gelu_tanh_grad: common.h (sigmoid form on v_exp_f32 + v_rcp_f32).
@@ -188,6 +189,10 @@ struct Args {
   int tfull, tS;
   float* tws;
   int* tcnt;
+  // algo 9 only: B is in the decode GEMM's packed order (ops/llm.py pack_decode_weight:
+  // per 128-row slab and 64-deep K-tile one contiguous swizzled 16 KiB image), so the
+  // serving prefill reads the same weight copy as decode
+  int bpack;
 };
 
 // Output tile staged through LDS: the MFMA fragments (each lane: 4 columns of one
@@ -245,6 +250,30 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
     __syncthreads();
     if constexpr (ABL & 8) continue;
     if (tid >= ACTIVE) continue;
+    if constexpr (EPI == EPI_SWIGLU) {
+      // chunk c of a gate block (c / 8 even) pairs with chunk c + 8 of the up block
+      // that follows it; the up-chunk threads have nothing to store
+      static_assert(BN % 128 == 0, "SwiGLU: whole 64-row gate/up block pairs per tile");
+      if ((c >> 3) & 1) continue;
+      const int on = (n0 >> 1) + (c >> 4) * 64 + (c & 7) * 8;
+      for (int it = 0; it < RITERS; ++it) {
+        const int ir = it * RG + rg;
+        if (ir >= HR) break;
+        const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
+        const int m = m0 + wr_ * (TM * 16) + h * (TMH * 16) + rem;
+        if (m >= p.M) continue;
+        const bf16x8_t g = *(lds_bf16x8*)(smem + ir * ROWB + c * 16);
+        const bf16x8_t u = *(lds_bf16x8*)(smem + ir * ROWB + (c + 8) * 16);
+        bf16x8_t o;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float gf = (float)g[r];
+          o[r] = (bf16)(__fdividef(gf, 1.f + __expf(-gf)) * (float)u[r]);
+        }
+        *reinterpret_cast<bf16x8_t*>((bf16*)p.C + (size_t)m * p.ldc + on) = o;
+      }
+      continue;
+    }
     for (int it = 0; it < RITERS; ++it) {
       const int ir = it * RG + rg;
       if (ir >= HR) break;
@@ -1553,14 +1582,23 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
   // (64 j rows) goes with the K offset into soffset.
   const int lrow = wid * 8 + (lane >> 3);
   const int lchunk = (lane & 7) ^ kswz(lrow);
-  const int voff_a = (lrow * p.lda + lchunk * 8) * 2, voff_b = (lrow * p.ldb + lchunk * 8) * 2;
+  const int voff_a = (lrow * p.lda + lchunk * 8) * 2;
+  // packed B: logical chunk c of slab row r sits at position c ^ s(r), s(r) = x ^ ((x & 1) << 2),
+  // x = (r >> 1) & 7 (decode_gemm.hip swz); rows r and r + 64 share s, so one lane offset
+  // serves every round and the slab / half-slab / K-tile offsets go into soffset
+  const int bx = (lrow >> 1) & 7;
+  const bool bpk = p.bpack != 0;
+  const int voff_b = bpk ? lrow * 128 + (lchunk ^ (bx ^ ((bx & 1) << 2))) * 16 : (lrow * p.ldb + lchunk * 8) * 2;
+  const int slab_bytes = 128 * p.K * 2;
   // round j of K-tile t -> buffer t & 1
 #define K64_DMA_ROUND(t_, j_)                                                                          \
   dma_lds16((j_) < NA ? ra : rb,                                                                      \
             smem + ((t_) & 1) * ST +                                                                  \
                 ((j_) < NA ? ((j_) * NTHR + wid * 64) * 16 : A_ST + (((j_) - NA) * NTHR + wid * 64) * 16), \
             (j_) < NA ? voff_a : voff_b,                                                              \
-            ((ABL & 32) ? t0 : t0 + (t_)) * 128 + ((j_) < NA ? (j_) * 64 * p.lda : ((j_) - NA) * 64 * p.ldb) * 2)
+            ((j_) >= NA && bpk)                                                                       \
+                ? (((j_) - NA) >> 1) * slab_bytes + (t0 + (t_)) * 16384 + (((j_) - NA) & 1) * 8192     \
+                : ((ABL & 32) ? t0 : t0 + (t_)) * 128 + ((j_) < NA ? (j_) * 64 * p.lda : ((j_) - NA) * 64 * p.ldb) * 2)
   // rounds of phase q: [lo, hi)
   auto rlo = [](int q) { return q >= DSPLIT ? NR : (NR * q) / DSPLIT; };
   f32x4 acc[TM][TN];
@@ -1764,6 +1802,9 @@ static hipError_t launch_k64(const Args& a, hipStream_t st) {
 
 template <int BM, int BN, bool AK, bool BK_, int EPI>
 static hipError_t launch_t(const Args& a, hipStream_t st) {
+  if (a.bpack && a.algo % 10 != 9) return hipErrorInvalidValue;
+  // SwiGLU: staged epilogue of the ping-pong (2) and full-line (9) kernels only
+  if (EPI == EPI_SWIGLU && (a.splitk != 1 || !(a.algo % 10 == 9 || a.algo == 2))) return hipErrorInvalidValue;
   if (a.algo % 10 == 9) {
     if constexpr (AK && BK_ && EPI != EPI_F32 && BM == 256) return launch_k64<BM, BN, EPI>(a, st);
     return hipErrorInvalidValue;
@@ -1859,6 +1900,9 @@ static hipError_t launch_epi(int layout, int epi, const Args& a, hipStream_t st)
     case EPI_F32: return launch_layout<BM, BN, EPI_F32>(layout, a, st);
     case EPI_BIAS_GELU: return launch_t<BM, BN, true, true, EPI_BIAS_GELU>(a, st);
     case EPI_DGELU: return launch_t<BM, BN, true, true, EPI_DGELU>(a, st);
+    case EPI_SWIGLU:
+      if constexpr (BN % 128 == 0) return launch_t<BM, BN, true, true, EPI_SWIGLU>(a, st);
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }
@@ -1898,9 +1942,10 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
                        const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
                        int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
-                       int tfull, int tS, float* tws, int* tcnt) {
+                       int tfull, int tS, float* tws, int* tcnt, int bpack) {
   gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk,
-               algo == 5 ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt};
+               algo == 5 ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt,
+               bpack};
   if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
   if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);
   if (bm == 128 && bn == 320) return gemm::launch_epi<128, 320>(layout, epi, a, st);

@@ -97,8 +97,9 @@ def test_drop_refs_in_flight_frees_objects(cluster):
     ray.get(a.pid.remote())
     w = context.worker
     deadline = time.time() + 10
-    while time.time() < deadline and w.store.used > 10 * 400_000:
-        time.sleep(0.1)
+    while time.time() < deadline and (w.store.used > 10 * 400_000 or w.refs.direct_pending
+                                      or w.refs.direct_dropped):
+        time.sleep(0.1)  # seal notifications of the dropped calls may still be in flight
     # the store must not keep 100 x 400 KB of orphaned results
     assert w.store.used < 10 * 400_000, w.store.used
     assert not w.refs.direct_pending and not w.refs.direct_dropped

@@ -303,3 +303,56 @@ def test_llama_decode_folded_norms_match(M, monkeypatch):
     assert m._dec["norm"] is False
     assert _rel(out["1"][0], out["0"][0]) < 2e-2
     assert _rel(torch.stack(out["1"][1]), torch.stack(out["0"][1])) < 1e-2
+
+
+def _rel2(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 2560, 1024), (2048, 2048, 4096), (256, 5632, 1024)])
+def test_prefill_gemm_packed_epilogues(M, N, K):
+    """gemm.hip full-line kernel reading B in the decode GEMM's packed order:
+    plain store, residual accumulate (o / down) and SwiGLU over the 64-row
+    interleaved gate/up weight, vs fp32 (K = 4096 exercises the split-K tail)."""
+    import torch.nn.functional as F
+
+    from cluster_anywhere_amd.ops import gemm as G
+
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    ref = x.float() @ w.float().t()
+    y = G.prefill_linear(x, L.pack_decode_weight(w))
+    assert _rel2(y, ref) < 5e-3
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    acc = r.clone()
+    G.prefill_linear(x, L.pack_decode_weight(w), out=acc, accumulate=True)
+    assert _rel2(acc, ref + r.float()) < 5e-3
+    a = G.prefill_linear(x, L.pack_decode_weight(L.interleave_gate_up(w)), epi=G.EPI_SWIGLU)
+    g, u = ref[:, : N // 2].bfloat16().float(), ref[:, N // 2:].bfloat16().float()
+    assert a.shape == (M, N // 2) and _rel2(a, F.silu(g) * u) < 1e-2
+
+
+def test_llama_packed_prefill_shares_weights():
+    """After prepare_decode the nn.Linear weights are released (one weight copy);
+    prefill on gemm.hip from the packed copies matches the dense forward's logits
+    at each sequence's last prompt token, and re-preparing restores the originals
+    bit-exactly."""
+    from cluster_anywhere_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(3)
+    m = Llama(LlamaConfig.named("llama-small")).to("cuda", torch.bfloat16).init_weights(std=0.02)
+    orig = {n: p.detach().clone() for n, p in m.named_parameters()}
+    B, T = 3, 200  # M = 600: padded to 768 rows inside
+    tok = torch.randint(0, m.cfg.vocab_size, (B, T), device="cuda")
+    dense = m(tok).float()
+    assert m.prepare_decode() and m._shared and m._dec["prefill"]
+    assert m.layers[0].w_gate_up.numel() == 0 and m.lm_head.numel() == 0
+    pos = torch.arange(T, device="cuda").expand(B, T)
+    last = torch.tensor([T - 1, 57, 120], device="cuda")
+    logits = m.prefill(tok, pos, None, None, None, last).float()
+    ref = dense[torch.arange(B), last]
+    assert _rel2(logits, ref) < 3e-2
+    assert (logits.argmax(-1) == ref.argmax(-1)).float().mean() >= 2 / 3
+    m._restore_originals()
+    assert all(torch.equal(p, orig[n]) for n, p in m.named_parameters())
