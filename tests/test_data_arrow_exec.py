@@ -138,7 +138,7 @@ class _Slow:
         self.pid = os.getpid()
 
     def __call__(self, batch):
-        time.sleep(0.05)
+        time.sleep(0.12)  # long enough that the pool scales up under a loaded CI box
         return {"id": batch["id"], "pid": np.full(len(batch["id"]), self.pid)}
 
 

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 4: GPU tests of the new paths (packed prefill GEMM, Serve IPC, ZeRO world-1),
+# weight-gradient K sweep, then the LLM bench A/B (packed prefill vs hipBLASLt prefill).
+set -o pipefail
+O=$GRAFT_REPO_ROOT/gpurun_out/batch1_r4
+mkdir -p $O
+cd $GRAFT_REPO_ROOT
+timeout -k 10 600 python -u -m pytest tests/test_gemm_gpu.py tests/test_llm_gpu.py tests/test_zero_gpu.py tests/test_serve_ipc_gpu.py -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" $O/pytest.log | head -30; exit $rc; }
+timeout -k 10 200 python -u tools/wgrad_bench.py --ksweep > $O/ksweep.jsonl 2> $O/ksweep.err || { echo "ksweep failed"; tail -5 $O/ksweep.err; exit 1; }
+cat $O/ksweep.jsonl
+A="--num-prompts 256 --max-num-seqs 128 --input-len 512 --output-len 128"
+for v in new old new old; do
+  case $v in
+    old) E="CAAMD_LLM_PACKED_PREFILL=0" ;;
+    *) E="" ;;
+  esac
+  env $E timeout -k 10 300 python -u tools/bench_llm.py $A > $O/bench_$v.log 2>&1 || { echo "bench $v failed"; tail -5 $O/bench_$v.log; exit 1; }
+  echo $v $(grep -o '"ttft_p50_s": [0-9.]*\|"steady_tpot_p50_ms": [0-9.]*\|"value": [0-9.]*\|"kv_blocks": [0-9]*' $O/bench_$v.log | tr '\n' ' ')
+  grep metric $O/bench_$v.log | tail -1 >> $O/bench.jsonl
+done
