@@ -122,7 +122,7 @@ def run2(a, b, c, layout, epi, bias=None, z=None, zout=None, dbias=None, max_spl
 def tail_plan(M: int, N: int, K: int, bm: int, bn: int, dev: torch.device, algo: int = None):
     """(full tiles, tail split) of a ping-pong launch; split 1 = no tail split."""
     algo = ALGO if algo is None else algo
-    if not TAIL or not (1 <= algo % 10 <= 3 or algo % 10 in (7, 9)) or K < 4096:
+    if not TAIL or not (1 <= algo % 10 <= 3 or algo % 10 == 9) or K < 4096:
         # K = 1600: the split slices and slab round trip cost more than the half-empty
         # last round (which the chip runs at a higher clock); profiles/gemm_tail_split.jsonl
         return (0, 1)
@@ -135,30 +135,14 @@ def tail_plan(M: int, N: int, K: int, bm: int, bn: int, dev: torch.device, algo:
     return p
 
 
-# persistent ping-pong kernel with the asynchronous staged epilogue (algo 8): NT
-# layout, 256 x 320 tiles, bf16 (+bias) / bias+GELU epilogues, shapes without a
-# split-K tail. Opt-in (CAAMD_GEMM_PST=1): it measured level or slower than the
-# per-tile kernel on every step shape (fc fwd 670 vs 652 us, proj fwd 176 vs 155 us)
-# and 86.6k vs 87.8k tok/s in the step (profiles/gemm_pst_r3.jsonl).
-PST = os.environ.get("CAAMD_GEMM_PST", "0") == "1"
-
-
-def pst_ok(layout: int, epi: int, bm: int, bn: int, M: int, N: int, K: int) -> bool:
-    return (PST and layout == 0 and (bm, bn) == (256, 320) and epi in (EPI_BF16, EPI_BIAS_GELU)
-            and M % bm == 0 and N % bn == 0 and K % 32 == 0 and K >= 128)
-
-
 def run_pp(a, b, c, layout, epi, bm, bn, bias=None, z=None, zout=None, dbias=None, algo=None):
-    """First-generation ping-pong kernel (gemm.hip) with the split-K tail; the
-    persistent async-epilogue kernel where it applies and no tail split is planned."""
+    """Ping-pong (algo 2) or full-line (algo 4009) kernel of gemm.hip with the split-K tail."""
     M, N = c.shape
     K = a.shape[0] if layout == 2 else a.shape[1]
     if algo is None and ALGO == 2 and k64_ok(layout, epi, bm, bn, N, K):
         algo = K64_ALGO
     algo = ALGO if algo is None else algo
     full, S = tail_plan(M, N, K, bm, bn, c.device, algo)
-    if S == 1 and algo == ALGO and pst_ok(layout, epi, bm, bn, M, N, K):
-        algo = 8
     ws = cnt = None
     if S > 1:
         ws, cnt = _workspace(c.device, ((M // bm) * (N // bn) - full) * S * bm * bn, (M // bm) * (N // bn) - full)

@@ -337,30 +337,8 @@ def paged_decode_attention(q, k_cache, v_cache, block_tables, ctx_lens, max_ctx:
     D = k_cache.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if use_gpu_kernel(q, k_cache) and q.dtype == torch.bfloat16:
-        tk = _pd_tickets(q.device, q.shape[0] * k_cache.shape[1])
-        return kernels().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, int(max_ctx), H, scale, -1, tk)
+        return kernels().paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, int(max_ctx), H, scale, -1)
     return paged_decode_ref(q, k_cache, v_cache, block_tables, ctx_lens, H, scale)
-
-
-_PD_TICKETS: dict = {}
-
-
-def _pd_tickets(dev, n: int) -> Optional[torch.Tensor]:
-    """Per-(sequence, kv head) arrival tickets of the MFMA paged decode (its last
-    partition block merges the partitions; each launch leaves them zeroed). One
-    buffer per device, sized generously at first use so a graph capture never has
-    to allocate it; None (separate reduce launch) where it is too small. Opt-in
-    (CAAMD_PAGED_MERGE=1): with one agent-scope release per partition block (3k per
-    layer at batch 128) the step measured 11.3 vs 6.65 ms TPOT
-    (profiles/llm_decode_ab_r3_paged_merge.txt); the 5 us reduce launch stays."""
-    if _os.environ.get("CAAMD_PAGED_MERGE", "0") != "1":
-        return None
-    t = _PD_TICKETS.get(dev.index)
-    if t is None:
-        if torch.cuda.is_current_stream_capturing():
-            return None
-        t = _PD_TICKETS[dev.index] = torch.zeros(max(n, 1 << 16), device=dev, dtype=torch.int32)
-    return t if t.numel() >= n else None
 
 
 def prefill_attention_ref(q, k, v, H, KVH, causal=True):

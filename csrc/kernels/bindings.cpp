@@ -481,7 +481,7 @@ bool paged_decode_launch(const bf16*, int, const bf16*, const bf16*, const int*,
 int paged_max_parts(int);
 int paged_mfma_max_parts(int);
 bool paged_decode_mfma_launch(const bf16*, int, const bf16*, const bf16*, const int*, int, const int*, bf16*,
-                              float*, float*, int, int, int, int, int, int, float, unsigned*, hipStream_t);
+                              float*, float*, int, int, int, int, int, int, float, hipStream_t);
 void fa_fwd_gqa_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
                        int, hipStream_t);
 }
@@ -592,8 +592,7 @@ void rope_cache_(Tensor& qkv, const Tensor& cos_sin, const Tensor& positions, co
 // impl: -1 auto (MFMA kernel for D=128 / 16-token pages / G <= 16 unless CAAMD_PAGED_MFMA=0),
 //        0 the VALU kernel, 1 the MFMA kernel
 Tensor paged_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_tables,
-                    const Tensor& ctx_lens, int64_t max_ctx, int64_t H, double scale, int64_t impl,
-                    c10::optional<Tensor> tickets) {
+                    const Tensor& ctx_lens, int64_t max_ctx, int64_t H, double scale, int64_t impl) {
   CHECK_GPU(q);
   CHECK_DT(q, at::kBFloat16);
   TORCH_CHECK(q.dim() == 2 && q.stride(1) == 1, "paged_decode: q must be [B, >=H*D] with unit inner stride");
@@ -626,19 +625,13 @@ Tensor paged_decode(const Tensor& q, const Tensor& k_cache, const Tensor& v_cach
     pml = at::empty({B, H, mp, 2}, q.options().dtype(at::kFloat));
   }
   if (B > 0) {
-    unsigned* tk = nullptr;  // MFMA kernel: the last partition block merges (no reduce launch)
-    if (impl == 1 && tickets.has_value()) {
-      TORCH_CHECK(tickets->is_cuda() && tickets->scalar_type() == at::kInt && tickets->numel() >= B * KVH,
-                  "paged_decode: tickets must be >= B * KVH zeroed int32");
-      tk = reinterpret_cast<unsigned*>(tickets->data_ptr<int>());
-    }
     float* pa = mp > 1 ? pacc.data_ptr<float>() : nullptr;
     float* pm = mp > 1 ? pml.data_ptr<float>() : nullptr;
     const bool ok = impl == 1
         ? caamd::paged_decode_mfma_launch(bp(q), (int)q.stride(0), bp(k_cache), bp(v_cache),
                                           block_tables.data_ptr<int>(), (int)block_tables.size(1),
                                           ctx_lens.data_ptr<int>(), bp(out), pa, pm, B, (int)H, KVH, D, BS,
-                                          (int)max_ctx, (float)scale, tk, cur_stream())
+                                          (int)max_ctx, (float)scale, cur_stream())
         : caamd::paged_decode_launch(bp(q), (int)q.stride(0), bp(k_cache), bp(v_cache), block_tables.data_ptr<int>(),
                                      (int)block_tables.size(1), ctx_lens.data_ptr<int>(), bp(out), pa, pm, B, (int)H,
                                      KVH, D, BS, (int)max_ctx, (float)scale, cur_stream());
@@ -908,8 +901,8 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   } else if (tail_split > 1) {
     const int64_t tiles = (M / bm) * (N / bn);
     TORCH_CHECK(ek != 2 && splitk == 1, "gemm: split tail is for the bf16 epilogues");
-    TORCH_CHECK((algo % 10 >= 1 && algo % 10 <= 3) || algo % 10 == 7 || algo % 10 == 9,
-                "gemm: split tail needs a ping-pong algo (1-3, 7, 9)");
+    TORCH_CHECK((algo % 10 >= 1 && algo % 10 <= 3) || algo % 10 == 9,
+                "gemm: split tail needs a ping-pong algo (1-3) or the full-line kernel (9)");
     TORCH_CHECK(tail_full >= 0 && tail_full < tiles && tail_full % 8 == 0 &&
                     ((tiles - tail_full) * tail_split) % 8 == 0, "gemm: bad tail plan");
     TORCH_CHECK(tail_ws.has_value() && tail_cnt.has_value(), "gemm: split tail needs ws and tickets");
@@ -1356,7 +1349,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rope_cache_", GUARDED(rope_cache_));
   m.def("paged_decode", GUARDED(paged_decode), pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
         pybind11::arg("block_tables"), pybind11::arg("ctx_lens"), pybind11::arg("max_ctx"), pybind11::arg("H"),
-        pybind11::arg("scale"), pybind11::arg("impl") = -1, pybind11::arg("tickets") = pybind11::none());
+        pybind11::arg("scale"), pybind11::arg("impl") = -1);
   m.def("flash_attn_gqa", GUARDED(flash_attn_gqa));
   m.def("image_normalize", GUARDED(image_normalize));
   m.def("add_relu_", GUARDED(add_relu_));

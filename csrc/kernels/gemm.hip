@@ -604,21 +604,11 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// DMA_IN_M (algo 7, one phase, distance 3): K-step t+3's DMA pieces are issued one at
-// a time between the MFMA groups of the M segment of step t instead of at the head of
-// the R segment. Barriers B1, B2, ... with the lagging row one behind: row 0 runs
-// R(t) in [B(2t+1), B(2t+2)] and M(t) in [B(2t+2), B(2t+3)], row 1 one barrier later;
-// stage t+1 is first read after B(2t+3), which closes row 0's M(t) (it waits there,
-// t+2 and t+3 in flight) and row 1's R(t) (it waits there, t+2 in flight); slot t-1,
-// overwritten during M(t), was last read in R(t-1), which both rows finished by B(2t+2). PMC (profiles/gemm_pp_pmc_r3_instep.txt): MFMA busy 58%, LDS stalls 6% --
-// the R segment (4-5 pieces at 100-185 issue cycles each beside 18 LDS reads,
-// MI355X_MICROARCH.md "LDS-DMA piece issue cost") outlasted the partner's 640-cycle
-// M segment; among bare MFMAs a piece costs about 60.
-template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL = 0, int PH = 2, int DIST = 2, bool DMA_IN_M = false>
+// (An algo-7 variant issued K-step t+3's DMA pieces between the MFMA groups of the M
+// segment: 1 % slower in the step, removed in round 4.)
+template <int BM, int BN, bool AK, bool BK_, int EPI, int ABL = 0, int PH = 2, int DIST = 2>
 __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
   static_assert(DIST == 2 || (DIST == 3 && PH == 1), "prefetch distance 3 is WAR-safe only with one phase");
-  static_assert(!DMA_IN_M || (PH == 1 && DIST == 3), "DMA in the M segment: one phase, distance 3 "
-                "(slot t-1 is free in both wave rows by M(t); see the barrier schedule above)");
   constexpr int WM = 2, WN = 4;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   constexpr int TMH = TM / PH;  // m-tiles per phase (PH phases per K-step)
@@ -690,21 +680,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
     dma_step32<BM, AK>(p.A, p.lda, m0, k0, base, wid, lane);
     dma_step32<BN, BK_>(p.B, p.ldb, n0, k0, base + A_ST, wid, lane);
   };
-  // piece q of step t's DMA for this wave, in dma()'s order (A rounds, then B rounds,
-  // then B's partial round on the waves that carry it)
-  constexpr int A_FULL = (BM * 32 * 2) / (NTHR * 16), B_FULL = (BN * 32 * 2) / (NTHR * 16);
-  constexpr int B_REM = BN * 32 * 2 - B_FULL * NTHR * 16;
-  auto dma_piece = [&](int t, int q) {
-    lds_char* base = smem + (t & (NST - 1)) * ST;
-    const int k0 = (s0 + t) * KS;
-    if (q < A_FULL) {
-      if constexpr (AK) dma_kmaj32_one<BM>(p.A, p.lda, m0, k0, base, q, wid, lane);
-      else dma_mmaj32_one<BM>(p.A, p.lda, m0, k0, base, q, wid, lane);
-    } else if (q < A_FULL + B_FULL || (B_REM > 0 && wid * 1024 < B_REM)) {
-      if constexpr (BK_) dma_kmaj32_one<BN>(p.B, p.ldb, n0, k0, base + A_ST, q - A_FULL, wid, lane);
-      else dma_mmaj32_one<BN>(p.B, p.ldb, n0, k0, base + A_ST, q - A_FULL, wid, lane);
-    }
-  };
   // per-step DMA count of this wave: the two wave rows differ when a stage is not a
   // whole number of 8 KiB rounds (BN = 320)
   const bool lo_grp = wr == 0;
@@ -742,7 +717,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
       for (int mh = 0; mh < PH; ++mh) {
         // ---- R segment
         if (mh == 0) {
-          if (!DMA_IN_M && !(ABL & 1) && t + DIST < nk) dma(t + DIST);
+          if (!(ABL & 1) && t + DIST < nk) dma(t + DIST);
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
             const int rr = wc * (TN * 16) + j * 16;
@@ -758,12 +733,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
           else if constexpr (AK) af[i] = frag_kmaj64(As, rr, lane);
           else af[i] = frag_mmaj<BM>(As, rr, 0, lane);
         }
-        if constexpr (DMA_IN_M) {
-          // step t+1 must have landed by the barrier that closes this segment for the
-          // lagging row (the leading row waits at the end of its M segment instead);
-          // step t+2 was issued in the previous M segment and stays in flight
-          if (!lo_grp) wait_ahead(min(nk - 1, t + DIST - 1) - (t + 1));
-        } else if (mh == PH - 1 && !(ABL & 32)) {
+        if (mh == PH - 1 && !(ABL & 32)) {
           wait_ahead(min(nk - 1, t + DIST) - (t + 1));
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -772,26 +742,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_pp_kernel(Args p) {
         __builtin_amdgcn_sched_barrier(0);
         // ---- M segment
         __builtin_amdgcn_s_setprio(1);
-        const bool dm = DMA_IN_M && t + DIST < nk;
 #pragma unroll
         for (int i = 0; i < TMH; ++i) {
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             if constexpr (ABL & 4) asm volatile("" :: "v"(bf[j]), "v"(af[i]));
             else acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[mh * TMH + i][j], 0, 0, 0);
-          if constexpr (DMA_IN_M) {
-            if (i < A_FULL + B_FULL + (B_REM > 0 ? 1 : 0) && dm) {
-              __builtin_amdgcn_sched_barrier(0);
-              dma_piece(t + DIST, i);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
         }
         __builtin_amdgcn_s_setprio(0);
-        // leading row: step t+1 landed before the barrier after which it reads it
-        if constexpr (DMA_IN_M) {
-          if (lo_grp) wait_ahead(min(nk - 1, t + DIST) - (t + 1));
-        }
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -980,258 +938,9 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_persist_kernel(Args p) {
 }
 
 
-// ================================================================================
-// Persistent ping-pong kernel with an ASYNCHRONOUS staged epilogue (algo 8; NT
-// layout, 256 x 320 tiles, bf16 (+bias) and bias+GELU epilogues). One 512-thread
-// workgroup per CU walks its XCD's contiguous tile range; the 4-stage LDS ring of
-// 32-deep K-steps runs continuously across tiles (the next tile's first two steps
-// are in flight while a tile's last steps compute), with the R / M segments,
-// counted vmcnt and wave-row stagger of gemm_pp_kernel (one phase per step).
-//
-// What the non-persistent kernels cannot hide (profiles/gemm_ablations_r3.jsonl:
-// "no epilogue stores" 486 vs 622 us at 32768 x 6400 x 1600): every CU stores its
-// 164-328 KB tile in the same chip-wide burst and only then starts the next tile.
-// Here the tile is staged through LDS (into the two ring slots of the tile's last
-// two K-steps plus the 16 KB of LDS past the ring, which are free at that point)
-// and streamed out with coalesced 16-byte stores, and the wave goes straight on to
-// the next tile: the stores are YOUNGER than the next tile's first two DMA steps,
-// so the first K-step's wait leaves them in flight (vmcnt(NS + CNT)), and they only
-// have to have drained one K-step later, when the next DMA step is retired.
-// Every wave issues exactly NS = 20 (bf16) / 40 (GELU: z and u) store instructions
-// per tile (10 / 20 per m-half: 128 rows x 40 chunks over 512 threads), so the
-// counted wait is exact. The staging image is accessed with inline-asm ds_read /
-// ds_write (the compiler would otherwise drain the in-flight LDS-DMA before them).
-// ================================================================================
-__device__ __forceinline__ void lds_write_b64(unsigned addr, bf16x4 v) {
-  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "v"(v) : "memory");
-}
-__device__ __forceinline__ bf16x8_t lds_read_b128(unsigned addr) {
-  bf16x8_t v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(addr) : "memory");
-  return v;
-}
-
-// workgroup barrier for LDS hand-offs only: unlike __syncthreads() (whose
-// workgroup-scope fence waits vmcnt(0)) it leaves global stores and LDS-DMA in flight
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int EPI>
-__global__ __launch_bounds__(NTHR, 2) void gemm_pst_kernel(Args p) {
-  constexpr int BM = 256, BN = 320, WM = 2, WN = 4;
-  constexpr int TM = BM / WM / 16, TN = BN / WN / 16, TMH = TM / 2;
-  constexpr int KS = 32, NST = 4, DIST = 2;
-  constexpr int A_ST = BM * KS * 2, B_ST = BN * KS * 2, ST = A_ST + B_ST;
-  constexpr int ROWB = BN * 2 + 16;          // staging image row (bytes)
-  constexpr int RPS = ST / ROWB;             // image rows per ring slot (56)
-  constexpr int SPARE = NST * ST;            // 16 KB past the ring
-  constexpr int HR = BM / 2, CPR = BN / 8;   // 128 image rows x 40 chunks per m-half
-  constexpr int ITS = HR * CPR / NTHR;       // 10 chunks per thread per half
-  static_assert(HR * CPR == ITS * NTHR, "uniform store count per wave");
-  static_assert(2 * RPS + (160 * 1024 - SPARE) / ROWB >= HR, "staging image must fit");
-  constexpr int NS = (EPI == EPI_BIAS_GELU ? 4 : 2) * ITS;  // store instructions per tile per wave
-  constexpr int BIAS_OFF = SPARE + 12288;    // 640 B bias row, past the staging rows
-  static_assert(BIAS_OFF - SPARE >= (HR - 2 * RPS) * ROWB && BIAS_OFF + BN * 2 <= 160 * 1024, "bias slot");
-  constexpr int HB = 5;                      // output chunks per batch
-  static_assert(EPI == EPI_BF16 || EPI == EPI_BIAS_GELU, "pst: bf16 / bias+GELU epilogues");
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char* smem = (lds_char*)smem_raw;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 2, wc = wid & 3;
-  const bool lo_grp = wr == 0;
-
-  const int T = p.tiles_m * p.tiles_n;
-  const int bid = blockIdx.x, G = gridDim.x;
-  const int xcd = bid & 7, loc = bid >> 3;
-  const int q8 = T >> 3, r8 = T & 7;
-  const int start = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
-  const int size = q8 + (xcd < r8 ? 1 : 0);
-  const int nbx = (G >> 3) + (xcd < (G & 7) ? 1 : 0);
-  const int my_tiles = loc < size ? (size - loc + nbx - 1) / nbx : 0;
-  constexpr int GROUP_M = 8;
-  auto tile_origin = [&](int i, int& m0, int& n0) {
-    const int tile = start + loc + i * nbx;
-    const int group_sz = GROUP_M * p.tiles_n;
-    const int g = tile / group_sz;
-    const int first_m = g * GROUP_M;
-    const int gm = min(p.tiles_m - first_m, GROUP_M);
-    const int tin = tile - g * group_sz;
-    m0 = (first_m + tin % gm) * BM;
-    n0 = (tin / gm) * BN;
-  };
-  const int nk = p.K / KS;
-  const int total = my_tiles * nk;
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // DMA cursor (wave-uniform, kept in SGPRs): tile / k-step / origin of the next step
-  // to load, advanced one step per dma() call
-  int d_ti = 0, d_ks = 0, d_m0 = 0, d_n0 = 0;
-  if (my_tiles > 0) tile_origin(0, d_m0, d_n0);
-  auto dma = [&](int gs) {
-    lds_char* base = smem + (gs & (NST - 1)) * ST;
-    const int m0 = __builtin_amdgcn_readfirstlane(d_m0), n0 = __builtin_amdgcn_readfirstlane(d_n0);
-    const int k0 = __builtin_amdgcn_readfirstlane(d_ks * KS);
-    dma_step32<BM, true>(p.A, p.lda, m0, k0, base, wid, lane);
-    dma_step32<BN, true>(p.B, p.ldb, n0, k0, base + A_ST, wid, lane);
-    if (++d_ks == nk) {
-      d_ks = 0;
-      if (++d_ti < my_tiles) tile_origin(d_ti, d_m0, d_n0);
-    }
-  };
-  constexpr int CNT_LO = dma_count32<BM>(0) + dma_count32<BN>(0);
-  constexpr int CNT_HI = dma_count32<BM>(4) + dma_count32<BN>(4);
-  static_assert(dma_count32<BM>(3) == dma_count32<BM>(0) && dma_count32<BN>(3) == dma_count32<BN>(0), "");
-  static_assert(dma_count32<BM>(7) == dma_count32<BM>(4) && dma_count32<BN>(7) == dma_count32<BN>(4), "");
-  // retire DMA step gs+1: `newer` DMA steps and (first step of a tile) the previous
-  // tile's NS stores are younger and stay in flight
-  auto wait_ahead = [&](int newer, bool stores) {
-    if (stores) {
-      if (newer >= 1) { if (lo_grp) wait_vm<NS + CNT_LO>(); else wait_vm<NS + CNT_HI>(); }
-      else wait_vm<NS>();
-    } else if (newer >= 1) {
-      if (lo_grp) wait_vm<CNT_LO>(); else wait_vm<CNT_HI>();
-    } else {
-      wait_vm<0>();
-    }
-  };
-
-  if (total > 0) {
-    dma(0);
-    if (total > 1) dma(1);
-    wait_ahead(min(total, DIST) - 1, false);
-    __builtin_amdgcn_s_barrier();
-    if (!lo_grp) __builtin_amdgcn_s_barrier();
-    int ti = 0, ks = 0;
-    int c_m0, c_n0;  // origin of the tile being computed
-    tile_origin(0, c_m0, c_n0);
-    bf16x8_t bf[TN];
-    bf16x8_t af[TM];
-    for (int gs = 0; gs < total; ++gs) {
-      const lds_char* As = smem + (gs & (NST - 1)) * ST;
-      const lds_char* Bs = As + A_ST;
-      // ---- R segment
-      if (gs + DIST < total) dma(gs + DIST);
-      if (ks == 0 && p.bias && wid == 0 && lane < CPR) {
-        // this tile's bias row -> LDS (landed by the end of step ks = 1's wait; the
-        // epilogue reads it); one extra, older-than-counted op for wave 0: its
-        // counted waits then over-wait by one piece, never under-wait
-        __builtin_amdgcn_global_load_lds((const void*)(p.bias + c_n0 + lane * 8),
-                                         (void __attribute__((address_space(3)))*)(smem + BIAS_OFF), 16, 0, 0);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = frag_kmaj64(Bs, wc * (TN * 16) + j * 16, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = frag_kmaj64(As, wr * (TM * 16) + i * 16, lane);
-      wait_ahead(min(total - 1, gs + DIST) - (gs + 1), ks == 0 && ti > 0);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- M segment
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (++ks < nk) continue;
-
-      // ---- tile done: staged epilogue into the free ring slots of steps gs-1, gs
-      if (lo_grp) __builtin_amdgcn_s_barrier();  // row 1 finishes its M(gs): rows aligned
-      const int m0 = c_m0, n0 = c_n0;
-      const unsigned sbase = (unsigned)(size_t)smem;
-      const unsigned slotA = sbase + (unsigned)(((gs + NST - 1) & (NST - 1)) * ST);
-      const unsigned slotB = sbase + (unsigned)((gs & (NST - 1)) * ST);
-      auto row_addr = [&](int r) -> unsigned {
-        return r < RPS ? slotA + r * ROWB : r < 2 * RPS ? slotB + (r - RPS) * ROWB
-                                                        : sbase + SPARE + (r - 2 * RPS) * ROWB;
-      };
-      const bool has_bias = p.bias != nullptr;
-      // opaque copies of the lane ids: keeps the compiler from hoisting the
-      // epilogue's per-lane address math out of the K loop (it would hold ~40
-      // VGPRs across the main loop and spill)
-      int tid_e, lane_e;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(tid_e) : "v"(tid));
-      asm volatile("v_mov_b32 %0, %1" : "=v"(lane_e) : "v"(lane));
-      const int mrow = lane_e & 15, ncol = 4 * (lane_e >> 4);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h) lds_barrier();  // image reads of half 0 done
-#pragma unroll
-        for (int i = 0; i < TMH; ++i) {
-          const int ir = wr * (TMH * 16) + i * 16 + mrow;
-          const unsigned ra = row_addr(ir);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const int nc = wc * (TN * 16) + j * 16 + ncol;
-            bf16x4 o;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[h * TMH + i][j][r];
-            lds_write_b64(ra + nc * 2, o);
-          }
-        }
-        lds_barrier();
-        static_assert(ITS % HB == 0, "batches");
-#pragma unroll
-        for (int b = 0; b < ITS / HB; ++b) {
-          bf16x8_t v[HB], bb[HB];
-#pragma unroll
-          for (int u = 0; u < HB; ++u) {
-            const int qq = (b * HB + u) * NTHR + tid_e, ir = qq / CPR, c = qq - (qq / CPR) * CPR;
-            v[u] = lds_read_b128(row_addr(ir) + c * 16);
-            bb[u] = lds_read_b128(sbase + BIAS_OFF + c * 16);
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-          for (int u = 0; u < HB; ++u) {
-            const int qq = (b * HB + u) * NTHR + tid_e, ir = qq / CPR, c = qq - (qq / CPR) * CPR;
-            const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
-            const int m = m0 + wr_ * (TM * 16) + h * (TMH * 16) + rem;
-            const size_t off = (size_t)m * p.ldc + n0 + c * 8;
-            bf16x8_t o;
-            if constexpr (EPI == EPI_BIAS_GELU) {
-              bf16x8_t z;
-#pragma unroll
-              for (int r = 0; r < 8; ++r) {
-                z[r] = (bf16)((float)v[u][r] + (has_bias ? (float)bb[u][r] : 0.f));
-                o[r] = (bf16)gelu_tanh((float)z[r]);
-              }
-              *reinterpret_cast<bf16x8_t*>(p.Zout + off) = z;
-            } else {
-#pragma unroll
-              for (int r = 0; r < 8; ++r) o[r] = (bf16)((float)v[u][r] + (has_bias ? (float)bb[u][r] : 0.f));
-            }
-            *reinterpret_cast<bf16x8_t*>((bf16*)p.C + off) = o;
-          }
-        }
-      }
-      lds_barrier();  // staging reads done before step gs+1's R issues DMA into slot A
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      ks = 0;
-      if (++ti < my_tiles) tile_origin(ti, c_m0, c_n0);
-      if (!lo_grp && ti < my_tiles) __builtin_amdgcn_s_barrier();  // re-stagger the second wave row
-    }
-  }
-}
+// (A persistent variant of the ping-pong kernel with an asynchronous staged epilogue,
+// algo 8, measured level or slower on every step shape -- fc fwd 670 vs 652 us, step
+// 86.6k vs 87.8k tok/s, profiles/gemm_pst_r3.jsonl -- and was removed in round 4.)
 
 // ================================================================================
 // Stream-K ping-pong kernel (weight gradients: K = tokens = 32768, only 95-280
@@ -1837,7 +1546,7 @@ static hipError_t launch_abl(const Args& a, hipStream_t st) {
   using C_ = Cfg<BM, BN, AK, BK_>;
   const int T = a.tiles_m * a.tiles_n;
   const int grid = a.tS > 1 ? a.tfull + (T - a.tfull) * a.tS : T * a.splitk;
-  if (a.tS > 1 && !((a.algo % 10 >= 1 && a.algo % 10 <= 3) || a.algo % 10 == 7) && a.algo != 5)
+  if (a.tS > 1 && !(a.algo % 10 >= 1 && a.algo % 10 <= 3) && a.algo != 5)
     return hipErrorInvalidValue;
   if (a.algo == 5) {  // stream-K: the weight-gradient layout (TN) on 256 x 320 tiles only
     if constexpr ((EPI == EPI_BF16 || EPI == EPI_BF16_ACC) && BM == 256 && BN == 320 && !AK && !BK_) {
@@ -1849,27 +1558,15 @@ static hipError_t launch_abl(const Args& a, hipStream_t st) {
     }
     return hipErrorInvalidValue;
   }
-  if (a.algo == 8 && a.splitk == 1) {
-    if constexpr (BM == 256 && BN == 320 && AK && BK_ && (EPI == EPI_BF16 || EPI == EPI_BIAS_GELU)) {
-      auto k = gemm_pst_kernel<EPI>;
-      constexpr int lds = 160 * 1024;
-      ensure_lds((const void*)k, lds);
-      const int tiles = a.tiles_m * a.tiles_n;
-      hipLaunchKernelGGL(k, dim3(tiles < 256 ? tiles : 256), dim3(NTHR), lds, st, a);
-      return hipGetLastError();
-    }
-    return hipErrorInvalidValue;
-  }
   if (a.algo % 10 == 4 && a.splitk == 1) {
     auto k = gemm_persist_kernel<BM, BN, AK, BK_, EPI>;
     constexpr int lds = 4 * (BM + BN) * 32 * 2;
     ensure_lds((const void*)k, lds);
     const int tiles = a.tiles_m * a.tiles_n;
     hipLaunchKernelGGL(k, dim3(tiles < 256 ? tiles : 256), dim3(NTHR), lds, st, a);
-  } else if ((a.algo % 10 >= 1 && a.algo % 10 <= 3) || a.algo % 10 == 7) {
+  } else if (a.algo % 10 >= 1 && a.algo % 10 <= 3) {
     auto k = (a.algo % 10 == 1) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 2, 2>
              : (a.algo % 10 == 2) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 2>
-             : (a.algo % 10 == 7) ? gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 3, true>
                                   : gemm_pp_kernel<BM, BN, AK, BK_, EPI, ABL, 1, 3>;
     constexpr int lds = 4 * (BM + BN) * 32 * 2;
     ensure_lds((const void*)k, lds);

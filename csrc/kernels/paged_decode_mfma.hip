@@ -75,8 +75,7 @@ template <int G>
 __global__ __launch_bounds__(256, 3) void paged_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int max_blocks, const int* __restrict__ ctx_lens, bf16* __restrict__ out,
-    float* __restrict__ part_acc, float* __restrict__ part_ml, int KVH, int max_parts, float scale_log2,
-    unsigned* __restrict__ tick) {
+    float* __restrict__ part_acc, float* __restrict__ part_ml, int KVH, int max_parts, float scale_log2) {
   __shared__ __attribute__((aligned(16))) bf16 vimg[WAVES][CH * D];  // 8 KB per wave
   __shared__ float wm[WAVES][16], wl[WAVES][16];
   __shared__ float wo[WAVES][G][D];
@@ -235,42 +234,9 @@ __global__ __launch_bounds__(256, 3) void paged_decode_mfma_kernel(
       }
     }
   }
-  if (nparts == 1 || tick == nullptr) return;  // (no tickets: pdm_reduce_kernel merges)
-  // the LAST partition block of this (seq, kv head) to finish merges all partitions
-  // (release / ticket / acquire, as the decode GEMM's split-K) and re-arms the ticket:
-  // no separate reduce launch
-  __shared__ int last_flag;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* t = tick + (size_t)seq * KVH + kvh;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == (unsigned)(nparts - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    last_flag = last;
-  }
-  __syncthreads();
-  if (!last_flag) return;
-  for (int e = threadIdx.x; e < G * D; e += 256) {
-    const int h = e / D, d = e % D;
-    const int hh = kvh * G + h;
-    const float* ml = part_ml + ((size_t)seq * H + hh) * max_parts * 2;
-    const float* pa = part_acc + ((size_t)seq * H + hh) * max_parts * D;
-    float M = -INFINITY;
-    for (int p = 0; p < nparts; ++p) M = fmaxf(M, ml[2 * p]);
-    float num = 0.f, den = 0.f;
-    for (int p = 0; p < nparts; ++p) {
-      const float w = __builtin_amdgcn_exp2f(ml[2 * p] - M);
-      num += w * pa[(size_t)p * D + d];
-      den += w * ml[2 * p + 1];
-    }
-    out[((size_t)seq * H + hh) * D + d] = (bf16)(num / den);
-  }
+  // (partitions are merged by pdm_reduce_kernel; a last-arriver merge in this kernel
+  // -- one agent-scope release per partition block -- measured 11.3 vs 6.65 ms TPOT
+  // and was removed in round 4, profiles/llm_decode_ab_r3_paged_merge.txt)
 }
 
 // one block (D threads) per (seq, head): merge partitions (exp2 domain)
@@ -298,8 +264,7 @@ int paged_mfma_max_parts(int max_ctx) { return (max_ctx + pdm::PART - 1) / pdm::
 
 bool paged_decode_mfma_launch(const bf16* q, int q_stride, const bf16* kc, const bf16* vc, const int* block_tables,
                               int max_blocks, const int* ctx_lens, bf16* out, float* part_acc, float* part_ml, int B,
-                              int H, int KVH, int D, int BS, int max_ctx, float scale, unsigned* tick,
-                              hipStream_t st) {
+                              int H, int KVH, int D, int BS, int max_ctx, float scale, hipStream_t st) {
   if (D != pdm::D || BS != pdm::BS) return false;
   const int G = H / KVH;
   const int mp = paged_mfma_max_parts(max_ctx);
@@ -308,8 +273,8 @@ bool paged_decode_mfma_launch(const bf16* q, int q_stride, const bf16* kc, const
 #define PDM_CASE(GG)                                                                                          \
   if (G == GG) {                                                                                              \
     hipLaunchKernelGGL((pdm::paged_decode_mfma_kernel<GG>), grid, block, 0, st, q, q_stride, kc, vc,          \
-                       block_tables, max_blocks, ctx_lens, out, part_acc, part_ml, KVH, mp, sl2, tick);       \
-    if (mp > 1 && tick == nullptr)                                                                            \
+                       block_tables, max_blocks, ctx_lens, out, part_acc, part_ml, KVH, mp, sl2);             \
+    if (mp > 1)                                                                                               \
       hipLaunchKernelGGL(pdm::pdm_reduce_kernel, dim3(H, B), dim3(pdm::D), 0, st, part_acc, part_ml, ctx_lens, \
                          out, H, mp);                                                                         \
     return true;                                                                                              \

@@ -19,7 +19,7 @@ def _mk(shape, seed):
 
 @pytest.mark.parametrize("layout", [0, 1, 2])
 @pytest.mark.parametrize("tile", [(256, 256), (256, 320), (128, 320)])
-@pytest.mark.parametrize("algo", [0, 1, 2, 3, 4, 7])
+@pytest.mark.parametrize("algo", [0, 1, 2, 3, 4])
 def test_gemm_layouts(layout, tile, algo):
     from cluster_anywhere_amd.ops.gemm import gemm
 
@@ -38,54 +38,12 @@ def test_gemm_layouts(layout, tile, algo):
     assert _rel(c, ref) < 5e-3
 
 
-@pytest.mark.parametrize("MN", [(256, 320), (512, 960), (2048, 1600), (768, 640)])
-@pytest.mark.parametrize("epi", ["plain", "bias", "gelu"])
-def test_gemm_persistent_async_epilogue(MN, epi):
-    """algo 8: tiles per workgroup 1..several (grid = min(tiles, 256)), the staged
-    epilogue in the ring slots of the tile's last two K-steps, stores left in flight."""
-    from cluster_anywhere_amd.ops import gemm as G
-    from cluster_anywhere_amd.ops import kernels
-
-    M, N = MN
-    K = 448
-    x, w = _mk((M, K), 11), _mk((N, K), 12) * 0.05
-    b = _mk((N,), 13) if epi != "plain" else None
-    ref = x.float() @ w.float().t() + (b.float() if b is not None else 0)
-    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    if epi == "gelu":
-        zo = torch.empty_like(c)
-        kernels().gemm_bf16(x, w, c, 0, G.EPI_BIAS_GELU, 256, 320, b, None, zo, None, 1, None, False, 8,
-                            None, None, 0, 1)
-        assert _rel(zo, ref) < 5e-3
-        assert _rel(c, F.gelu(zo.float(), approximate="tanh")) < 1e-2
-    else:
-        kernels().gemm_bf16(x, w, c, 0, G.EPI_BF16, 256, 320, b, None, None, None, 1, None, False, 8,
-                            None, None, 0, 1)
-        assert _rel(c, ref) < 5e-3
-
-
-def test_gemm_persistent_many_tiles_per_cu():
-    from cluster_anywhere_amd.ops import gemm as G
-    from cluster_anywhere_amd.ops import kernels
-
-    M, N, K = 256 * 24, 320 * 25, 192  # 600 tiles: 2-3 per workgroup, 6 K-steps each
-    x, w = _mk((M, K), 14), _mk((N, K), 15) * 0.05
-    b = _mk((N,), 16)
-    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    kernels().gemm_bf16(x, w, c, 0, G.EPI_BF16, 256, 320, b, None, None, None, 1, None, False, 8,
-                        None, None, 0, 1)
-    ref = x.float() @ w.float().t() + b.float()
-    assert _rel(c, ref) < 5e-3
-    c2 = G.linear_nt(x, w, b)  # the dispatcher picks algo 8 for this shape
-    assert torch.equal(c, c2)
-
-
 def test_gemm_short_k():
     from cluster_anywhere_amd.ops.gemm import gemm
 
     for K in (64, 128, 192):  # fewer K-steps than the prefetch distance
         a, b = _mk((256, K), 3), _mk((320, K), 4)
-        for algo in (3, 7):
+        for algo in (3, 9):
             assert _rel(gemm(a, b, 0, algo=algo), a.float() @ b.float().t()) < 5e-3
 
 

@@ -41,11 +41,28 @@ def _run(port, q):
             m = GPT2(cfg).cuda()
             st = DataParallelStep(m, lr=1e-3, zero=zero, max_grad_norm=1.0, bucket_cap_mb=0.5)
             assert st.zero == (zero == "always")
+            signals = {}
+            if st.zero:  # every parameter must signal "gradient final" exactly once per step
+                orig = st.reducer._on_grad
+
+                def counted(p, orig=orig):
+                    signals[id(p)] = signals.get(id(p), 0) + 1
+                    orig(p)
+
+                for sl in st.flat.slots:
+                    sl.param._ca_grad_ready = counted
+                for h in st.reducer._hooks:
+                    h.remove()
+                st.reducer._hooks = [sl.param.register_post_accumulate_grad_hook(counted) for sl in st.flat.slots]
             losses = [float(st(x[:, :-1], x[:, 1:])) for x in data]
             st.wait_params()
             torch.cuda.synchronize()
+            names = {id(sl.param): sl.name for sl in st.flat.slots}
+            bad = {names[k]: v for k, v in signals.items() if v != len(data)}
+            missing = [sl.name for sl in st.flat.slots if id(sl.param) not in signals] if st.zero else []
+            slots = [(sl.name, sl.offset, sl.numel) for sl in st.flat.slots]
             out[str(zero)] = (st.flat.param_buffer.float().cpu().numpy(), losses,
-                              len(getattr(st.reducer, "buckets", [])))
+                              len(getattr(st.reducer, "buckets", [])), bad, missing, slots)
         q.put(out)
     finally:
         dist.destroy_process_group()
@@ -59,11 +76,14 @@ def test_zero1_world1_rccl_matches_plain_step():
     out = q.get(timeout=300)
     p.join(60)
     assert p.exitcode == 0
-    (pz, lz, nb), (pp, lp, _) = out["always"], out["False"]
+    (pz, lz, nb, bad, missing, slots), (pp, lp, *_) = out["always"], out["False"]
     assert nb > 1  # several buckets: the per-bucket reduce-scatter / all-gather order ran
+    assert not bad and not missing, (bad, missing)  # one readiness signal per param per step
+    a, b = torch.from_numpy(pz), torch.from_numpy(pp)
+    per = sorted(((((a[o:o + n] - b[o:o + n]).norm() / (b[o:o + n].norm() + 1e-12)).item(), nm)
+                  for nm, o, n in slots), reverse=True)[:5]
     assert lz[0] == pytest.approx(lp[0], rel=1e-6)
     assert all(abs(a - b) <= 1e-3 * abs(b) for a, b in zip(lz, lp)), (lz, lp)
-    a, b = torch.from_numpy(pz), torch.from_numpy(pp)
     assert a.shape == b.shape
     rel = ((a - b).norm() / b.norm()).item()
-    assert rel <= 1e-3, rel
+    assert rel <= 1e-3, (rel, per)

@@ -21,7 +21,7 @@ namespace caamd {
 hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
                        const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N, int K,
                        int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st, int tfull, int tS,
-                       float* tws, int* tcnt);
+                       float* tws, int* tcnt, int bpack);
 void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
 }  // namespace caamd
 using caamd::bf16;
@@ -124,7 +124,7 @@ int main(int argc, char** argv) {
     auto launch = [&](int algo) {
       return caamd::gemm_launch(0, s.epi, bm, bn, A, B, C, s.epi == 4 ? nullptr : bias, s.epi == 4 ? Z : nullptr,
                                 s.epi == 3 ? Zo : nullptr, s.epi == 4 ? dbias : nullptr, s.M, s.N, s.K, s.K, s.K,
-                                s.N, 1, algo, 0, tfull, tS, tws, tcnt);
+                                s.N, 1, algo, 0, tfull, tS, tws, tcnt, 0);
     };
     // ---- numerics: first RR rows and a block of rows in the last tile row
     for (int algo : algos) {
