@@ -163,6 +163,9 @@ WGRAD_WINNERS = {(6400, 1600): 250, (1600, 1600): 245}
 # slice-major lockstep order (one token window per XCD at a time) for run counts
 # that are a whole number of slices per tile (CAAMD_WGRAD_LOCKSTEP=0: stream-K order)
 WGRAD_LOCKSTEP = os.environ.get("CAAMD_WGRAD_LOCKSTEP", "1") == "1"
+# lockstep slabs combined by a separate reduce launch over all CUs (algo 15) instead
+# of by each tile's last-arriving slice (CAAMD_WGRAD_EXT=0: in-kernel combine)
+WGRAD_EXT = os.environ.get("CAAMD_WGRAD_EXT", "1") == "1"
 # extra entries for A/B runs: CAAMD_WGRAD_EXTRA="1600x6400:420,4800x1600:190"
 for _e in filter(None, os.environ.get("CAAMD_WGRAD_EXTRA", "").split(",")):
     _shape, _runs = _e.split(":")
@@ -204,8 +207,9 @@ def run_sk(a, b, c, layout: int, accumulate: bool, runs: Optional[int] = None):
         runs = sk_runs(M, N, K, c.device)
     ws, cnt = _workspace(c.device, 2 * runs * 256 * 320, tiles)
     slices = runs // tiles if WGRAD_LOCKSTEP and runs % tiles == 0 and runs > tiles else 0
+    algo = 15 if (slices > 1 and WGRAD_EXT) else 5
     kernels().gemm_bf16(a, b, c, layout, EPI_BF16_ACC if accumulate else EPI_BF16, 256, 320, None, None,
-                        None, None, 1, None, accumulate, 5, ws, cnt, slices, runs)
+                        None, None, 1, None, accumulate, algo, ws, cnt, slices, runs)
     return c
 
 

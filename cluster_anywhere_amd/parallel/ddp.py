@@ -58,6 +58,7 @@ class BucketedDDP:
         self.buckets: List[_Bucket] = []
         self._hooks = []
         self._next = 0
+        self._signaled = set()
         if self.world == 1:
             return
         if broadcast_init:
@@ -99,6 +100,7 @@ class BucketedDDP:
             b.handle = None
             b.launched = False
         self._next = 0
+        self._signaled = set()
 
     def _launch_ready(self):
         while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
@@ -112,8 +114,13 @@ class BucketedDDP:
 
     def _on_grad(self, p):
         bi = self._owner.get(id(p))
-        if bi is None:
+        if bi is None or id(p) in self._signaled:
+            # a fused op signals its parameter directly AND torch still fires the
+            # post-accumulate-grad hook for it (its Function returned None): count
+            # each parameter once per step, or a bucket launches before the rest
+            # of its gradients exist
             return
+        self._signaled.add(id(p))
         self.buckets[bi].pending -= 1
         self._launch_ready()
 

@@ -108,6 +108,7 @@ class Zero1Reducer:
             max_grad_norm=max_grad_norm,
         )
         self._next = 0
+        self._signaled = set()
         self._hooks = [s.param.register_post_accumulate_grad_hook(self._on_grad) for s in slots]
         for s in slots:
             s.param._ca_grad_ready = self._on_grad
@@ -145,6 +146,7 @@ class Zero1Reducer:
         for b in self.buckets:
             b.pending, b.handle, b.launched = b.nparams, None, False
         self._next = 0
+        self._signaled = set()
 
     def _launch_ready(self):
         while self._next < len(self.buckets) and self.buckets[self._next].pending <= 0:
@@ -159,7 +161,10 @@ class Zero1Reducer:
 
     def _on_grad(self, p):
         bi = self._owner.get(id(p))
-        if bi is not None:
+        if bi is not None and id(p) not in self._signaled:
+            # once per parameter per step (a fused op's direct signal is followed by
+            # torch's post-accumulate-grad hook for the same parameter)
+            self._signaled.add(id(p))
             self.buckets[bi].pending -= 1
             self._launch_ready()
 

@@ -830,7 +830,7 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
     TORCH_CHECK(algo % 10 == 9 && layout == 0 && bn % 128 == 0 && N % 128 == 0,
                 "gemm: packed B needs algo 9, layout 0 and 128-row-aligned tiles");
   TORCH_CHECK((bm == 256 && (bn == 256 || bn == 320)) || (bm == 128 && bn == 320), "gemm: tile");
-  if (algo == 5) {  // stream-K: ragged M allowed (8-aligned), bf16 / accumulate epilogues
+  if (algo == 5 || algo == 15) {  // stream-K / lockstep: ragged M allowed (8-aligned), bf16 / accumulate epilogues
     TORCH_CHECK(M % 8 == 0 && N % bn == 0 && K % 64 == 0, "gemm(stream-K): M%8, N%BN, K%64 must be 0");
     TORCH_CHECK(epi == 0 || epi == 1, "gemm(stream-K): bf16 epilogues only");
     TORCH_CHECK(layout == 2 && bm == 256 && bn == 320, "gemm(stream-K): layout 2 with 256 x 320 tiles");
@@ -882,7 +882,7 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   const int lda = (int)a.size(1), ldb = (int)b.size(1), ldc = (int)(epi == 5 ? N / 2 : N);
   float* twp = nullptr;
   int* tcp = nullptr;
-  if (algo == 5) {
+  if (algo == 5 || algo == 15) {
     const int64_t tiles = ((M + bm - 1) / bm) * (N / bn);
     const int64_t runs = tail_split;
     TORCH_CHECK(runs >= 1 && runs <= 4096, "gemm(stream-K): 1 <= runs <= 4096");
@@ -896,6 +896,7 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
     // tail_full > 0: lockstep split-K over tail_full slices, one run per (slice, tile)
     TORCH_CHECK(tail_full <= 0 || (runs == tiles * tail_full && K / 32 >= tail_full),
                 "gemm(stream-K lockstep): runs must be tiles x slices, slices <= K-steps");
+    TORCH_CHECK(algo != 15 || tail_full > 1, "gemm(algo 15): the external combine needs a lockstep split");
     twp = tail_ws->data_ptr<float>();
     tcp = tail_cnt->data_ptr<int>();
   } else if (tail_split > 1) {
@@ -918,7 +919,7 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   hipError_t e = caamd::gemm_launch((int)layout, ek, (int)bm, (int)bn, (const bf16*)a.data_ptr(),
                                     (const bf16*)b.data_ptr(), cp, bp, zp, zop, dbp, (int)M, (int)N,
                                     (int)K, lda, ldb, ldc, (int)splitk, (int)algo, cur_stream(),
-                                    (int)tail_full, (tail_split > 1 || algo == 5) ? (int)tail_split : 1, twp, tcp,
+                                    (int)tail_full, (tail_split > 1 || algo == 5 || algo == 15) ? (int)tail_split : 1, twp, tcp,
                                     bpack ? 1 : 0);
   TORCH_CHECK(e == hipSuccess, "gemm launch failed: ", hipGetErrorString(e));
   if (ek == 2) {

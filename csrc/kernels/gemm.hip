@@ -232,8 +232,26 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
       for (int r = 0; r < 8; ++r) bv[r] = (float)b8[r];
     }
   }
+  // the epilogue's global reads (dGELU: Z; accumulate: the previous C) for this
+  // half's rows, issued before the LDS staging so their latency overlaps it: loaded
+  // inside the row loop they serialise behind that loop's stores (C may alias Z for
+  // the compiler), one HBM round trip per row iteration
+  constexpr bool PRE = EPI == EPI_DGELU || EPI == EPI_BF16_ACC;
+  bf16x8_t pre[PRE ? RITERS : 1];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
+    if constexpr (PRE) {
+      if (tid < ACTIVE && !(ABL & 8)) {
+        const bf16* src = EPI == EPI_DGELU ? p.Z : (const bf16*)p.C;
+#pragma unroll
+        for (int it = 0; it < RITERS; ++it) {
+          const int ir = it * RG + rg;
+          const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
+          const int m = m0 + wr_ * (TM * 16) + h * (TMH * 16) + rem;
+          if (ir < HR && m < p.M) pre[it] = *reinterpret_cast<const bf16x8_t*>(src + (size_t)m * p.ldc + n);
+        }
+      }
+    }
     __syncthreads();  // image free
 #pragma unroll
     for (int i = 0; i < TMH; ++i) {
@@ -274,7 +292,8 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
       }
       continue;
     }
-    for (int it = 0; it < RITERS; ++it) {
+#pragma unroll
+    for (int it = 0; it < RITERS; ++it) {  // unrolled: pre[] stays in registers
       const int ir = it * RG + rg;
       if (ir >= HR) break;
       const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
@@ -290,7 +309,7 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
 #pragma unroll
         for (int r = 0; r < 8; ++r) o[r] = (bf16)f[r];
       } else if constexpr (EPI == EPI_BF16_ACC) {
-        bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>((bf16*)p.C + off);
+        const bf16x8_t prev = pre[it];
 #pragma unroll
         for (int r = 0; r < 8; ++r) o[r] = (bf16)(f[r] + (float)prev[r]);
       } else if constexpr (EPI == EPI_BIAS_GELU) {
@@ -302,7 +321,7 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
         }
         *reinterpret_cast<bf16x8_t*>(p.Zout + off) = z;
       } else if constexpr (EPI == EPI_DGELU) {
-        bf16x8_t z = *reinterpret_cast<const bf16x8_t*>(p.Z + off);
+        const bf16x8_t z = pre[it];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           o[r] = (bf16)(f[r] * gelu_tanh_grad((float)z[r]));
@@ -1121,6 +1140,18 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
 
     if (nk < nk_tile) {
       // ---- shared tile: publish, and combine if this is the last contributor -----
+      if (LS > 0 && p.algo == 15) {
+        // algo 15: every slice only publishes its slab; sk_reduce_kernel combines
+        // all tiles in its own launch over every CU (the in-kernel last-arriver
+        // combine leaves one workgroup per tile re-reading LS slabs at the end)
+        float* mine = p.tws + (size_t)g * (BM * BN);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+        continue;
+      }
       const long long t_first = (long long)tile * nk_tile;
       const int c0 = LS > 0 ? 0 : run_of(t_first), c1 = LS > 0 ? LS - 1 : run_of(tile_end - 1);
       constexpr int SLAB = BM * BN;
@@ -1169,6 +1200,50 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
     }
     epilogue_staged<BM, BN, TM, TN, EPI, 0>(p, acc, m0, n0, wr, wc, lane, smem, tid);
   }
+}
+
+// Combine of the lockstep weight-gradient slabs (algo 15): one thread per f32x4 of
+// a tile, the LS slices summed in slice order (same bits as the in-kernel
+// combine), rounded to bf16 as the staged epilogue does (+ the previous C for the
+// accumulate epilogue). Ragged M rows are skipped.
+template <int BM, int BN, bool ACC>
+__global__ __launch_bounds__(256) void sk_reduce_kernel(Args p, int LS) {
+  constexpr int WM = 2, WN = 4, TM = BM / WM / 16, TN = BN / WN / 16, SLAB = BM * BN;
+  const int T = p.tiles_m * p.tiles_n;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)T * (SLAB / 4)) return;
+  const int tile = (int)(idx / (SLAB / 4));
+  const int e = (int)(idx - (long long)tile * (SLAB / 4));
+  const int lane = e & 63;
+  int q = e >> 6;
+  const int j = q % TN;
+  q /= TN;
+  const int i = q % TM, wid = q / TM;
+  const int wr = wid >> 2, wc = wid & 3;
+  constexpr int GROUP_M = 8;  // tile -> (m0, n0) exactly as gemm_sk_kernel
+  const int group_sz = GROUP_M * p.tiles_n;
+  const int gq = tile / group_sz;
+  const int first_m = gq * GROUP_M;
+  const int gm = min(p.tiles_m - first_m, GROUP_M);
+  const int tin = tile - gq * group_sz;
+  const int m0 = (first_m + tin % gm) * BM, n0 = (tin / gm) * BN;
+  const int row = m0 + wr * (TM * 16) + i * 16 + (lane & 15);
+  const int col = n0 + wc * (TN * 16) + j * 16 + 4 * (lane >> 4);
+  if (row >= p.M) return;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < LS; ++k)
+    s += *reinterpret_cast<const f32x4*>(p.tws + ((size_t)k * T + tile) * SLAB + (size_t)e * 4);
+  bf16* out = (bf16*)p.C + (size_t)row * p.ldc + col;
+  bf16x4 o;
+  if constexpr (ACC) {
+    const bf16x4 prev = *reinterpret_cast<const bf16x4*>(out);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (bf16)((float)(bf16)s[r] + (float)prev[r]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (bf16)s[r];
+  }
+  *reinterpret_cast<bf16x4*>(out) = o;
 }
 
 // ================================================================================
@@ -1548,12 +1623,18 @@ static hipError_t launch_abl(const Args& a, hipStream_t st) {
   const int grid = a.tS > 1 ? a.tfull + (T - a.tfull) * a.tS : T * a.splitk;
   if (a.tS > 1 && !(a.algo % 10 >= 1 && a.algo % 10 <= 3) && a.algo != 5)
     return hipErrorInvalidValue;
-  if (a.algo == 5) {  // stream-K: the weight-gradient layout (TN) on 256 x 320 tiles only
+  if (a.algo == 5 || a.algo == 15) {  // stream-K / lockstep: the weight-gradient layout (TN), 256 x 320 tiles
     if constexpr ((EPI == EPI_BF16 || EPI == EPI_BF16_ACC) && BM == 256 && BN == 320 && !AK && !BK_) {
       auto k = gemm_sk_kernel<BM, BN, AK, BK_, EPI>;
       constexpr int lds = 4 * (BM + BN) * 32 * 2;
       ensure_lds((const void*)k, lds);
       hipLaunchKernelGGL(k, dim3(a.tS), dim3(NTHR), lds, st, a);  // tS = number of runs
+      if (a.algo == 15) {  // lockstep slabs combined by their own launch
+        if (a.tfull <= 0) return hipErrorInvalidValue;
+        const long long n4 = (long long)a.tiles_m * a.tiles_n * (BM * BN / 4);
+        hipLaunchKernelGGL((sk_reduce_kernel<BM, BN, EPI == EPI_BF16_ACC>), dim3((unsigned)((n4 + 255) / 256)),
+                           dim3(256), 0, st, a, a.tfull);
+      }
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
@@ -1641,7 +1722,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
                        int tfull, int tS, float* tws, int* tcnt, int bpack) {
   gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk,
-               algo == 5 ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt,
+               (algo == 5 || algo == 15) ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt,
                bpack};
   if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
   if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);

@@ -209,9 +209,9 @@ def test_gemm_k64_split_tail():
     assert _rel(c, c1) < 2e-3
 
 
-@pytest.mark.parametrize("lockstep", [True, False])
+@pytest.mark.parametrize("lockstep,ext", [(True, True), (True, False), (False, False)])
 @pytest.mark.parametrize("MN,runs", [((1600, 1600), 245), ((640, 960), 18), ((1600, 640), 56)])
-def test_wgrad_stream_k_and_lockstep(lockstep, MN, runs):
+def test_wgrad_stream_k_and_lockstep(lockstep, ext, MN, runs):
     """Weight-gradient kernel (algo 5, TN layout): dW (+)= dY^T X over 4096 tokens,
     ragged M (1600 = 6.25 x 256), stream-K order and the slice-major lockstep order
     (runs = tiles x slices, slices not dividing the 128 K-steps), overwrite and
@@ -222,8 +222,8 @@ def test_wgrad_stream_k_and_lockstep(lockstep, MN, runs):
     K = 4096
     dy, x = _mk((K, M), 31), _mk((K, N), 32)
     ref = dy.float().t() @ x.float()
-    old = G.WGRAD_LOCKSTEP
-    G.WGRAD_LOCKSTEP = lockstep
+    old = G.WGRAD_LOCKSTEP, G.WGRAD_EXT
+    G.WGRAD_LOCKSTEP, G.WGRAD_EXT = lockstep, ext
     try:
         c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         G.run_sk(dy, x, c, 2, False, runs)
@@ -236,4 +236,26 @@ def test_wgrad_stream_k_and_lockstep(lockstep, MN, runs):
         G.run_sk(dy, x, c3, 2, False, runs)  # tickets were reset by the last arrivers
         assert torch.equal(c, c3)
     finally:
-        G.WGRAD_LOCKSTEP = old
+        G.WGRAD_LOCKSTEP, G.WGRAD_EXT = old
+
+
+def test_wgrad_external_combine_matches_in_kernel_bits():
+    """algo 15 (lockstep slabs + separate reduce launch) gives the same bits as the
+    in-kernel last-arriver combine, for both the overwrite and accumulate epilogues."""
+    from cluster_anywhere_amd.ops import gemm as G
+
+    dy, x = _mk((8192, 1600), 41), _mk((8192, 1600), 42)
+    c0 = _mk((1600, 1600), 43)
+    out = {}
+    old = G.WGRAD_EXT
+    try:
+        for ext in (True, False):
+            G.WGRAD_EXT = ext
+            a = torch.empty(1600, 1600, device="cuda", dtype=torch.bfloat16)
+            G.run_sk(dy, x, a, 2, False, 245)
+            b = c0.clone()
+            G.run_sk(dy, x, b, 2, True, 245)
+            out[ext] = (a, b)
+    finally:
+        G.WGRAD_EXT = old
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])

@@ -44,21 +44,24 @@ def _run(port, q):
             signals = {}
             if st.zero:  # every parameter must signal "gradient final" exactly once per step
                 orig = st.reducer._on_grad
+                via = {}
 
-                def counted(p, orig=orig):
+                def counted(p, orig=orig, how="ready"):
                     signals[id(p)] = signals.get(id(p), 0) + 1
+                    via.setdefault(id(p), []).append(how)
                     orig(p)
 
                 for sl in st.flat.slots:
                     sl.param._ca_grad_ready = counted
                 for h in st.reducer._hooks:
                     h.remove()
-                st.reducer._hooks = [sl.param.register_post_accumulate_grad_hook(counted) for sl in st.flat.slots]
+                st.reducer._hooks = [sl.param.register_post_accumulate_grad_hook(
+                    lambda p: counted(p, how="hook")) for sl in st.flat.slots]
             losses = [float(st(x[:, :-1], x[:, 1:])) for x in data]
             st.wait_params()
             torch.cuda.synchronize()
             names = {id(sl.param): sl.name for sl in st.flat.slots}
-            bad = {names[k]: v for k, v in signals.items() if v != len(data)}
+            bad = {names[k]: "".join(h[0] for h in via[k]) for k, v in signals.items() if v != len(data)}
             missing = [sl.name for sl in st.flat.slots if id(sl.param) not in signals] if st.zero else []
             slots = [(sl.name, sl.offset, sl.numel) for sl in st.flat.slots]
             out[str(zero)] = (st.flat.param_buffer.float().cpu().numpy(), losses,

@@ -37,14 +37,17 @@ def main():
     from cluster_anywhere_amd.ops import gemm as G
 
     if a.ksweep:
-        for (M, N, runs) in ((1600, 1600, 245), (1600, 1600, 35), (6400, 1600, 250)):
-            for K in (8192, 16384, 32768):
+        for (M, N, runs) in ((1600, 1600, 245), (1600, 1600, 210), (6400, 1600, 250), (4800, 1600, 190)):
+            for K in (8192, 32768):
                 dy = torch.randn(K, M, device="cuda").bfloat16()
                 x = torch.randn(K, N, device="cuda").bfloat16()
                 c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-                med, mn = timeit(lambda: G.run_sk(dy, x, c, 2, False, runs), a.iters)
-                print(json.dumps({"M": M, "N": N, "K": K, "impl": "sk", "runs": runs, "us_med": round(med, 1),
-                                  "us_min": round(mn, 1), "pfs": round(2.0 * M * N * K / med / 1e9, 3)}), flush=True)
+                for ext in (True, False):
+                    G.WGRAD_EXT = ext
+                    med, mn = timeit(lambda: G.run_sk(dy, x, c, 2, True, runs), a.iters)
+                    print(json.dumps({"M": M, "N": N, "K": K, "impl": "sk", "runs": runs, "ext": ext,
+                                      "us_med": round(med, 1), "us_min": round(mn, 1),
+                                      "pfs": round(2.0 * M * N * K / med / 1e9, 3)}), flush=True)
         return
 
     K = a.tokens
