@@ -1621,7 +1621,7 @@ static hipError_t launch_abl(const Args& a, hipStream_t st) {
   using C_ = Cfg<BM, BN, AK, BK_>;
   const int T = a.tiles_m * a.tiles_n;
   const int grid = a.tS > 1 ? a.tfull + (T - a.tfull) * a.tS : T * a.splitk;
-  if (a.tS > 1 && !(a.algo % 10 >= 1 && a.algo % 10 <= 3) && a.algo != 5)
+  if (a.tS > 1 && !(a.algo % 10 >= 1 && a.algo % 10 <= 3) && a.algo != 5 && a.algo != 15)
     return hipErrorInvalidValue;
   if (a.algo == 5 || a.algo == 15) {  // stream-K / lockstep: the weight-gradient layout (TN), 256 x 320 tiles
     if constexpr ((EPI == EPI_BF16 || EPI == EPI_BF16_ACC) && BM == 256 && BN == 320 && !AK && !BK_) {
