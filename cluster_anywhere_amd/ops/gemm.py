@@ -282,7 +282,7 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: int = 0, *, algo: Optional[in
 # 64-row-interleaved gate/up weight and the residual adds of o / down in the
 # epilogues, so prefill keeps no second copy of the weights and no [M, 2F]
 # intermediate.
-PREFILL_ALGO = int(os.environ.get("CAAMD_PREFILL_ALGO", "4009"))
+PREFILL_ALGO = int(os.environ.get("CAAMD_PREFILL_ALGO", "9"))  # 256 x 256: four phases, DMA over two (tools/bench_prefill_gemm.py)
 
 
 def prefill_ok(M: int, N: int, K: int) -> bool:

@@ -236,13 +236,15 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
   // half's rows, issued before the LDS staging so their latency overlaps it: loaded
   // inside the row loop they serialise behind that loop's stores (C may alias Z for
   // the compiler), one HBM round trip per row iteration
-  constexpr bool PRE = EPI == EPI_DGELU || EPI == EPI_BF16_ACC;
+  // (dGELU only: for the accumulate epilogue the extra live registers pushed the
+  // stream-K weight-gradient kernel's main loop into scratch spills -- 3x slower)
+  constexpr bool PRE = EPI == EPI_DGELU;
   bf16x8_t pre[PRE ? RITERS : 1];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if constexpr (PRE) {
       if (tid < ACTIVE && !(ABL & 8)) {
-        const bf16* src = EPI == EPI_DGELU ? p.Z : (const bf16*)p.C;
+        const bf16* src = p.Z;
 #pragma unroll
         for (int it = 0; it < RITERS; ++it) {
           const int ir = it * RG + rg;
@@ -309,7 +311,7 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
 #pragma unroll
         for (int r = 0; r < 8; ++r) o[r] = (bf16)f[r];
       } else if constexpr (EPI == EPI_BF16_ACC) {
-        const bf16x8_t prev = pre[it];
+        const bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>((bf16*)p.C + off);
 #pragma unroll
         for (int r = 0; r < 8; ++r) o[r] = (bf16)(f[r] + (float)prev[r]);
       } else if constexpr (EPI == EPI_BIAS_GELU) {
@@ -1140,18 +1142,6 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
 
     if (nk < nk_tile) {
       // ---- shared tile: publish, and combine if this is the last contributor -----
-      if (LS > 0 && p.algo == 15) {
-        // algo 15: every slice only publishes its slab; sk_reduce_kernel combines
-        // all tiles in its own launch over every CU (the in-kernel last-arriver
-        // combine leaves one workgroup per tile re-reading LS slabs at the end)
-        float* mine = p.tws + (size_t)g * (BM * BN);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
-        continue;
-      }
       const long long t_first = (long long)tile * nk_tile;
       const int c0 = LS > 0 ? 0 : run_of(t_first), c1 = LS > 0 ? LS - 1 : run_of(tile_end - 1);
       constexpr int SLAB = BM * BN;
@@ -1166,6 +1156,10 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_sk_kernel(Args p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+      // algo 15: slices only publish; sk_reduce_kernel combines every tile in its own
+      // launch over all CUs (the last-arriver combine leaves one workgroup per tile
+      // re-reading LS slabs at the end: ~120 us of fixed cost at 1600 x 1600)
+      if (p.algo == 15) continue;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       lds_int* flag = (lds_int*)smem;
