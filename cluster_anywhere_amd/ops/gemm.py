@@ -207,7 +207,8 @@ def run_sk(a, b, c, layout: int, accumulate: bool, runs: Optional[int] = None):
         runs = sk_runs(M, N, K, c.device)
     ws, cnt = _workspace(c.device, 2 * runs * 256 * 320, tiles)
     slices = runs // tiles if WGRAD_LOCKSTEP and runs % tiles == 0 and runs > tiles else 0
-    algo = 15 if (slices > 1 and WGRAD_EXT) else 5
+    # (two slices: level with the in-kernel combine; 7 slices at 1600 x 1600: 225 vs 301 us)
+    algo = 15 if (slices > 2 and WGRAD_EXT) else 5
     kernels().gemm_bf16(a, b, c, layout, EPI_BF16_ACC if accumulate else EPI_BF16, 256, 320, None, None,
                         None, None, 1, None, accumulate, algo, ws, cnt, slices, runs)
     return c

@@ -89,8 +89,11 @@ int main(int argc, char** argv) {
       {"qkv_fwd", 32768, 4800, 1600, 0},  {"proj_fwd", 32768, 1600, 1600, 0}, {"fc_fwd", 32768, 6400, 1600, 3},
       {"fc2_fwd", 32768, 1600, 6400, 0},  {"qkv_dgrad", 32768, 1600, 4800, 0}, {"fc2_dgrad", 32768, 6400, 1600, 4},
       {"fc_fwd_plain", 32768, 6400, 1600, 0},
+      // Llama-3-8B prefill at 16384 tokens (256 x 256 tiles)
+      {"pf_qkv", 16384, 6144, 4096, 0},   {"pf_o", 16384, 4096, 4096, 0},      {"pf_gate_up", 16384, 28672, 4096, 0},
+      {"pf_down", 16384, 4096, 14336, 0},
   };
-  const size_t maxA = (size_t)32768 * 6400, maxB = (size_t)6400 * 6400, maxC = (size_t)32768 * 6400;
+  const size_t maxA = (size_t)16384 * 14336, maxB = (size_t)28672 * 4096, maxC = (size_t)16384 * 28672;
   bf16 *A, *B, *C, *Z, *Zo, *bias;
   float *dbias, *ref, *tws;
   int* tcnt;
@@ -117,18 +120,21 @@ int main(int argc, char** argv) {
 
   for (const Shape& s : shapes) {
     if (*filter && !strstr(s.name, filter)) continue;
-    const int bm = 256, bn = (s.N % 320 == 0) ? 320 : 256;
-    const int tiles = (s.M / bm) * (s.N / bn);
-    int tfull = tiles, tS = 1;
-    if (s.K >= 4096) caamd::gemm_tail_plan(tiles, s.K, 32, cus, 4, &tfull, &tS);
+    const int bm = 256, bn0 = (s.N % 320 == 0) ? 320 : 256;
+    // algo 20 (four-wave kernel): 256 x 256 tiles, no split-K tail
     auto launch = [&](int algo) {
+      const int bn = algo == 20 ? 256 : bn0;
+      const int tiles = (s.M / bm) * (s.N / bn);
+      int tfull = tiles, tS = 1;
+      if (s.K >= 4096 && algo != 20) caamd::gemm_tail_plan(tiles, s.K, algo % 10 == 9 ? 64 : 32, cus, 4, &tfull, &tS);
       return caamd::gemm_launch(0, s.epi, bm, bn, A, B, C, s.epi == 4 ? nullptr : bias, s.epi == 4 ? Z : nullptr,
                                 s.epi == 3 ? Zo : nullptr, s.epi == 4 ? dbias : nullptr, s.M, s.N, s.K, s.K, s.K,
                                 s.N, 1, algo, 0, tfull, tS, tws, tcnt, 0);
     };
     // ---- numerics: first RR rows and a block of rows in the last tile row
     for (int algo : algos) {
-      if ((algo / 10) % 100) continue;  // timing ablations compute garbage by design
+      if ((algo / 10) % 100 && algo != 20) continue;  // timing ablations compute garbage by design
+      if (algo == 20 && s.N % 256) continue;
       CK(hipMemset(dbias, 0, 8192 * 4));
       CK(hipMemset(C, 0, (size_t)s.M * s.N * 2));
       CK(launch(algo));
@@ -160,13 +166,16 @@ int main(int argc, char** argv) {
       }
     }
     // ---- timing: rounds x (every algo: iters launches), interleaved
-    std::vector<std::vector<float>> ts(algos.size());
-    for (int algo : algos) CK(launch(algo));
+    std::vector<int> run;
+    for (int algo : algos)
+      if (!(algo == 20 && s.N % 256)) run.push_back(algo);
+    std::vector<std::vector<float>> ts(run.size());
+    for (int algo : run) CK(launch(algo));
     CK(hipDeviceSynchronize());
     for (int r = 0; r < rounds; ++r) {
-      for (size_t a = 0; a < algos.size(); ++a) {
+      for (size_t a = 0; a < run.size(); ++a) {
         CK(hipEventRecord(e0, 0));
-        for (int i = 0; i < iters; ++i) CK(launch(algos[a]));
+        for (int i = 0; i < iters; ++i) CK(launch(run[a]));
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -175,13 +184,13 @@ int main(int argc, char** argv) {
       }
     }
     const double fl = 2.0 * s.M * s.N * s.K;
-    for (size_t a = 0; a < algos.size(); ++a) {
+    for (size_t a = 0; a < run.size(); ++a) {
       std::vector<float> v = ts[a];
       std::sort(v.begin(), v.end());
       const float med = v[v.size() / 2], mn = v[0];
       printf("{\"shape\": \"%s\", \"M\": %d, \"N\": %d, \"K\": %d, \"epi\": %d, \"algo\": %d, \"us_med\": %.1f, "
              "\"us_min\": %.1f, \"pfs_med\": %.3f}\n",
-             s.name, s.M, s.N, s.K, s.epi, algos[a], med, mn, fl / med / 1e9);
+             s.name, s.M, s.N, s.K, s.epi, run[a], med, mn, fl / med / 1e9);
       fflush(stdout);
     }
   }
