@@ -1578,272 +1578,14 @@ static hipError_t launch_k64(const Args& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-// ================================================================================
-// Four-wave kernel (algo 20; NT layout, 256 x 256 tiles, BK = 64): one 256-thread
-// workgroup per CU, each wave a 128 x 128 quarter of the tile (64 accumulator
-// blocks of 16 x 16 = 256 registers, held in AGPRs: one wave per SIMD owns the
-// whole 512-entry register file). Against the 8-wave kernels (128 x 80 per wave)
-// a wave reads (1/128 + 1/128) instead of (1/128 + 1/80) bytes of LDS fragments per
-// MAC (-23 %), and the schedule is software-pipelined inside the wave instead of
-// ping-ponged between two waves of a SIMD:
-//   ... MFMAs(k-sub 0 of t)          | frag reads of k-sub 1 in flight
-//   lgkmcnt(0), vmcnt(0), barrier    | t+1's LDS image complete, t's image free
-//   frag reads of k-sub 0 of t+1, DMA of t+2 into t's buffer
-//   MFMAs(k-sub 1 of t)              | both in flight
-// so neither the fragment reads nor the LDS-DMA issue sit between barriers and
-// MFMAs. Same K-major swizzled LDS images, XCD-aware tile order and packed-B
-// option as the full-line kernel.
-// ================================================================================
-template <int EPI>
-__device__ __forceinline__ void w4_epilogue(const Args& p, f32x4 (&acc)[8][8], int m0, int n0, int wr, int wc,
-                                            int lane, lds_char* smem, int tid) {
-  constexpr int BN = 256, ROWB = BN * 2 + 16, HR = 128, CPR = BN / 8, NT = 256, RG = NT / CPR;  // RG = 8
-  constexpr int RITERS = HR / RG;                                                                // 16
-  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-  typedef __attribute__((address_space(3))) const bf16x8_t lds_bf16x8;
-  const int mrow = lane & 15, ncol = 4 * (lane >> 4);
-  const int c = tid % CPR, rg = tid / CPR;
-  const int n = n0 + c * 8;
-  float bv[8], dsum[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) bv[r] = dsum[r] = 0.f;
-  if constexpr (EPI == EPI_BF16 || EPI == EPI_BF16_ACC || EPI == EPI_BIAS_GELU) {
-    if (p.bias) {
-      const bf16x8_t b8 = *reinterpret_cast<const bf16x8_t*>(p.bias + n);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) bv[r] = (float)b8[r];
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    // image rows: wave row wr's m-half h -> rows [wr * 64, wr * 64 + 64)
-    bf16x8_t zpre[EPI == EPI_DGELU ? RITERS : 1];
-    if constexpr (EPI == EPI_DGELU) {
-#pragma unroll
-      for (int it = 0; it < RITERS; ++it) {
-        const int ir = it * RG + rg;
-        const int m = m0 + (ir >> 6) * 128 + h * 64 + (ir & 63);
-        zpre[it] = *reinterpret_cast<const bf16x8_t*>(p.Z + (size_t)m * p.ldc + n);
-      }
-    }
-    __syncthreads();  // image free
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ir = wr * 64 + i * 16 + mrow;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int nc = wc * 128 + j * 16 + ncol;
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[h * 4 + i][j][r];
-        *(lds_bf16x4*)(smem + ir * ROWB + nc * 2) = o;
-      }
-    }
-    __syncthreads();
-    if constexpr (EPI == EPI_SWIGLU) {
-      if (!((c >> 3) & 1)) {
-        const int on = (n0 >> 1) + (c >> 4) * 64 + (c & 7) * 8;
-#pragma unroll
-        for (int it = 0; it < RITERS; ++it) {
-          const int ir = it * RG + rg;
-          const int m = m0 + (ir >> 6) * 128 + h * 64 + (ir & 63);
-          const bf16x8_t g = *(lds_bf16x8*)(smem + ir * ROWB + c * 16);
-          const bf16x8_t u = *(lds_bf16x8*)(smem + ir * ROWB + (c + 8) * 16);
-          bf16x8_t o;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const float gf = (float)g[r];
-            o[r] = (bf16)(__fdividef(gf, 1.f + __expf(-gf)) * (float)u[r]);
-          }
-          *reinterpret_cast<bf16x8_t*>((bf16*)p.C + (size_t)m * p.ldc + on) = o;
-        }
-      }
-      continue;
-    }
-#pragma unroll
-    for (int it = 0; it < RITERS; ++it) {
-      const int ir = it * RG + rg;
-      const int m = m0 + (ir >> 6) * 128 + h * 64 + (ir & 63);
-      const bf16x8_t v = *(lds_bf16x8*)(smem + ir * ROWB + c * 16);
-      const size_t off = (size_t)m * p.ldc + n;
-      float f[8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) f[r] = (float)v[r] + bv[r];
-      bf16x8_t o;
-      if constexpr (EPI == EPI_BF16) {
-#pragma unroll
-        for (int r = 0; r < 8; ++r) o[r] = (bf16)f[r];
-      } else if constexpr (EPI == EPI_BF16_ACC) {
-        const bf16x8_t prev = *reinterpret_cast<const bf16x8_t*>((bf16*)p.C + off);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) o[r] = (bf16)(f[r] + (float)prev[r]);
-      } else if constexpr (EPI == EPI_BIAS_GELU) {
-        bf16x8_t z;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          z[r] = (bf16)f[r];
-          o[r] = (bf16)gelu_tanh((float)z[r]);
-        }
-        *reinterpret_cast<bf16x8_t*>(p.Zout + off) = z;
-      } else if constexpr (EPI == EPI_DGELU) {
-        const bf16x8_t z = zpre[it];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          o[r] = (bf16)(f[r] * gelu_tanh_grad((float)z[r]));
-          dsum[r] += (float)o[r];
-        }
-      }
-      *reinterpret_cast<bf16x8_t*>((bf16*)p.C + off) = o;
-    }
-  }
-  if constexpr (EPI == EPI_DGELU) {
-    typedef __attribute__((address_space(3))) float lds_float;
-    lds_float* red = (lds_float*)smem;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 8; ++r) red[rg * (CPR * 8) + c * 8 + r] = dsum[r];
-    __syncthreads();
-    for (int col = tid; col < CPR * 8; col += NT) {
-      float t = 0.f;
-#pragma unroll
-      for (int g = 0; g < RG; ++g) t += red[g * (CPR * 8) + col];
-      atomicAdd(p.dbias + n0 + col, t);
-    }
-  }
-}
-
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_w4_kernel(Args p) {
-  constexpr int BM = 256, BN = 256, NT = 256;
-  constexpr int A_ST = BM * 128, B_ST = BN * 128, ST = A_ST + B_ST;  // 64 KiB per K-tile
-  constexpr int NA = A_ST / (NT * 16), NB = B_ST / (NT * 16);          // 8 + 8 DMA rounds
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  lds_char* smem = (lds_char*)smem_raw;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
-
-  int tile;
-  {
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int xcd = bid & 7, loc = bid >> 3, q = nwg >> 3, r = nwg & 7;
-    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
-  }
-  constexpr int GROUP_M = 8;
-  const int group_sz = GROUP_M * p.tiles_n;
-  const int g = tile / group_sz;
-  const int first_m = g * GROUP_M;
-  const int gm = min(p.tiles_m - first_m, GROUP_M);
-  const int tin = tile - g * group_sz;
-  const int m0 = (first_m + tin % gm) * BM, n0 = (tin / gm) * BN;
-  const int nk = p.K / 64;
-
-  // DMA: round j covers rows 32 j + (wid * 8 + lane / 8); every row's swizzle
-  // depends only on that lane part, so one lane offset per operand
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A + (size_t)m0 * p.lda, (unsigned)(BM * p.lda * 2));
-  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B + (size_t)n0 * p.ldb, (unsigned)(BN * p.ldb * 2));
-  const int lrow = wid * 8 + (lane >> 3);
-  const int lchunk = (lane & 7) ^ kswz(lrow);
-  const int voff_a = (lrow * p.lda + lchunk * 8) * 2;
-  const int bx = (lrow >> 1) & 7;
-  const bool bpk = p.bpack != 0;
-  const int voff_b = bpk ? lrow * 128 + (lchunk ^ (bx ^ ((bx & 1) << 2))) * 16 : (lrow * p.ldb + lchunk * 8) * 2;
-  const int slab_bytes = 128 * p.K * 2;
-  auto dma_tile = [&](int t) {
-    lds_char* base = smem + (t & 1) * ST;
-#pragma unroll
-    for (int j = 0; j < NA; ++j)
-      dma_lds16(ra, base + (j * NT + wid * 64) * 16, voff_a, t * 128 + j * 32 * p.lda * 2);
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-      dma_lds16(rb, base + A_ST + (j * NT + wid * 64) * 16, voff_b,
-                bpk ? (j >> 2) * slab_bytes + t * 16384 + (j & 3) * 4096 : t * 128 + j * 32 * p.ldb * 2);
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  bf16x8_t a0[8], b0[8], a1[8], b1[8];
-  // fragment i of k-sub ks of K-tile t (A rows / B rows of this wave)
-  auto rda = [&](int t, int ks, int i) {
-    return frag_kmaj(smem + (t & 1) * ST, wr * 128 + i * 16, ks, lane);
-  };
-  auto rdb = [&](int t, int ks, int j) {
-    return frag_kmaj(smem + (t & 1) * ST + A_ST, wc * 128 + j * 16, ks, lane);
-  };
-  // 8 MFMAs of accumulator row i; the next fragments' reads (and DMA rounds) are
-  // interleaved one row group at a time, so they overlap the matrix cores
-  auto mrow = [&](const bf16x8_t& af, const bf16x8_t (&bf)[8], int i) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af, acc[i][j], 0, 0, 0);
-  };
-
-  if (nk > 0) {
-    dma_tile(0);
-    if (nk > 1) dma_tile(1);
-    wait_vm<0>();
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a0[i] = rda(0, 0, i), b0[i] = rdb(0, 0, i);
-    for (int t = 0; t < nk; ++t) {
-      // ---- k-sub 0 of t; k-sub 1's fragments read underneath
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        a1[i] = rda(t, 1, i);
-        b1[i] = rdb(t, 1, i);
-        __builtin_amdgcn_sched_barrier(0);
-        mrow(a0[i], b0, i);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      wait_vm<0>();  // K-tile t+1 landed (issued a full K-tile ago)
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();  // every wave is past its reads of buffer t; t+1 visible
-      __builtin_amdgcn_sched_barrier(0);
-      // ---- k-sub 1 of t; k-sub 0 of t+1 read and t+2's DMA issued underneath
-      const bool nxt = t + 1 < nk, dm = t + 2 < nk;
-      lds_char* dbase = smem + (t & 1) * ST;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        if (nxt) {
-          a0[i] = rda(t + 1, 0, i);
-          b0[i] = rdb(t + 1, 0, i);
-        }
-        if (dm) {
-          dma_lds16(ra, dbase + (i * NT + wid * 64) * 16, voff_a, (t + 2) * 128 + i * 32 * p.lda * 2);
-          dma_lds16(rb, dbase + A_ST + (i * NT + wid * 64) * 16, voff_b,
-                    bpk ? (i >> 2) * slab_bytes + (t + 2) * 16384 + (i & 3) * 4096
-                        : (t + 2) * 128 + i * 32 * p.ldb * 2);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mrow(a1[i], b1, i);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  w4_epilogue<EPI>(p, acc, m0, n0, wr, wc, lane, smem, tid);
-}
-
-template <int EPI>
-static hipError_t launch_w4(const Args& a, hipStream_t st) {
-  if (a.splitk != 1 || a.tS > 1) return hipErrorInvalidValue;
-  auto k = gemm_w4_kernel<EPI>;
-  constexpr int lds = 2 * (256 + 256) * 128;
-  ensure_lds((const void*)k, lds);
-  hipLaunchKernelGGL(k, dim3(a.tiles_m * a.tiles_n), dim3(256), lds, st, a);
-  return hipGetLastError();
-}
+// (A four-wave 256 x 256 variant -- 128 x 128 per wave in AGPRs, one wave per SIMD,
+// fragment reads and DMA software-pipelined under the MFMAs -- measured 12-18 % slower
+// than the full-line kernel on the prefill shapes (qkv 688 vs 611 us, o 474 vs 402 us
+// at 16384 tokens): with one wave per SIMD nothing covers the per-K-tile barrier.
+// Removed in round 4.)
 
 template <int BM, int BN, bool AK, bool BK_, int EPI>
 static hipError_t launch_t(const Args& a, hipStream_t st) {
-  if (a.algo == 20) {  // four-wave kernel: NT, 256 x 256, no split-K
-    if constexpr (BM == 256 && BN == 256 && AK && BK_ && EPI != EPI_F32) return launch_w4<EPI>(a, st);
-    return hipErrorInvalidValue;
-  }
   if (a.bpack && a.algo % 10 != 9) return hipErrorInvalidValue;
   // SwiGLU: staged epilogue of the ping-pong (2) and full-line (9) kernels only
   if (EPI == EPI_SWIGLU && (a.splitk != 1 || !(a.algo % 10 == 9 || a.algo == 2))) return hipErrorInvalidValue;
