@@ -300,7 +300,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
   // one 64-key tile; need_mask (wave-uniform): causal diagonal / sequence tail.
   // The mask compares kb*32 + crow(i, h) (an immediate + 4h) against one
   // per-lane limit, so the unmasked tiles carry no index arithmetic.
-  auto tile = [&](bool need_mask, const lds_t* kimg, unsigned vimg, int k0) {
+  auto tile = [&](auto need_mask_c, const lds_t* kimg, unsigned vimg, int k0) {
+    // compile-time: the unmasked tiles (all but the diagonal / tail ones) carry no
+    // compare / select code (as a runtime flag the compiler predicated it onto every tile)
+    constexpr bool need_mask = decltype(need_mask_c)::value;
     typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
     f32x16 sacc[QS][2];
     // the four K fragments of each 32-key half in flight at once (one LDS latency)
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
     });
 #pragma unroll
     for (int qs = 0; qs < QS; ++qs) {
-      if (need_mask) {
+      if constexpr (need_mask) {
         const int q = q0w + qs * 32 + r;
         const int lim = (causal ? min(q, T - 1) : T - 1) - k0 - 4 * h;
 #pragma unroll
@@ -401,7 +404,10 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
   };
 
   const unsigned smem_u = (unsigned)(size_t)smem;
-  for (int kt = 0; kt < nkt; ++kt) {
+  // key tiles [0, mfirst) are below every query of the block (no mask); the causal
+  // diagonal and a partial last tile run the masked tile body in their own loop (a
+  // runtime mask flag was predicated onto every tile)
+  auto iter = [&](int kt, auto mask_c) {
     const int k0 = kt * 64;
     const int st = kt % 3;
     const lds_t* kimg = smem + st * STAGE;
@@ -413,13 +419,19 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
       dma_tile<NT>(vbase, krs, k0 + 128, T, nb + IMG, wave, lane);
     }
     const bool active = !(causal && k0 > q0w + 32 * QS - 1) && q0w < T && !(ABL & 8);  // wave-uniform
-    if (active) {
-      tile((causal && k0 + 63 > q0w) || (k0 + 64 > T), kimg, vimg, k0);
-    }
+    if (active) tile(mask_c, kimg, vimg, k0);
     if constexpr (!(ABL & 2)) {
       wait_next<DMA_N>(ahead);
       barrier_keep_dma();
     }
+  };
+  {
+    const int qblk0 = qb * QBLK;  // the block's first query
+    // first tile with k0 + 63 > (first query of any wave of the block)
+    const int mfirst = min(nkt, min(T / 64, causal ? (qblk0 >= 63 ? (qblk0 - 63) / 64 + 1 : 0) : nkt));
+    int kt = 0;
+    for (; kt < mfirst; ++kt) iter(kt, std::false_type{});
+    for (; kt < nkt; ++kt) iter(kt, std::true_type{});
   }
 #pragma unroll
   for (int qs = 0; qs < QS; ++qs) {
@@ -539,7 +551,10 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
   wait_dma();
   __syncthreads();
 
-  auto tile = [&](bool need_mask, const lds_t* kimg, unsigned kimg_u, int k0) {
+  auto tile = [&](auto need_mask_c, const lds_t* kimg, unsigned kimg_u, int k0) {
+    // compile-time: the unmasked tiles (all but the diagonal / tail ones) carry no
+    // compare / select code (as a runtime flag the compiler predicated it onto every tile)
+    constexpr bool need_mask = decltype(need_mask_c)::value;
     typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
     static_for<2>([&](auto kb_c) {
       constexpr int kb = decltype(kb_c)::value;
@@ -576,7 +591,7 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
       for (int qs = 0; qs < QS; ++qs) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sacc[qs][i] = fexp2(__builtin_fmaf(sacc[qs][i], scale_log2, -lse2[qs]));
-        if (need_mask) {
+        if constexpr (need_mask) {
           const int q = q0w + qs * 32 + r;
           const int lim = (q >= T ? -1 : (causal ? min(q, T - 1) : T - 1)) - k0 - 4 * h;
 #pragma unroll
@@ -603,7 +618,9 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
   };
 
   const unsigned smem_u = (unsigned)(size_t)smem;
-  for (int kt = 0; kt < nkt; ++kt) {
+  // unmasked key tiles first, then the causal diagonal / partial last tile with the
+  // masked body (as in the forward)
+  auto iter = [&](int kt, auto mask_c) {
     const int k0 = kt * 64;
     const int st = kt % 3;
     const bool ahead = kt + 2 < nkt;
@@ -613,9 +630,16 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
       dma_tile(vbase, rs, k0 + 128, T, nb + IMG, wave, lane);
     }
     if (!(causal && k0 > q0w + 32 * QS - 1) && q0w < T)  // wave-uniform
-      tile((causal && k0 + 63 > q0w) || (k0 + 64 > T), smem + st * STAGE, smem_u + st * STAGE, k0);
+      tile(mask_c, smem + st * STAGE, smem_u + st * STAGE, k0);
     wait_next<4>(ahead);
     barrier_keep_dma();
+  };
+  {
+    const int qblk0 = qb * QBLK;
+    const int mfirst = min(nkt, min(T / 64, causal ? (qblk0 >= 63 ? (qblk0 - 63) / 64 + 1 : 0) : nkt));
+    int kt = 0;
+    for (; kt < mfirst; ++kt) iter(kt, std::false_type{});
+    for (; kt < nkt; ++kt) iter(kt, std::true_type{});
   }
   if (dbias) {  // q-bias gradient: rows past T hold zeros (never-computed tiles)
     f32x16 sum[2];
@@ -713,7 +737,10 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
   // mask: query q0 + 4h + c (c = qh*32 + 8g + j, an immediate) is dropped when
   // c < key - q0 - 4h (causal) or c > T - 1 - q0 - 4h (tail). Lanes with key >= T
   // compute on zero K/V and are never stored.
-  auto tile = [&](bool need_mask, const lds_t* qimg, unsigned qimg_u, int q0) {
+  auto tile = [&](auto need_mask_c, const lds_t* qimg, unsigned qimg_u, int q0) {
+    // compile-time: the unmasked tiles (all but the diagonal / tail ones) carry no
+    // compare / select code (as a runtime flag the compiler predicated it onto every tile)
+    constexpr bool need_mask = decltype(need_mask_c)::value;
     typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
     const float* st = (const float*)(qimg + 2 * IMG);
     const int lo_lim = causal ? key - q0 - 4 * h : -0x7fffffff;
@@ -755,7 +782,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
           float p = fexp2(__builtin_fmaf(sacc[i], scale_log2, -l4[j]));
-          if (need_mask) {
+          if constexpr (need_mask) {
             const int c = qh * 32 + 8 * g + j;
             p = (c < lo_lim || c > hi_lim) ? 0.f : p;
           }
@@ -778,17 +805,27 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
   };
 
   const unsigned smem_u = (unsigned)(size_t)smem;
-  for (int qt = qt0; qt < nqt; ++qt) {
+  // One iteration per 64-query tile. Only the first two tiles of a key block (the
+  // causal diagonal) and a partial last tile need the mask: they run in their own
+  // loops with the masked tile body, the rest with the unmasked one (a runtime flag
+  // was predicated onto every tile: 96 compares / selects per tile).
+  auto iter = [&](int qt, auto mask_c) {
     const int q0 = qt * 64;
     const int stg = (qt - qt0) % 3;
     const bool ahead = qt + 2 < nqt;
     if (ahead) issue(qt + 2, smem + ((qt + 2 - qt0) % 3) * STAGE);
     if (!(causal && q0 + 63 < key0w) && key0w < T)  // wave-uniform
-      tile((causal && q0 < key0w + 31) || (q0 + 64 > T), smem + stg * STAGE, smem_u + stg * STAGE, q0);
+      tile(mask_c, smem + stg * STAGE, smem_u + stg * STAGE, q0);
     if (wave < 2) wait_next<5>(ahead);  // waves 0 / 1 also DMA the lse2 / delta rows
     else wait_next<4>(ahead);
     barrier_keep_dma();
-  }
+  };
+  const int nfull = T / 64;  // tiles entirely inside the sequence
+  const int pro = min(nqt, qt0 + (causal ? 2 : 0));
+  int qt = qt0;
+  for (; qt < pro; ++qt) iter(qt, std::true_type{});
+  for (; qt < nfull; ++qt) iter(qt, std::false_type{});
+  for (; qt < nqt; ++qt) iter(qt, std::true_type{});
   if (dbias) {  // k / v bias gradients (block-uniform; keys past T contribute zeros)
     __shared__ float red[256];
     f32x16 k2[2], v2[2];

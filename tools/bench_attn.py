@@ -15,7 +15,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cluster_anywhere_amd.ops._lib import kernels  # noqa: E402
 
 B, T, H, D = (int(v) for v in os.environ.get("ATTN_SHAPE", "32,1024,25,64").split(","))
-C = kernels()
+if os.environ.get("ATTN_SO"):  # another build of the extension (same-box A/B of kernel versions)
+    import importlib.machinery
+    import importlib.util
+
+    _ld = importlib.machinery.ExtensionFileLoader("caamd_ab._C", os.environ["ATTN_SO"])
+    _spec = importlib.util.spec_from_loader("caamd_ab._C", _ld)
+    C = importlib.util.module_from_spec(_spec)
+    _ld.exec_module(C)
+else:
+    C = kernels()
 qkv = torch.randn(B, T, 3 * H * D, device="cuda", dtype=torch.bfloat16)
 out, lse = C.flash_attn_fwd(qkv, H, True)
 dout = torch.randn_like(out)
