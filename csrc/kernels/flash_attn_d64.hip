@@ -860,48 +860,27 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
 
 void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int kv_rs, int group, bf16* out,
                      float* lse, int B, int T, int H, int causal, hipStream_t st) {
-  // CAAMD_FA64_QS: 32-query sub-blocks per wave (2: 256-query blocks at 2 waves
-  // per SIMD; 1: 128-query blocks at 3 waves per SIMD)
-  static const int qs = [] {
-    const char* e = std::getenv("CAAMD_FA64_QS");
-    return (e && e[0] == '2') ? 2 : 1;
-  }();
+  // 128-query blocks of four waves, three waves per SIMD. (256-query blocks -- two
+  // 32-query sub-blocks per wave, or eight waves per block -- measured slower,
+  // 267 vs 243 us at B32 T1024 H25, and were removed in round 4.)
   const float scale_log2 = 1.44269504089f / 8.f;
-  if (qs == 2) {
-    const int nqb = (T + 255) / 256;
-    hipLaunchKernelGGL(fa64::fwd_kernel<2>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs,
-                       kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
-  } else {
-    static const int abl = [] {
-      const char* e = std::getenv("CAAMD_FA64_ABL");
-      return e ? std::atoi(e) : 0;
-    }();
-    // CAAMD_FA64_FWD_WAVES=8: 256-query blocks of 8 waves (half the K/V re-reads,
-    // 4 waves per SIMD at 128 VGPRs) -- measured 267 vs 243 us at B32 T1024 H25, not default
-    static const int nw = [] {
-      const char* e = std::getenv("CAAMD_FA64_FWD_WAVES");
-      return (e && e[0] == '8') ? 8 : 4;
-    }();
-    if (nw == 8 && abl == 0) {
-      const int nqb = (T + 255) / 256;
-      hipLaunchKernelGGL((fa64::fwd_kernel<1, 0, 8>), dim3(B * H * nqb), dim3(512), 6 * fa64::IMG, st, q, k, v, q_rs,
-                         kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
-      return;
-    }
-    const int nqb = (T + 127) / 128;
-    auto kern = fa64::fwd_kernel<1, 0>;
-    switch (abl) {
-      case 1: kern = fa64::fwd_kernel<1, 1>; break;
-      case 2: kern = fa64::fwd_kernel<1, 2>; break;
-      case 3: kern = fa64::fwd_kernel<1, 3>; break;
-      case 4: kern = fa64::fwd_kernel<1, 4>; break;
-      case 7: kern = fa64::fwd_kernel<1, 7>; break;
-      case 8: kern = fa64::fwd_kernel<1, 8>; break;
-      default: break;
-    }
-    hipLaunchKernelGGL(kern, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs,
-                       kv_rs, group, out, lse, T, H, nqb, scale_log2, causal);
+  static const int abl = [] {  // development timing ablations (tools/gpu/attn_abl.sh)
+    const char* e = std::getenv("CAAMD_FA64_ABL");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int nqb = (T + 127) / 128;
+  auto kern = fa64::fwd_kernel<1, 0>;
+  switch (abl) {
+    case 1: kern = fa64::fwd_kernel<1, 1>; break;
+    case 2: kern = fa64::fwd_kernel<1, 2>; break;
+    case 3: kern = fa64::fwd_kernel<1, 3>; break;
+    case 4: kern = fa64::fwd_kernel<1, 4>; break;
+    case 7: kern = fa64::fwd_kernel<1, 7>; break;
+    case 8: kern = fa64::fwd_kernel<1, 8>; break;
+    default: break;
   }
+  hipLaunchKernelGGL(kern, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, q, k, v, q_rs, kv_rs, group, out, lse, T,
+                     H, nqb, scale_log2, causal);
 }
 
 // ws: 2 * B * H * T floats (delta, then lse * log2 e)
@@ -912,19 +891,9 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
   const float scale_log2 = 1.44269504089f * scale;
   float* delta = ws;
   float* lse2 = ws + (size_t)B * H * T;
-  static const int qs = [] {
-    const char* e = std::getenv("CAAMD_FA64_DQ_QS");
-    return (e && e[0] == '2') ? 2 : 1;
-  }();
-  if (qs == 2) {
-    const int nqb = (T + 255) / 256;
-    hipLaunchKernelGGL(fa64::bwd_dq_kernel<2>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout,
-                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
-  } else {
-    const int nqb = (T + 127) / 128;
-    hipLaunchKernelGGL(fa64::bwd_dq_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout,
-                       lse, delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
-  }
+  const int nqb = (T + 127) / 128;  // (a 256-query dQ block variant spilled and was removed in round 4)
+  hipLaunchKernelGGL(fa64::bwd_dq_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout, lse,
+                     delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
   hipLaunchKernelGGL(fa64::bwd_dkdv_kernel, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
                      lse2, delta, dqkv, T, H, nkb, scale_log2, scale, causal, dbias);
 }

@@ -467,6 +467,40 @@ void colsum_bf16_launch(const float* partial, int nrow, int ncol, int split, bf1
   colsum_bf16_launch_ld(partial, nrow, ncol, ncol, split, o0, o1, st, accumulate);
 }
 
+// The three column sums of the column-split LayerNorm backward in one launch:
+// partial [nrow][3D] -> dg = cols [0, D), db = [D, 2D) (overwritten), dxsum = [2D, 3D)
+// (accumulated into the residual producer's bias main-grad). Two launches before.
+__global__ __launch_bounds__(1024) void colsum3_bf16_kernel(const float* __restrict__ partial, int nrow, int D,
+                                                            bf16* __restrict__ dg, bf16* __restrict__ db,
+                                                            bf16* __restrict__ dxsum) {
+  __shared__ float red[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ncol = 3 * D;
+  const int c = blockIdx.x * 64 + lane;
+  float acc = 0.f;
+  if (c < ncol) {
+    int r = wave;
+    for (; r + 7 * 16 < nrow; r += 8 * 16) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = partial[(size_t)(r + u * 16) * ncol + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += t[u];
+    }
+    for (; r < nrow; r += 16) acc += partial[(size_t)r * ncol + c];
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < ncol) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) s += red[w][lane];
+    if (c < D) dg[c] = (bf16)s;
+    else if (c < 2 * D) db[c - D] = (bf16)s;
+    else dxsum[c - 2 * D] = (bf16)(s + (float)dxsum[c - 2 * D]);
+  }
+}
+
 template <int NV>
 static void ln_fwd_dispatch(const bf16* x, const bf16* r, bf16* s, const bf16* g, const bf16* b,
                             bf16* y, float* mean, float* rstd, int rows, int D, float eps,
@@ -564,8 +598,8 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
     else
       hipLaunchKernelGGL((ln_bwd_cs_kernel<2, false, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd,
                          dres, dx, partial, rows, D);
-    colsum_bf16_launch_ld(partial, nb, 2 * D, 3 * D, D, dg, db, st, 0);
-    colsum_bf16_launch_ld(partial + 2 * D, nb, D, 3 * D, D, dxsum, dxsum, st, 1);
+    hipLaunchKernelGGL(colsum3_bf16_kernel, dim3((3 * D + 63) / 64), dim3(1024), 0, st, partial, nb, D, dg, db,
+                       dxsum);
     return;
   }
   if (ln_bwd_cs_ok(D)) {
