@@ -193,6 +193,7 @@ struct Args {
   // per 128-row slab and 64-deep K-tile one contiguous swizzled 16 KiB image), so the
   // serving prefill reads the same weight copy as decode
   int bpack;
+  int group_m;  // algo 9: m-tiles per tile-order group (0: 8); a tuning knob (gemm_set_group_m)
 };
 
 // Output tile staged through LDS: the MFMA fragments (each lane: 4 columns of one
@@ -1339,7 +1340,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
       nsplit = 1;
     }
   }
-  constexpr int GROUP_M = 8;
+  const int GROUP_M = p.group_m > 0 ? p.group_m : 8;
   const int group_sz = GROUP_M * p.tiles_n;
   const int g = tile / group_sz;
   const int first_m = g * GROUP_M;
@@ -1717,13 +1718,16 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 }  // namespace gemm
 
 // Host entry: shapes are validated by the caller (bindings.cpp).
+static int g_group_m = 0;  // 0: the kernels' default tile-order group (8 m-tiles)
+void gemm_set_group_m(int g) { g_group_m = g; }
+
 hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
                        const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
                        int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
                        int tfull, int tS, float* tws, int* tcnt, int bpack) {
   gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk,
                (algo == 5 || algo == 15) ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt,
-               bpack};
+               bpack, g_group_m};
   if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
   if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);
   if (bm == 128 && bn == 320) return gemm::launch_epi<128, 320>(layout, epi, a, st);

@@ -23,6 +23,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st, int tfull, int tS,
                        float* tws, int* tcnt, int bpack);
 void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
+void gemm_set_group_m(int g);
 }  // namespace caamd
 using caamd::bf16;
 
@@ -82,6 +83,8 @@ int main(int argc, char** argv) {
   } else {
     algos = {2, 9, 1009, 3009};
   }
+  // argv[5] (optional): m-tiles per tile-order group of the full-line kernel
+  if (argc > 5) caamd::gemm_set_group_m(atoi(argv[5]));
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;

@@ -11,6 +11,8 @@ tail -3 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "FAILED|Error|error" $O/pytest
 timeout -k 10 300 python -u -m pytest tests/test_zero_gpu.py -x -v --timeout 240 --timeout-method thread > $O/zero.log 2>&1; zrc=$?
 echo "zero rc=$zrc"; grep -E "AssertionError|^E |passed|failed" $O/zero.log | head -20
 [ $zrc -eq 0 ] || [ $zrc -eq 1 ] || exit $zrc
+timeout -k 10 200 tools/gemm_lab/gemm_lab fc2_dgrad 10 5 2,4009 > $O/lab_dgelu.log 2>&1 || { echo "lab failed"; tail -5 $O/lab_dgelu.log; exit 1; }
+grep shape $O/lab_dgelu.log
 timeout -k 10 200 python -u tools/wgrad_bench.py --ksweep > $O/ksweep.jsonl 2> $O/ksweep.err || { echo "ksweep failed"; tail -5 $O/ksweep.err; exit 1; }
 cat $O/ksweep.jsonl
 A="--num-prompts 256 --max-num-seqs 128 --input-len 512 --output-len 128"
