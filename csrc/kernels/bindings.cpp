@@ -1031,7 +1031,8 @@ static void decode_gemm(const Tensor& x, const Tensor& w, Tensor& y, c10::option
   TORCH_CHECK(epi >= 0 && epi <= 2, "decode_gemm: epi 0, 1 or 2");
   const int64_t NY = epi == 2 ? N / 2 : N;
   TORCH_CHECK(y.size(0) == M && y.size(1) == NY && y.stride(1) == 1, "decode_gemm: y shape");
-  TORCH_CHECK(splits >= 1 && K % (64 * splits) == 0, "decode_gemm: K % (64 * splits) == 0");
+  TORCH_CHECK(splits >= 1 && K % 64 == 0 && (splits - 1) * ((K / 64 + splits - 1) / splits) < K / 64,
+              "decode_gemm: K % 64 == 0 and every split non-empty");
   const caamd::bf16* rp = nullptr;
   if (epi == 1) {
     TORCH_CHECK(residual.has_value(), "decode_gemm: residual epilogue needs a residual");
@@ -1076,7 +1077,8 @@ static void decode_gemm_qkv_rope(const Tensor& x, const Tensor& w, Tensor& y, Te
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && w.size(1) == K && w.is_contiguous(), "decode_gemm_qkv_rope: x, w");
   TORCH_CHECK(M >= 1 && M <= 128 && K % 64 == 0 && N == (H + 2 * KVH) * 128, "decode_gemm_qkv_rope: shapes");
   TORCH_CHECK(y.dim() == 2 && y.size(0) == M && y.size(1) == N && y.stride(1) == 1, "decode_gemm_qkv_rope: y");
-  TORCH_CHECK(splits >= 2 && K % (64 * splits) == 0, "decode_gemm_qkv_rope: 2 <= splits, K % (64 * splits) == 0");
+  TORCH_CHECK(splits >= 2 && K % 64 == 0 && (splits - 1) * ((K / 64 + splits - 1) / splits) < K / 64,
+              "decode_gemm_qkv_rope: 2 <= splits, K % 64 == 0, every split non-empty");
   TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= (N / 128) * splits * 16384,
               "decode_gemm_qkv_rope: partial workspace too small");
   TORCH_CHECK(cos_sin.dim() == 3 && cos_sin.size(1) == 64 && cos_sin.size(2) == 2, "decode_gemm_qkv_rope: cos_sin");

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
   const int slab = blockIdx.x, split = blockIdx.y;
   const int n0 = slab * BN;
   const int kb0 = split * p.kchunk;
-  const int nsteps = p.kchunk / KS;
+  const int nsteps = min(p.kchunk, p.K - kb0) / KS;  // the last split may be shorter (ragged split-K)
 
   auto issue_w = [&](int t) {
     lds_t* st = wring + (t % NWS) * IMG;
@@ -489,7 +489,7 @@ static void ensure_lds(const void* k, int bytes) {
 }  // namespace dg
 
 // Host entry (shapes validated by the binding): M <= 128, N % 128 == 0,
-// K % (64 * splits) == 0; part >= (N/128) * splits * 128*128 floats when splits > 1;
+// K % 64 == 0 and every split non-empty (dg_kchunk); part >= (N/128) * splits * 128*128 floats when splits > 1;
 // tick >= N/128 zeroed uints (left zeroed by every launch).
 template <int EPI, bool PK, int NWS, int NXS>
 static void launch_cfg(const dg::Args& a, dim3 grid, hipStream_t st) {
@@ -515,15 +515,26 @@ static int g_dg_ext = [] {
   return e ? atoi(e) : 1;
 }();
 
+// K range per split, in whole 64-k steps: ceil(steps / splits); the last split takes
+// the rest, so any split count with (splits - 1) * chunk < K works (e.g. 5 splits of
+// K = 4096 fill 240 of 256 CUs with the 48 qkv slabs, where 4 equal ones fill 192).
+// Returns 0 when some split would be empty.
+static int dg_kchunk(int K, int splits) {
+  if (K % dg::KS || splits < 1) return 0;
+  const int steps = K / dg::KS, per = (steps + splits - 1) / splits;
+  return (splits - 1) * per < steps ? per * dg::KS : 0;
+}
+
 // 0: last-arriver combine inside the GEMM; 1: separate dg_reduce_kernel launch
 void decode_gemm_config(int ext) { g_dg_ext = ext; }
 
 hipError_t decode_gemm_launch(int epi, const bf16* X, const bf16* W, bf16* Y, const bf16* R, float* part,
                               unsigned* tick, int M, int N, int K, int ldx, int ldy, int splits, bool packed,
                               float* ssp, float eps, hipStream_t st) {
-  if (M < 1 || M > 128 || N % dg::BN || splits < 1 || K % (dg::KS * splits)) return hipErrorInvalidValue;
+  const int kchunk = dg_kchunk(K, splits);
+  if (M < 1 || M > 128 || N % dg::BN || !kchunk) return hipErrorInvalidValue;
   const int ext = (splits > 1 && epi != dg::EPI_SWIGLU && g_dg_ext) ? 1 : 0;
-  dg::Args a{X, W, Y, R, part, tick, M, N, K, ldx, ldy, splits, K / splits, ext, ssp, eps};
+  dg::Args a{X, W, Y, R, part, tick, M, N, K, ldx, ldy, splits, kchunk, ext, ssp, eps};
   dim3 grid(N / dg::BN, splits);
   switch (epi * 2 + (packed ? 1 : 0)) {
     case 0: launch_one<dg::EPI_STORE, false>(a, grid, st); break;
@@ -551,9 +562,10 @@ hipError_t decode_gemm_qkv_rope_launch(const bf16* X, const bf16* W, bf16* Y, fl
                                        int ldx, int ldy, int splits, const float* cs, const int* pos,
                                        const int* slot, bf16* kc, bf16* vc, int H, int KVH, int BS,
                                        float* ssp, float eps, hipStream_t st) {
-  if (M < 1 || M > 128 || N % dg::BN || splits < 2 || K % (dg::KS * splits) || N != (H + 2 * KVH) * dg::BN)
+  const int kchunk = dg_kchunk(K, splits);
+  if (M < 1 || M > 128 || N % dg::BN || splits < 2 || !kchunk || N != (H + 2 * KVH) * dg::BN)
     return hipErrorInvalidValue;
-  dg::Args a{X, W, Y, nullptr, part, nullptr, M, N, K, ldx, ldy, splits, K / splits, 1, ssp, eps};
+  dg::Args a{X, W, Y, nullptr, part, nullptr, M, N, K, ldx, ldy, splits, kchunk, 1, ssp, eps};
   launch_one<dg::EPI_STORE, true>(a, dim3(N / dg::BN, splits), st);
   hipLaunchKernelGGL(dg::dg_reduce_rope_kernel, dim3(N / dg::BN, 8), dim3(256), 0, st, part, Y, M, ldy, splits, cs,
                      pos, slot, kc, vc, H, KVH, BS, (const float*)ssp, K, eps);

@@ -178,10 +178,12 @@ def test_decode_gemm_v3_epilogues(M, N, K, packed):
     assert torch.equal(L.unpack_decode_weight(L.pack_decode_weight(w)), w)
 
 
-@pytest.mark.parametrize("N,K,splits", [(6144, 4096, 4), (4096, 4096, 8), (4096, 14336, 8), (256, 512, 2)])
+@pytest.mark.parametrize("N,K,splits", [(6144, 4096, 4), (4096, 4096, 8), (4096, 14336, 8), (256, 512, 2),
+                                         (6144, 4096, 5), (4096, 14336, 9), (256, 640, 3)])
 def test_decode_gemm_reduce_launch_matches(N, K, splits):
     """Split-K combined by the separate reduce launch (decode_gemm_config(1)) gives
-    the same bits as the in-kernel last-arriver combine, store and residual epilogues."""
+    the same bits as the in-kernel last-arriver combine, store and residual epilogues;
+    the last three cases have a shorter last split (ragged split-K)."""
     torch.manual_seed(N + K)
     x = torch.randn(128, K, device="cuda", dtype=torch.bfloat16)
     w = L.pack_decode_weight(torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05)
