@@ -70,7 +70,11 @@ def test_hb_bohb_with_tunebohb(cluster, tmp_path):
 
 
 def test_pb2_explores_inside_bounds(cluster, tmp_path):
-    sched = tune.PB2(perturbation_interval=3, hyperparam_bounds={"q": [0.1, 3.0]}, seed=1)
+    # bottom half, checked every 2 iterations: a trial is ranked against whatever the
+    # others last reported, so under a loaded CI box (trials running one after another)
+    # a bottom-quartile check every 3 iterations could miss every time
+    sched = tune.PB2(perturbation_interval=2, hyperparam_bounds={"q": [0.1, 3.0]}, seed=1,
+                     quantile_fraction=0.5)
     grid = tune.Tuner(ckpt_trial, param_space={"q": tune.uniform(0.1, 1.0)},
                       tune_config=tune.TuneConfig(metric="acc", mode="max", scheduler=sched, num_samples=4),
                       run_config=tune.RunConfig(storage_path=str(tmp_path), name="pb2",
