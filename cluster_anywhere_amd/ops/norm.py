@@ -19,10 +19,16 @@ def ln_bias_fusion_ok(x: torch.Tensor) -> bool:
     return use_gpu_kernel(x) and x.dtype == torch.bfloat16 and bool(kernels().ln_bwd_dxsum_ok(x.shape[-1]))
 
 
+def _main_ok(mg, g) -> bool:
+    return (mg.dtype == torch.bfloat16 and mg.is_contiguous() and mg.numel() == g.numel()
+            and mg.device == g.device)
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, g, b, eps, res_bias=None):
         ctx.res_bias = res_bias
+        ctx.gb = (g, b)
         C = kernels()
         x = x.contiguous()
         if res is not None:
@@ -48,14 +54,20 @@ class _LayerNormFn(torch.autograd.Function):
         if dy is None:
             dy = torch.zeros_like(saved)
         rb = ctx.res_bias
-        if rb is not None:
-            # bias gradient of the residual branch's producer (its main-grad view)
-            dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres, rb.main_grad)
-            from .linear import _ready
+        from .linear import _ready
 
-            _ready(rb)
-        else:
-            dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres)
+        # the LayerNorm's own weight / bias gradients go straight into their main-grad
+        # views (flat DDP buffer) when both have one: no per-tensor accumulate launch
+        gm, bm = (getattr(p, "main_grad", None) for p in ctx.gb)
+        own = gm is not None and bm is not None and _main_ok(gm, g) and _main_ok(bm, g)
+        dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres,
+                                     rb.main_grad if rb is not None else None,
+                                     gm if own else None, bm if own else None)
+        if rb is not None:
+            _ready(rb)  # bias gradient of the residual branch's producer (its main-grad view)
+        if own:
+            for p in ctx.gb:
+                _ready(p)
         if ctx.has_res:
             return dx, dx, dg, db, None, None
         return dx, None, dg, db, None, None

@@ -14,7 +14,7 @@ typedef __bf16 bf16;
 void ln_fwd_launch(const bf16*, const bf16*, bf16*, const bf16*, const bf16*, bf16*, float*, float*,
                    int, int, float, hipStream_t);
 void ln_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, const float*, const bf16*,
-                   bf16*, float*, bf16*, bf16*, int, int, hipStream_t, bf16*);
+                   bf16*, float*, bf16*, bf16*, int, int, hipStream_t, bf16*, int);
 bool ln_bwd_dxsum_ok(int D);
 int ln_nv_for(int D);
 int ln_bwd_num_blocks(int rows);
@@ -143,7 +143,9 @@ std::vector<Tensor> layernorm_fwd(const Tensor& x, const c10::optional<Tensor>& 
 std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tensor& g,
                                   const Tensor& mean, const Tensor& rstd,
                                   const c10::optional<Tensor>& dres,
-                                  const c10::optional<Tensor>& dxsum) {
+                                  const c10::optional<Tensor>& dxsum,
+                                  const c10::optional<Tensor>& g_main,
+                                  const c10::optional<Tensor>& b_main) {
   CHECK_BF16(dy);
   CHECK_BF16(x);
   CHECK_BF16(g);
@@ -158,8 +160,23 @@ std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tenso
     TORCH_CHECK(dres->sizes() == x.sizes(), "layernorm_bwd: dres shape mismatch");
   }
   auto dx = at::empty_like(x);
-  auto dg = at::empty_like(g);
-  auto db = at::empty_like(g);
+  // g_main / b_main: the LayerNorm's own main-grad views; the column sums are added into
+  // them in the same launch and dg / db come back undefined (None)
+  const bool acc = g_main.has_value() && g_main->defined();
+  TORCH_CHECK(acc == (b_main.has_value() && b_main->defined()), "layernorm_bwd: g_main and b_main go together");
+  Tensor dg, db;
+  if (acc) {
+    for (const Tensor* t : {&*g_main, &*b_main}) {
+      CHECK_BF16(*t);
+      TORCH_CHECK(t->numel() == D && t->is_contiguous() && t->device() == x.device(),
+                  "layernorm_bwd: main grads must be contiguous [D] on the input's device");
+    }
+    dg = *g_main;
+    db = *b_main;
+  } else {
+    dg = at::empty_like(g);
+    db = at::empty_like(g);
+  }
   caamd::bf16* dxs = nullptr;
   if (dxsum.has_value() && dxsum->defined()) {
     CHECK_BF16(*dxsum);
@@ -171,12 +188,13 @@ std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& x, const Tenso
   if (rows > 0) {
     caamd::ln_bwd_launch(bp(dy), bp(x), bp(g), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                          bp_opt(dres), bp(dx), partial.data_ptr<float>(), bp(dg), bp(db), rows, D,
-                         cur_stream(), dxs);
+                         cur_stream(), dxs, acc ? 1 : 0);
     LAUNCH_CHECK();
-  } else {
+  } else if (!acc) {
     dg.zero_();
     db.zero_();
   }
+  if (acc) return {dx, Tensor(), Tensor()};
   return {dx, dg, db};
 }
 
@@ -1324,7 +1342,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("transpose_bf16", GUARDED(transpose_bf16));
   m.def("layernorm_fwd", GUARDED(layernorm_fwd));
   m.def("layernorm_bwd", GUARDED(layernorm_bwd), pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("g"),
-        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("dres"), pybind11::arg("dxsum") = pybind11::none());
+        pybind11::arg("mean"), pybind11::arg("rstd"), pybind11::arg("dres"), pybind11::arg("dxsum") = pybind11::none(),
+        pybind11::arg("g_main") = pybind11::none(), pybind11::arg("b_main") = pybind11::none());
   m.def("ln_bwd_dxsum_ok", [](int64_t D) { return caamd::ln_bwd_dxsum_ok((int)D); });
   m.def("ln_bwd_config", [](int variant, int max_blocks) {
     TORCH_CHECK(variant >= 0 && variant <= 3, "ln_bwd_config: variant must be 0-3");

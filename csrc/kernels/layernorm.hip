@@ -468,11 +468,12 @@ void colsum_bf16_launch(const float* partial, int nrow, int ncol, int split, bf1
 }
 
 // The three column sums of the column-split LayerNorm backward in one launch:
-// partial [nrow][3D] -> dg = cols [0, D), db = [D, 2D) (overwritten), dxsum = [2D, 3D)
-// (accumulated into the residual producer's bias main-grad). Two launches before.
+// partial [nrow][3D] -> dg = cols [0, D), db = [D, 2D) (overwritten, or accumulated into
+// the LayerNorm's own main-grads with acc_gb), dxsum = [2D, 3D) (accumulated into the
+// residual producer's bias main-grad). Two launches before.
 __global__ __launch_bounds__(1024) void colsum3_bf16_kernel(const float* __restrict__ partial, int nrow, int D,
                                                             bf16* __restrict__ dg, bf16* __restrict__ db,
-                                                            bf16* __restrict__ dxsum) {
+                                                            bf16* __restrict__ dxsum, int acc_gb) {
   __shared__ float red[16][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ncol = 3 * D;
@@ -495,8 +496,8 @@ __global__ __launch_bounds__(1024) void colsum3_bf16_kernel(const float* __restr
     float s = 0.f;
 #pragma unroll
     for (int w = 0; w < 16; ++w) s += red[w][lane];
-    if (c < D) dg[c] = (bf16)s;
-    else if (c < 2 * D) db[c - D] = (bf16)s;
+    if (c < D) dg[c] = (bf16)(acc_gb ? s + (float)dg[c] : s);
+    else if (c < 2 * D) db[c - D] = (bf16)(acc_gb ? s + (float)db[c - D] : s);
     else dxsum[c - 2 * D] = (bf16)(s + (float)dxsum[c - 2 * D]);
   }
 }
@@ -586,10 +587,11 @@ int ln_bwd_partial_rows(int rows, int D) {
 bool ln_bwd_dxsum_ok(int D) { return ln_bwd_cs_ok(D); }
 
 // dxsum (optional, cs path only; partial sized [rows][3D] then): bf16 vector += the
-// column sums of dx (accumulated into an existing main gradient).
+// column sums of dx (accumulated into an existing main gradient). acc_gb: dg / db are
+// the LayerNorm's main-grad views and take += (no separate accumulate launch per tensor).
 void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* mean,
                    const float* rstd, const bf16* dres, bf16* dx, float* partial, bf16* dg,
-                   bf16* db, int rows, int D, hipStream_t st, bf16* dxsum) {
+                   bf16* db, int rows, int D, hipStream_t st, bf16* dxsum, int acc_gb) {
   if (dxsum && ln_bwd_cs_ok(D)) {
     const int nb = ln_bwd_cs_blocks(rows);
     if (dres)
@@ -599,7 +601,7 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
       hipLaunchKernelGGL((ln_bwd_cs_kernel<2, false, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd,
                          dres, dx, partial, rows, D);
     hipLaunchKernelGGL(colsum3_bf16_kernel, dim3((3 * D + 63) / 64), dim3(1024), 0, st, partial, nb, D, dg, db,
-                       dxsum);
+                       dxsum, acc_gb);
     return;
   }
   if (ln_bwd_cs_ok(D)) {
@@ -611,7 +613,7 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
       else
         hipLaunchKernelGGL((ln_bwd_cs_kernel<2, false>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd, dres,
                            dx, partial, rows, D);
-      colsum_bf16_launch(partial, nb, 2 * D, D, dg, db, st, 0);
+      colsum_bf16_launch(partial, nb, 2 * D, D, dg, db, st, acc_gb);
       return;
     }
     if (dres)
@@ -620,7 +622,7 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
     else
       hipLaunchKernelGGL((ln_bwd_cs_kernel<LN_CS_RB, false>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd,
                          dres, dx, partial, rows, D);
-    colsum_bf16_launch(partial, nb, 2 * D, D, dg, db, st, 0);
+    colsum_bf16_launch(partial, nb, 2 * D, D, dg, db, st, acc_gb);
     return;
   }
   const int nblk = ln_bwd_num_blocks(rows);
@@ -630,7 +632,7 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
     case 4: ln_bwd_dispatch<4>(dy, x, g, mean, rstd, dres, dx, partial, nblk, rows, D, st); break;
     case 8: ln_bwd_dispatch<8>(dy, x, g, mean, rstd, dres, dx, partial, nblk, rows, D, st); break;
   }
-  colsum_bf16_launch(partial, nblk, 2 * D, D, dg, db, st, 0);
+  colsum_bf16_launch(partial, nblk, 2 * D, D, dg, db, st, acc_gb);
 }
 
 }  // namespace caamd

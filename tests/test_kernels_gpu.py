@@ -376,3 +376,27 @@ def test_layernorm_bwd_dxsum(C, with_res):
     assert torch.equal(dx, dx2) and torch.equal(dg, dg2) and torch.equal(db, db2)
     ref = dx.float().sum(0) + 0.5
     assert _rel(acc, ref) < 1e-2
+
+
+@pytest.mark.parametrize("with_dxsum", [False, True])
+def test_layernorm_bwd_into_main_grads(C, with_dxsum):
+    """g_main / b_main: the weight and bias gradients are added into the given bf16
+    main-grad vectors in the same launch (and come back as None); the result equals
+    the plain backward's dg / db added to the prior contents."""
+    torch.manual_seed(9)
+    rows, D = 777, 1600
+    x = torch.randn(rows, D, device="cuda").bfloat16()
+    g = (1 + 0.1 * torch.randn(D, device="cuda")).bfloat16()
+    b = torch.zeros(D, device="cuda").bfloat16()
+    y, mean, rstd, s = C.layernorm_fwd(x, None, g, b, 1e-5)
+    dy = torch.randn_like(x)
+    gm = torch.full((D,), 0.25, device="cuda").bfloat16()
+    bm = torch.full((D,), -0.5, device="cuda").bfloat16()
+    acc = torch.zeros(D, device="cuda").bfloat16() if with_dxsum else None
+    dx, dg, db = C.layernorm_bwd(dy, x, g, mean, rstd, None, acc, gm, bm)
+    assert dg is None and db is None
+    dx2, dg2, db2 = C.layernorm_bwd(dy, x, g, mean, rstd, None)
+    assert torch.equal(dx, dx2)
+    assert _rel(gm, dg2.float() + 0.25) < 1e-2 and _rel(bm, db2.float() - 0.5) < 1e-2
+    ref_g = ((x.float() - mean[:, None]) * rstd[:, None] * dy.float()).sum(0)
+    assert _rel(gm, ref_g + 0.25) < 2e-2 and _rel(bm, dy.float().sum(0) - 0.5) < 2e-2
