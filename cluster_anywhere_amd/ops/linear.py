@@ -31,6 +31,18 @@ from . import gemm as _g
 from ._lib import kernels, use_gpu_kernel
 
 
+_DBIAS_ACC: dict = {}
+
+
+def _dbias_acc(dev, n: int) -> torch.Tensor:
+    """Zeroed fp32 accumulator of ``n`` floats per device (left zeroed by drain_f32_)."""
+    key = (dev, n)
+    t = _DBIAS_ACC.get(key)
+    if t is None:
+        t = _DBIAS_ACC[key] = torch.zeros(n, device=dev, dtype=torch.float32)
+    return t
+
+
 def _ready(p):
     h = getattr(p, "_ca_grad_ready", None)
     if h is not None:
@@ -130,11 +142,20 @@ class _MainGradMLP(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         gw2 = _wgrad(w2, dy2, u, ctx.needs_input_grad[3])
         gb2 = _bgrad(b2, dy2, ctx.needs_input_grad[4])
-        db1 = torch.zeros(w1.shape[0], device=dy2.device, dtype=torch.float32)
+        bmg = getattr(b1, "main_grad", None)
+        drain = (bmg is not None and bmg.dtype == torch.bfloat16 and bmg.is_contiguous()
+                 and bmg.device == dy2.device)
+        # the epilogue adds its bias-gradient column sums atomically into an fp32 vector:
+        # a persistent zeroed one that drain_f32_ empties into the main gradient (one
+        # launch), else a fresh zeros() converted below
+        db1 = (_dbias_acc(dy2.device, w1.shape[0]) if drain
+               else torch.zeros(w1.shape[0], device=dy2.device, dtype=torch.float32))
         dz = _g.dgrad_dgelu(dy2, _wt(w2), z, db1)
         gb1 = None
-        bmg = getattr(b1, "main_grad", None)
-        if bmg is not None:
+        if drain:
+            kernels().drain_f32_(db1, bmg)
+            _ready(b1)
+        elif bmg is not None:
             bmg.add_(db1.to(bmg.dtype))
             _ready(b1)
         elif ctx.needs_input_grad[2]:

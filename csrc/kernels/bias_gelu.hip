@@ -115,6 +115,21 @@ __global__ __launch_bounds__(256) void rowsum_partial_kernel(const bf16* __restr
   for (int j = 0; j < 8; ++j) p[j] = acc[j];
 }
 
+// dst (bf16 main gradient) += src (fp32 accumulator, e.g. the dGELU GEMM epilogue's
+// atomic bias-gradient sums), then src = 0 for its next use: one launch in place of
+// zero-fill + convert + add.
+__global__ __launch_bounds__(256) void drain_f32_kernel(float* __restrict__ src, bf16* __restrict__ dst, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    dst[i] = (bf16)((float)dst[i] + src[i]);
+    src[i] = 0.f;
+  }
+}
+
+void drain_f32_launch(float* src, bf16* dst, int n, hipStream_t st) {
+  hipLaunchKernelGGL(drain_f32_kernel, dim3((n + 255) / 256), dim3(256), 0, st, src, dst, n);
+}
+
 void bias_grad_launch(const bf16* dy, float* partial, bf16* out, int rows, int N, int accumulate,
                       hipStream_t st) {
   const int ncv = N / 8;

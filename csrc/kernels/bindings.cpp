@@ -243,6 +243,21 @@ std::vector<Tensor> bias_gelu_bwd(const Tensor& dy, const Tensor& h,
 // ---- bias gradient (column sum of dy), optionally accumulated in place -----------
 namespace caamd {
 void bias_grad_launch(const bf16*, float*, bf16*, int, int, int, hipStream_t);
+void drain_f32_launch(float*, bf16*, int, hipStream_t);
+}
+
+// dst (bf16) += src (fp32); src = 0 (an fp32 bias-gradient accumulator drained into a
+// main gradient, ready for its next use)
+void drain_f32_(Tensor& src, Tensor& dst) {
+  CHECK_F32(src);
+  CHECK_BF16(dst);
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous() && src.numel() == dst.numel() &&
+                  src.device() == dst.device(),
+              "drain_f32_: contiguous src/dst of equal size on one device");
+  if (src.numel() > 0) {
+    caamd::drain_f32_launch(src.data_ptr<float>(), bp(dst), (int)src.numel(), cur_stream());
+    LAUNCH_CHECK();
+  }
 }
 
 void bias_grad_(const Tensor& dy2d, Tensor& out, bool accumulate) {
@@ -1353,6 +1368,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bias_gelu_fwd", GUARDED(bias_gelu_fwd));
   m.def("bias_gelu_bwd", GUARDED(bias_gelu_bwd));
   m.def("bias_grad_", GUARDED(bias_grad_));
+  m.def("drain_f32_", GUARDED(drain_f32_));
   m.def("xent_fwd", GUARDED(xent_fwd));
   m.def("xent_bwd_", GUARDED(xent_bwd_));
   m.def("xent_fused_", GUARDED(xent_fused_));

@@ -142,6 +142,14 @@ def test_fused_mlp_matches_unfused_reference():
     assert _rel(x.grad, xf.grad) < 3e-2
     for p, r in ((w1, w1f), (b1, b1f), (w2, w2f), (b2, b2f)):
         assert _rel(p.main_grad, r.grad) < 3e-2, (p.shape, _rel(p.main_grad, r.grad))
+    # a second backward accumulates (the fc bias gradient's fp32 accumulator was drained
+    # into b1.main_grad and left zeroed)
+    L._FUSED_MLP = True
+    try:
+        L.mlp(x, w1, b1, w2, b2).backward(dy)
+    finally:
+        L._FUSED_MLP = old
+    assert _rel(b1.main_grad, 2 * b1f.grad) < 3e-2
 
 
 @pytest.mark.parametrize("algo", [9, 1009, 3009, 4009])

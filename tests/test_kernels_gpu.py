@@ -400,3 +400,13 @@ def test_layernorm_bwd_into_main_grads(C, with_dxsum):
     assert _rel(gm, dg2.float() + 0.25) < 1e-2 and _rel(bm, db2.float() - 0.5) < 1e-2
     ref_g = ((x.float() - mean[:, None]) * rstd[:, None] * dy.float()).sum(0)
     assert _rel(gm, ref_g + 0.25) < 2e-2 and _rel(bm, dy.float().sum(0) - 0.5) < 2e-2
+
+
+def test_drain_f32_into_bf16(C):
+    """drain_f32_: bf16 destination += fp32 source, and the source is left zeroed."""
+    torch.manual_seed(10)
+    src = torch.randn(6400, device="cuda")
+    dst = torch.randn(6400, device="cuda").bfloat16()
+    ref = dst.float() + src
+    C.drain_f32_(src, dst)
+    assert _rel(dst, ref) < 1e-2 and int((src != 0).sum()) == 0
