@@ -68,6 +68,37 @@ def _default_cpus() -> int:
         return os.cpu_count() or 1
 
 
+def _sweep_stale_stores() -> int:
+    """Unlink ``/dev/shm/caamd_[node_]<pid>_*`` object-store segments whose owner pid
+    is gone (a head or node agent killed before its shutdown could unlink them: with
+    tmpfs the pages stay charged to memory until the file is removed). Segments of
+    live pids (and of reused pids) are left alone. Returns the number removed."""
+    import re
+
+    n = 0
+    try:
+        names = os.listdir("/dev/shm")
+    except OSError:
+        return 0
+    for name in names:
+        m = re.match(r"^caamd_(?:node_)?(\d+)_[0-9a-f]{8}$", name)
+        if not m:
+            continue
+        try:
+            os.kill(int(m.group(1)), 0)
+            continue  # owner alive
+        except ProcessLookupError:
+            pass
+        except (PermissionError, OverflowError):
+            continue  # someone else's live process, or not a pid
+        try:
+            os.unlink(os.path.join("/dev/shm", name))
+            n += 1
+        except OSError:
+            pass
+    return n
+
+
 def _default_store_bytes() -> int:
     try:
         import psutil
@@ -168,6 +199,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
             if gpus:
                 res["GPU"] = float(len(gpus))
             res["memory"] = float(_mem_bytes())
+            _sweep_stale_stores()  # before sizing the store from the free /dev/shm space
             store_bytes = int(object_store_memory or _default_store_bytes())
             res["object_store_memory"] = float(store_bytes)
             node_id = os.urandom(16)

@@ -33,6 +33,10 @@ class Log:
     def get(self):
         return list(self.items)
 
+    def slow_add(self, x):
+        time.sleep(0.05)  # keeps calls queued at the actor when it is killed
+        return self.add(x)
+
     def big(self, n):
         return np.arange(n, dtype=np.int64)
 
@@ -110,7 +114,7 @@ def test_actor_death_without_retries_fails_calls(cluster):
     pid = ray.get(a.pid.remote())
     ray.get(a.pid.remote())
     assert _direct_client(a) is not None
-    slow = [a.add.remote(i) for i in range(50)]
+    slow = [a.slow_add.remote(i) for i in range(50)]
     os.kill(pid, signal.SIGKILL)
     errors = 0
     for r in slow:
