@@ -70,17 +70,35 @@ def _default_cpus() -> int:
 
 def _sweep_stale_stores() -> int:
     """Unlink ``/dev/shm/caamd_[node_]<pid>_*`` object-store segments whose owner pid
-    is gone (a head or node agent killed before its shutdown could unlink them: with
-    tmpfs the pages stay charged to memory until the file is removed). Segments of
-    live pids (and of reused pids) are left alone. Returns the number removed."""
+    is gone and that no live process maps (a head or node agent killed before its
+    shutdown could unlink them: with tmpfs the pages stay charged to memory until the
+    file is removed). Segments of live pids (and of reused pids) are left alone, and
+    so is an arena that a dead head's workers still map: a restarted head reattaches
+    to it (head_main._previous_session). Returns the number removed."""
     import re
 
     n = 0
     try:
-        names = os.listdir("/dev/shm")
+        names = [x for x in os.listdir("/dev/shm") if x.startswith("caamd_")]
     except OSError:
         return 0
+    if not names:
+        return 0
+    mapped = set()
+    for pid in os.listdir("/proc"):
+        if not pid.isdigit():
+            continue
+        try:
+            with open(f"/proc/{pid}/maps") as f:
+                for ln in f:
+                    i = ln.find("/dev/shm/caamd_")
+                    if i >= 0:
+                        mapped.add(ln[i + 9:].split()[0])
+        except OSError:
+            continue
     for name in names:
+        if name in mapped:
+            continue
         m = re.match(r"^caamd_(?:node_)?(\d+)_[0-9a-f]{8}$", name)
         if not m:
             continue

@@ -1,6 +1,8 @@
 """Stale object-store segments (owner pid gone) are unlinked when a new head
-starts; segments of live pids and unrelated files stay (reference role:
+starts; segments of live pids, segments a live process still maps (a dead head's
+arena that its workers hold for a restarted head) and unrelated files stay (reference role:
 python/ray/_private/node.py cleans up the previous session's plasma files)."""
+import mmap
 import os
 import subprocess
 import sys
@@ -18,11 +20,18 @@ def test_sweep_removes_only_dead_owner_segments():
     for p in (stale, stale_node, live, other):
         with open(p, "wb") as f:
             f.write(b"x")
+    mapped = f"/dev/shm/caamd_{dead}_fedcba98"  # dead owner, but a live process maps it
+    with open(mapped, "wb") as f:
+        f.write(b"x" * 4096)
+    f = open(mapped, "r+b")
+    mm = mmap.mmap(f.fileno(), 4096)
     try:
         assert _sweep_stale_stores() >= 2
         assert not os.path.exists(stale) and not os.path.exists(stale_node)
-        assert os.path.exists(live) and os.path.exists(other)
+        assert os.path.exists(live) and os.path.exists(other) and os.path.exists(mapped)
     finally:
-        for p in (stale, stale_node, live, other):
+        mm.close()
+        f.close()
+        for p in (stale, stale_node, live, other, mapped):
             if os.path.exists(p):
                 os.unlink(p)
