@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the A/B environment knob this script sets was removed after the measurement;
+#  the script records how the committed profile was produced)
 # Llama decode with qkv / o on the decode GEMM + split-K reduce launch vs before.
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/dgllm

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the A/B environment knob this script sets was removed after the measurement;
+#  the script records how the committed profile was produced)
 # Round 4: wave priority (s_setprio) placement in the dK/dV kernel: none / MFMA bursts / VALU pass.
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/attn_prio

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the A/B environment knob this script sets was removed after the measurement;
+#  the script records how the committed profile was produced)
 # Round 4: ragged split-K in the decode GEMM (Llama-3-8B qkv: 5 splits on 240 CUs vs 4 on 192) --
 # decode GEMM tests, then the LLM serving bench alternating ragged / equal splits.
 set -o pipefail

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (historical: the A/B environment knob this script sets was removed after the measurement;
+#  the script records how the committed profile was produced)
 # Round 4: decode GEMM per-shape times, ragged vs equal split-K (bench_decode_gemm3.py, cache-cold weights).
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/dg_ragged_k
