@@ -1932,8 +1932,9 @@ class Head:
             self.pending_spawn[wid] = ("actor", a.actor_id)
             self._spawn_worker(a.node, a.gpu_ids or (), worker_id=wid, env=a.spec.runtime_env)
             return
-        self._set_actor_state(a, "DEAD")
+        # the cause first: the DEAD transition's cluster event takes its severity from it
         a.death_cause = a.death_cause or "the actor's worker process died"
+        self._set_actor_state(a, "DEAD")
         self._fail_actor_queue(a, "ActorDiedError", a.death_cause)
         if a.name:
             self.named_actors.pop((a.namespace, a.name), None)
