@@ -68,13 +68,33 @@ def _default_cpus() -> int:
         return os.cpu_count() or 1
 
 
+def _pid_ns() -> str:
+    """This process's PID-namespace id (the inode of /proc/self/ns/pid), in hex."""
+    try:
+        return format(os.stat("/proc/self/ns/pid").st_ino, "x")
+    except OSError:
+        return "0"
+
+
+def store_segment_name(node: bool = False) -> str:
+    """Object-store arena name ``/caamd_[node_]<pid>_<pidns>_<8 hex>``. The PID
+    namespace is part of the name because /dev/shm is often shared between containers
+    (``--ipc=host``) while PIDs are not: the stale-arena sweep may only judge segments
+    created in its own PID namespace."""
+    return f"/caamd_{'node_' if node else ''}{os.getpid()}_{_pid_ns()}_{uuid.uuid4().hex[:8]}"
+
+
 def _sweep_stale_stores() -> int:
-    """Unlink ``/dev/shm/caamd_[node_]<pid>_*`` object-store segments whose owner pid
-    is gone and that no live process maps (a head or node agent killed before its
-    shutdown could unlink them: with tmpfs the pages stay charged to memory until the
-    file is removed). Segments of live pids (and of reused pids) are left alone, and
-    so is an arena that a dead head's workers still map: a restarted head reattaches
-    to it (head_main._previous_session). Returns the number removed."""
+    """Unlink ``/dev/shm/caamd_[node_]<pid>_<pidns>_*`` object-store segments created
+    in THIS PID namespace whose owner pid is gone and that no live process maps (a
+    head or node agent killed before its shutdown could unlink them: with tmpfs the
+    pages stay charged to memory until the file is removed). Segments of live pids
+    (and of reused pids) are left alone, and so is an arena that a dead head's
+    workers still map: a restarted head reattaches to it
+    (head_main._previous_session). Segments of other PID namespaces (another
+    container sharing /dev/shm: its pids are invisible here and its mappings are not
+    in this /proc) and names without a namespace are never touched. Returns the
+    number removed."""
     import re
 
     n = 0
@@ -84,6 +104,7 @@ def _sweep_stale_stores() -> int:
         return 0
     if not names:
         return 0
+    ns = _pid_ns()
     mapped = set()
     for pid in os.listdir("/proc"):
         if not pid.isdigit():
@@ -99,8 +120,8 @@ def _sweep_stale_stores() -> int:
     for name in names:
         if name in mapped:
             continue
-        m = re.match(r"^caamd_(?:node_)?(\d+)_[0-9a-f]{8}$", name)
-        if not m:
+        m = re.match(r"^caamd_(?:node_)?(\d+)_([0-9a-f]+)_[0-9a-f]{8}$", name)
+        if not m or m.group(2) != ns:
             continue
         try:
             os.kill(int(m.group(1)), 0)
@@ -225,7 +246,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
             res["node:__internal_head__"] = 1.0
             for k, v in (resources or {}).items():
                 res[k] = float(v)
-            store_name = f"/caamd_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+            store_name = store_segment_name()
             if os.environ.get("CAAMD_HEAD_IN_PROCESS", "0") == "1":
                 head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
                             namespace=namespace or "default",

@@ -32,7 +32,7 @@ def main(argv=None):
     a = ap.parse_args(argv)
 
     from .. import _native
-    from .api import _default_cpus, _default_store_bytes, _mem_bytes, detect_gpus
+    from .api import _default_cpus, _default_store_bytes, _mem_bytes, detect_gpus, store_segment_name
     from .object_server import ObjectServer
     from .protocol import ConnectionClosed, connect
 
@@ -44,7 +44,7 @@ def main(argv=None):
     store_bytes = int(a.object_store_memory or _default_store_bytes())
     res["object_store_memory"] = float(store_bytes)
     res.update({k: float(v) for k, v in json.loads(a.resources).items()})
-    store_name = f"/caamd_node_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+    store_name = store_segment_name(node=True)
     store = _native.ObjectStore(store_name, store_bytes, 1 << 18, True)
     store.prefault_async(int(os.environ.get("CAAMD_OBJECT_STORE_PREFAULT_BYTES", str(2 << 30))))
     osrv = ObjectServer(store, a.node_ip_address)

@@ -592,8 +592,10 @@ class CoreWorker:
         head): a handle decref held back for them may go now."""
         from .actor import handle_ref_id
 
-        if self.refs.held_handles:
-            self.refs.release_held_handle(handle_ref_id(actor_id))
+        # no unlocked `if held_handles` shortcut: a remover that saw this actor busy may
+        # be adding the handle right now, under the RefCounter lock; release_held_handle
+        # takes that lock, so it runs after the add and finds the handle
+        self.refs.release_held_handle(handle_ref_id(actor_id))
 
     def _to_head_path(self, actor_id, drop: bool = False):
         """Route this caller's later calls to ``actor_id`` through the head. Calls

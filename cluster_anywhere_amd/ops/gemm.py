@@ -214,6 +214,39 @@ def run_sk(a, b, c, layout: int, accumulate: bool, runs: Optional[int] = None):
     return c
 
 
+# weight gradients on the TN full-line kernel (gemm.hip algo 25: 64-deep K-tiles, every
+# LDS / DMA address precomputed, lockstep split-K + reduce launch). (N_out, K_in) ->
+# (tile rows, slices): 250 / 245 / 250 runs for 256 CUs. CAAMD_WGRAD_TN=0: stream-K kernel.
+WGRAD_TN = os.environ.get("CAAMD_WGRAD_TN", "1") == "1"
+TN_PLANS = {(6400, 1600): (256, 2), (4800, 1600): (192, 2), (1600, 1600): (256, 7)}
+
+
+def tn_plan(M: int, N: int, K: int) -> Optional[Tuple[int, int]]:
+    """(tile rows, slices) of the TN weight-gradient kernel for dW[M, N] over K tokens,
+    or None (shape not tuned / not tileable). Outputs of >= 768 tiles (the LM head,
+    50432 x 1600: 985 tiles) fill the CUs without a split: 256 rows, one slice
+    (2.0 ms vs 2.5 ms on the stream-K kernel per 16384-token chunk,
+    profiles/wgrad_tn64_r5.jsonl)."""
+    if not (ENABLED and WGRAD_TN) or M % 8 or N % 320 or K % 64 or K < 16384:
+        return None
+    plan = TN_PLANS.get((M, N))
+    if plan is None and -(-M // 256) * (N // 320) >= 768:
+        plan = (256, 1)
+    return plan
+
+
+def run_tn(a, b, c, accumulate: bool, bm: int = 256, slices: int = 1):
+    """c[M, N] (+)= a[K, M]^T b[K, N] on gemm_tn64_kernel (``slices`` > 1: lockstep
+    split-K, fp32 slabs combined in slice order by a reduce launch)."""
+    M, N = c.shape
+    ws = None
+    if slices > 1:
+        tiles = -(-M // bm) * (N // 320)
+        ws, _ = _workspace(c.device, slices * tiles * bm * 320, 1)
+    kernels().gemm_tn64(a, b, c, bm, accumulate, slices, ws)
+    return c
+
+
 def _run(a, b, c, epi, bias=None, z=None, zout=None, dbias=None):
     M, N = c.shape
     K = a.shape[1]

@@ -55,10 +55,13 @@ def _wgrad(w, dy2, x2, needs):
         a, b, c = dy2, x2, mg
         if mg.dim() == 2 and not mg.is_contiguous() and mg.t().is_contiguous():
             a, b, c = x2, dy2, mg.t()  # transposed storage: dW^T += X^T dY
-        runs = None
+        runs = tn = None
         if c.is_cuda and c.dtype == torch.bfloat16 and _g._ok(a, b, c):
+            tn = _g.tn_plan(c.shape[0], c.shape[1], a.shape[0])
             runs = _g.wgrad_runs(c.shape[0], c.shape[1], a.shape[0])
-        if runs is not None:
+        if tn is not None:
+            _g.run_tn(a, b, c, True, *tn)  # c += a^T b (gemm.hip TN full-line kernel)
+        elif runs is not None:
             _g.run_sk(a, b, c, 2, True, runs=runs)  # c += a^T b (gemm.hip, split-K / stream-K)
         else:
             c.addmm_(a.t(), b)

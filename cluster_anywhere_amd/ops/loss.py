@@ -108,7 +108,11 @@ class _LinearXentFn(torch.autograd.Function):
             loss_c, _ = k.xent_fused_(lg, target[c0:c1], scale, vocab)  # lg <- scale*(p - onehot)
             losses.append(loss_c)
             _g._run(lg, wt, dh[c0:c1], _g.EPI_BF16)                  # dh = dlogits w
-            _g.run_sk(lg, hc, dw, 2, accumulate=c0 > 0)              # dw (+)= dlogits^T h
+            tn = _g.tn_plan(V, D, c1 - c0)
+            if tn is not None:
+                _g.run_tn(lg, hc, dw, c0 > 0, *tn)                   # dw (+)= dlogits^T h
+            else:
+                _g.run_sk(lg, hc, dw, 2, accumulate=c0 > 0)
         ctx.save_for_backward(dh, dw)
         ctx.w = w
         return torch.cat(losses).sum() * scale[0]

@@ -24,11 +24,49 @@ def _main_ok(mg, g) -> bool:
             and mg.device == g.device)
 
 
+class _Use:
+    """One pending forward use of a LayerNorm's parameters. The backward writes
+    dgamma / dbeta straight into their main-grad views and signals readiness itself,
+    which is only right when the norm ran ONCE in the step: a shared norm (the same
+    module applied twice) must let autograd sum every use before the one
+    post-accumulate hook fires. The count of pending uses lives on the weight; a use
+    ends at its backward, or when its graph is freed without one (``__del__``)."""
+
+    __slots__ = ("p", "live")
+
+    def __init__(self, p):
+        self.p = p
+        self.live = True
+        p._ca_ln_uses = getattr(p, "_ca_ln_uses", 0) + 1
+
+    def shared(self) -> bool:
+        """Called in the backward, before finish(): was the norm used more than once?"""
+        p = self.p
+        if getattr(p, "_ca_ln_uses", 0) > 1:
+            p._ca_ln_shared = True
+        return getattr(p, "_ca_ln_shared", False)
+
+    def finish(self):
+        if self.live:
+            self.live = False
+            p = self.p
+            p._ca_ln_uses = max(0, getattr(p, "_ca_ln_uses", 1) - 1)
+            if p._ca_ln_uses == 0:
+                p._ca_ln_shared = False
+
+    def __del__(self):
+        try:
+            self.finish()
+        except Exception:
+            pass
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, g, b, eps, res_bias=None):
         ctx.res_bias = res_bias
         ctx.gb = (g, b)
+        ctx.use = _Use(g) if torch.is_grad_enabled() and getattr(g, "main_grad", None) is not None else None
         C = kernels()
         x = x.contiguous()
         if res is not None:
@@ -60,6 +98,9 @@ class _LayerNormFn(torch.autograd.Function):
         # views (flat DDP buffer) when both have one: no per-tensor accumulate launch
         gm, bm = (getattr(p, "main_grad", None) for p in ctx.gb)
         own = gm is not None and bm is not None and _main_ok(gm, g) and _main_ok(bm, g)
+        if ctx.use is not None:
+            own = own and not ctx.use.shared()  # shared norm: autograd sums the uses
+            ctx.use.finish()
         dx, dg, db = C.layernorm_bwd(dy.contiguous(), saved, g, mean, rstd, dres,
                                      rb.main_grad if rb is not None else None,
                                      gm if own else None, bm if own else None)

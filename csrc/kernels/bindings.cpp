@@ -47,6 +47,8 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
                        int tfull, int tS, float* tws, int* tcnt, int bpack);
 void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
+hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
+                            int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st);
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
@@ -962,6 +964,36 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   }
 }
 
+// TN weight gradient on the full-line kernel (gemm.hip algo 25): c[M,N] (+)= a[K,M]^T b[K,N],
+// 256- or 192-row tiles x 320 columns, lockstep split over `slices` (ws: slices x tiles fp32 slabs)
+static void gemm_tn64(Tensor a, Tensor b, Tensor c, int64_t bm, bool accumulate, int64_t slices,
+                      c10::optional<Tensor> ws) {
+  CHECK_BF16(a);
+  CHECK_BF16(b);
+  CHECK_BF16(c);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_tn64: 2-D operands");
+  const int64_t K = a.size(0), M = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && c.size(0) == M && c.size(1) == N, "gemm_tn64: shape mismatch");
+  TORCH_CHECK(bm == 256 || bm == 192, "gemm_tn64: bm must be 256 or 192");
+  TORCH_CHECK(M % 8 == 0 && M >= 8 && N % 320 == 0 && K % 64 == 0 && K > 0, "gemm_tn64: M%8, N%320, K%64 must be 0");
+  TORCH_CHECK(K < (1 << 20) && (int64_t)K * a.size(1) * 2 < (1LL << 32) && (int64_t)K * b.size(1) * 2 < (1LL << 32),
+              "gemm_tn64: operands must fit a 32-bit buffer descriptor");
+  TORCH_CHECK(slices >= 1 && slices <= K / 64, "gemm_tn64: 1 <= slices <= K/64");
+  const int64_t tiles = ((M + bm - 1) / bm) * (N / 320);
+  float* wp = nullptr;
+  if (slices > 1) {
+    TORCH_CHECK(ws.has_value(), "gemm_tn64: split needs a slab workspace");
+    CHECK_F32(*ws);
+    TORCH_CHECK(ws->numel() >= slices * tiles * bm * 320, "gemm_tn64: slab workspace too small");
+    wp = ws->data_ptr<float>();
+  }
+  hipError_t e = caamd::gemm_tn64_launch((int)bm, accumulate, (const caamd::bf16*)a.data_ptr(),
+                                         (const caamd::bf16*)b.data_ptr(), (caamd::bf16*)c.data_ptr(), (int)M,
+                                         (int)N, (int)K, (int)a.size(1), (int)b.size(1), (int)c.size(1),
+                                         (int)slices, wp, cur_stream());
+  TORCH_CHECK(e == hipSuccess, "gemm_tn64 launch failed: ", hipGetErrorString(e));
+}
+
 // ---- second-generation GEMM (gemm2.hip): 256 x 160 tiles, 2 workgroups per CU -------------
 // layout 0: a[M,K] b[N,K] · 2: a[K,M] b[K,N]. epi 0: c = acc(+bias) · 1: c += acc(+bias)
 // 3: zout = acc+bias, c = gelu(zout) · 4: c = acc*gelu'(z), dbias += colsum(c)
@@ -1344,6 +1376,9 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("algo") = 1, pybind11::arg("tail_ws") = pybind11::none(),
         pybind11::arg("tail_cnt") = pybind11::none(), pybind11::arg("tail_full") = -1,
         pybind11::arg("tail_split") = 1, pybind11::arg("bpack") = false);
+  m.def("gemm_tn64", GUARDED(gemm_tn64), pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
+        pybind11::arg("bm"), pybind11::arg("accumulate"), pybind11::arg("slices"),
+        pybind11::arg("ws") = pybind11::none());
   m.def("gemm_tail_plan", [](int64_t tiles, int64_t K, int64_t ks, int64_t slots, int64_t max_split) {
     int full, S;
     caamd::gemm_tail_plan((int)tiles, (int)K, (int)ks, (int)slots, (int)max_split, &full, &S);

@@ -1715,7 +1715,284 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
   }
 }
 
+// ================================================================================
+// TN full-line weight-gradient kernel (algo 25): C[M][N] (+)= sum_k A[k][m] B[k][n]
+// with BOTH operands MN-major (A = dY [tokens][N_out], B = X [tokens][K_in]).
+//
+// What held the stream-K kernel above at 0.45 MFMA utilisation against 0.58 for the
+// NT full-line kernel on the same tile (PERF.md, round 4): its ISA spends, per 32-deep
+// K-step and wave, 53 VALU + 40 SALU + 26 tr16 reads + 5 LDS-DMA pieces around 40
+// MFMAs -- a v_add per tr16 read (the swizzled fragment address plus the stage base:
+// inline asm cannot fold an immediate) and a 64-bit v_mad per DMA piece. The full-line
+// NT kernel needs 7 VALU per 80 MFMAs. This kernel keeps the NT kernel's schedule and
+// removes that overhead:
+//  * 64-deep K-tiles in two LDS buffers, [A0][A1][B0][B1], images [k][BM] / [k][BN]
+//    with the mswz XOR swizzle (the same conflict-free tr16 images as the stream-K
+//    kernel; K-sub 1 and the hi half of a fragment move only k bits 5 / 2, which the
+//    swizzle does not use).
+//  * Every per-lane address is computed ONCE: one VGPR per fragment (the swizzle
+//    folded in) and one per DMA round. The loop is unrolled over the two stages, so a
+//    tr16 read is `ds_read_b64_tr_b16 v, vaddr offset:<stage + k-sub + half>` and a
+//    DMA piece is `buffer_load_dword ... lds` with the K-tile's row offset in soffset:
+//    no VALU in the main loop.
+//  * Four phases per K-tile ((k-sub, m-half) as the NT kernel), the two wave rows
+//    staggered by one barrier so each SIMD pairs one wave's reads with the other's
+//    MFMAs; K-tile t+1's DMA rounds spread over phases 0-1 of K-tile t (same RAW / WAR
+//    argument as gemm_k64_kernel: buffer (t+1)&1 last held K-tile t-1, retired before
+//    the barrier that opens phase 0 of t).
+//  * Lockstep split-K: grid = tiles x S, run g = slice g / tiles of tile g % tiles,
+//    slice-major so the ~31 runs of one XCD stream the same token window at the same
+//    time (their dY / X rows are fetched once into that XCD's L2). S > 1: each run
+//    stores an fp32 slab, sk_reduce_kernel sums the slices in order (deterministic).
+//  * Ragged M (1600 = 6.25 x 256): A columns past M are clamped on load (the lane's
+//    round offsets are computed once), rows past M are never stored.
+// BM = 192 serves the 4800-row qkv gradient: 25 x 5 tiles x 2 slices = 250 runs for
+// 256 CUs (256-row tiles: 95 tiles, 190 runs).
+// ================================================================================
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
+  constexpr int WM = 2, WN = 4;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16, TMH = TM / 2;
+  static_assert(TM % 2 == 0 && TN == 5, "two m-halves; 5 B fragments per wave");
+  constexpr int A_ST = 64 * BM * 2, B_ST = 64 * BN * 2;
+  constexpr int NA = A_ST / (NTHR * 16), NB = B_ST / (NTHR * 16), NR = NA + NB;
+  static_assert(A_ST % (NTHR * 16) == 0 && B_ST % (NTHR * 16) == 0, "whole DMA rounds");
+  constexpr int B_BASE = 2 * A_ST;
+  // largest immediate: stage 1 + k-sub 1 + hi half
+  static_assert(A_ST + 32 * BM * 2 + 4 * BM * 2 < 65536 && B_ST + 32 * BN * 2 + 4 * BN * 2 < 65536,
+                "ds_read offsets must fit 16 bits");
+  constexpr int DSPLIT = 2;  // DMA rounds of K-tile t+1 over phases 0 and 1 of t
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_char* smem = (lds_char*)smem_raw;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const bool lo_grp = wr == 0;
+
+  // ---- run -> (slice, tile) ------------------------------------------------------------
+  const int G = gridDim.x;
+  int g;
+  {
+    const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q = G >> 3, r = G & 7;
+    g = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  }
+  const int T = p.tiles_m * p.tiles_n;
+  const int LS = p.tfull > 0 ? p.tfull : 1;
+  const int sl = g / T, tile = g - sl * T;
+  const int nkt = p.K / 64;
+  const int t0 = (int)((long long)sl * nkt / LS);
+  const int nk = (int)((long long)(sl + 1) * nkt / LS) - t0;
+  constexpr int GROUP_M = 8;  // tile order as gemm_sk_kernel / sk_reduce_kernel
+  const int group_sz = GROUP_M * p.tiles_n;
+  const int gq = tile / group_sz;
+  const int first_m = gq * GROUP_M;
+  const int gm = min(p.tiles_m - first_m, GROUP_M);
+  const int tin = tile - gq * group_sz;
+  const int m0 = (first_m + tin % gm) * BM, n0 = (tin / gm) * BN;
+
+  // ---- DMA: one descriptor per operand, one lane offset per round ------------------------
+  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A + m0, (unsigned)(((size_t)p.K * p.lda - m0) * 2));
+  const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B + n0, (unsigned)(((size_t)p.K * p.ldb - n0) * 2));
+  int voa[NA], vob[NB];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    constexpr int CPR = BM / 8;
+    const int lin = j * NTHR + wid * 64 + lane;
+    const int k = lin / CPR, pos = lin - k * CPR;
+    const int col = min(m0 + (pos ^ mswz<BM>(k)) * 8, p.M - 8) - m0;  // ragged M: clamp
+    voa[j] = (k * p.lda + col) * 2;
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    constexpr int CPR = BN / 8;
+    const int lin = j * NTHR + wid * 64 + lane;
+    const int k = lin / CPR, pos = lin - k * CPR;
+    vob[j] = (k * p.ldb + (pos ^ mswz<BN>(k)) * 8) * 2;
+  }
+  const int arow = 64 * p.lda * 2, brow = 64 * p.ldb * 2;  // bytes per K-tile
+  auto dma_round = [&](int t, int stage, int j) {
+    if (j < NA)
+      dma_lds16(ra, smem + stage * A_ST + (j * NTHR + wid * 64) * 16, voa[j], (t0 + t) * arow);
+    else
+      dma_lds16(rb, smem + B_BASE + stage * B_ST + ((j - NA) * NTHR + wid * 64) * 16, vob[j - NA],
+                (t0 + t) * brow);
+  };
+
+  // ---- fragment lane addresses (tr16 reads of k rows 8g+q and 8g+4+q) ----------------------
+  unsigned fa[TM], fb[TN];
+  {
+    const int g4 = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+    const int kk = 8 * g4 + q;
+    const int within = (pp & 1) * 8;
+    const unsigned base = (unsigned)(size_t)smem;
+#pragma unroll
+    for (int f = 0; f < TM; ++f) {
+      const int chunk = (wr * TM * 16 + f * 16 + 4 * pp) >> 3;
+      fa[f] = base + kk * (BM * 2) + (chunk ^ mswz<BM>(kk)) * 16 + within;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int chunk = (wc * TN * 16 + j * 16 + 4 * pp) >> 3;
+      fb[j] = base + B_BASE + kk * (BN * 2) + (chunk ^ mswz<BN>(kk)) * 16 + within;
+    }
+  }
+#define TN64_TR(dst, addr, imm) asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(imm) : "memory")
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8_t bf[TN];
+  bf16x8_t af[TMH];
+  // one K-tile out of LDS stage S (compile-time: every read offset is an immediate)
+  auto ktile = [&](auto S_, int t) {
+    constexpr int S = decltype(S_)::value;
+    const bool pre = t >= 1 && t + 1 < nk;  // K-tile t+1 (t = 0: issued in the prologue)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mh = q & 1, ks = q >> 1;
+      // ---- R segment
+      if (pre && q < DSPLIT) {
+#pragma unroll
+        for (int j = (NR * q) / DSPLIT; j < (NR * (q + 1)) / DSPLIT; ++j) dma_round(t + 1, S ^ 1, j);
+      }
+      if (mh == 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          s16x4 lo, hi;
+          if (ks == 0) {
+            TN64_TR(lo, fb[j], S * B_ST);
+            TN64_TR(hi, fb[j], S * B_ST + 4 * BN * 2);
+          } else {
+            TN64_TR(lo, fb[j], S * B_ST + 32 * BN * 2);
+            TN64_TR(hi, fb[j], S * B_ST + 32 * BN * 2 + 4 * BN * 2);
+          }
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          bf[j] = __builtin_bit_cast(bf16x8_t, v);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TMH; ++i) {
+        s16x4 lo, hi;
+        const unsigned a = fa[mh * TMH + i];
+        if (ks == 0) {
+          TN64_TR(lo, a, S * A_ST);
+          TN64_TR(hi, a, S * A_ST + 4 * BM * 2);
+        } else {
+          TN64_TR(lo, a, S * A_ST + 32 * BM * 2);
+          TN64_TR(hi, a, S * A_ST + 32 * BM * 2 + 4 * BM * 2);
+        }
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        af[i] = __builtin_bit_cast(bf16x8_t, v);
+      }
+      if (q == 3 && !lo_grp) wait_vm<0>();  // lagging row: K-tile t+1 landed
+      // the asm reads are invisible to the compiler's counters: wait here, naming the
+      // fragment registers so no MFMA is scheduled above the wait
+      if constexpr (TMH == 4) {
+        if (mh == 0)
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(bf[0]), "+v"(bf[1]), "+v"(bf[2]), "+v"(bf[3]), "+v"(bf[4]), "+v"(af[0]), "+v"(af[1]),
+                         "+v"(af[2]), "+v"(af[3])::"memory");
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2]), "+v"(af[3])::"memory");
+      } else {
+        static_assert(TMH == 3, "3 or 4 A fragments per phase");
+        if (mh == 0)
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(bf[0]), "+v"(bf[1]), "+v"(bf[2]), "+v"(bf[3]), "+v"(bf[4]), "+v"(af[0]), "+v"(af[1]),
+                         "+v"(af[2])::"memory");
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[0]), "+v"(af[1]), "+v"(af[2])::"memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // ---- M segment
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TMH; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[mh * TMH + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j], af[i], acc[mh * TMH + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (q == 3 && lo_grp) wait_vm<0>();  // leading row: K-tile t+1 landed
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  if (nk > 0) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j) dma_round(0, 0, j);
+    if (nk > 1) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) dma_round(1, 1, j);
+      wait_vm<NR>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    if (!lo_grp) __builtin_amdgcn_s_barrier();  // stagger the second wave row by one barrier
+    for (int t = 0; t < nk; t += 2) {
+      ktile(std::integral_constant<int, 0>{}, t);
+      if (t + 1 < nk) ktile(std::integral_constant<int, 1>{}, t + 1);
+    }
+    if (lo_grp) __builtin_amdgcn_s_barrier();  // equal barrier counts for both rows
+  }
+#undef TN64_TR
+  if (LS > 1) {
+    // slice partial: fp32 slab in fragment order (sk_reduce_kernel's layout)
+    constexpr int SLAB = BM * BN;
+    float* mine = p.tws + ((size_t)sl * T + tile) * SLAB;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+    return;
+  }
+  __syncthreads();  // the last phase's LDS reads are done before the staging overwrites
+  epilogue_staged<BM, BN, TM, TN, EPI, 0>(p, acc, m0, n0, wr, wc, lane, smem, tid);
+}
+
+template <int BM, int EPI>
+static hipError_t launch_tn64(const Args& a, hipStream_t st) {
+  constexpr int BN = 320;
+  auto k = gemm_tn64_kernel<BM, BN, EPI>;
+  constexpr int lds = 2 * 64 * (BM + BN) * 2;
+  ensure_lds((const void*)k, lds);
+  const int T = a.tiles_m * a.tiles_n;
+  const int LS = a.tfull > 0 ? a.tfull : 1;
+  hipLaunchKernelGGL(k, dim3(T * LS), dim3(NTHR), lds, st, a);
+  if (LS > 1) {
+    const long long n4 = (long long)T * (BM * BN / 4);
+    hipLaunchKernelGGL((sk_reduce_kernel<BM, BN, EPI == EPI_BF16_ACC>), dim3((unsigned)((n4 + 255) / 256)),
+                       dim3(256), 0, st, a, LS);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace gemm
+
+// TN weight-gradient GEMM on the full-line kernel (algo 25): c[M][N] (+)= a[K][M]^T b[K][N],
+// lockstep split over `slices` (> 1: fp32 slabs in ws, combined by a reduce launch).
+hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
+                            int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st) {
+  gemm::Args a{A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, 1,
+               (M + bm - 1) / bm, N / 320, 0, 25, slices, 0, ws, nullptr, 0, 0};
+  if (bm == 256) return accumulate ? gemm::launch_tn64<256, gemm::EPI_BF16_ACC>(a, st)
+                                   : gemm::launch_tn64<256, gemm::EPI_BF16>(a, st);
+  if (bm == 192) return accumulate ? gemm::launch_tn64<192, gemm::EPI_BF16_ACC>(a, st)
+                                   : gemm::launch_tn64<192, gemm::EPI_BF16>(a, st);
+  return hipErrorInvalidValue;
+}
 
 // Host entry: shapes are validated by the caller (bindings.cpp).
 static int g_group_m = 0;  // 0: the kernels' default tile-order group (8 m-tiles)

@@ -92,6 +92,8 @@ PYBIND11_MODULE(_native, m) {
              s.copy_in(off, info.ptr, n, threads);
            },
            py::arg("offset"), py::arg("data"), py::arg("threads") = 8)
+      .def("copy_threads_claimed", &ObjectStore::copy_threads_claimed)
+      .def("_debug_plant_claim", &ObjectStore::debug_plant_claim)
       .def("prefault_async", &ObjectStore::prefault_async)
       .def("largest_free", &ObjectStore::largest_free)
       .def("unlink", &ObjectStore::unlink)

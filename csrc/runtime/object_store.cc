@@ -3,6 +3,7 @@
 #include <immintrin.h>
 
 #include <errno.h>
+#include <signal.h>
 #include <fcntl.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -59,7 +60,7 @@ ObjectStore::ObjectStore(const std::string& name, uint64_t capacity, uint64_t ta
     hdr_->used_bytes = 0;
     hdr_->num_objects = 0;
     hdr_->tick = 0;
-    hdr_->copy_threads_active = 0;
+    for (int i = 0; i < Header::kCopyClaims; ++i) hdr_->copy_claims[i] = 0;
     hdr_->copy_threads_budget = std::max(2u, std::thread::hardware_concurrency() / 2);
     pthread_mutexattr_t a;
     pthread_mutexattr_init(&a);
@@ -376,6 +377,47 @@ static void big_copy(uint8_t* d, const uint8_t* s, uint64_t n) {
   memcpy(d + body, s + body, n - body);
 }
 
+// Claim up to `want` extra copy threads from the node-wide budget. Returns
+// (slot << 16) | threads; threads == 0: nothing claimed. Slots of dead processes are
+// reclaimed while summing the active claims; the count is advisory (two claimers may
+// both see room and overshoot briefly), which is all a copy-thread budget needs.
+uint32_t ObjectStore::claim_copy_threads(uint32_t want, uint32_t budget) {
+  uint32_t active = 0;
+  int free_slot = -1;
+  for (int i = 0; i < Header::kCopyClaims; ++i) {
+    uint64_t v = __atomic_load_n(&hdr_->copy_claims[i], __ATOMIC_ACQUIRE);
+    if (v == 0) {
+      if (free_slot < 0) free_slot = i;
+      continue;
+    }
+    const pid_t pid = (pid_t)(v >> 32);
+    if (kill(pid, 0) != 0 && errno == ESRCH) {  // claimant died mid-put: reclaim
+      if (__atomic_compare_exchange_n(&hdr_->copy_claims[i], &v, 0ull, false, __ATOMIC_ACQ_REL,
+                                      __ATOMIC_RELAXED) && free_slot < 0)
+        free_slot = i;
+      continue;
+    }
+    active += (uint32_t)(v & 0xffffffffu);
+  }
+  if (active >= budget || free_slot < 0) return 0;
+  const uint32_t take = std::min(want, budget - active);
+  if (take == 0) return 0;
+  const uint64_t mine = ((uint64_t)(uint32_t)getpid() << 32) | take;
+  for (int i = free_slot; i < Header::kCopyClaims; ++i) {
+    uint64_t e = 0;
+    if (__atomic_compare_exchange_n(&hdr_->copy_claims[i], &e, mine, false, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED))
+      return ((uint32_t)i << 16) | take;
+  }
+  return 0;
+}
+
+uint32_t ObjectStore::copy_threads_claimed() {
+  uint32_t active = 0;
+  for (int i = 0; i < Header::kCopyClaims; ++i)
+    active += (uint32_t)(__atomic_load_n(&hdr_->copy_claims[i], __ATOMIC_ACQUIRE) & 0xffffffffu);
+  return active;
+}
+
 void ObjectStore::copy_in(uint64_t off, const void* src, uint64_t n, int threads) {
   uint8_t* dst = base_ + off;
   const uint8_t* s = (const uint8_t*)src;
@@ -388,22 +430,20 @@ void ObjectStore::copy_in(uint64_t off, const void* src, uint64_t n, int threads
   // claim extra threads from the node-wide budget (the caller's own thread is free)
   uint32_t budget = __atomic_load_n(&hdr_->copy_threads_budget, __ATOMIC_RELAXED);
   if (budget == 0) budget = 4;
-  uint32_t cur = __atomic_load_n(&hdr_->copy_threads_active, __ATOMIC_RELAXED);
-  uint32_t take;
-  do {
-    take = cur >= budget ? 0 : std::min<uint32_t>((uint32_t)(want - 1), budget - cur);
-  } while (take && !__atomic_compare_exchange_n(&hdr_->copy_threads_active, &cur, cur + take, true,
-                                                 __ATOMIC_ACQ_REL, __ATOMIC_RELAXED));
-  const int nt = 1 + (int)take;
+  const uint32_t take = claim_copy_threads((uint32_t)(want - 1), budget);
+  const int nt = 1 + (int)(take & 0xffff);
   if (nt <= 1) {
     big_copy(dst, s, n);
     return;
   }
   struct Release {
-    uint32_t* a;
-    uint32_t k;
-    ~Release() { __atomic_fetch_sub(a, k, __ATOMIC_ACQ_REL); }
-  } release{&hdr_->copy_threads_active, take};
+    uint64_t* slot;
+    uint64_t v;
+    ~Release() {
+      uint64_t e = v;  // our claim, unless a claimer wrongly judged us dead and reclaimed it
+      __atomic_compare_exchange_n(slot, &e, 0ull, false, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED);
+    }
+  } release{&hdr_->copy_claims[take >> 16], ((uint64_t)(uint32_t)getpid() << 32) | (take & 0xffff)};
   const uint64_t chunk = ((n + nt - 1) / nt + 4095) & ~4095ull;
   std::vector<std::thread> ts;
   for (int i = 1; i < nt; ++i) {  // chunk 0 on the calling thread

@@ -59,9 +59,15 @@ struct Header {
   pthread_mutex_t mu;
   // copy threads currently running in copy_in() across every process of the node:
   // concurrent large puts share one node-wide budget instead of each spawning its
-  // own full set (10 putters x 4 threads on 8 cores thrashed the memory system)
-  uint32_t copy_threads_active;
+  // own full set (10 putters x 4 threads on 8 cores thrashed the memory system).
+  // One slot per in-flight claim, packed (pid << 32 | threads) so that a claim is
+  // taken, released and reclaimed by a single 64-bit CAS: a claim whose process died
+  // mid-put (SIGKILL, OOM kill) is reclaimed by the next claimer instead of leaking
+  // its threads out of the budget for the life of the store.
+  static constexpr int kCopyClaims = 64;
+  uint64_t copy_claims[kCopyClaims];
   uint32_t copy_threads_budget;
+  uint32_t pad_claims;
 };
 
 class ObjectStore {
@@ -95,11 +101,23 @@ class ObjectStore {
   // puts: first-touch page faults of fresh shm pages cost ~1 GB/s on one core;
   // spread over cores they scale, and faulted pages copy at memcpy speed).
   void copy_in(uint64_t off, const void* src, uint64_t n, int threads);
+  // copy threads claimed node-wide right now (sum over the live claim slots)
+  uint32_t copy_threads_claimed();
+  // test hook: plant a claim as process `pid` would (a dead pid models a SIGKILLed putter)
+  void debug_plant_claim(uint32_t pid, uint32_t threads) {
+    for (int i = 0; i < Header::kCopyClaims; ++i) {
+      uint64_t e = 0;
+      if (__atomic_compare_exchange_n(&hdr_->copy_claims[i], &e, ((uint64_t)pid << 32) | threads, false,
+                                      __ATOMIC_ACQ_REL, __ATOMIC_RELAXED))
+        return;
+    }
+  }
   // Touch (fault in) the first `max_bytes` of the data region in a detached
   // background thread, so the first large puts do not pay page faults.
   void prefault_async(uint64_t max_bytes);
 
  private:
+  uint32_t claim_copy_threads(uint32_t want, uint32_t budget);
   void lock();
   void unlock();
   ObjectEntry* find(const uint8_t* id, bool for_insert);

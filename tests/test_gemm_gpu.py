@@ -267,3 +267,44 @@ def test_wgrad_external_combine_matches_in_kernel_bits():
     finally:
         G.WGRAD_EXT = old
     assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
+
+
+@pytest.mark.parametrize("bm", [256, 192])
+@pytest.mark.parametrize("MN,slices", [((1600, 1600), 7), ((640, 960), 1), ((1600, 640), 3), ((960, 320), 2),
+                                       ((4800, 1600), 2)])
+def test_wgrad_tn64(bm, MN, slices):
+    """TN full-line weight-gradient kernel (algo 25): dW (+)= dY^T X over 4160 tokens
+    (65 K-tiles: odd, and not divisible by the slice counts), ragged M (1600 = 6.25 x 256,
+    8.33 x 192), single run per tile and lockstep split-K with the reduce launch,
+    overwrite and accumulate, repeatable bits, vs fp32."""
+    from cluster_anywhere_amd.ops import gemm as G
+
+    M, N = MN
+    K = 4160
+    dy, x = _mk((K, M), 51), _mk((K, N), 52)
+    ref = dy.float().t() @ x.float()
+    c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    G.run_tn(dy, x, c, False, bm, slices)
+    assert _rel(c, ref) < 5e-3
+    c0 = _mk((M, N), 53)
+    c2 = c0.clone()
+    G.run_tn(dy, x, c2, True, bm, slices)
+    assert _rel(c2, ref + c0.float()) < 5e-3
+    c3 = torch.empty_like(c)
+    G.run_tn(dy, x, c3, False, bm, slices)
+    assert torch.equal(c, c3)
+
+
+def test_wgrad_tn64_strided_views_and_dispatch():
+    """The TN kernel on the GPT-2-XL wgrad shapes it is planned for (fewer tokens), and
+    through ops.linear._wgrad into a transposed main-grad view (fc2 storage)."""
+    from cluster_anywhere_amd.ops import gemm as G
+
+    K = 16384
+    for (M, N) in ((6400, 1600), (4800, 1600), (1600, 1600)):
+        plan = G.tn_plan(M, N, K)
+        assert plan is not None
+        dy, x = _mk((K, M), 61), _mk((K, N), 62)
+        c = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        G.run_tn(dy, x, c, True, *plan)
+        assert _rel(c, dy.float().t() @ x.float()) < 5e-3

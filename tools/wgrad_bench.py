@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--tokens", type=int, default=32768)
     ap.add_argument("--ksweep", action="store_true", help="proj / fc wgrad at several token counts (fixed runs)")
+    ap.add_argument("--tn", action="store_true", help="TN full-line kernel (algo 25) vs stream-K vs hipBLASLt")
+    ap.add_argument("--head", action="store_true", help="LM-head weight gradient (50432 x 1600, 16384-token chunk)")
     a = ap.parse_args()
     from cluster_anywhere_amd.ops import gemm as G
 
@@ -51,6 +53,45 @@ def main():
         return
 
     K = a.tokens
+    if a.head:
+        M, N, Kc = 50432, 1600, 16384
+        dy = torch.randn(Kc, M, device="cuda").bfloat16()
+        x = torch.randn(Kc, N, device="cuda").bfloat16()
+        c = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+        fl = 2.0 * M * N * Kc
+        rows = []
+        for rnd in range(2):
+            med, _ = timeit(lambda: G.run_sk(dy, x, c, 2, True), a.iters)
+            rows.append(("sk", "auto", med))
+            for (bm, S) in ((256, 1), (192, 1)):
+                med, _ = timeit(lambda: G.run_tn(dy, x, c, True, bm, S), a.iters)
+                rows.append(("tn64", f"{bm}x{S}", med))
+        for impl, cfg, med in rows:
+            print(json.dumps({"M": M, "N": N, "K": Kc, "impl": impl, "cfg": cfg, "us_med": round(med, 1),
+                              "pfs": round(fl / med / 1e9, 3)}), flush=True)
+        return
+    if a.tn:
+        plans = {(6400, 1600): [(256, 2), (256, 1)], (4800, 1600): [(192, 2), (256, 2), (192, 1)],
+                 (1600, 1600): [(256, 7), (256, 6), (256, 5), (192, 5)]}
+        sk = {(6400, 1600): 250, (4800, 1600): 190, (1600, 1600): 245}
+        for (M, N), pl in plans.items():
+            dy = torch.randn(K, M, device="cuda").bfloat16()
+            x = torch.randn(K, N, device="cuda").bfloat16()
+            c = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+            fl = 2.0 * M * N * K
+            rows = []
+            for rnd in range(2):  # interleaved rounds
+                med, _ = timeit(lambda: c.addmm_(dy.t(), x), a.iters)
+                rows.append(("hipblaslt", None, med))
+                med, _ = timeit(lambda: G.run_sk(dy, x, c, 2, True, sk[(M, N)]), a.iters)
+                rows.append(("sk", sk[(M, N)], med))
+                for (bm, S) in pl:
+                    med, _ = timeit(lambda: G.run_tn(dy, x, c, True, bm, S), a.iters)
+                    rows.append(("tn64", f"{bm}x{S}", med))
+            for impl, cfg, med in rows:
+                print(json.dumps({"M": M, "N": N, "K": K, "impl": impl, "cfg": cfg, "us_med": round(med, 1),
+                                  "pfs": round(fl / med / 1e9, 3)}), flush=True)
+        return
     cases = {(1600, 1600): [140, 175, 210, 245], (6400, 1600): [250], (4800, 1600): [190, 228]}
     for (M, N), runs_list in cases.items():
         dy = torch.randn(K, M, device="cuda").bfloat16()
