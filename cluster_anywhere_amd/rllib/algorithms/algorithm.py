@@ -103,6 +103,21 @@ class AlgorithmConfig:
         # learner actors of a LearnerGroup are re-created from the last learner state
         self.restart_failed_learners = True
         self.max_num_learner_restarts = 100
+        # offline data (reference: AlgorithmConfig.offline_data): input for BC / MARWIL /
+        # CQL, streamed through a Data pipeline; `output` records env-runner episodes
+        self.input_ = None
+        self.input_read_method = "read_parquet"
+        self.input_read_method_kwargs: Dict = {}
+        self.map_batches_kwargs: Dict = {}
+        self.iter_batches_kwargs: Dict = {}
+        self.prelearner_class = None
+        self.shuffle_buffer_rows = None
+        self.output = None
+        self.output_max_rows_per_file = 10_000
+        self.output_write_episodes = True
+        # off-policy estimation on offline episodes at evaluation time
+        self.off_policy_estimation_methods: Dict = {}
+        self.ope_max_rows = 50_000
         # misc
         self.seed = None
         self.evaluation_interval = None
@@ -228,8 +243,39 @@ class AlgorithmConfig:
                 out[mid] = (sp.observation_space, sp.action_space)
         return out
 
-    def evaluation(self, *, evaluation_interval=NotProvided, evaluation_duration=NotProvided, **_):
-        return self._set(evaluation_interval=evaluation_interval, evaluation_duration=evaluation_duration)
+    def evaluation(self, *, evaluation_interval=NotProvided, evaluation_duration=NotProvided,
+                   off_policy_estimation_methods=NotProvided, **_):
+        """``off_policy_estimation_methods``: ``{name: {"type": ImportanceSampling |
+        WeightedImportanceSampling | DirectMethod | DoublyRobust (or "is" / "wis" /
+        "dm" / "dr"), **kwargs}}`` -- estimated on the offline ``input_`` episodes
+        (which must carry the behaviour policy's ``action_prob``)."""
+        return self._set(evaluation_interval=evaluation_interval, evaluation_duration=evaluation_duration,
+                         off_policy_estimation_methods=(dict(off_policy_estimation_methods or {})
+                                                        if off_policy_estimation_methods is not NotProvided
+                                                        else NotProvided))
+
+    def offline_data(self, *, input_=NotProvided, input_read_method=NotProvided,
+                     input_read_method_kwargs=NotProvided, map_batches_kwargs=NotProvided,
+                     iter_batches_kwargs=NotProvided, prelearner_class=NotProvided, shuffle_buffer_rows=NotProvided,
+                     output=NotProvided, output_max_rows_per_file=NotProvided, output_write_episodes=NotProvided,
+                     **_):
+        """Offline input (paths / a Dataset -> streamed; column dicts -> in memory) and
+        episode output (reference: ``AlgorithmConfig.offline_data``)."""
+        return self._set(input_=input_, input_read_method=input_read_method,
+                         input_read_method_kwargs=input_read_method_kwargs, map_batches_kwargs=map_batches_kwargs,
+                         iter_batches_kwargs=iter_batches_kwargs, prelearner_class=prelearner_class,
+                         shuffle_buffer_rows=shuffle_buffer_rows, output=output,
+                         output_max_rows_per_file=output_max_rows_per_file,
+                         output_write_episodes=output_write_episodes)
+
+    def build_offline_data(self, columns=None):
+        from ..offline import OfflineData
+
+        return OfflineData(self.input_, gamma=self.gamma, columns=columns, input_read_method=self.input_read_method,
+                           input_read_method_kwargs=self.input_read_method_kwargs,
+                           map_batches_kwargs=self.map_batches_kwargs, iter_batches_kwargs=self.iter_batches_kwargs,
+                           prelearner_class=self.prelearner_class, shuffle_buffer_rows=self.shuffle_buffer_rows,
+                           seed=self.seed)
 
     def debugging(self, *, seed=NotProvided, **_):
         return self._set(seed=seed)
@@ -325,6 +371,8 @@ class AlgorithmConfig:
                 "gamma": self.gamma, "module_factory": self.module_factory(),
                 "metrics_num_episodes_for_smoothing": self.metrics_num_episodes_for_smoothing,
                 "need_next_obs": False,
+                "output": self.output, "output_max_rows_per_file": self.output_max_rows_per_file,
+                "output_write_episodes": self.output_write_episodes,
                 "env_to_module_connector": self.env_to_module_connector,
                 "module_to_env_connector": self.module_to_env_connector,
                 "callbacks_class": self.callbacks_class, "callbacks_functions": dict(self.callbacks_functions),
@@ -472,12 +520,32 @@ class Algorithm(Trainable):
         r.reset_envs(10_000)
         rets = r.sample_episodes(c.evaluation_duration, explore=False)
         out = {"env_runners": {"episode_return_mean": float(np.mean(rets)), "num_episodes": len(rets)}}
+        if c.off_policy_estimation_methods:
+            out["off_policy_estimator"] = self.estimate_off_policy()
         if self.is_multi_agent:
             m = r.get_metrics()
             out["env_runners"]["module_episode_returns_mean"] = {
                 k: float(np.mean(v[-len(rets):])) for k, v in m["module_episode_returns_mean"].items() if v}
         self.callbacks.on_evaluate_end(algorithm=self, metrics_logger=None, evaluation_metrics=out)
         return out
+
+    def estimate_off_policy(self, episodes=None) -> Dict[str, Dict[str, float]]:
+        """Every configured off-policy estimator on offline episodes (default: up to
+        ``ope_max_rows`` rows of ``input_``), with the current module as the target
+        policy (reference: ``evaluation/off_policy_estimator/<name>``)."""
+        from ..offline import make_estimator
+
+        c = self.algo_config
+        if episodes is None:
+            od = getattr(self, "offline_data", None)
+            if od is None:
+                if c.input_ is None:
+                    raise ValueError("off-policy estimation needs config.offline_data(input_=...)")
+                od = self.offline_data = c.build_offline_data()
+            episodes = list(od.iter_episodes(max_rows=c.ope_max_rows))
+        module = self.get_module()
+        return {name: make_estimator(spec, module, c.gamma).estimate(episodes)
+                for name, spec in c.off_policy_estimation_methods.items()}
 
     def compute_single_action(self, obs, explore: bool = False, policy_id: Optional[str] = None):
         module = self.get_module(policy_id)

@@ -17,7 +17,6 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from .marwil import _load_offline
 from .sac import SAC, SACConfig, SACLearner, _Param
 
 
@@ -30,13 +29,8 @@ class CQLConfig(SACConfig):
         self.lagrangian = False
         self.lagrangian_thresh = 5.0
         self.min_q_weight = 5.0
-        self.input_ = None
         self.updates_per_iteration = 1
         self.num_steps_sampled_before_learning_starts = 0
-
-    def offline_data(self, *, input_=None, **_):
-        self.input_ = input_
-        return self
 
 
 class CQLLearner(SACLearner):
@@ -134,27 +128,20 @@ class CQL(SAC):
     supports_multi_agent = False  # offline: one static dataset
 
     def setup_algo(self):
-        c = self.algo_config
-        cols = _load_offline(c.input_)
-        need = ("obs", "actions", "rewards", "next_obs", "terminateds")
-        miss = [k for k in need if k not in cols]
-        if miss:
-            raise ValueError(f"CQL offline data needs columns {need}; missing {miss}")
-        self.data = {"obs": cols["obs"].astype(np.float32), "actions": cols["actions"].astype(np.float32),
-                     "rewards": cols["rewards"].astype(np.float32),
-                     "next_obs": np.asarray(cols["next_obs"]).astype(np.float32),
-                     "terminateds": cols["terminateds"].astype(np.float32)}
-        if self.data["actions"].ndim == 1:
-            self.data["actions"] = self.data["actions"][:, None]
-        self.n = len(self.data["obs"])
-        self.rng = np.random.default_rng(c.seed)
+        # (s, a, r, s', terminated) rows, streamed from paths / a Dataset or sampled
+        # from in-memory columns; recorded episodes carry s' as `new_obs`
+        self.offline_data = self.algo_config.build_offline_data(
+            columns=("obs", "actions", "rewards", "next_obs", "terminateds"))
 
     def training_step(self):
         c = self.algo_config
         stats = {}
         for _ in range(c.updates_per_iteration):
-            idx = self.rng.integers(0, self.n, size=min(c.train_batch_size, self.n))
-            b = {k: v[idx] for k, v in self.data.items()}
+            raw = self.offline_data.sample(c.train_batch_size)
+            b = {k: np.asarray(v).astype(np.float32) for k, v in raw.items()}
+            if b["actions"].ndim == 1:
+                b["actions"] = b["actions"][:, None]
+            idx = b["rewards"]
             if self.learner_group.local is not None:
                 stats, _td = self.learner_group.local.train_on(b)
             else:

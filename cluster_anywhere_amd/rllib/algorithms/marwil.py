@@ -26,12 +26,7 @@ class MARWILConfig(AlgorithmConfig):
         self.moving_average_sqd_adv_norm_start = 100.0
         self.lr = 1e-4
         self.train_batch_size = 2000
-        self.input_ = None
         self.updates_per_iteration = 1
-
-    def offline_data(self, *, input_=None, **_):
-        self.input_ = input_
-        return self
 
 
 class MARWILLearner(Learner):
@@ -61,33 +56,16 @@ class MARWILLearner(Learner):
 
 
 def _load_offline(inp) -> Dict[str, np.ndarray]:
-    if inp is None:
-        raise ValueError("config.offline_data(input_=...) is required for offline algorithms")
-    if isinstance(inp, (str, list)) and (isinstance(inp, str) or (inp and isinstance(inp[0], str))):
-        from ... import data
+    """All of a small offline input as one column dict (used by tools; training
+    samples through :class:`~cluster_anywhere_amd.rllib.offline.OfflineData`)."""
+    from ..offline import OfflineData
 
-        inp = data.read_parquet(inp)
-    if hasattr(inp, "iter_batches"):
-        parts = list(inp.iter_batches(batch_size=None, batch_format="numpy"))
-        cols = {k: np.concatenate([np.asarray(p[k]) for p in parts]) for k in parts[0]}
-    elif isinstance(inp, dict):
-        cols = {k: np.asarray(v) for k, v in inp.items()}
-    else:
-        cols = {k: np.concatenate([np.asarray(p[k]) for p in inp]) for k in inp[0]}
-    if cols["obs"].dtype == object:
-        cols["obs"] = np.stack(cols["obs"])
-    return cols
-
-
-def _discounted_returns(rew, term, gamma):
-    out = np.zeros_like(rew, dtype=np.float32)
-    acc = 0.0
-    for i in range(len(rew) - 1, -1, -1):
-        if term[i]:
-            acc = 0.0
-        acc = rew[i] + gamma * acc
-        out[i] = acc
-    return out
+    od = OfflineData(inp)
+    if od.memory is not None:
+        return od.memory
+    parts = [od.prelearner_class(od.gamma, None)(b) for b in od.dataset.iter_batches(batch_size=None,
+                                                                                       batch_format="numpy")]
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
 
 
 class MARWIL(Algorithm):
@@ -95,23 +73,18 @@ class MARWIL(Algorithm):
     learner_class = MARWILLearner
 
     def setup_algo(self):
-        c = self.algo_config
-        cols = _load_offline(c.input_)
-        if "returns" not in cols:
-            cols["returns"] = _discounted_returns(cols["rewards"].astype(np.float32),
-                                                  cols["terminateds"].astype(bool), c.gamma)
-        self.data = {"obs": cols["obs"], "actions": cols["actions"], "returns": cols["returns"].astype(np.float32)}
-        self.n = len(self.data["obs"])
-        self.rng = np.random.default_rng(c.seed)
+        # streamed (paths / Dataset) or in-memory (column dicts) offline input; the
+        # pre-learner adds per-episode discounted returns
+        self.offline_data = self.algo_config.build_offline_data(columns=("obs", "actions", "returns"))
 
     def training_step(self):
         c = self.algo_config
         stats = {}
         for _ in range(c.updates_per_iteration):
-            idx = self.rng.integers(0, self.n, size=min(c.train_batch_size, self.n))
-            b = {k: v[idx] for k, v in self.data.items()}
+            b = self.offline_data.sample(c.train_batch_size)
+            b["returns"] = b["returns"].astype(np.float32, copy=False)
             stats = self.learner_group.update(b)
-            self.env_steps_trained += len(idx)
+            self.env_steps_trained += len(b["returns"])
         self._sync_weights()
         return stats
 

@@ -68,6 +68,14 @@ class EnvRunner:
         self.new_episodes: List[float] = []
         self.total_steps = 0
         self.explore_extra: Dict[str, Any] = {}
+        # config.offline_data(output=...): record every sampled step (whole episodes per file)
+        self.recorder = None
+        if config.get("output"):
+            from ..offline.io import EpisodeRecorder
+
+            self.recorder = EpisodeRecorder(config["output"], worker_index, self.env.num_envs,
+                                            config.get("output_max_rows_per_file") or 10_000,
+                                            config.get("output_write_episodes", True))
 
     # ------------------------------------------------------------ episodes / connectors
     def _new_episode(self, i: int, raw_obs) -> SingleAgentEpisode:
@@ -123,7 +131,8 @@ class EnvRunner:
         T = num_timesteps or self.cfg.get("rollout_fragment_length", 64)
         N = self.env.num_envs
         gamma = self.cfg.get("gamma", 0.99)
-        need_next = self.cfg.get("need_next_obs", False)
+        rec = self.recorder
+        need_next = self.cfg.get("need_next_obs", False) or rec is not None
         obs_buf = np.empty((T, N) + self.obs.shape[1:], dtype=self.obs.dtype)
         next_buf = np.empty_like(obs_buf) if need_next else None
         acts, logps, vfs, rews, raw, terms, truncs, dist = [], [], [], [], [], [], [], []
@@ -197,6 +206,12 @@ class EnvRunner:
                                                    metrics_logger=self.metrics, env=self.env, env_index=int(i),
                                                    rl_module=self.module)
             self.obs = self._to_module(nraw, self.episodes) if track else nraw
+            if rec is not None:
+                lp = out["action_logp"].cpu().numpy() if "action_logp" in out else None
+                vf = out["vf_preds"].cpu().numpy() if "vf_preds" in out else None
+                for i in range(N):
+                    rec.add_step(i, obs_buf[t][i], mfinal[i] if done[i] else self.obs[i], a[i], r[i], te[i], tr[i],
+                                 None if lp is None else lp[i], None if vf is None else vf[i])
             if stateful:  # episodes that ended start again from the initial state
                 for k in new_state:
                     new_state[k][done] = 0.0
@@ -253,6 +268,19 @@ class EnvRunner:
         return m
 
     def ping(self):
+        return True
+
+    def flush_output(self, include_open: bool = True) -> List[str]:
+        """Write the recorded episodes (``config.offline_data(output=...)``) still
+        buffered; with ``include_open`` unfinished episodes too (as truncated).
+        Returns every file this runner has written."""
+        if self.recorder is None:
+            return []
+        self.recorder.flush(include_open=include_open)
+        return list(self.recorder.files_written)
+
+    def stop(self):
+        self.flush_output()
         return True
 
 
@@ -469,9 +497,25 @@ class EnvRunnerGroup:
             out.update(strip_meta(custom))
         return out
 
+    def flush_output(self) -> List[str]:
+        """Flush every runner's recorded episodes; the files written so far."""
+        if self.local is not None:
+            return self.local.flush_output()
+        out = []
+        for v in self._fanout("flush_output").values():
+            out.extend(v)
+        return sorted(out)
+
     def stop(self):
         from ...core import api as core
 
+        if self.local is not None and hasattr(self.local, "stop"):
+            self.local.stop()
+        elif self.remote:
+            try:
+                self.flush_output()
+            except Exception:
+                pass
         for r in self.remote:
             try:
                 core.kill(r)
