@@ -337,6 +337,16 @@ class Head:
             self._gcs_restore()
         self.thread = threading.Thread(target=self._loop, name="caamd-head", daemon=True)
         self.thread.start()
+        # physical metrics of the head's own node (other nodes push theirs: _h_node_stats)
+        self.node_info[self.head_hex]["IsHeadNode"] = True
+        self._reporter = None
+        try:
+            from ..dashboard.reporter import NodeReporter
+
+            info = self.node_info[self.head_hex]
+            self._reporter = NodeReporter(lambda st: info.__setitem__("stats", st), self.session_dir).start()
+        except Exception:
+            self._reporter = None
         for _ in range(self._prestart):
             self.call(lambda: self._spawn_worker(self.node_id.hex(), ()))
 
@@ -2655,6 +2665,13 @@ class Head:
         self._retry_infeasible()
         self._schedule()
 
+    def _h_node_stats(self, c, stats):
+        """A node agent's physical-metrics sample (dashboard/reporter.py)."""
+        node = self.clients.get(c, {}).get("node")
+        info = self.node_info.get(node)
+        if info is not None:
+            info["stats"] = stats
+
     def _register_node(self, c, node_hex, extra):
         """A node agent joined (reference: raylet registering with the GCS node manager)."""
         res = {k: float(v) for k, v in extra["resources"].items()}
@@ -2670,7 +2687,7 @@ class Head:
         self.node_resources[node_hex] = dict(res)
         self.node_info[node_hex] = {"NodeID": node_hex, "Alive": True, "NodeManagerAddress": addr,
                                     "Resources": dict(res), "local": False, "pid": extra.get("pid"),
-                                    "Labels": dict(self.node_labels[node_hex])}
+                                    "Labels": dict(self.node_labels[node_hex]), "IsHeadNode": False}
         self._send(c, ("registered", {"store_name": extra["store_name"], "node_id": node_hex,
                                       "namespace": self.namespace, "session_dir": self.session_dir,
                                       "head_tcp": self.tcp_address, "reconnect_s": self.reconnect_s}))
@@ -2713,6 +2730,8 @@ class Head:
         if not self.running:
             return
         self.running = False
+        if getattr(self, "_reporter", None) is not None:
+            self._reporter.stop()
         for w in list(self.workers.values()):
             try:
                 if w.conn is not None:

@@ -93,6 +93,18 @@ def main(argv=None):
 
     signal.signal(signal.SIGTERM, cleanup)
     print(f"node {node_hex} joined {a.address} with {res}", flush=True)
+    # physical metrics of this node, pushed to the head (dashboard/reporter.py)
+    link = {"conn": conn}
+
+    def push_stats(st):
+        try:
+            link["conn"].send(("node_stats", st))
+        except Exception:
+            pass
+
+    from ..dashboard.reporter import NodeReporter
+
+    NodeReporter(push_stats, session_dir).start()
     try:
         while True:
             try:
@@ -101,7 +113,7 @@ def main(argv=None):
                 nc = reconnect() if reconnect_s > 0 else None
                 if nc is None:
                     break
-                conn = nc
+                conn = link["conn"] = nc
                 continue
             if m[0] == "spawn":
                 _, wid, gpu_ids, extra = m

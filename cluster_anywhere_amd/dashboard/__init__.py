@@ -54,6 +54,9 @@ def render_prometheus(state: Callable) -> str:
         lines += ["# TYPE ray_object_store_memory gauge",
                   f'ray_object_store_memory{{Type="USED"}} {st.get("used", 0)}',
                   f'ray_object_store_memory{{Type="CAPACITY"}} {st.get("capacity", 0)}']
+    from .reporter import prometheus_lines
+
+    lines += prometheus_lines(nodes)
     for name, m in sorted(state("metrics").items()):
         kind = m["kind"]
         lines.append(f"# HELP {name} {m['desc']}")
@@ -75,7 +78,7 @@ def render_prometheus(state: Callable) -> str:
     return "\n".join(lines) + "\n"
 
 
-def build_app(state: Callable, jobs: JobManager, session_dir: Optional[str] = None):
+def build_app(state: Callable, jobs: JobManager, session_dir: Optional[str] = None, serve_agent=None):
     from starlette.applications import Starlette
     from starlette.requests import Request
     from starlette.responses import HTMLResponse, JSONResponse, PlainTextResponse, Response
@@ -168,7 +171,27 @@ def build_app(state: Callable, jobs: JobManager, session_dir: Optional[str] = No
             text = "".join(f.readlines()[-lines:])
         return j({"name": name, "text": text})
 
-    routes = [Route("/", ui), Route("/ui", ui), Route("/api/v0/logs", list_logs),
+    async def serve_apps(req: Request):
+        """Serve REST API (dashboard/serve_agent.py): PUT deploys a ServeDeploySchema,
+        GET returns the instance details, DELETE shuts Serve down."""
+        import asyncio
+
+        if serve_agent is None:
+            return j({"error": "Serve REST API unavailable (no cluster address)"}, 503)
+        body = None
+        if req.method == "PUT":
+            try:
+                body = await req.json()
+            except Exception:
+                return j({"error": "body must be a ServeDeploySchema JSON object"}, 400)
+        op = {"GET": "get", "PUT": "put", "DELETE": "delete"}[req.method]
+        r = await asyncio.get_running_loop().run_in_executor(None, serve_agent.request, op, body)
+        if not r.get("ok"):
+            return j({"error": r.get("error"), "trace": r.get("trace")}, r.get("status", 500))
+        return j(r.get("body") or {}) if op == "get" else Response(status_code=200)
+
+    routes = [Route("/", ui),
+              Route("/api/serve/applications/", serve_apps, methods=["GET", "PUT", "DELETE"]), Route("/ui", ui), Route("/api/v0/logs", list_logs),
               Route("/api/v0/logs/file", log_file),
               Route("/api/version", version), Route("/api/cluster_status", cluster_status),
               Route("/api/v0/nodes", lister("nodes")), Route("/api/v0/actors", lister("actors")),
@@ -200,7 +223,10 @@ def start_dashboard(host: str = "127.0.0.1", port: int = 8265, head=None, contro
     if session_dir is None:
         session_dir = head.session_dir if head is not None else "/tmp/caamd"
     jobs = JobManager(control_address, os.path.join(session_dir, "jobs"))
-    app = build_app(state, jobs, session_dir)
+    from .serve_agent import ServeAgentClient
+
+    serve_agent = ServeAgentClient(control_address) if control_address and control_address != "auto" else None
+    app = build_app(state, jobs, session_dir, serve_agent)
     cfg = uvicorn.Config(app, host=host, port=port, log_level="warning", lifespan="off", access_log=False)
     server = uvicorn.Server(cfg)
     t = threading.Thread(target=server.run, name="caamd-dashboard", daemon=True)
@@ -208,7 +234,7 @@ def start_dashboard(host: str = "127.0.0.1", port: int = 8265, head=None, contro
     deadline = time.time() + 30
     while not server.started and time.time() < deadline:
         time.sleep(0.02)
-    _server = (server, jobs)
+    _server = (server, jobs, serve_agent)
     return f"http://{host}:{port}"
 
 
@@ -217,4 +243,6 @@ def stop_dashboard():
     if _server is not None:
         _server[0].should_exit = True
         _server[1].stop_all()
+        if _server[2] is not None:
+            _server[2].close()
         _server = None

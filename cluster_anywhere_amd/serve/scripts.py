@@ -40,10 +40,36 @@ def _load_config(path):
         return ServeDeploySchema.model_validate(yaml.safe_load(f))
 
 
+def _is_http(address) -> bool:
+    return bool(address) and str(address).startswith(("http://", "https://"))
+
+
+def _rest(address: str, method: str, body=None):
+    """The dashboard's Serve REST API (``/api/serve/applications/``)."""
+    import json
+    import urllib.error
+    import urllib.request
+
+    data = None if body is None else json.dumps(body).encode()
+    req = urllib.request.Request(address.rstrip("/") + "/api/serve/applications/", data=data, method=method,
+                                 headers={"Content-Type": "application/json"})
+    try:
+        with urllib.request.urlopen(req, timeout=600) as r:
+            raw = r.read()
+    except urllib.error.HTTPError as e:
+        raise SystemExit(f"Serve REST {method} failed ({e.code}): {e.read().decode(errors='replace')[:2000]}")
+    return json.loads(raw) if raw else {}
+
+
 def cmd_deploy(a):
     from .schema import deploy_config
 
     cfg = _load_config(a.config_file)
+    if _is_http(a.address):  # through the dashboard (reference: serve deploy --address http://...)
+        _rest(a.address, "PUT", cfg.model_dump(mode="json"))
+        print(f"Sent deploy request for {len(cfg.applications)} application(s): "
+              + ", ".join(x.name for x in cfg.applications))
+        return 0
     _init(a.address)
     deploy_config(cfg)
     print(f"Sent deploy request for {len(cfg.applications)} application(s): "
@@ -102,6 +128,16 @@ def _status_dict():
 
 
 def cmd_status(a):
+    if _is_http(a.address):
+        d = _rest(a.address, "GET")
+        st = {"proxies": {k: v.get("status") for k, v in (d.get("proxies") or {}).items()},
+              "applications": {n: {"status": x["status"], "route_prefix": x["route_prefix"],
+                                   "deployments": {dn: {"status": dd["status"],
+                                                        "replica_states": dd.get("replica_states", {})}
+                                                   for dn, dd in x["deployments"].items()}}
+                               for n, x in (d.get("applications") or {}).items()}}
+        sys.stdout.write(yaml.safe_dump(st, sort_keys=False))
+        return 0
     _init(a.address)
     sys.stdout.write(yaml.safe_dump(_status_dict(), sort_keys=False))
     return 0
@@ -133,6 +169,10 @@ def cmd_shutdown(a):
     if not a.yes:
         print("Pass -y/--yes to shut down Serve on the cluster.")
         return 1
+    if _is_http(a.address):
+        _rest(a.address, "DELETE")
+        print("Serve shut down.")
+        return 0
     _init(a.address)
     api.shutdown()
     print("Serve shut down.")

@@ -93,11 +93,13 @@ def test_gpt2_xl_width_gradients_match_fp32_autograd():
     ref = _ref_loss(P, cfg, x, y)
     ref.backward()
     assert abs(loss.item() - ref.item()) < 2e-3 * abs(ref.item()), (loss.item(), ref.item())
-    bad = []
+    bad, errs = [], []
     for n, p in model.named_parameters():
         r = _rel(p.main_grad, P[n].grad)
+        errs.append((round(r, 5), n))
         if not r < 3e-2:
             bad.append((n, round(r, 4)))
+    print("loss", loss.item(), "ref", ref.item(), "worst grad rel errors:", sorted(errs)[-6:])
     assert not bad, bad
 
 
@@ -126,6 +128,7 @@ def test_gpt2_xl_width_three_steps_match_torch_adamw():
     bad = []
     masters = {s.name: _slot_view(st.flat.master, s.offset, s.param) for s in st.flat.slots}
     d = cfg.n_embd
+    worst = []
     for n, p in model.named_parameters():
         got = masters[n] - master0[n]
         want = P[n].detach() - master0[n]
@@ -137,6 +140,8 @@ def test_gpt2_xl_width_three_steps_match_torch_adamw():
             got, want = torch.cat([got[:d], got[2 * d:]]), torch.cat([want[:d], want[2 * d:]])
         cos = F.cosine_similarity(got.reshape(1, -1), want.reshape(1, -1)).item()
         nr = (got.norm() / (want.norm() + 1e-12)).item()
+        worst.append((round(cos, 4), round(nr, 4), n))
         if not (cos >= 0.97 and 0.9 <= nr <= 1.1):
             bad.append((n, round(cos, 4), round(nr, 4)))
+    print("losses", losses, "ref", ref_losses, "lowest update cosines:", sorted(worst)[:6])
     assert not bad, bad
