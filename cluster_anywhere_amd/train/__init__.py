@@ -9,8 +9,10 @@ TRAIN_DATASET_KEY = "train"
 
 
 class SyncConfig:
-    """Checkpoint/artifact sync options (reference: train/_internal/syncer.py). Storage
-    here is a shared filesystem path, so syncing is a no-op kept for API parity."""
+    """Checkpoint / artifact sync options (reference: train/_internal/syncer.py).
+    Train workers upload checkpoints to the run's storage filesystem themselves
+    (train/storage.py); Tune mirrors its locally staged experiment directory to a
+    remote storage every ``sync_period`` seconds and at the end (tune/tuner.py)."""
 
     def __init__(self, sync_period: int = 300, sync_timeout: int = 1800, sync_artifacts: bool = False,
                  sync_artifacts_on_checkpoint: bool = True, **_kw):

@@ -9,7 +9,7 @@ import threading
 import time
 from typing import Any, Dict, Optional
 
-from .checkpoint import Checkpoint, persist
+from .checkpoint import Checkpoint
 
 
 class TrainContext:
@@ -64,11 +64,18 @@ class TrainContext:
 
 class _Session:
     def __init__(self, ctx: TrainContext, checkpoint: Optional[Checkpoint], dataset_shards=None,
-                 run_dir: str = "", ckpt_index_start: int = 0):
+                 storage=None, ckpt_index_start: int = 0):
         self.ctx = ctx
         self.loaded_checkpoint = checkpoint
         self.dataset_shards = dataset_shards or {}
-        self.run_dir = run_dir
+        # train/storage.py StorageContext (None: checkpoints stay where they are); a
+        # plain directory string is accepted as a local storage root
+        if isinstance(storage, str):
+            from .storage import StorageContext
+
+            storage = StorageContext(os.path.dirname(storage), os.path.basename(storage)) if storage else None
+        self.storage = storage
+        self.run_dir = storage.experiment_fs_path if storage is not None else ""
         self.reports: "queue.Queue" = queue.Queue()
         self.ckpt_index = ckpt_index_start
         self.iteration = 0
@@ -83,8 +90,13 @@ class _Session:
         persisted = None
         if checkpoint is not None:
             name = checkpoint_dir_name or f"checkpoint_{self.ckpt_index:06d}"
-            dest = os.path.join(self.run_dir, name) if self.run_dir else checkpoint.path
-            persisted = persist(checkpoint, dest).path
+            if self.storage is not None:
+                # upload from THIS worker's process: its directory may be node-local
+                # (reference: StorageContext.persist_current_checkpoint)
+                with checkpoint.as_directory() as local:
+                    persisted = self.storage.persist_checkpoint(local, name)
+            else:
+                persisted = checkpoint.path
             self.ckpt_index += 1
         m = dict(metrics)
         m.setdefault("training_iteration", self.iteration)

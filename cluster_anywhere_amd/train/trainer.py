@@ -66,15 +66,30 @@ class Result:
         return f"Result(metrics={self.metrics}, path={self.path}, checkpoint={self.checkpoint}, error={self.error!r})"
 
     @classmethod
-    def from_path(cls, path: str) -> "Result":
+    def from_path(cls, path: str, storage_filesystem=None) -> "Result":
+        """A finished run's result from its experiment directory (a local path, a
+        URI, or a path inside ``storage_filesystem``)."""
+        from .storage import StorageContext
+
+        st = StorageContext(os.path.dirname(path.rstrip("/")) if not "://" in path else path.rstrip("/").rsplit("/", 1)[0],
+                            os.path.basename(path.rstrip("/")), storage_filesystem)
         hist = []
-        p = os.path.join(path, "result.json")
-        if os.path.exists(p):
-            with open(p) as f:
-                hist = [json.loads(l) for l in f if l.strip()]
-        ckpts = sorted(d for d in os.listdir(path) if d.startswith("checkpoint_"))
-        ck = Checkpoint(os.path.join(path, ckpts[-1])) if ckpts else None
-        return cls(hist[-1] if hist else {}, ck, None, path, hist)
+        try:
+            if st.local:
+                with open(os.path.join(st.experiment_fs_path, "result.json")) as f:
+                    text = f.read()
+            else:
+                with st.storage_filesystem.open_input_stream(st._join("result.json")) as f:
+                    text = f.read().decode()
+            hist = [json.loads(l) for l in text.splitlines() if l.strip()]
+        except (OSError, FileNotFoundError):
+            pass
+        ckpts = st.list_checkpoints()
+        fs = None if st.local else st.storage_filesystem
+        ck = Checkpoint(st.checkpoint_fs_path(ckpts[-1]), filesystem=fs) if ckpts else None
+        r = cls(hist[-1] if hist else {}, ck, None, st.experiment_fs_path, hist)
+        r.filesystem = fs
+        return r
 
 
 class Backend:
@@ -125,9 +140,9 @@ class _TrainWorker:
         backend.on_start(rank, world_size, master_addr, master_port, device_id)
         return True
 
-    def run(self, fn, config, ckpt_path, shards, ctx_kwargs, run_dir, ckpt_index):
-        ckpt = Checkpoint(ckpt_path) if ckpt_path else None
-        self.session = _Session(TrainContext(**ctx_kwargs), ckpt, shards, run_dir, ckpt_index)
+    def run(self, fn, config, ckpt_path, shards, ctx_kwargs, storage, ckpt_index, ckpt_fs=None):
+        ckpt = Checkpoint(ckpt_path, filesystem=ckpt_fs) if ckpt_path else None
+        self.session = _Session(TrainContext(**ctx_kwargs), ckpt, shards, storage, ckpt_index)
         init_session(self.session)
 
         def target():
@@ -195,11 +210,19 @@ class DataParallelTrainer:
 
     # ------------------------------------------------------------------ helpers
     def _run_dir(self):
+        """Create the experiment directory on the run's storage (RunConfig
+        storage_path / storage_filesystem, train/storage.py); returns its path there."""
+        from .storage import StorageContext
+
         name = self.run_config.name or f"{type(self).__name__}_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
         self.run_config.name = name
-        d = os.path.join(self.run_config.storage_path, name)
-        os.makedirs(d, exist_ok=True)
-        return d
+        self._storage = StorageContext(self.run_config.storage_path, name, self.run_config.storage_filesystem)
+        return self._storage.create_experiment_dir()
+
+    def _ckpt(self, path) -> Checkpoint:
+        """A checkpoint persisted on the run's storage."""
+        st = getattr(self, "_storage", None)
+        return Checkpoint(path, filesystem=None if st is None or st.local else st.storage_filesystem)
 
     def _split_datasets(self, n):
         shards = [dict() for _ in range(n)]
@@ -227,7 +250,7 @@ class DataParallelTrainer:
                            int(os.environ.get("GROUP_RANK", "0")), self.run_config.name,
                            self.run_config.name, "spmd", self.run_config.storage_path, self.metadata, run_dir)
         shards = self._split_datasets(world)[rank] if self.datasets else {}
-        s = _Session(ctx, self.resume_from_checkpoint, shards, run_dir if rank == 0 else "", 0)
+        s = _Session(ctx, self.resume_from_checkpoint, shards, self._storage if rank == 0 else None, 0)
         init_session(s)
         history, last, ckpt = [], {}, None
         error = None
@@ -248,10 +271,10 @@ class DataParallelTrainer:
             history.append(m)
             last = m
             if p:
-                ckpt = Checkpoint(p)
+                ckpt = self._ckpt(p)
         if error is not None:
             raise error
-        return Result(last, ckpt, None, run_dir, history)
+        return self._result(last, ckpt, None, run_dir, history)
 
     # ------------------------------------------------------------ actor mode
     def fit(self) -> Result:
@@ -279,35 +302,45 @@ class DataParallelTrainer:
                 if af.history:
                     last_metrics = af.history[-1]
                 for m, p in af.ckpts:
-                    latest_ckpt = Checkpoint(p)
+                    latest_ckpt = self._ckpt(p)
                     kept = self._track_checkpoint(kept, m, p)
                 ckpt_index = af.ckpt_index
                 failures += 1
                 if fc.max_failures >= 0 and failures > fc.max_failures:
                     err = TrainingFailedError(f"Training failed after {failures} attempt(s): {af.error}")
                     err.__cause__ = af.error if isinstance(af.error, BaseException) else None
-                    result = Result(last_metrics, latest_ckpt, err, run_dir, history,
-                                    [(Checkpoint(p), m) for m, p in kept])
+                    result = self._result(last_metrics, latest_ckpt, err, run_dir, history,
+                                          [(self._ckpt(p), m) for m, p in kept])
                     self._write_history(run_dir, history)
                     raise err
                 continue
             hist, ckpts, ckpt_index = res
             history.extend(hist)
             for m, p in ckpts:
-                latest_ckpt = Checkpoint(p)
+                latest_ckpt = self._ckpt(p)
                 kept = self._track_checkpoint(kept, m, p)
             if hist:
                 last_metrics = hist[-1]
             break
         self._write_history(run_dir, history)
-        return Result(last_metrics, latest_ckpt, None, run_dir, history,
-                      [(Checkpoint(p), m) for m, p in kept])
+        return self._result(last_metrics, latest_ckpt, None, run_dir, history,
+                            [(self._ckpt(p), m) for m, p in kept])
+
+    def _result(self, *a) -> Result:
+        r = Result(*a)
+        st = getattr(self, "_storage", None)
+        r.filesystem = None if st is None or st.local else st.storage_filesystem
+        return r
 
     def _write_history(self, run_dir, history):
+        text = "".join(json.dumps({k: v for k, v in m.items() if _jsonable(v)}) + "\n" for m in history)
         try:
-            with open(os.path.join(run_dir, "result.json"), "w") as f:
-                for m in history:
-                    f.write(json.dumps({k: v for k, v in m.items() if _jsonable(v)}) + "\n")
+            st = getattr(self, "_storage", None)
+            if st is not None:
+                st.write_text("result.json", text)
+            else:
+                with open(os.path.join(run_dir, "result.json"), "w") as f:
+                    f.write(text)
         except OSError:
             pass
 
@@ -328,7 +361,11 @@ class DataParallelTrainer:
                 drop = [d for d in drop if d is not latest]
                 keep.append(latest)
             for m, p in drop:
-                shutil.rmtree(p, ignore_errors=True)
+                st = getattr(self, "_storage", None)
+                if st is not None:
+                    st.delete(p)
+                else:
+                    shutil.rmtree(p, ignore_errors=True)
             kept = [k for k in kept if k in keep]
         return kept
 
@@ -428,8 +465,9 @@ class _WorkerGroup:
                        storage_path=tr.run_config.storage_path, metadata=tr.metadata,
                        trial_dir=self.run_dir)
             runs.append(w.run.remote(tr.train_loop_per_worker, tr.train_loop_config,
-                                     self.ckpt.path if self.ckpt else None, shards[rank], ctx, self.run_dir,
-                                     self.ckpt_index))
+                                     self.ckpt.path if self.ckpt else None, shards[rank], ctx,
+                                     getattr(tr, "_storage", None), self.ckpt_index,
+                                     getattr(self.ckpt, "filesystem", None) if self.ckpt else None))
         core.get(runs, timeout=600)
         self.done = [False] * n
         self.started_at = time.time()

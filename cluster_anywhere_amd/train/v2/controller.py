@@ -121,7 +121,7 @@ class TrainController:
             return
         self.history.extend(wg.history)
         for m, p in wg.ckpts:
-            self.latest_ckpt = Checkpoint(p)
+            self.latest_ckpt = self.trainer._ckpt(p)
             self.kept = self.trainer._track_checkpoint(self.kept, m, p)
         self.ckpt_index = wg.ckpt_index
         wg.history, wg.ckpts = [], []
@@ -233,8 +233,8 @@ class TrainController:
     def get_result(self) -> Result:
         last = self.history[-1] if self.history else {}
         err = self.state.error if self.state.type == TrainControllerStateType.ERRORED else None
-        res = Result(last, self.latest_ckpt, err, self.run_dir, self.history,
-                     [(Checkpoint(p), m) for m, p in self.kept])
+        res = self.trainer._result(last, self.latest_ckpt, err, self.run_dir, self.history,
+                                   [(self.trainer._ckpt(p), m) for m, p in self.kept])
         if err is not None:
             raise err
         return res

@@ -228,7 +228,8 @@ class _TrialRunner:
 
 class TuneController:
     def __init__(self, trainable, param_space: Dict, tune_config, run_config, exp_dir: str,
-                 trials: Optional[List[Trial]] = None):
+                 trials: Optional[List[Trial]] = None, syncer=None):
+        self.syncer = syncer  # mirror of exp_dir to remote storage (tuner._Syncer) or None
         self.trainable = trainable
         self.param_space = param_space or {}
         self.tc = tune_config
@@ -513,6 +514,11 @@ class TuneController:
             self.searcher.save(os.path.join(self.exp_dir, "searcher_state.pkl"))
         except Exception:
             pass
+        if self.syncer is not None:
+            try:
+                self.syncer.sync(force=force)
+            except Exception as e:  # storage hiccup: keep running, retry at the next save
+                print(f"tune: syncing the experiment to storage failed: {e}", flush=True)
 
     def run(self):
         budget = self.tc.time_budget_s

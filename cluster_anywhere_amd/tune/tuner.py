@@ -158,7 +158,13 @@ class Tuner:
         name = self.run_config.name or f"{getattr(self.trainable, '__name__', type(self.trainable).__name__)}" \
                                        f"_{time.strftime('%Y-%m-%d_%H-%M-%S')}"
         self.run_config.name = name
-        d = os.path.join(self.run_config.storage_path, name)
+        self._storage = _remote_storage(self.run_config)
+        if self._storage is not None:
+            # remote storage (URI / storage_filesystem): the experiment is staged in a
+            # local directory of the driver and mirrored to the storage filesystem
+            d = os.path.join(_staging_root(), name)
+        else:
+            d = os.path.join(self.run_config.storage_path, name)
         os.makedirs(d, exist_ok=True)
         self._exp_dir = d
         return d
@@ -167,11 +173,20 @@ class Tuner:
         core._ensure_init()
         exp_dir = self._experiment_dir()
         self._save_tuner(exp_dir)
+        st = getattr(self, "_storage", None)
+        syncer = None
+        if st is not None:
+            st.create_experiment_dir()
+            period = float(getattr(self.run_config.sync_config, "sync_period", 60) or 60)
+            syncer = _Syncer(exp_dir, st, period)
         ctl = TuneController(self.trainable, self.param_space, self.tune_config, self.run_config,
-                             exp_dir, self._restored)
+                             exp_dir, self._restored, syncer=syncer)
         trials = ctl.run()
         self._restored = trials
-        return ResultGrid(trials, exp_dir, self.tune_config.metric, self.tune_config.mode)
+        grid = ResultGrid(trials, exp_dir, self.tune_config.metric, self.tune_config.mode)
+        if st is not None:
+            grid.storage_filesystem, grid.storage_path = st.storage_filesystem, st.experiment_fs_path
+        return grid
 
     def get_results(self) -> ResultGrid:
         if self._restored is None:
@@ -190,15 +205,36 @@ class Tuner:
             pass
 
     @classmethod
-    def can_restore(cls, path: str) -> bool:
+    def can_restore(cls, path: str, storage_filesystem=None) -> bool:
+        if storage_filesystem is not None or "://" in path:
+            from ..train.storage import get_fs_and_path
+            import pyarrow.fs as pafs
+
+            fs, p = get_fs_and_path(path, storage_filesystem)
+            return fs.get_file_info(p.rstrip("/") + "/experiment_state.json").type == pafs.FileType.File
         return os.path.exists(os.path.join(path, "experiment_state.json"))
 
     @classmethod
     def restore(cls, path: str, trainable, *, resume_unfinished: bool = True, resume_errored: bool = False,
-                restart_errored: bool = False, param_space: Optional[Dict] = None) -> "Tuner":
+                restart_errored: bool = False, param_space: Optional[Dict] = None, **kw) -> "Tuner":
         """Resume an interrupted experiment: finished trials are kept, unfinished
-        ones relaunch from their latest checkpoint (errored ones on request)."""
+        ones relaunch from their latest checkpoint (errored ones on request).
+        ``path`` may be a URI or a path inside ``storage_filesystem``: the
+        experiment is downloaded into the local staging directory first."""
         import cloudpickle
+
+        storage_filesystem = kw.get("storage_filesystem")
+        remote = storage_filesystem is not None or "://" in path
+        if remote:
+            from ..train.storage import download_dir, get_fs_and_path
+
+            fs, fs_path = get_fs_and_path(path, storage_filesystem)
+            fs_path = fs_path.rstrip("/")
+            local = os.path.join(_staging_root(), os.path.basename(fs_path))
+            download_dir(fs, fs_path, local)
+            remote_root = (path.rstrip("/").rsplit("/", 1)[0] if "://" in path
+                           else os.path.dirname(fs_path) if storage_filesystem is None else fs_path.rsplit("/", 1)[0])
+            path = local
 
         with open(os.path.join(path, "experiment_state.json")) as f:
             st = json.load(f)
@@ -211,7 +247,10 @@ class Tuner:
             tc, rc = saved["tune_config"], saved["run_config"]
             ps = param_space or saved["param_space"]
         tc._searcher_finished = st.get("searcher_finished", False)
-        rc.storage_path = os.path.dirname(os.path.abspath(path))
+        if remote:  # keep mirroring to where it came from
+            rc.storage_path, rc.storage_filesystem = remote_root, storage_filesystem
+        else:
+            rc.storage_path = os.path.dirname(os.path.abspath(path))
         rc.name = os.path.basename(os.path.abspath(path))
         trials = []
         for ts in st["trials"]:
@@ -301,3 +340,39 @@ def run(run_or_experiment, *, config: Optional[Dict] = None, name: Optional[str]
     tuner = Tuner(trainable, param_space=config or {}, tune_config=tc, run_config=rc)
     grid = tuner.fit()
     return ExperimentAnalysis(grid._trials, grid.experiment_path, metric, mode)
+
+
+def _staging_root() -> str:
+    import tempfile
+
+    return os.environ.get("CAAMD_TUNE_STAGING_DIR") or os.path.join(tempfile.gettempdir(), "caamd_tune_staging")
+
+
+def _remote_storage(run_config):
+    """A StorageContext when the run's storage is not a plain local path."""
+    sp, fs = run_config.storage_path, getattr(run_config, "storage_filesystem", None)
+    if fs is None and not (isinstance(sp, str) and "://" in sp):
+        return None
+    from ..train.storage import StorageContext
+
+    st = StorageContext(sp, run_config.name, fs)
+    return None if st.local and fs is None and not sp.startswith("file://") else st
+
+
+class _Syncer:
+    """Mirror of the local experiment staging directory to the storage filesystem
+    (reference role: tune/syncer.py): at most every ``period_s`` seconds, and on
+    ``sync(force=True)`` (end of the experiment)."""
+
+    def __init__(self, local_dir: str, storage, period_s: float = 60.0):
+        self.local_dir, self.storage, self.period_s = local_dir, storage, period_s
+        self.last = 0.0
+
+    def sync(self, force: bool = False):
+        now = time.time()
+        if not force and now - self.last < self.period_s:
+            return
+        self.last = now
+        from ..train.storage import upload_dir
+
+        upload_dir(self.local_dir, self.storage.storage_filesystem, self.storage.experiment_fs_path)
