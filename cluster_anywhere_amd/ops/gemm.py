@@ -42,9 +42,14 @@ K64 = os.environ.get("CAAMD_GEMM_K64", "1") == "1"
 K64_ALGO = 4009
 
 
+# 256 x 256 tiles on the full-line kernel too (the LM-head logits GEMM: vocab 50432 is
+# not a multiple of 320); CAAMD_GEMM_K64_256=0: those stay on the ping-pong kernel
+K64_256 = os.environ.get("CAAMD_GEMM_K64_256", "1") == "1"
+
+
 def k64_ok(layout: int, epi: int, bm: int, bn: int, N: int, K: int) -> bool:
-    return (K64 and layout == 0 and (bm, bn) == (256, 320) and epi != EPI_F32 and max(N, K) >= 4096
-            and K % 64 == 0)
+    tiles = (bm, bn) == (256, 320) or (K64_256 and (bm, bn) == (256, 256))
+    return (K64 and layout == 0 and tiles and epi != EPI_F32 and max(N, K) >= 4096 and K % 64 == 0)
 MAX_TAIL_SPLIT = int(os.environ.get("CAAMD_GEMM_TAIL_SPLIT", "4"))
 
 EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_BIAS_GELU, EPI_DGELU, EPI_SWIGLU = range(6)

@@ -68,6 +68,10 @@ class AlgorithmConfig:
         self.num_envs_per_env_runner = 1
         self.rollout_fragment_length: Any = "auto"
         self.num_cpus_per_env_runner = 1
+        # > 0: env runners act on a (fractional) GPU -- their module forward runs on
+        # the device instead of the runner's one CPU thread (reference:
+        # AlgorithmConfig.env_runners(num_gpus_per_env_runner=...))
+        self.num_gpus_per_env_runner = 0
         # learners
         self.num_learners = 0
         self.num_gpus_per_learner = 1
@@ -140,10 +144,12 @@ class AlgorithmConfig:
 
     def env_runners(self, *, num_env_runners=NotProvided, num_envs_per_env_runner=NotProvided,
                     rollout_fragment_length=NotProvided, num_cpus_per_env_runner=NotProvided,
+                    num_gpus_per_env_runner=NotProvided,
                     env_to_module_connector=NotProvided, module_to_env_connector=NotProvided, **_):
         return self._set(num_env_runners=num_env_runners, num_envs_per_env_runner=num_envs_per_env_runner,
                          rollout_fragment_length=rollout_fragment_length,
                          num_cpus_per_env_runner=num_cpus_per_env_runner,
+                         num_gpus_per_env_runner=num_gpus_per_env_runner,
                          env_to_module_connector=env_to_module_connector,
                          module_to_env_connector=module_to_env_connector)
 
@@ -370,7 +376,7 @@ class AlgorithmConfig:
                 "rollout_fragment_length": self.get_rollout_fragment_length(), "seed": self.seed,
                 "gamma": self.gamma, "module_factory": self.module_factory(),
                 "metrics_num_episodes_for_smoothing": self.metrics_num_episodes_for_smoothing,
-                "need_next_obs": False,
+                "need_next_obs": False, "num_gpus_per_env_runner": self.num_gpus_per_env_runner,
                 "output": self.output, "output_max_rows_per_file": self.output_max_rows_per_file,
                 "output_write_episodes": self.output_write_episodes,
                 "env_to_module_connector": self.env_to_module_connector,
@@ -443,6 +449,7 @@ class Algorithm(Trainable):
         runner_cls = MultiAgentEnvRunner if self.is_multi_agent else EnvRunner
         self.env_runner_group = EnvRunnerGroup(
             c.runner_config(), c.num_env_runners, c.num_cpus_per_env_runner, runner_cls=runner_cls,
+            num_gpus_per_env_runner=c.num_gpus_per_env_runner,
             restart_failed=c.restart_failed_env_runners, ignore_failures=c.ignore_env_runner_failures,
             max_restarts=c.max_num_env_runner_restarts, restart_delay_s=c.delay_between_env_runner_restarts_s,
             on_recreated=self._on_env_runners_recreated)
@@ -475,7 +482,30 @@ class Algorithm(Trainable):
                                         env_runner_indices=indices, is_evaluation=False)
 
     def _sync_weights(self, extra: Optional[Dict] = None):
-        self.env_runner_group.sync_weights(self.learner_group.get_module_state(), extra)
+        g = self.env_runner_group
+        if self._ipc_weights():
+            # GPU runners on this node: a device snapshot shared by HIP IPC handles
+            g.sync_weights(self.learner_group.get_module_state(on_device=True), extra, transport="ipc")
+            return
+        g.sync_weights(self.learner_group.get_module_state(), extra)
+
+    def _ipc_weights(self) -> bool:
+        """Weights go to the env runners over HIP IPC: remote runners acting on GPUs
+        and a local learner whose module lives on a GPU of this node (single node)."""
+        c = self.algo_config
+        if not (c.num_gpus_per_env_runner and self.env_runner_group.remote and not self.is_multi_agent):
+            return False
+        lg = self.learner_group
+        loc = getattr(lg, "local", None)
+        if loc is None or not hasattr(loc, "module"):
+            return False
+        try:
+            p = next(loc.module.parameters())
+        except StopIteration:
+            return False
+        from ...core import api as core
+
+        return p.is_cuda and len([n for n in core.nodes() if n.get("Alive")]) == 1
 
     def training_step(self) -> Dict[str, Any]:
         raise NotImplementedError

@@ -216,7 +216,11 @@ class Learner:
         return ent
 
     # ---------------------------------------------------------------- state
-    def get_module_state(self):
+    def get_module_state(self, on_device: bool = False):
+        """CPU state dict; ``on_device``: a detached snapshot on the learner's device
+        (for HIP-IPC weight broadcast to GPU env runners: no host copy)."""
+        if on_device:
+            return {k: v.detach().clone() for k, v in self.module.state_dict().items()}
         return self.module.get_state()
 
     def get_state(self):
@@ -450,7 +454,9 @@ class LearnerGroup:
             self._checkpoint()
         return out
 
-    def get_module_state(self):
+    def get_module_state(self, on_device: bool = False):
+        if on_device and self.local is not None:
+            return self.local.get_module_state(on_device=True)
         return self.call("get_module_state")
 
     def get_state(self):

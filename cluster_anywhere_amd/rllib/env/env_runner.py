@@ -55,6 +55,11 @@ class EnvRunner:
         self.obs_space = self.env_to_module.recompute_output_observation_space(env_obs, env_act)
         self.act_space = env_act
         self.module = config["module_factory"](self.obs_space, self.act_space)
+        # num_gpus_per_env_runner > 0: act on the runner's (fractional) GPU
+        self.device = torch.device("cpu")
+        if config.get("num_gpus_per_env_runner", 0) and torch.cuda.is_available():
+            self.device = torch.device("cuda", 0)
+            self.module.to(self.device)
         self.module.eval()
         self.episodes: List[SingleAgentEpisode] = []
         raw = self.env.reset()
@@ -146,11 +151,12 @@ class EnvRunner:
         t0 = time.time()
         for t in range(T):
             obs_buf[t] = self.obs
-            batch = {"obs": torch.from_numpy(self.obs)}
+            dev = self.device
+            batch = {"obs": torch.from_numpy(self.obs).to(dev, non_blocking=True)}
             if stateful:
                 for k, v in self.state.items():
                     st_buf[k][t] = v
-                batch["state_in"] = {k: torch.from_numpy(v) for k, v in self.state.items()}
+                batch["state_in"] = {k: torch.from_numpy(v).to(dev) for k, v in self.state.items()}
             batch.update(self.explore_extra)
             out = self.module.forward_exploration(batch) if explore else self.module.forward_inference(batch)
             new_state = {k: v.cpu().numpy() for k, v in out["state_out"].items()} if stateful else None
@@ -167,9 +173,9 @@ class EnvRunner:
             if tr.any() and hasattr(self.module, "compute_values"):
                 idx = np.nonzero(tr & ~te)[0]
                 if len(idx):
-                    vb = {"obs": torch.from_numpy(mfinal[idx])}
+                    vb = {"obs": torch.from_numpy(mfinal[idx]).to(self.device)}
                     if stateful:
-                        vb["state_in"] = {k: torch.from_numpy(v[idx]) for k, v in new_state.items()}
+                        vb["state_in"] = {k: torch.from_numpy(v[idx]).to(self.device) for k, v in new_state.items()}
                     v = self.module.compute_values(vb).cpu().numpy()
                     r_aug[idx] += gamma * v
             if need_next:
@@ -303,7 +309,8 @@ class EnvRunnerGroup:
     the failure is raised. A fan-out never waits on a dead runner's result."""
 
     def __init__(self, config: Dict[str, Any], num_env_runners: int = 0, num_cpus_per_env_runner: float = 1,
-                 runner_cls=None, *, restart_failed: bool = True, ignore_failures: bool = False,
+                 runner_cls=None, *, num_gpus_per_env_runner: float = 0, restart_failed: bool = True,
+                 ignore_failures: bool = False,
                  max_restarts: int = 1000, restart_delay_s: float = 0.0, on_recreated=None):
         self.config = config
         self.runner_cls = runner_cls or EnvRunner
@@ -324,7 +331,8 @@ class EnvRunnerGroup:
             from ...core.actor import ActorClass
 
             Remote = ActorClass(self.runner_cls, {})
-            self._spawn = lambda i: Remote.options(num_cpus=num_cpus_per_env_runner).remote(config, i + 1)
+            self._spawn = lambda i: Remote.options(num_cpus=num_cpus_per_env_runner,
+                                                   num_gpus=num_gpus_per_env_runner).remote(config, i + 1)
             self.remote = [self._spawn(i) for i in range(num_env_runners)]
             self.healthy = [True] * num_env_runners
             core.get([r.ping.remote() for r in self.remote])
@@ -428,13 +436,15 @@ class EnvRunnerGroup:
             if res:
                 return next(iter(res.values()))
 
-    def sync_weights(self, state, extra: Optional[Dict] = None):
+    def sync_weights(self, state, extra: Optional[Dict] = None, transport: Optional[str] = None):
+        """``transport="ipc"``: ``state`` holds GPU tensors that same-node GPU runners
+        map through HIP IPC handles and copy device-to-device (no host round trip)."""
         from ...core import api as core
 
         if self.local is not None:
             self.local.set_weights(state, extra)
             return
-        self._weights = (core.put(state), extra)
+        self._weights = (core.put(state, _tensor_transport=transport), extra)
         self._fanout("set_weights", *self._weights)
 
     def sync_weights_to(self, state, indices: List[int], extra: Optional[Dict] = None):

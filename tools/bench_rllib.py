@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--minibatch", type=int, default=500)
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--runner-gpus", type=float, default=0.0,
+                    help="num_gpus_per_env_runner: runners act on a GPU share (weights over HIP IPC)")
     ap.add_argument("--seconds", type=float, default=0.0,
                     help="run timed iterations until at least this many seconds passed (>= --iters)")
     args = ap.parse_args()
@@ -36,9 +38,11 @@ def main():
     from cluster_anywhere_amd import rllib
 
     gpu = torch.cuda.is_available() and args.gpus > 0
+    # the local learner uses the GPU outside the scheduler; runner shares are booked against it
     ray.init(num_cpus=args.runners + 2, num_gpus=args.gpus if gpu else 0)
     cfg = (rllib.PPOConfig().environment("FakeAtari-v0")
-           .env_runners(num_env_runners=args.runners, num_envs_per_env_runner=args.envs_per_runner)
+           .env_runners(num_env_runners=args.runners, num_envs_per_env_runner=args.envs_per_runner,
+                        num_gpus_per_env_runner=args.runner_gpus if gpu else 0)
            .learners(num_learners=0, num_gpus_per_learner=1 if gpu else 0)
            .training(train_batch_size=args.train_batch, minibatch_size=args.minibatch,
                      num_epochs=args.epochs, lr=2.5e-4, lambda_=0.95, clip_param=0.1, entropy_coeff=0.01)
@@ -69,7 +73,9 @@ def main():
         "higher_is_better": True, "data": "synthetic Atari-shaped env, random-init weights",
         "config": {"runners": args.runners, "envs_per_runner": args.envs_per_runner,
                    "train_batch_size": args.train_batch, "minibatch_size": args.minibatch,
-                   "num_epochs": args.epochs, "learner_device": "cuda" if gpu else "cpu"},
+                   "num_epochs": args.epochs, "learner_device": "cuda" if gpu else "cpu",
+                   "runner_device": "cuda" if gpu and args.runner_gpus else "cpu",
+                   "weights_transport": "ipc" if algo._ipc_weights() else "object store"},
         "sample_s": round(samp, 2), "learn_s": round(learn, 2),
         "learner_samples_per_s": round(steps * args.epochs / max(learn, 1e-9), 1),
     }), flush=True)
