@@ -240,15 +240,25 @@ def tn_plan(M: int, N: int, K: int) -> Optional[Tuple[int, int]]:
     return plan
 
 
-def run_tn(a, b, c, accumulate: bool, bm: int = 256, slices: int = 1):
+# two-slice splits combined inside the GEMM by each tile's last-arriving slice
+# (write-through slabs + ticket, algo 26) instead of a reduce launch (algo 25): measured
+# level (fc 500.7 vs 500.3 us, qkv 413.0 vs 414.2 incl. the reduce launch,
+# profiles/wgrad_tn64_inkernel_r5.jsonl), so opt-in: CAAMD_WGRAD_TN_INKERNEL=1
+TN_INKERNEL = os.environ.get("CAAMD_WGRAD_TN_INKERNEL", "0") == "1"
+
+
+def run_tn(a, b, c, accumulate: bool, bm: int = 256, slices: int = 1, inkernel: Optional[bool] = None):
     """c[M, N] (+)= a[K, M]^T b[K, N] on gemm_tn64_kernel (``slices`` > 1: lockstep
-    split-K, fp32 slabs combined in slice order by a reduce launch)."""
+    split-K, fp32 slabs summed in slice order -- by the tile's last arriving slice,
+    or by a reduce launch with ``inkernel=False``)."""
     M, N = c.shape
-    ws = None
+    ws = cnt = None
     if slices > 1:
         tiles = -(-M // bm) * (N // 320)
-        ws, _ = _workspace(c.device, slices * tiles * bm * 320, 1)
-    kernels().gemm_tn64(a, b, c, bm, accumulate, slices, ws)
+        ws, cnt = _workspace(c.device, slices * tiles * bm * 320, tiles)
+        if slices != 2 or not (TN_INKERNEL if inkernel is None else inkernel):
+            cnt = None  # the in-kernel combine takes two slices; others use the reduce launch
+    kernels().gemm_tn64(a, b, c, bm, accumulate, slices, ws, cnt)
     return c
 
 

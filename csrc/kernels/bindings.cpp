@@ -48,7 +48,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int tfull, int tS, float* tws, int* tcnt, int bpack);
 void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
 hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
-                            int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st);
+                            int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st, int* tickets);
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
@@ -967,7 +967,7 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
 // TN weight gradient on the full-line kernel (gemm.hip algo 25): c[M,N] (+)= a[K,M]^T b[K,N],
 // 256- or 192-row tiles x 320 columns, lockstep split over `slices` (ws: slices x tiles fp32 slabs)
 static void gemm_tn64(Tensor a, Tensor b, Tensor c, int64_t bm, bool accumulate, int64_t slices,
-                      c10::optional<Tensor> ws) {
+                      c10::optional<Tensor> ws, c10::optional<Tensor> tickets) {
   CHECK_BF16(a);
   CHECK_BF16(b);
   CHECK_BF16(c);
@@ -987,10 +987,17 @@ static void gemm_tn64(Tensor a, Tensor b, Tensor c, int64_t bm, bool accumulate,
     TORCH_CHECK(ws->numel() >= slices * tiles * bm * 320, "gemm_tn64: slab workspace too small");
     wp = ws->data_ptr<float>();
   }
+  int* tp = nullptr;
+  if (tickets.has_value() && slices == 2) {  // in-kernel last-arriver combine (two slices); tickets zero between launches
+    TORCH_CHECK(tickets->is_cuda() && tickets->scalar_type() == at::kInt && tickets->is_contiguous() &&
+                    tickets->numel() >= tiles, "gemm_tn64: tickets must be >= tiles contiguous int32");
+    TORCH_CHECK(slices * tiles * bm * 320 * 4 < (1LL << 32), "gemm_tn64: slabs must fit a 32-bit descriptor");
+    tp = tickets->data_ptr<int>();
+  }
   hipError_t e = caamd::gemm_tn64_launch((int)bm, accumulate, (const caamd::bf16*)a.data_ptr(),
                                          (const caamd::bf16*)b.data_ptr(), (caamd::bf16*)c.data_ptr(), (int)M,
                                          (int)N, (int)K, (int)a.size(1), (int)b.size(1), (int)c.size(1),
-                                         (int)slices, wp, cur_stream());
+                                         (int)slices, wp, cur_stream(), tp);
   TORCH_CHECK(e == hipSuccess, "gemm_tn64 launch failed: ", hipGetErrorString(e));
 }
 
@@ -1378,7 +1385,7 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("tail_split") = 1, pybind11::arg("bpack") = false);
   m.def("gemm_tn64", GUARDED(gemm_tn64), pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
         pybind11::arg("bm"), pybind11::arg("accumulate"), pybind11::arg("slices"),
-        pybind11::arg("ws") = pybind11::none());
+        pybind11::arg("ws") = pybind11::none(), pybind11::arg("tickets") = pybind11::none());
   m.def("gemm_tail_plan", [](int64_t tiles, int64_t K, int64_t ks, int64_t slots, int64_t max_split) {
     int full, S;
     caamd::gemm_tail_plan((int)tiles, (int)K, (int)ks, (int)slots, (int)max_split, &full, &S);

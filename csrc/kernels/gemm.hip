@@ -1749,7 +1749,7 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 // BM = 192 serves the 4800-row qkv gradient: 25 x 5 tiles x 2 slices = 250 runs for
 // 256 CUs (256-row tiles: 95 tiles, 190 runs).
 // ================================================================================
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, bool COMBINE = false>
 __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
   constexpr int WM = 2, WN = 4;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16, TMH = TM / 2;
@@ -1950,13 +1950,66 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
   if (LS > 1) {
     // slice partial: fp32 slab in fragment order (sk_reduce_kernel's layout)
     constexpr int SLAB = BM * BN;
-    float* mine = p.tws + ((size_t)sl * T + tile) * SLAB;
+    if constexpr (!COMBINE) {  // algo 25: a separate reduce launch combines the slabs
+      float* mine = p.tws + ((size_t)sl * T + tile) * SLAB;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
+      return;
+    } else {
+    // algo 26: the tile's LAST arriving slice combines (no reduce launch). Hand-off
+    // with write-through slabs (cdna_hip_programming.md Guideline 16, R1): every slab
+    // byte is stored `sc1` and drained by its wave before the workgroup barrier, one
+    // lane then adds to the tile's ticket (relaxed, agent scope); the last arriver
+    // reads the other slabs with `sc1` loads only (no release / acquire fences: the
+    // L2 write-backs they cost were what made the stream-K kernel's combine slow).
+    // Slices are summed in slice order: the same bits as sk_reduce_kernel.
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rw =
+        make_rsrc(p.tws, (unsigned)min((size_t)0xFFFFFFF0u, (size_t)LS * T * SLAB * 4));
+    // lane part of every slab address in one VGPR, the rest wave-uniform (soffset):
+    // 40 per-fragment VGPR offsets spilled the main loop
+    const int vlane = lane * 16;
+    auto frag_soff = [&](int s_, int i, int j) {
+      return __builtin_amdgcn_readfirstlane(
+          (int)((((size_t)s_ * T + tile) * SLAB + (size_t)((wid * TM + i) * TN + j) * 256) * 4));
+    };
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        *reinterpret_cast<f32x4*>(mine + ((size_t)((wid * TM + i) * TN + j) * 64 + lane) * 4) = acc[i][j];
-    return;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, acc[i][j]), rw, vlane, frag_soff(sl, i, j), 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains (Pitfall 14)
+    __syncthreads();
+    typedef __attribute__((address_space(3))) int lds_int;
+    lds_int* flag = (lds_int*)smem;
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(p.tcnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == LS - 1;
+      if (last) __hip_atomic_store(p.tcnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads below the ticket
+    // two slices (the host allows no other count here): the other slice's partial
+    // added to this one's registers -- a0 + a1, the bits of sk_reduce_kernel's
+    // (0 + a0) + a1. One m-row of fragments at a time: the sched barriers keep the
+    // compiler from hoisting all 40 slab loads (160 more live VGPRs spilled the
+    // main loop).
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 o[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        o[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, vlane, frag_soff(sl ^ 1, i, j), 16));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += o[j];
+    }
+    }
   }
   __syncthreads();  // the last phase's LDS reads are done before the staging overwrites
   epilogue_staged<BM, BN, TM, TN, EPI, 0>(p, acc, m0, n0, wr, wc, lane, smem, tid);
@@ -1965,13 +2018,13 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
 template <int BM, int EPI>
 static hipError_t launch_tn64(const Args& a, hipStream_t st) {
   constexpr int BN = 320;
-  auto k = gemm_tn64_kernel<BM, BN, EPI>;
+  auto k = a.algo == 26 ? gemm_tn64_kernel<BM, BN, EPI, true> : gemm_tn64_kernel<BM, BN, EPI, false>;
   constexpr int lds = 2 * 64 * (BM + BN) * 2;
   ensure_lds((const void*)k, lds);
   const int T = a.tiles_m * a.tiles_n;
   const int LS = a.tfull > 0 ? a.tfull : 1;
   hipLaunchKernelGGL(k, dim3(T * LS), dim3(NTHR), lds, st, a);
-  if (LS > 1) {
+  if (LS > 1 && a.algo != 26) {
     const long long n4 = (long long)T * (BM * BN / 4);
     hipLaunchKernelGGL((sk_reduce_kernel<BM, BN, EPI == EPI_BF16_ACC>), dim3((unsigned)((n4 + 255) / 256)),
                        dim3(256), 0, st, a, LS);
@@ -1984,9 +2037,10 @@ static hipError_t launch_tn64(const Args& a, hipStream_t st) {
 // TN weight-gradient GEMM on the full-line kernel (algo 25): c[M][N] (+)= a[K][M]^T b[K][N],
 // lockstep split over `slices` (> 1: fp32 slabs in ws, combined by a reduce launch).
 hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
-                            int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st) {
+                            int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st, int* tickets) {
+  // tickets != null: the last arriving slice of each tile combines (algo 26), else a reduce launch (25)
   gemm::Args a{A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, 1,
-               (M + bm - 1) / bm, N / 320, 0, 25, slices, 0, ws, nullptr, 0, 0};
+               (M + bm - 1) / bm, N / 320, 0, tickets ? 26 : 25, slices, 0, ws, tickets, 0, 0};
   if (bm == 256) return accumulate ? gemm::launch_tn64<256, gemm::EPI_BF16_ACC>(a, st)
                                    : gemm::launch_tn64<256, gemm::EPI_BF16>(a, st);
   if (bm == 192) return accumulate ? gemm::launch_tn64<192, gemm::EPI_BF16_ACC>(a, st)

@@ -269,10 +269,11 @@ def test_wgrad_external_combine_matches_in_kernel_bits():
     assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
 
 
+@pytest.mark.parametrize("inkernel", [True, False])
 @pytest.mark.parametrize("bm", [256, 192])
 @pytest.mark.parametrize("MN,slices", [((1600, 1600), 7), ((640, 960), 1), ((1600, 640), 3), ((960, 320), 2),
                                        ((4800, 1600), 2)])
-def test_wgrad_tn64(bm, MN, slices):
+def test_wgrad_tn64(bm, MN, slices, inkernel):
     """TN full-line weight-gradient kernel (algo 25): dW (+)= dY^T X over 4160 tokens
     (65 K-tiles: odd, and not divisible by the slice counts), ragged M (1600 = 6.25 x 256,
     8.33 x 192), single run per tile and lockstep split-K with the reduce launch,
@@ -284,15 +285,18 @@ def test_wgrad_tn64(bm, MN, slices):
     dy, x = _mk((K, M), 51), _mk((K, N), 52)
     ref = dy.float().t() @ x.float()
     c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    G.run_tn(dy, x, c, False, bm, slices)
+    G.run_tn(dy, x, c, False, bm, slices, inkernel)
     assert _rel(c, ref) < 5e-3
     c0 = _mk((M, N), 53)
     c2 = c0.clone()
-    G.run_tn(dy, x, c2, True, bm, slices)
+    G.run_tn(dy, x, c2, True, bm, slices, inkernel)
     assert _rel(c2, ref + c0.float()) < 5e-3
     c3 = torch.empty_like(c)
-    G.run_tn(dy, x, c3, False, bm, slices)
+    G.run_tn(dy, x, c3, False, bm, slices, inkernel)  # tickets were reset by the last arrivers
     assert torch.equal(c, c3)
+    c4 = torch.empty_like(c)
+    G.run_tn(dy, x, c4, False, bm, slices, not inkernel)  # both combines sum the slices in order
+    assert torch.equal(c, c4)
 
 
 def test_wgrad_tn64_strided_views_and_dispatch():

@@ -86,8 +86,9 @@ def main():
                 med, _ = timeit(lambda: G.run_sk(dy, x, c, 2, True, sk[(M, N)]), a.iters)
                 rows.append(("sk", sk[(M, N)], med))
                 for (bm, S) in pl:
-                    med, _ = timeit(lambda: G.run_tn(dy, x, c, True, bm, S), a.iters)
-                    rows.append(("tn64", f"{bm}x{S}", med))
+                    for ink in ((True, False) if S > 1 else (False,)):
+                        med, _ = timeit(lambda: G.run_tn(dy, x, c, True, bm, S, ink), a.iters)
+                        rows.append(("tn64" + ("_ink" if ink else ""), f"{bm}x{S}", med))
             for impl, cfg, med in rows:
                 print(json.dumps({"M": M, "N": N, "K": K, "impl": impl, "cfg": cfg, "us_med": round(med, 1),
                                   "pfs": round(fl / med / 1e9, 3)}), flush=True)
