@@ -1733,12 +1733,23 @@ class Head:
                     w = cand
                     break
             if w is None:
-                self.sched.release(node, demand)
-                if self.starting[key] < max(1, int(self.cpu_count)):
+                # no idle worker: start as many as the rest of the request can use
+                # right now (resources permitting), not one per round trip
+                n_fit = 1
+                while n_fit < want - len(out) and self.sched.acquire(node, demand):
+                    n_fit += 1
+                for _ in range(n_fit):
+                    self.sched.release(node, demand)
+                if gamt > 0:
+                    n_fit = 1  # GPU ids are picked per worker
+                for _ in range(n_fit):
+                    if self.starting[key] >= max(1, int(self.cpu_count)):
+                        break
                     if self._num_workers(node) >= self.max_workers and ek is not None:
                         self._evict_idle(node, key)
-                    if self._num_workers(node) < self.max_workers:
-                        self._spawn_worker(node, gpu_ids, env=env)
+                    if self._num_workers(node) >= self.max_workers:
+                        break
+                    self._spawn_worker(node, gpu_ids, env=env)
                 break
             self._take_gpus(node, gpu_ids, gamt)
             w.idle = False

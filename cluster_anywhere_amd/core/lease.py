@@ -57,6 +57,12 @@ DEPTH = int(os.environ.get("CAAMD_LEASE_DEPTH", "8"))
 LINGER = float(os.environ.get("CAAMD_LEASE_LINGER_S", "0.02"))
 SLICE = float(os.environ.get("CAAMD_LEASE_SLICE_S", "0.25"))
 MAX_WANT = int(os.environ.get("CAAMD_LEASE_MAX_WANT", "16"))
+# tasks that run longer than this (or not measured yet) go one at a time per lease, so a
+# backlog of them asks for (and spreads over) as many workers as it can use instead
+# of queueing behind one another on a few (reference: max_tasks_in_flight_per_worker=1);
+# short ones keep DEEP pipelines that hide the owner<->worker round trip
+LONG_TASK_S = float(os.environ.get("CAAMD_LEASE_LONG_TASK_S", "0.002"))
+SHORT_DEPTH = 1
 RETRY_S = 0.02
 _LEN = struct.Struct("<Q")
 
@@ -93,7 +99,8 @@ def _frame(msg) -> bytes:
 
 
 class _Key:
-    __slots__ = ("resources", "strategy", "env", "queue", "leases", "requesting", "mode", "retry_at", "active")
+    __slots__ = ("resources", "strategy", "env", "queue", "leases", "requesting", "mode", "retry_at", "active",
+                 "avg_run_s")
 
     def __init__(self, resources, strategy=None, env=None):
         self.resources = dict(resources)
@@ -105,6 +112,13 @@ class _Key:
         self.mode = "lease"  # "never": this shape cannot run on our node (head path)
         self.retry_at = 0.0
         self.active = False  # leases / queue / request outstanding (read by submitters)
+        self.avg_run_s: Optional[float] = None  # EWMA of the key's task run time (None: not seen yet)
+
+    def depth(self) -> int:
+        """Tasks in flight per lease: deep pipelines for short tasks (hide the
+        round trip), shallow ones for long or not-yet-measured tasks (parallelism)."""
+        a = self.avg_run_s
+        return DEPTH if (a is not None and a < LONG_TASK_S) else min(DEPTH, SHORT_DEPTH)
 
 
 class _Lease:
@@ -287,6 +301,12 @@ class LeaseManager:
                 continue
             task_id, results, error_kind, t0, t1, pid = msg[1:7]
             retryable = msg[7] if len(msg) > 7 else False
+            try:
+                run = max(0.0, float(t1) - float(t0))
+                st = lc.key
+                st.avg_run_s = run if st.avg_run_s is None else 0.8 * st.avg_run_s + 0.2 * run
+            except (TypeError, ValueError):
+                pass
             rec = lc.pending.pop(task_id, None)
             lc.blocked = False
             if rec is None:
@@ -327,10 +347,11 @@ class LeaseManager:
     def _pump(self, st: _Key, now: float):
         q = st.queue
         live = [lc for lc in st.leases if lc.alive and not lc.blocked and now - lc.granted_at < SLICE]
+        depth = st.depth()
         touched = []
         while q and live:
             lc = min(live, key=lambda x: len(x.pending))
-            if len(lc.pending) >= DEPTH:
+            if len(lc.pending) >= depth:
                 break
             spec, keep, resolved = q.popleft()
             fn_blob = None
@@ -346,11 +367,11 @@ class LeaseManager:
         for lc in touched:
             self._flush(lc)
         if q and not st.requesting and now >= st.retry_at:
-            cap = sum(DEPTH - len(lc.pending) for lc in live)
-            need = len(q) - max(0, cap)
+            cap = sum(max(0, depth - len(lc.pending)) for lc in live)
+            need = len(q) - cap
             if need > 0:
                 st.requesting = True
-                want = min(MAX_WANT, (need + DEPTH - 1) // DEPTH)
+                want = min(MAX_WANT, (need + depth - 1) // depth)
                 opts = {"strategy": st.strategy, "env": st.env} if (st.strategy or st.env) else None
                 self.w.request_cb(lambda r: ("lease", r, st.resources, want, opts),
                                   lambda res, st=st: self._granted_cb(st, res))

@@ -208,6 +208,22 @@ class FusedResNet(nn.Module):
             self.blocks.append((convs, down))
         self.fc_w = net.fc.weight.detach().to(device=device, dtype=dtype)
         self.fc_b = net.fc.bias.detach().to(device=device, dtype=dtype)
+        self.num_classes = self.fc_w.shape[0]
+        # classifier on the framework's MFMA GEMM (ops/gemm.py, 256 x 256 tiles) at
+        # batch sizes that are a multiple of 256: the weight is padded to a multiple of
+        # 256 rows whose bias is -inf (never the argmax). Keeps hipBLASLt (its
+        # first-call load is ~0.17 s of a fresh Data actor's start-up) out of the
+        # own-kernel forward.
+        self.fc_wp = self.fc_bp = None
+        if self.own:
+            n_pad = -(-self.num_classes // 256) * 256
+            k = self.fc_w.shape[1]
+            if k % 64 == 0:
+                wp = torch.zeros((n_pad, k), device=device, dtype=dtype)
+                wp[: self.num_classes] = self.fc_w
+                bp = torch.full((n_pad,), float("-inf"), device=device, dtype=dtype)
+                bp[: self.num_classes] = self.fc_b
+                self.fc_wp, self.fc_bp = wp, bp
 
     @torch.no_grad()
     def forward(self, x):
@@ -234,6 +250,10 @@ class FusedResNet(nn.Module):
                 y = c.own(y)
             x = convs[-1].own(y, residual=idt)
         x = x.mean(dim=(1, 2))
+        if self.fc_wp is not None and x.shape[0] % 256 == 0:
+            from ..ops.gemm import linear_nt
+
+            return linear_nt(x.contiguous(), self.fc_wp, self.fc_bp)[:, : self.num_classes]
         return F.linear(x, self.fc_w, self.fc_b)
 
     @torch.no_grad()
@@ -276,6 +296,19 @@ class ResNetPredictor:
                        if os.environ.get("CAAMD_PREDICTOR_STATS") == "1" else None)
         if dev.type == "cuda":
             torch.cuda.init()
+        # When this process registers the object-store arena with HIP (the copies of
+        # batches in it then DMA straight from shm), CAAMD_PREDICTOR_PIN_AT:
+        #   first   (default) after the first batch is out -- the registration
+        #           (~0.12 s/GB) blocks this process's HIP calls while it runs, so it
+        #           must not sit between a fresh actor and its first result;
+        #   capture right after the graph capture (time to first batch +0.5 s);
+        #   init    on a thread right after HIP init (contends with model init and
+        #           capture: measured time to first batch 1.53-1.67 s vs 1.18-1.20 s).
+        pin_at = os.environ.get("CAAMD_PREDICTOR_PIN_AT", "first")
+        self._pin_at_init = dev.type == "cuda" and pin_at == "init"
+        self._pin_after_first = False
+        if self._pin_at_init:
+            self._start_pinning()
         t1 = time.perf_counter()
         if dev.type == "cuda":
             with torch.device(dev):  # random init straight in HBM
@@ -311,7 +344,8 @@ class ResNetPredictor:
                 self._pending_capture = False
                 self.init_profile["capture_s"] = time.perf_counter() - t4
             self._early_pin = os.environ.get("CAAMD_PREDICTOR_EARLY_PIN", "0") == "1"
-            if not self._pending_capture or self._early_pin:
+            self._pin_after_first = pin_at == "first" and not self._early_pin
+            if not self._pin_at_init and (self._early_pin or (pin_at == "capture" and not self._pending_capture)):
                 self._start_pinning()
         self.init_profile["total_s"] = time.perf_counter() - t0
 
@@ -334,8 +368,15 @@ class ResNetPredictor:
         if warm:
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
-            with torch.cuda.stream(s):  # warm up MIOpen algorithm selection outside the graph
-                self._run(self.static_in)
+            with torch.cuda.stream(s):
+                # outside the graph: load every kernel / library handle the forward uses
+                # (and, for the MIOpen path, run its algorithm selection at the real
+                # shape). The own-kernel path has no per-shape selection: a smaller
+                # batch does
+                # (at a multiple of 256 where the batch is one, so the classifier
+                # takes the same GEMM path as in the graph)
+                n = (256 if self.bs % 256 == 0 else self.bs) if getattr(self.model, "own", False) else self.bs
+                self._run(self.static_in[:n])
             torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.init_profile["warmup_runs_s"] = time.perf_counter() - tw
@@ -357,7 +398,7 @@ class ResNetPredictor:
             self._capture(warm=False)
             self._pending_capture = False
             self.init_profile["capture_s"] = time.perf_counter() - tc
-            if not self._early_pin:
+            if not self._early_pin and not self._pin_at_init and not self._pin_after_first:
                 self._start_pinning()
         out = []
         st = self._stats
@@ -391,6 +432,9 @@ class ResNetPredictor:
                 res = self._run(self.static_in)
                 self._ran_eager = True
             out.append(res[:m].to("cpu", non_blocking=False).numpy())
+        if self._pin_after_first and self.graph is not None:
+            self._pin_after_first = False
+            self._start_pinning()
         if st is not None:
             st["calls"] += 1
             st["ms"] += (time.perf_counter() - t0) * 1e3

@@ -49,6 +49,25 @@ def test_burst_runs_on_leases(cluster):
     assert all(len(b) == 1 << 20 for b in out)
 
 
+@ray.remote
+def nap(s):
+    t = time.time()
+    time.sleep(s)
+    return t, os.getpid()
+
+
+def test_long_tasks_spread_over_workers(cluster):
+    """A burst of long tasks gets one lease per task (pipelining depth 1), so it
+    runs in parallel on the node's CPUs instead of queueing behind one worker."""
+    ray.get([nap.remote(0.0) for _ in range(4)])
+    for _ in range(2):  # the second burst finds the (short-then-long) key measured
+        t0 = time.time()
+        out = ray.get([nap.remote(0.3) for _ in range(4)])
+        starts = sorted(t - t0 for t, _ in out)
+        assert len({p for _, p in out}) == 4, out
+        assert starts[-1] < 0.25, starts  # all four started together (4 CPUs)
+
+
 def test_owner_local_results_escape(cluster):
     refs = [sq.remote(i) for i in range(50)]
     ray.wait(refs, num_returns=len(refs))

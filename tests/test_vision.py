@@ -86,6 +86,28 @@ def test_fused_resnet50_gpu_matches_fp32():
 
 
 @C
+def test_fused_resnet_own_classifier_gemm():
+    """At batch 256 the own-kernel forward runs the classifier on the MFMA GEMM with
+    the padded weight: logits match the hipBLASLt F.linear of the same features."""
+    torch.manual_seed(0)
+    f = resnet("resnet50").eval().fuse_for_inference(torch.bfloat16, "cuda")
+    if not f.own:
+        pytest.skip("own-kernel path disabled")
+    assert f.fc_wp is not None and f.fc_wp.shape[0] == 1024
+    x = torch.randint(0, 256, (256, 64, 64, 3), dtype=torch.uint8, device="cuda")
+    out = f.predict_uint8(x)
+    assert out.shape == (256, 1000)
+    feats = torch.randn(256, 2048, device="cuda").to(torch.bfloat16)
+    from cluster_anywhere_amd.ops.gemm import linear_nt
+
+    mine = linear_nt(feats, f.fc_wp, f.fc_bp)
+    ref = feats.float() @ f.fc_w.float().t() + f.fc_b.float()
+    torch.testing.assert_close(mine[:, :1000].float(), ref, rtol=2e-2, atol=2e-2)
+    assert torch.isneginf(mine[:, 1000:].float()).all()
+    assert torch.equal(out.argmax(1), out.float().argmax(1))
+
+
+@C
 def test_predictor_hip_graph_matches_eager():
     imgs = np.random.randint(0, 256, (300, 224, 224, 3), dtype=np.uint8)
     g = ResNetPredictor("resnet50", batch_size=128, use_graph=True, lazy_capture=False)

@@ -32,6 +32,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def make_images(batch, hw=224):
     ids = batch["id"]
+    if os.environ.get("CAAMD_BENCH_DATA_TRACE") == "1":
+        print("READ " + json.dumps({"id0": int(ids[0]), "t": time.time(), "pid": os.getpid()}), flush=True)
     img = np.empty((len(ids), hw, hw, 3), dtype=np.uint8)
     img[:] = (ids % 251).astype(np.uint8)[:, None, None, None]
     return {"image": img, "id": ids}
@@ -51,11 +53,22 @@ class StubActor:
 
 class ResNet50Actor:
     def __init__(self, model="resnet50", batch_size=512, hw=224):
+        t_enter = time.time()
         from cluster_anywhere_amd.models.resnet import ResNetPredictor
 
         self.p = ResNetPredictor(model, batch_size=batch_size, hw=hw)
+        if os.environ.get("CAAMD_BENCH_DATA_TRACE") == "1":  # start-up timeline (worker log -> driver)
+            print("ACTOR_TIMES " + json.dumps({"enter": t_enter, "ready": time.time(), "pid": os.getpid(),
+                                               **{k: round(v, 3) for k, v in self.p.init_profile.items()}}),
+                  flush=True)
 
     def __call__(self, batch):
+        if os.environ.get("CAAMD_BENCH_DATA_TRACE") == "1" and not getattr(self, "_traced", False):
+            self._traced = True
+            t = time.time()
+            out = {"id": batch["id"], "label": self.p(batch["image"])}
+            print("ACTOR_FIRST_CALL " + json.dumps({"t": t, "done": time.time(), "pid": os.getpid()}), flush=True)
+            return out
         return {"id": batch["id"], "label": self.p(batch["image"])}
 
 
@@ -109,11 +122,15 @@ def main():
     ds = pipeline(args.batch_size * max(1, args.gpus) * 2)
     warm = sum(len(b["label"]) for b in ds.iter_batches(batch_size=None))
     t0 = time.perf_counter()
+    if os.environ.get("CAAMD_BENCH_DATA_TRACE") == "1":
+        print("T0 " + json.dumps({"t0": time.time()}), flush=True)
     ds = pipeline(args.rows)
     n, n_first, t_first = 0, 0, None
     for b in ds.iter_batches(batch_size=None):
         if t_first is None:  # the actor pool is built per execution: model init + graph capture
             t_first, n_first = time.perf_counter(), len(b["label"])
+            if os.environ.get("CAAMD_BENCH_DATA_TRACE") == "1":
+                print("FIRST " + json.dumps({"t_first": time.time()}), flush=True)
         n += len(b["label"])
     dt = time.perf_counter() - t0
     t_end = time.perf_counter()
