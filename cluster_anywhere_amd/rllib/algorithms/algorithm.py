@@ -75,6 +75,9 @@ class AlgorithmConfig:
         # learners
         self.num_learners = 0
         self.num_gpus_per_learner = 1
+        self.learner_batch_transport = None
+        self.learner_checkpoint_interval = 10
+        self.learner_dist_backend = None
         self.num_cpus_per_learner = 1
         # training
         self.gamma = 0.99
@@ -156,9 +159,17 @@ class AlgorithmConfig:
     rollouts = env_runners
 
     def learners(self, *, num_learners=NotProvided, num_gpus_per_learner=NotProvided,
-                 num_cpus_per_learner=NotProvided, **_):
+                 num_cpus_per_learner=NotProvided, learner_batch_transport=NotProvided,
+                 learner_checkpoint_interval=NotProvided, learner_dist_backend=NotProvided, **_):
+        """``learner_batch_transport``: "ipc" / "shm" / "pickle" (None: ipc for GPU
+        learners on one node, else shm; see LearnerGroup); ``learner_checkpoint_interval``:
+        updates between the learner-state snapshots a restarted group restores;
+        ``learner_dist_backend``: the learners' process-group backend (None: nccl =
+        RCCL on GPU, gloo on CPU)."""
         return self._set(num_learners=num_learners, num_gpus_per_learner=num_gpus_per_learner,
-                         num_cpus_per_learner=num_cpus_per_learner)
+                         num_cpus_per_learner=num_cpus_per_learner, learner_batch_transport=learner_batch_transport,
+                         learner_checkpoint_interval=learner_checkpoint_interval,
+                         learner_dist_backend=learner_dist_backend)
 
     def training(self, **kw):
         if "model" in kw:

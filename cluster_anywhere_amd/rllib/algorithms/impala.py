@@ -13,7 +13,10 @@ network providing the KL anchor.
 Multi-agent: every module learns from its own padded ``[T_m, S_m]`` fragment
 (one column per agent segment, ``mask`` marks real steps; a segment's last
 step is terminal or cut, so V-trace never crosses into the padding); the loss
-averages over real steps only."""
+averages over real steps only. Recurrent modules (``use_lstm`` / ``use_attention``),
+single- or multi-agent, unroll each column as one T-step sequence from the state
+the runner recorded at its first step (``state_in_*``), reset at episode starts.
+"""
 from __future__ import annotations
 
 import copy
@@ -68,12 +71,28 @@ class IMPALALearner(Learner):
         else:
             msum = mask.sum().clamp(min=1.0)
             mean = lambda x: (x * mask.reshape(x.shape)).sum() / msum
-        out = self.module.forward_train({"obs": flat(b["obs"])})
+        stateful = bool(getattr(self.module, "is_stateful", lambda: False)())
+        if stateful:
+            # recurrent module: each env / agent-segment column is ONE sequence of T
+            # steps, unrolled from the state recorded at the fragment's first step
+            # and reset where an episode starts inside it (reference role:
+            # add_states_from_episodes_to_batch.py for IMPALA / APPO)
+            train_in = self._seq_batch(b, T, N)
+            out = self.module.forward_train(train_in)
+            tm = lambda x: x.view((N, T) + tuple(x.shape[1:])).transpose(0, 1).reshape((T * N,) + tuple(x.shape[1:]))  # noqa: E731
+            out = {k: tm(v) for k, v in out.items() if isinstance(v, torch.Tensor)}
+        else:
+            train_in = {"obs": flat(b["obs"])}
+            out = self.module.forward_train(train_in)
         dist = self.module.dist_cls(out["action_dist_inputs"])
         logp = dist.logp(flat(b["actions"])).view(T, N)
         values = out["vf_preds"].view(T, N)
         with torch.no_grad():
-            boot = self.module.compute_values({"obs": b["last_obs"]})
+            vb = {"obs": b["last_obs"]}
+            last_st = {k[len("last_state_"):]: v for k, v in b.items() if k.startswith("last_state_")}
+            if stateful and last_st:
+                vb["state_in"] = last_st
+            boot = self.module.compute_values(vb)
             disc = c["gamma"] * (1.0 - b["terminateds"].float())
             vs, pg_adv = vtrace(logp.detach() - b["action_logp"], disc, b["rewards"], values.detach(), boot,
                                 c["vtrace_clip_rho_threshold"], c["vtrace_clip_pg_rho_threshold"])
@@ -92,11 +111,24 @@ class IMPALALearner(Learner):
                  "entropy": ent.detach()}
         if self.appo and c.get("use_kl_loss"):
             with torch.no_grad():
-                old = self.target.forward_train({"obs": flat(b["obs"])})["action_dist_inputs"]
+                old = self.target.forward_train(train_in)["action_dist_inputs"]
+                if stateful:
+                    old = tm(old)
             kl = mean(self.module.dist_cls(old).kl(dist).view(T, N))
             loss = loss + c["kl_coeff"] * kl
             stats["mean_kl_loss"] = kl.detach()
         return {"default": loss}, stats
+
+    @staticmethod
+    def _seq_batch(b, T, N):
+        seq = lambda x: x.transpose(0, 1).contiguous()  # noqa: E731  [T, N, ...] -> [N, T, ...]
+        prev_term = torch.zeros_like(b["terminateds"], dtype=torch.float32)
+        prev_term[1:] = b["terminateds"][:-1].float()
+        st = {k[len("state_in_"):]: v[0].float() for k, v in b.items() if k.startswith("state_in_")}
+        out = {"obs": seq(b["obs"]), "resets": seq(prev_term)}
+        if st:
+            out["state_in"] = st
+        return out
 
     def after_update(self):
         if self.appo:
@@ -110,6 +142,9 @@ class IMPALALearner(Learner):
         b = {k: _to_tensor(frag[k], self.device) for k in keys}
         b["rewards"] = b["rewards"].float()
         b["last_obs"] = _to_tensor(frag["last_obs"], self.device)
+        for k in frag:  # recurrent modules: per-step states and the state after the last step
+            if k.startswith(("state_in_", "last_state_")):
+                b[k] = _to_tensor(frag[k], self.device)
         if "mask" in frag:
             b["mask"] = _to_tensor(frag["mask"], self.device).float()
         return {k: float(v) for k, v in self.update_once(b).items()}
@@ -123,6 +158,7 @@ class IMPALA(Algorithm):
     config_class = IMPALAConfig
     learner_class = IMPALALearner
     supports_multi_agent = True
+    supports_recurrent_multi_agent = True
 
     def setup_algo(self):
         self._inflight: Dict[int, Any] = {}

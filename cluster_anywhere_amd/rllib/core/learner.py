@@ -331,7 +331,7 @@ class _LearnerActor:
 
             os.environ.update({"MASTER_ADDR": addr, "MASTER_PORT": str(port), "RANK": str(rank),
                                "WORLD_SIZE": str(world)})
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = config.get("learner_dist_backend") or ("nccl" if torch.cuda.is_available() else "gloo")
             if torch.cuda.is_available():
                 gpus = [int(g) for g in os.environ.get("CAAMD_GPU_IDS", "").split(",") if g]
                 torch.cuda.set_device(gpus[0] if gpus else 0)
@@ -344,6 +344,40 @@ class _LearnerActor:
 
     def call(self, method, *args, **kwargs):
         return getattr(self.learner, method)(*args, **kwargs)
+
+    def info(self):
+        from ...runtime_context import get_runtime_context
+
+        return {"node": get_runtime_context().get_node_id(), "cuda": self.learner.device.type == "cuda"}
+
+    # -- sample-batch hand-off (LearnerGroup.update) -------------------------------
+    def stage_ipc(self, batch):
+        """Rank 0 of the HIP-IPC hand-off: the whole train batch (an object-store
+        argument, host) goes to THIS learner's HBM once; returns ``[ref]`` whose GPU
+        tensors the other learners of the node map through HIP IPC handles."""
+        from ...core import api as core
+
+        self._staged = {k: _to_tensor(v, self.learner.device) for k, v in batch.items()}
+        return [core.put(self._staged, _tensor_transport="ipc")]
+
+    def update_shard(self, staged, i, n, mbs, num_epochs, shuffle):
+        """Train on shard ``i`` of ``n``: of rank 0's staged HBM batch (``staged``
+        None on rank 0 itself; the IPC-mapped dict elsewhere, copied device to
+        device into this learner's own memory) or of a host batch (``host=True``
+        path, ``update_shard_host``)."""
+        b = self._staged if staged is None else staged
+        per = next(iter(b.values())).shape[0] // n
+        shard = {k: v[i * per:(i + 1) * per] for k, v in b.items()}
+        if staged is not None:
+            shard = {k: v.to(self.learner.device, copy=True) for k, v in shard.items()}
+        del b, staged
+        if i == 0:
+            self._staged = None  # peers keep their IPC mappings alive (torch IPC refcounts)
+        return self.learner.update(shard, mbs, num_epochs, shuffle)
+
+    def update_shard_host(self, batch, i, n, mbs, num_epochs, shuffle):
+        return self.learner.update(_shard_nested(batch, i, n), mbs, num_epochs, shuffle)
+
 
 
 def _free_port():
@@ -363,7 +397,19 @@ class LearnerGroup:
     group down (its process group is broken), starts a new one on a fresh
     rendezvous port, restores the last learner state this group saw (the state of
     the last completed update: module weights, optimizer moments, update count)
-    and runs the call again."""
+    and runs the call again. The state to restore is rank 0's ``get_state``
+    result, kept as an object-store ref owned by the group, after the first update
+    and then every
+    ``learner_checkpoint_interval`` updates (default 10: a restart may replay up
+    to that many updates; 1 = after every update), never pulled to the driver.
+
+    Train batches reach the learner actors (``learner_batch_transport``):
+    ``"ipc"`` (default when every learner is a GPU learner on one node; BASELINE
+    config 4's hipIpc sample-batch hand-off): the batch is put into the object
+    store once, rank 0 copies it host->HBM once, and the other learners copy their
+    shards HBM->HBM out of rank 0's memory through HIP IPC handles; ``"shm"``
+    (default otherwise): put once, every learner slices its shard out of the
+    shared-memory object; ``"pickle"``: one pickled shard per learner."""
 
     def __init__(self, learner_cls, config: Dict[str, Any], module_factory, obs_space, act_space):
         self.n = config.get("num_learners", 0)
@@ -371,8 +417,11 @@ class LearnerGroup:
         self.actors = []
         self.restart_failed = bool(config.get("restart_failed_learners", True))
         self.max_restarts = int(config.get("max_num_learner_restarts", 100))
+        self.ckpt_every = max(1, int(config.get("learner_checkpoint_interval", 10)))
         self.num_restarts = 0
         self._last_state = None
+        self._updates = 0
+        self._info = []
         self._spec = (learner_cls, config, module_factory, obs_space, act_space)
         if self.n == 0:
             self.local = learner_cls(config, module_factory, obs_space, act_space)
@@ -392,7 +441,7 @@ class LearnerGroup:
                                                            "HSA_ENABLE_IPC_MODE_LEGACY": "0"}})
                        .remote(learner_cls, config, module_factory, obs_space, act_space, i, self.n,
                                "127.0.0.1", port) for i in range(self.n)]
-        core.get([a.call.remote("get_module_state") for a in self.actors])
+        self._info = core.get([a.info.remote() for a in self.actors])
 
     def _restart(self, err):
         import logging
@@ -411,37 +460,71 @@ class LearnerGroup:
                 pass
         self._start()
         if self._last_state is not None:
+            # an object-store ref (rank 0's snapshot) or a state dict (set_state)
             core.get([a.call.remote("set_state", self._last_state) for a in self.actors])
 
     def _run(self, make_calls):
         """``make_calls()`` -> refs, one per learner actor; their results. Restarts
-        the group and retries when an actor died."""
+        the group and retries when an actor died (also while making the calls)."""
         from ...core import api as core
         from ...exceptions import RayActorError, WorkerCrashedError
 
         while True:
-            refs = make_calls()
             try:
-                return core.get(refs)
+                return core.get(make_calls())
             except (RayActorError, WorkerCrashedError) as e:
                 self._restart(e)
 
-    def _checkpoint(self):
-        """Remember the state to restore after a restart (rank 0's, host tensors)."""
+    def _checkpoint(self, force: bool = False):
+        """Snapshot the state to restore after a restart: rank 0 puts it into the
+        object store and the group keeps the ref (first update, then every
+        ``ckpt_every`` updates)."""
         if self.restart_failed and self.local is None:
-            from ...core import api as core
+            self._updates += 1
+            if force or self._last_state is None or self._updates % self.ckpt_every == 0:
+                from ...core import api as core
 
-            self._last_state = core.get(self.actors[0].call.remote("get_state"))
+                # the RETURN value of rank 0's get_state: owned by this process (it
+                # outlives the actor), kept as a ref and never deserialised here
+                ref = self.actors[0].call.remote("get_state")
+                core.wait([ref], num_returns=1)
+                self._last_state = ref
 
     def _shard(self, batch, i):
         return _shard_nested(batch, i, self.n)
 
+    def batch_transport(self, batch=None) -> str:
+        t = self._spec[1].get("learner_batch_transport")
+        flat = batch is None or all(not isinstance(v, dict) for v in batch.values())
+        if t == "ipc" and not flat:
+            t = "shm"  # multi-module (nested) batches: shared-memory hand-off
+        if t:
+            return t
+        one_node = len({i["node"] for i in self._info}) == 1
+        return "ipc" if (flat and one_node and self._info and all(i["cuda"] for i in self._info)) else "shm"
+
     def update(self, batch, minibatch_size=None, num_epochs=1, shuffle=True):
         if self.local is not None:
             return self.local.update(batch, minibatch_size, num_epochs, shuffle)
+        from ...core import api as core
+
         mbs = None if minibatch_size is None else max(1, minibatch_size // self.n)
-        res = self._run(lambda: [a.call.remote("update", self._shard(batch, i), mbs, num_epochs, shuffle)
-                                 for i, a in enumerate(self.actors)])
+        t = self.batch_transport(batch)
+        if t == "pickle":
+            res = self._run(lambda: [a.call.remote("update", self._shard(batch, i), mbs, num_epochs, shuffle)
+                                     for i, a in enumerate(self.actors)])
+        else:
+            bref = core.put(batch)  # one host copy for every learner
+
+            def calls():
+                if t == "ipc":
+                    staged = core.get(self.actors[0].stage_ipc.remote(bref))[0]
+                    return [a.update_shard.remote(None if i == 0 else staged, i, self.n, mbs, num_epochs, shuffle)
+                            for i, a in enumerate(self.actors)]
+                return [a.update_shard_host.remote(bref, i, self.n, mbs, num_epochs, shuffle)
+                        for i, a in enumerate(self.actors)]
+
+            res = self._run(calls)
         self._checkpoint()
         return _mean_nested(res)
 
@@ -468,6 +551,7 @@ class LearnerGroup:
         self._run(lambda: [a.call.remote("set_state", st) for a in self.actors])
         if self.restart_failed:
             self._last_state = st
+            self._updates = 0
 
     def stop(self):
         from ...core import api as core

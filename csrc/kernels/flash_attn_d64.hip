@@ -676,6 +676,10 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
 // {Q image, dO image, lse2[64], delta[64]} double-buffered. Q and dO are read
 // by rows (S^T, dP^T) and transposed (dK^T, dV^T) from the same image.
 // ----------------------------------------------------------------------------
+// ABL (timing ablations, tools/bench_attn.py with CAAMD_FA64_BWD_ABL; production 0):
+// bit 0 no DMA inside the loop (stale tiles), bit 1 no per-tile wait + barrier,
+// bit 2 no softmax / dS VALU (P = S, dS = dP).
+template <int ABL = 0>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ dout,
                                                           const float* __restrict__ lse2g,
@@ -781,6 +785,9 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
+          if constexpr (ABL & 4) {
+            continue;
+          }
           float p = fexp2(__builtin_fmaf(sacc[i], scale_log2, -l4[j]));
           if constexpr (need_mask) {
             const int c = qh * 32 + 8 * g + j;
@@ -812,13 +819,15 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
   auto iter = [&](int qt, auto mask_c) {
     const int q0 = qt * 64;
     const int stg = (qt - qt0) % 3;
-    const bool ahead = qt + 2 < nqt;
+    const bool ahead = (ABL & 1) ? false : qt + 2 < nqt;
     if (ahead) issue(qt + 2, smem + ((qt + 2 - qt0) % 3) * STAGE);
     if (!(causal && q0 + 63 < key0w) && key0w < T)  // wave-uniform
       tile(mask_c, smem + stg * STAGE, smem_u + stg * STAGE, q0);
-    if (wave < 2) wait_next<5>(ahead);  // waves 0 / 1 also DMA the lse2 / delta rows
-    else wait_next<4>(ahead);
-    barrier_keep_dma();
+    if constexpr (!(ABL & 2)) {
+      if (wave < 2) wait_next<5>(ahead);  // waves 0 / 1 also DMA the lse2 / delta rows
+      else wait_next<4>(ahead);
+      barrier_keep_dma();
+    }
   };
   const int nfull = T / 64;  // tiles entirely inside the sequence
   const int pro = min(nqt, qt0 + (causal ? 2 : 0));
@@ -894,7 +903,20 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
   const int nqb = (T + 127) / 128;  // (a 256-query dQ block variant spilled and was removed in round 4)
   hipLaunchKernelGGL(fa64::bwd_dq_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout, lse,
                      delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
-  hipLaunchKernelGGL(fa64::bwd_dkdv_kernel, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
+  static const int abl = [] {  // development timing ablations of dK/dV (tools/bench_attn.py)
+    const char* e = std::getenv("CAAMD_FA64_BWD_ABL");
+    return e ? std::atoi(e) : 0;
+  }();
+  auto kern = fa64::bwd_dkdv_kernel<0>;
+  switch (abl) {
+    case 1: kern = fa64::bwd_dkdv_kernel<1>; break;
+    case 2: kern = fa64::bwd_dkdv_kernel<2>; break;
+    case 3: kern = fa64::bwd_dkdv_kernel<3>; break;
+    case 4: kern = fa64::bwd_dkdv_kernel<4>; break;
+    case 7: kern = fa64::bwd_dkdv_kernel<7>; break;
+    default: break;
+  }
+  hipLaunchKernelGGL(kern, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
                      lse2, delta, dqkv, T, H, nkb, scale_log2, scale, causal, dbias);
 }
 

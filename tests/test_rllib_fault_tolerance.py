@@ -115,13 +115,16 @@ def test_impala_async_sampling_survives_runner_death(cluster):
         algo.stop()
 
 
-def test_learner_sigkilled_group_restarts_from_last_state(cluster):
+@pytest.mark.parametrize("victim", [1, 0])
+def test_learner_sigkilled_group_restarts_from_last_state(cluster, victim):
+    """victim 0: the rank whose get_state snapshot the group keeps dies -- the
+    snapshot is owned by the driver and outlives it."""
     algo = _ppo(num_runners=1, num_learners=2).build()
     try:
         algo.train()
         lg = algo.learner_group
         before = lg.get_state()
-        os.kill(_pid(lg.actors[1]), signal.SIGKILL)
+        os.kill(_pid(lg.actors[victim]), signal.SIGKILL)
         time.sleep(0.3)
         r = algo.train()
         assert lg.num_restarts == 1

@@ -170,6 +170,29 @@ def test_multi_agent_refusals():
     with pytest.raises(NotImplementedError, match="multi-agent"):
         CQLConfig().environment(CooperativeMatchEnv).multi_agent(policies=["pa"], policy_mapping_fn=_map).validate()
     with pytest.raises(NotImplementedError, match="recurrent"):
-        (rllib.IMPALAConfig().environment(CooperativeMatchEnv)
+        (rllib.DQNConfig().environment(CooperativeMatchEnv)
          .multi_agent(policies=["pa", "pb"], policy_mapping_fn=_map)
          .training(model={"use_lstm": True}).validate())
+
+
+@pytest.mark.parametrize("algo_name", ["IMPALA", "APPO"])
+def test_recurrent_impala_appo_multi_agent_learn_memory_task(algo_name):
+    """LSTM modules per agent under V-trace: each agent-segment column is unrolled
+    from the state its runner recorded at the column's first step."""
+    env_cls = make_multi_agent("RepeatAfterMe-v0")
+    cfg = (getattr(rllib, algo_name + "Config")().environment(env_cls, env_config={"num_agents": 2})
+           .env_runners(num_envs_per_env_runner=8, rollout_fragment_length=40)
+           .multi_agent(policies=["p0", "p1"], policy_mapping_fn=_map)
+           .training(lr=3e-3, train_batch_size=320, gamma=0.5, vf_loss_coeff=0.5, entropy_coeff=0.0,
+                     model={"fcnet_hiddens": [64], "use_lstm": True, "lstm_cell_size": 64, "max_seq_len": 20})
+           .reporting(metrics_num_episodes_for_smoothing=16).debugging(seed=0))
+    algo = cfg.build()
+    best = {"p0": 0.0, "p1": 0.0}
+    for _ in range(150):
+        r = algo.train()
+        for m, v in r["env_runners"]["module_episode_returns_mean"].items():
+            best[m] = max(best[m], v)
+        if min(best.values()) > 16:
+            break
+    assert min(best.values()) > 16, best  # chance is ~9.5 per agent, the optimum 19
+    algo.stop()
