@@ -73,14 +73,20 @@ def _details() -> Dict[str, Any]:
     from ..core import api as core
     from ..serve import api
 
+    from ..exceptions import RayActorError
+
+    empty = {"controller_info": {}, "proxy_location": None, "http_options": None, "grpc_options": None,
+             "proxies": {}, "deploy_mode": "UNSET", "applications": {}}
     ctl = api._get_controller(create=False)
     if ctl is None:
-        return {"controller_info": {}, "proxy_location": None, "http_options": None, "grpc_options": None,
-                "proxies": {}, "deploy_mode": "UNSET", "applications": {}}
-    raw = core.get(ctl.status.remote())
-    cfg = core.get(ctl.get_deploy_config.remote()) or {}
+        return empty
+    try:
+        raw = core.get(ctl.status.remote(), timeout=30)
+        cfg = core.get(ctl.get_deploy_config.remote(), timeout=30) or {}
+        proxy, port = core.get(ctl.get_proxy.remote(), timeout=30)
+    except RayActorError:  # the controller is gone or going (right after a DELETE): no Serve instance
+        return empty
     app_cfg = {a["name"]: a for a in cfg.get("applications", [])}
-    proxy, port = core.get(ctl.get_proxy.remote())
     apps = {}
     for name, a in raw.items():
         apps[name] = {"name": name, "route_prefix": a["route_prefix"], "docs_path": None, "status": a["status"],

@@ -679,7 +679,11 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
 // ABL (timing ablations, tools/bench_attn.py with CAAMD_FA64_BWD_ABL; production 0):
 // bit 0 no DMA inside the loop (stale tiles), bit 1 no per-tile wait + barrier,
 // bit 2 no softmax / dS VALU (P = S, dS = dP).
-template <int ABL = 0>
+// OPT (schedule variants, CAAMD_FA64_DKDV_OPT): bit 0 = the second half's Q / dO
+// row fragments loaded during the first half's VALU pass (into the registers the
+// first half's S / dP MFMAs just released); bit 1 = the transposed fragments of a
+// half requested before its S / dP MFMAs instead of after them.
+template <int ABL = 0, int OPT = 0>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ dout,
                                                           const float* __restrict__ lse2g,
@@ -749,16 +753,32 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
     const float* st = (const float*)(qimg + 2 * IMG);
     const int lo_lim = causal ? key - q0 - 4 * h : -0x7fffffff;
     const int hi_lim = T - 1 - q0 - 4 * h;
-    // one 32-query half at a time (S^T, dP^T live for 16 MFMAs only)
-    static_for<2>([&](auto qh_c) {
+    // the half's eight row fragments in flight at once (one LDS latency)
+    bf16x8 qr[4], dr[4];
+    auto load_rows = [&](auto qh_c) {
       constexpr int qh = decltype(qh_c)::value;
-      // the half's eight row fragments in flight at once (one LDS latency)
-      bf16x8 qr[4], dr[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         qr[s] = *(lds_bf16x8*)(qimg + qoff[s] + qh * 4096);
         dr[s] = *(lds_bf16x8*)(qimg + IMG + qoff[s] + qh * 4096);
       }
+    };
+    load_rows(std::integral_constant<int, 0>{});
+    // one 32-query half at a time (S^T, dP^T live for 16 MFMAs only)
+    static_for<2>([&](auto qh_c) {
+      constexpr int qh = decltype(qh_c)::value;
+      if constexpr (qh == 1 && !(OPT & 1)) load_rows(std::integral_constant<int, 1>{});
+      TrFrag tv[2][2], tk[2][2];
+      auto issue_tr = [&]() {
+        static_for<2>([&](auto s_c) {
+          constexpr int s = decltype(s_c)::value;
+          tr_frag<qh * 32 + s * 16, 0>(tv[s][0], qimg_u + IMG, tb);
+          tr_frag<qh * 32 + s * 16, 1>(tv[s][1], qimg_u + IMG, tb);
+          tr_frag<qh * 32 + s * 16, 0>(tk[s][0], qimg_u, tb);
+          tr_frag<qh * 32 + s * 16, 1>(tk[s][1], qimg_u, tb);
+        });
+      };
+      if constexpr (OPT & 2) issue_tr();
       __builtin_amdgcn_sched_barrier(0);
       f32x16 sacc = mfma32(qr[0], kf[0], zero16());
       f32x16 dp = mfma32(dr[0], vf[0], zero16());
@@ -769,14 +789,8 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
       }
       // transposed dO / Q fragments requested now, consumed after the VALU pass
       __builtin_amdgcn_sched_barrier(0);
-      TrFrag tv[2][2], tk[2][2];
-      static_for<2>([&](auto s_c) {
-        constexpr int s = decltype(s_c)::value;
-        tr_frag<qh * 32 + s * 16, 0>(tv[s][0], qimg_u + IMG, tb);
-        tr_frag<qh * 32 + s * 16, 1>(tv[s][1], qimg_u + IMG, tb);
-        tr_frag<qh * 32 + s * 16, 0>(tk[s][0], qimg_u, tb);
-        tr_frag<qh * 32 + s * 16, 1>(tk[s][1], qimg_u, tb);
-      });
+      if constexpr (!(OPT & 2)) issue_tr();
+      if constexpr (qh == 0 && (OPT & 1)) load_rows(std::integral_constant<int, 1>{});
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int qi = qh * 32 + 8 * g + 4 * h;
@@ -907,7 +921,17 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     const char* e = std::getenv("CAAMD_FA64_BWD_ABL");
     return e ? std::atoi(e) : 0;
   }();
+  static const int opt = [] {  // dK/dV schedule variants (see bwd_dkdv_kernel)
+    const char* e = std::getenv("CAAMD_FA64_DKDV_OPT");
+    return e ? std::atoi(e) : 0;
+  }();
   auto kern = fa64::bwd_dkdv_kernel<0>;
+  switch (opt) {
+    case 1: kern = fa64::bwd_dkdv_kernel<0, 1>; break;
+    case 2: kern = fa64::bwd_dkdv_kernel<0, 2>; break;
+    case 3: kern = fa64::bwd_dkdv_kernel<0, 3>; break;
+    default: break;
+  }
   switch (abl) {
     case 1: kern = fa64::bwd_dkdv_kernel<1>; break;
     case 2: kern = fa64::bwd_dkdv_kernel<2>; break;

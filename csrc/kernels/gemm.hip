@@ -31,6 +31,10 @@
 //    activation), and dGELU (dz = acc * gelu'(z)) with fused bias-grad column sums.
 #include "common.h"
 
+#ifndef CAAMD_EPI_SYNC
+#define CAAMD_EPI_SYNC 0  // 1: staging passes wait for the previous pass's stores (pre-round-5)
+#endif
+
 #include <mutex>
 #include <unordered_set>
 
@@ -202,6 +206,17 @@ struct Args {
 // row with 16-byte vectors (a 320-wide row = 40 lanes = 5 full 128-B lines),
 // applying the elementwise epilogue on the way. Direct per-fragment stores touch
 // 16 rows x 32 B per instruction and ran the store path at ~1.6 TB/s.
+// Workgroup barrier for the LDS image only: waits for this wave's LDS reads / writes
+// (lgkmcnt), NOT for its global stores -- __syncthreads() also waits vmcnt(0), so every
+// staging pass waited for the previous pass's stores to reach memory and the tile's
+// output write (up to 327 KB per tile) never overlapped anything. The memory clobbers
+// keep the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <int BM, int BN, int TM, int TN, int EPI, int ABL>
 __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][TN], int m0, int n0,
                                                 int wr, int wc, int lane, lds_char* smem, int tid) {
@@ -255,7 +270,11 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
         }
       }
     }
-    __syncthreads();  // image free
+#if CAAMD_EPI_SYNC
+    __syncthreads();
+#else
+    lds_barrier();  // image free (the previous pass's stores stay in flight)
+#endif
 #pragma unroll
     for (int i = 0; i < TMH; ++i) {
       const int ir = wr * (TMH * 16) + i * 16 + mrow;
@@ -268,7 +287,11 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
         *(lds_bf16x4*)(smem + ir * ROWB + nc * 2) = o;
       }
     }
+#if CAAMD_EPI_SYNC
     __syncthreads();
+#else
+    lds_barrier();  // image written
+#endif
     if constexpr (ABL & 8) continue;
     if (tid >= ACTIVE) continue;
     if constexpr (EPI == EPI_SWIGLU) {
@@ -339,12 +362,12 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
     // atomic per output column per tile
     typedef __attribute__((address_space(3))) float lds_float;
     lds_float* red = (lds_float*)smem;
-    __syncthreads();  // image reads done
+    lds_barrier();  // image reads done
     if (tid < ACTIVE) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) red[rg * (CPR * 8) + c * 8 + r] = dsum[r];
     }
-    __syncthreads();
+    lds_barrier();
     for (int col = tid; col < CPR * 8; col += NTHR) {
       float t = 0.f;
 #pragma unroll
