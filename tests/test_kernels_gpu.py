@@ -410,3 +410,16 @@ def test_drain_f32_into_bf16(C):
     ref = dst.float() + src
     C.drain_f32_(src, dst)
     assert _rel(dst, ref) < 1e-2 and int((src != 0).sum()) == 0
+
+
+@pytest.mark.parametrize("rows,N", [(32768, 1600), (1000, 72), (31, 8)])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_bias_grad_rowsum(C, rows, N, accumulate):
+    """bias_grad_: column sums of dy (32-row fp32 slab partials + column reduce) vs an
+    fp32 torch sum; accumulate adds into the existing bf16 gradient."""
+    torch.manual_seed(0)
+    dy = torch.randn(rows, N, device="cuda").to(torch.bfloat16)
+    out = torch.randn(N, device="cuda").to(torch.bfloat16)
+    ref = dy.float().sum(0) + (out.float() if accumulate else 0.0)
+    C.bias_grad_(dy, out, accumulate)
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2 * max(1.0, rows ** 0.5 / 10))
