@@ -304,7 +304,8 @@ class LeaseManager:
             try:
                 run = max(0.0, float(t1) - float(t0))
                 st = lc.key
-                st.avg_run_s = run if st.avg_run_s is None else 0.8 * st.avg_run_s + 0.2 * run
+                # a long run flips the key to long at once; short runs decay it back
+                st.avg_run_s = run if (st.avg_run_s is None or run > st.avg_run_s) else 0.8 * st.avg_run_s + 0.2 * run
             except (TypeError, ValueError):
                 pass
             rec = lc.pending.pop(task_id, None)

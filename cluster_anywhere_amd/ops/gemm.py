@@ -124,9 +124,25 @@ def run2(a, b, c, layout, epi, bias=None, z=None, zout=None, dbias=None, max_spl
     return c
 
 
+# De-phased full-line launches (CAAMD_GEMM_DEPHASE=1, experimental): on grids that are a
+# whole number of CU rounds, a quarter round of tiles is split in two K-halves and those
+# half-tiles are dispatched first, so half the CUs run half a tile out of phase with the
+# other half and the two groups' output-store bursts do not coincide.
+DEPHASE = os.environ.get("CAAMD_GEMM_DEPHASE", "0") == "1"
+_DEPHASE_SET: dict = {}
+
+
 def tail_plan(M: int, N: int, K: int, bm: int, bn: int, dev: torch.device, algo: int = None):
     """(full tiles, tail split) of a ping-pong launch; split 1 = no tail split."""
     algo = ALGO if algo is None else algo
+    if DEPHASE and algo % 10 == 9:
+        slots = torch.cuda.get_device_properties(dev).multi_processor_count
+        T = (M // bm) * (N // bn)
+        if _DEPHASE_SET.get(dev.index) is None:
+            kernels().gemm_set_tail_first(1)
+            _DEPHASE_SET[dev.index] = True
+        if T % slots == 0 and T >= 4 * slots and (K // 64) // 2 >= 8 and slots % 32 == 0:
+            return (T - slots // 4, 2)
     if not TAIL or not (1 <= algo % 10 <= 3 or algo % 10 == 9) or K < 4096:
         # K = 1600: the split slices and slab round trip cost more than the half-empty
         # last round (which the chip runs at a higher clock); profiles/gemm_tail_split.jsonl

@@ -47,6 +47,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int K, int lda, int ldb, int ldc, int splitk, int algo, hipStream_t st,
                        int tfull, int tS, float* tws, int* tcnt, int bpack);
 void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
+void gemm_set_tail_first(int v);
 hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
                             int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st, int* tickets);
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
@@ -1386,6 +1387,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn64", GUARDED(gemm_tn64), pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
         pybind11::arg("bm"), pybind11::arg("accumulate"), pybind11::arg("slices"),
         pybind11::arg("ws") = pybind11::none(), pybind11::arg("tickets") = pybind11::none());
+  m.def("gemm_set_tail_first", [](int64_t v) { caamd::gemm_set_tail_first((int)v); });
   m.def("gemm_tail_plan", [](int64_t tiles, int64_t K, int64_t ks, int64_t slots, int64_t max_split) {
     int full, S;
     caamd::gemm_tail_plan((int)tiles, (int)K, (int)ks, (int)slots, (int)max_split, &full, &S);

@@ -198,14 +198,12 @@ struct Args {
   // serving prefill reads the same weight copy as decode
   int bpack;
   int group_m;  // algo 9: m-tiles per tile-order group (0: 8); a tuning knob (gemm_set_group_m)
+  // algo 9 with a split tail: dispatch the split (tail) workgroups FIRST, so the CUs
+  // that start on a half-length slice run half a tile out of phase with the rest for the
+  // whole launch and the output-store bursts of the two groups no longer coincide
+  int tail_first;
 };
 
-// Output tile staged through LDS: the MFMA fragments (each lane: 4 columns of one
-// row) are rounded to bf16 and written into a padded [BM/2][BN] image, one m-half
-// of every wave at a time, then the whole workgroup streams the image out row by
-// row with 16-byte vectors (a 320-wide row = 40 lanes = 5 full 128-B lines),
-// applying the elementwise epilogue on the way. Direct per-fragment stores touch
-// 16 rows x 32 B per instruction and ran the store path at ~1.6 TB/s.
 // Workgroup barrier for the LDS image only: waits for this wave's LDS reads / writes
 // (lgkmcnt), NOT for its global stores -- __syncthreads() also waits vmcnt(0), so every
 // staging pass waited for the previous pass's stores to reach memory and the tile's
@@ -217,6 +215,12 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Output tile staged through LDS: the MFMA fragments (each lane: 4 columns of one
+// row) are rounded to bf16 and written into a padded [BM/2][BN] image, one m-half
+// of every wave at a time, then the whole workgroup streams the image out row by
+// row with 16-byte vectors (a 320-wide row = 40 lanes = 5 full 128-B lines),
+// applying the elementwise epilogue on the way. Direct per-fragment stores touch
+// 16 rows x 32 B per instruction and ran the store path at ~1.6 TB/s.
 template <int BM, int BN, int TM, int TN, int EPI, int ABL>
 __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][TN], int m0, int n0,
                                                 int wr, int wc, int lane, lds_char* smem, int tid) {
@@ -1345,12 +1349,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_k64_kernel(Args p) {
     const int xcd = bid & 7, loc = bid >> 3;
     if (p.tS > 1) {
       const int nfx = p.tfull >> 3, ntx = (nwg - p.tfull) >> 3;
-      if (loc < nfx) {
-        tile = xcd * nfx + loc;
+      const int lf = p.tail_first ? loc - ntx : loc;  // full-tile index (tail_first: after the tail)
+      const int lt = p.tail_first ? loc : loc - nfx;  // tail index
+      if (p.tail_first ? loc >= ntx : loc < nfx) {
+        tile = xcd * nfx + lf;
         slice = 0;
         nsplit = 1;
       } else {
-        const int s = xcd * ntx + (loc - nfx);
+        const int s = xcd * ntx + lt;
         tile = p.tfull + s / p.tS;
         slice = s - (s / p.tS) * p.tS;
         nsplit = p.tS;
@@ -2063,7 +2069,7 @@ hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* 
                             int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st, int* tickets) {
   // tickets != null: the last arriving slice of each tile combines (algo 26), else a reduce launch (25)
   gemm::Args a{A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, 1,
-               (M + bm - 1) / bm, N / 320, 0, tickets ? 26 : 25, slices, 0, ws, tickets, 0, 0};
+               (M + bm - 1) / bm, N / 320, 0, tickets ? 26 : 25, slices, 0, ws, tickets, 0, 0, 0};
   if (bm == 256) return accumulate ? gemm::launch_tn64<256, gemm::EPI_BF16_ACC>(a, st)
                                    : gemm::launch_tn64<256, gemm::EPI_BF16>(a, st);
   if (bm == 192) return accumulate ? gemm::launch_tn64<192, gemm::EPI_BF16_ACC>(a, st)
@@ -2074,6 +2080,8 @@ hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* 
 // Host entry: shapes are validated by the caller (bindings.cpp).
 static int g_group_m = 0;  // 0: the kernels' default tile-order group (8 m-tiles)
 void gemm_set_group_m(int g) { g_group_m = g; }
+static int g_tail_first = 0;  // algo 9 split tails dispatched first (see Args::tail_first)
+void gemm_set_tail_first(int v) { g_tail_first = v; }
 
 hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const bf16* B, void* C,
                        const bf16* bias, const bf16* Z, bf16* Zout, float* dbias, int M, int N,
@@ -2081,7 +2089,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int tfull, int tS, float* tws, int* tcnt, int bpack) {
   gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk,
                (algo == 5 || algo == 15) ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt,
-               bpack, g_group_m};
+               bpack, g_group_m, g_tail_first};
   if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
   if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);
   if (bm == 128 && bn == 320) return gemm::launch_epi<128, 320>(layout, epi, a, st);

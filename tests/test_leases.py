@@ -59,8 +59,10 @@ def nap(s):
 def test_long_tasks_spread_over_workers(cluster):
     """A burst of long tasks gets one lease per task (pipelining depth 1), so it
     runs in parallel on the node's CPUs instead of queueing behind one worker."""
-    ray.get([nap.remote(0.0) for _ in range(4)])
-    for _ in range(2):  # the second burst finds the (short-then-long) key measured
+    # (a key measured SHORT pipelines a following burst up to 8 deep per lease until its
+    # first long run completes; the warm-up makes the key's run time known)
+    ray.get([nap.remote(0.05) for _ in range(4)])
+    for _ in range(2):
         t0 = time.time()
         out = ray.get([nap.remote(0.3) for _ in range(4)])
         starts = sorted(t - t0 for t, _ in out)
