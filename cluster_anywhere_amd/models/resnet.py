@@ -43,6 +43,8 @@ from ..ops.vision import (IMAGENET_MEAN, IMAGENET_STD, bias_act_, conv2d_nhwc, c
                           maxpool3s2_nhwc, normalize_pad8)
 
 OWN_CONV = os.environ.get("CAAMD_OWN_CONV", "1") == "1"
+# pixel-pair stem (see FusedResNet); CAAMD_RESNET_PAIR_STEM=0: the 8-channel stem
+PAIR_STEM = os.environ.get("CAAMD_RESNET_PAIR_STEM", "1") == "1"
 
 
 def _conv(cin, cout, k, stride=1):
@@ -201,6 +203,14 @@ class FusedResNet(nn.Module):
             kernels()  # fail loudly if the HIP extension is missing
         o = self.own
         self.stem = _FConv(net.conv1, net.bn1, True, dtype, device, own=o, cin_pad=8)
+        # pixel-pair stem (conv.hip normalize_pairs_kernel): the 7x7 / 3-channel stem as a
+        # 7x4-tap convolution over two-pixel virtual pixels, K = 224 instead of 416
+        self.stem_pair = None
+        if o and PAIR_STEM and net.conv1.kernel_size == (7, 7) and net.conv1.in_channels == 3 \
+                and net.conv1.stride == (2, 2) and net.conv1.padding == (3, 3):
+            from ..ops.vision import conv_weight_pairs
+
+            self.stem_pair = conv_weight_pairs(self.stem.w.float()).to(dtype)
         self.blocks: List[tuple] = []
         for b in net.blocks:
             convs = [_FConv(c, bn, r, dtype, device, own=o) for c, bn, r in b.convs()]
@@ -239,10 +249,11 @@ class FusedResNet(nn.Module):
         return F.linear(x, self.fc_w, self.fc_b)
 
     @torch.no_grad()
-    def forward_own(self, x8):
+    def forward_own(self, x8, stem_out=None):
         """x8: normalised NHWC bf16 [N, H, W, 8] (RGB + zero channels) -> logits, every
-        conv on conv.hip with its epilogue fused."""
-        x = maxpool3s2_nhwc(self.stem.own(x8))
+        conv on conv.hip with its epilogue fused (``stem_out``: the stem's output,
+        already computed by the pixel-pair stem)."""
+        x = maxpool3s2_nhwc(self.stem.own(x8) if stem_out is None else stem_out)
         for convs, down in self.blocks:
             idt = x if down is None else down.own(x)
             y = x
@@ -260,6 +271,12 @@ class FusedResNet(nn.Module):
     def predict_uint8(self, images: torch.Tensor, mean=IMAGENET_MEAN, std=IMAGENET_STD):
         """uint8 NHWC on this device -> logits."""
         if self.own:
+            if self.stem_pair is not None and images.shape[1] % 2 == 0 and images.shape[2] % 2 == 0:
+                from ..ops.vision import conv2d_nhwc_ex, normalize_pairs
+
+                xv = normalize_pairs(images, mean, std)
+                y = conv2d_nhwc_ex(xv, self.stem_pair, self.stem.b, 7, 4, 2, 1, 0, 0, True)
+                return self.forward_own(None, stem_out=y)
             return self.forward_own(normalize_pad8(images, mean, std))
         x = image_normalize(images, mean, std)
         if x.dtype != self.dtype:

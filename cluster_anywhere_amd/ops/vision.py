@@ -105,6 +105,38 @@ def conv2d_nhwc(x: torch.Tensor, w2d: torch.Tensor, bias: torch.Tensor, ks: int,
     return kernels().conv2d_nhwc(x, w2d, bias, residual, ks, stride, pad, relu, tile, _zero_page(x.device))
 
 
+def conv2d_nhwc_ex(x: torch.Tensor, w2d: torch.Tensor, bias: torch.Tensor, kh: int, kw: int, stride: int,
+                   stride_w: int, pad: int, pad_w: int, relu: bool, residual=None, tile=None) -> torch.Tensor:
+    """:func:`conv2d_nhwc` with a kh x kw kernel and per-direction stride / padding."""
+    n, h, wd, _ = x.shape
+    ho = (h + 2 * pad - kh) // stride + 1
+    wo = (wd + 2 * pad_w - kw) // stride_w + 1
+    if tile is None:
+        tile = conv_tile(n * ho * wo, w2d.shape[0], x.shape[3] * kh * kw, residual is not None)
+    return kernels().conv2d_nhwc_ex(x, w2d, bias, residual, kh, kw, stride, stride_w, pad, pad_w, relu, tile,
+                                    _zero_page(x.device))
+
+
+def conv_weight_pairs(w: torch.Tensor) -> torch.Tensor:
+    """Stem weight [Cout, 3, 7, 7] -> the pixel-pair form [Cout, 224] for
+    :func:`normalize_pairs` input: virtual tap (kh, j) covers real taps kw = 2j, 2j+1,
+    channel c8 = 4 * (kw - 2j) + c (c < 3; the 4th channel and tap kw = 7 are zero);
+    k = (kh * 4 + j) * 8 + c8."""
+    cout, cin, kh, kw = w.shape
+    assert cin == 3 and kh == 7 and kw == 7, "pixel-pair stem: [Cout, 3, 7, 7]"
+    wp = torch.zeros(cout, 7, 8, 4, dtype=w.dtype, device=w.device)  # [cout, kh, kw (8), c (4)]
+    wp[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    return wp.reshape(cout, 7, 4, 2, 4).reshape(cout, 7 * 4 * 8).contiguous()
+
+
+def normalize_pairs(x: torch.Tensor, mean: Sequence[float] = IMAGENET_MEAN,
+                    std: Sequence[float] = IMAGENET_STD) -> torch.Tensor:
+    """uint8 [N, H, W, 3] -> bf16 [N, H + 6, (W + 6) / 2, 8]: normalised RGB + a zero
+    channel per pixel, a 3-pixel zero border, two horizontally adjacent pixels per
+    8-channel "virtual pixel" (the pixel-pair stem's input, conv.hip)."""
+    return kernels().normalize_pairs(x.contiguous(), list(mean), list(std))
+
+
 def conv2d_nhwc_ref(x: torch.Tensor, w4: torch.Tensor, bias: torch.Tensor, stride: int, pad: int, relu: bool,
                     residual=None) -> torch.Tensor:
     """fp32 reference of :func:`conv2d_nhwc` with the 4-D [Cout, Cin, KH, KW] weight."""

@@ -27,8 +27,10 @@ int bias_gelu_bwd_slabs(int rows);
 void xent_fwd_launch(const bf16*, const int64_t*, float*, float*, int, int, int, hipStream_t);
 void xent_bwd_launch(bf16*, const int64_t*, const float*, const float*, int, int, int, hipStream_t);
 hipError_t conv2d_launch(const bf16* X, const bf16* Wt, const bf16* bias, const bf16* R, bf16* Y, const bf16* zero,
-                         int N, int H, int W, int lcin, int Ho, int Wo, int KS, int stride, int pad, int Cout, int Kp,
-                         bool relu, int tile, hipStream_t st);
+                         int N, int H, int W, int lcin, int Ho, int Wo, int KH, int KW, int stride_h, int stride_w,
+                         int pad_h, int pad_w, int Cout, int Kp, bool relu, int tile, hipStream_t st);
+void normalize_pairs_launch(const uint8_t* in, bf16* out, int N, int H, int W, const float* sc, const float* bi,
+                            hipStream_t st);
 void normalize_pad8_launch(const uint8_t* in, bf16* out, int64_t npix, const float* sc, const float* bi,
                            hipStream_t st);
 void maxpool3s2_launch(const bf16* x, bf16* y, int N, int H, int W, int C, int Ho, int Wo, hipStream_t st);
@@ -754,8 +756,20 @@ Tensor image_normalize(const Tensor& x, std::vector<double> mean, std::vector<do
 // x [N, H, W, Cin] (plain contiguous NHWC), w [Cout, Kp] with k = (kh*KS + kw)*Cin + ci
 // (zero-padded to Kp % 32 == 0), bias [Cout]; residual [N, Ho, Wo, Cout] or None.
 // y = act(conv(x, w) + bias (+ residual)); tile 0 = 256x128, 1 = 256x64, 2 = 128x128.
+Tensor conv2d_nhwc_ex(const Tensor& x, const Tensor& w, const Tensor& bias, c10::optional<Tensor> residual,
+                      int64_t kh, int64_t kw, int64_t stride, int64_t stride_w, int64_t pad, int64_t pad_w, bool relu,
+                      int64_t tile, const Tensor& zero);
+
 Tensor conv2d_nhwc(const Tensor& x, const Tensor& w, const Tensor& bias, c10::optional<Tensor> residual,
                    int64_t ks, int64_t stride, int64_t pad, bool relu, int64_t tile, const Tensor& zero) {
+  return conv2d_nhwc_ex(x, w, bias, residual, ks, ks, stride, stride, pad, pad, relu, tile, zero);
+}
+
+// General form: kh x kw kernel (1x1, 3x3, 7x7, or the pixel-pair stem's 7x4), stride and
+// padding per direction (stride / pad: vertical, stride_w / pad_w: horizontal).
+Tensor conv2d_nhwc_ex(const Tensor& x, const Tensor& w, const Tensor& bias, c10::optional<Tensor> residual,
+                      int64_t kh, int64_t kw, int64_t stride, int64_t stride_w, int64_t pad, int64_t pad_w, bool relu,
+                      int64_t tile, const Tensor& zero) {
   CHECK_BF16(x);
   CHECK_BF16(w);
   CHECK_BF16(bias);
@@ -764,13 +778,14 @@ Tensor conv2d_nhwc(const Tensor& x, const Tensor& w, const Tensor& bias, c10::op
   const int64_t N = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
   const int64_t Cout = w.size(0), Kp = w.size(1);
   TORCH_CHECK(Cin >= 8 && (Cin & (Cin - 1)) == 0, "conv2d_nhwc: Cin must be a power of two >= 8");
-  TORCH_CHECK(ks == 1 || ks == 3 || ks == 7, "conv2d_nhwc: kernel size 1, 3 or 7");
-  TORCH_CHECK(stride >= 1 && pad >= 0, "conv2d_nhwc: stride / pad");
-  TORCH_CHECK(Kp % 32 == 0 && Kp >= ks * ks * Cin, "conv2d_nhwc: Kp must cover KS*KS*Cin, multiple of 32");
+  TORCH_CHECK((kh == kw && (kh == 1 || kh == 3 || kh == 7)) || (kh == 7 && kw == 4),
+              "conv2d_nhwc: kernel 1x1, 3x3, 7x7 or 7x4");
+  TORCH_CHECK(stride >= 1 && stride_w >= 1 && pad >= 0 && pad_w >= 0, "conv2d_nhwc: stride / pad");
+  TORCH_CHECK(Kp % 32 == 0 && Kp >= kh * kw * Cin, "conv2d_nhwc: Kp must cover KH*KW*Cin, multiple of 32");
   TORCH_CHECK(bias.numel() == Cout && zero.numel() >= 8, "conv2d_nhwc: bias / zero page");
   const int64_t bn = tile == 1 ? 64 : 128;
   TORCH_CHECK(tile >= 0 && tile <= 2 && Cout % bn == 0, "conv2d_nhwc: Cout must be a multiple of the tile width");
-  const int64_t Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
+  const int64_t Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad_w - kw) / stride_w + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "conv2d_nhwc: empty output");
   TORCH_CHECK(N * H * W * Cin < (1LL << 31) && N * Ho * Wo < (1LL << 31), "conv2d_nhwc: size");
   for (const Tensor* t : {&x, &w, &zero})
@@ -787,8 +802,9 @@ Tensor conv2d_nhwc(const Tensor& x, const Tensor& w, const Tensor& bias, c10::op
   while ((1LL << lcin) < Cin) ++lcin;
   if (N * Ho * Wo > 0) {
     const hipError_t e = caamd::conv2d_launch(bp(x), bp(w), bp(bias), rp, bp(y), bp(zero), (int)N, (int)H, (int)W,
-                                              lcin, (int)Ho, (int)Wo, (int)ks, (int)stride, (int)pad, (int)Cout,
-                                              (int)Kp, relu, (int)tile, cur_stream());
+                                              lcin, (int)Ho, (int)Wo, (int)kh, (int)kw, (int)stride, (int)stride_w,
+                                              (int)pad, (int)pad_w, (int)Cout, (int)Kp, relu, (int)tile,
+                                              cur_stream());
     TORCH_CHECK(e == hipSuccess, "conv2d_nhwc: launch failed: ", hipGetErrorString(e));
   }
   return y;
@@ -809,6 +825,27 @@ Tensor normalize_pad8(const Tensor& x, std::vector<double> mean, std::vector<dou
   }
   const int64_t npix = x.size(0) * x.size(1) * x.size(2);
   if (npix) caamd::normalize_pad8_launch(x.data_ptr<uint8_t>(), bp(out), npix, sc, bi, cur_stream());
+  LAUNCH_CHECK();
+  return out;
+}
+
+// uint8 [N, H, W, 3] -> bf16 [N, H + 6, (W + 6) / 2, 8]: the pixel-pair stem input
+// (3-pixel zero border, RGB + 0 per pixel, two pixels per 16-byte virtual pixel)
+Tensor normalize_pairs(const Tensor& x, std::vector<double> mean, std::vector<double> std) {
+  CHECK_GPU(x);
+  CHECK_CONTIG(x);
+  CHECK_DT(x, at::kByte);
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == 3 && mean.size() == 3 && std.size() == 3, "normalize_pairs: NHWC C=3");
+  TORCH_CHECK(x.size(2) % 2 == 0, "normalize_pairs: even width");
+  auto out = at::empty({x.size(0), x.size(1) + 6, (x.size(2) + 6) / 2, 8}, x.options().dtype(at::kBFloat16));
+  float sc[3], bi[3];
+  for (int c = 0; c < 3; ++c) {
+    sc[c] = (float)(1.0 / (255.0 * std[c]));
+    bi[c] = (float)(-mean[c] / std[c]);
+  }
+  if (out.numel())
+    caamd::normalize_pairs_launch(x.data_ptr<uint8_t>(), bp(out), (int)x.size(0), (int)x.size(1), (int)x.size(2), sc,
+                                  bi, cur_stream());
   LAUNCH_CHECK();
   return out;
 }
@@ -1436,7 +1473,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("image_normalize", GUARDED(image_normalize));
   m.def("add_relu_", GUARDED(add_relu_));
   m.def("conv2d_nhwc", GUARDED(conv2d_nhwc));
+  m.def("conv2d_nhwc_ex", GUARDED(conv2d_nhwc_ex));
   m.def("normalize_pad8", GUARDED(normalize_pad8));
+  m.def("normalize_pairs", GUARDED(normalize_pairs));
   m.def("maxpool3s2_nhwc", GUARDED(maxpool3s2_nhwc));
   m.def("bias_act_", GUARDED(bias_act_));
   m.def("rl_gemm", GUARDED(rl_gemm_));

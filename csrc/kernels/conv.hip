@@ -49,6 +49,7 @@ struct Args {
   bf16* Y;           // [M, Cout]
   const bf16* zero;  // 16-byte zero page (16-byte aligned)
   int H, W, lcin, Ho, Wo, stride, pad, Cout, Kp, M, tiles_n;
+  int stride_w, pad_w;  // horizontal stride / padding (stride, pad: vertical)
 };
 
 constexpr int NTHR = 256;
@@ -77,7 +78,7 @@ struct Cfg {
   static_assert((BM * 4) % NTHR == 0 && (BN * 4) % NTHR == 0, "tile / DMA mismatch");
 };
 
-template <int BM, int BN, int WM, int WN, int KS, bool RES, bool RELU>
+template <int BM, int BN, int WM, int WN, int KH, int KW, bool RES, bool RELU>
 __global__ __launch_bounds__(NTHR, 2) void conv_kernel(Args p) {
   using C_ = Cfg<BM, BN>;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(NTHR, 2) void conv_kernel(Args p) {
       const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
       a_base[j] = img * p.H;
       a_hi[j] = ho * p.stride - p.pad;
-      a_wi[j] = wo * p.stride - p.pad;
+      a_wi[j] = wo * p.stride_w - p.pad_w;
     } else {
       a_base[j] = 0;
       a_hi[j] = -(1 << 20);  // never in range
@@ -129,8 +130,8 @@ __global__ __launch_bounds__(NTHR, 2) void conv_kernel(Args p) {
     const int k0 = t * 32;
     const int kc = k0 + c * 8;
     const int tap = kc >> p.lcin, ci = kc & cmask;
-    const int kh = tap / KS, kw = tap - (tap / KS) * KS;
-    const bool tap_ok = tap < KS * KS;
+    const int kh = tap / KW, kw = tap - (tap / KW) * KW;
+    const bool tap_ok = tap < KH * KW;
 #pragma unroll
     for (int j = 0; j < AP; ++j) {
       const int hi = a_hi[j] + kh, wi = a_wi[j] + kw;
@@ -267,6 +268,41 @@ __global__ __launch_bounds__(256) void normalize_pad8_kernel(const uint8_t* __re
   }
 }
 
+// ---- stem input, pixel-pair form: uint8 [N, H, W, 3] -> bf16 [N, H + 6, (W + 6) / 2, 8] ---
+// The 7x7 / stride-2 / pad-3 stem convolution on 3 channels padded to 8 spends 5/8 of
+// its MFMA work on zero channels. Here the image is zero-bordered by 3 pixels and
+// stored with 4 channels (RGB + 0) per pixel, two horizontally adjacent pixels per
+// 16-byte "virtual pixel": the stem becomes a 7 x 4-tap convolution, stride (2, 1),
+// no padding, over 8 virtual channels (tap pair (2j, 2j+1) = virtual tap j; the 8th
+// real tap's weights are zero), K = 7 * 4 * 8 = 224 instead of 7 * 7 * 8 = 392 (+32 pad).
+// One thread per virtual pixel: two 3-byte reads, one 16-byte store.
+__global__ __launch_bounds__(256) void normalize_pairs_kernel(const uint8_t* __restrict__ in, bf16* __restrict__ out,
+                                                              int N, int H, int W, float s0, float s1, float s2,
+                                                              float b0, float b1, float b2) {
+  const int Hp = H + 6, Wv = (W + 6) / 2;
+  const int64_t total = (int64_t)N * Hp * Wv;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int xv = (int)(i % Wv);
+    const int64_t r = i / Wv;
+    const int yp = (int)(r % Hp), n = (int)(r / Hp);
+    const int y = yp - 3;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int x = 2 * xv + q - 3;
+      if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) {
+        const uint8_t* px = in + (((int64_t)n * H + y) * W + x) * 3;
+        o[4 * q + 0] = (bf16)__builtin_fmaf((float)px[0], s0, b0);
+        o[4 * q + 1] = (bf16)__builtin_fmaf((float)px[1], s1, b1);
+        o[4 * q + 2] = (bf16)__builtin_fmaf((float)px[2], s2, b2);
+      }
+    }
+    reinterpret_cast<bf16x8*>(out)[i] = o;
+  }
+}
+
 // ---- 3x3 / stride-2 / pad-1 max pool, NHWC, 8 channels per lane -------------------
 __global__ __launch_bounds__(256) void maxpool3s2_kernel(const bf16* __restrict__ x, bf16* __restrict__ y, int N,
                                                           int H, int W, int C, int Ho, int Wo) {
@@ -302,10 +338,10 @@ __global__ __launch_bounds__(256) void maxpool3s2_kernel(const bf16* __restrict_
 }  // namespace conv
 
 // ---- host launchers ----------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int KS, bool RES, bool RELU>
+template <int BM, int BN, int WM, int WN, int KH, int KW, bool RES, bool RELU>
 static hipError_t conv_go(const conv::Args& a, hipStream_t st) {
   using C_ = conv::Cfg<BM, BN>;
-  auto k = conv::conv_kernel<BM, BN, WM, WN, KS, RES, RELU>;
+  auto k = conv::conv_kernel<BM, BN, WM, WN, KH, KW, RES, RELU>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, C_::LDS);
@@ -318,33 +354,44 @@ static hipError_t conv_go(const conv::Args& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, int KS>
+template <int BM, int BN, int WM, int WN, int KH, int KW>
 static hipError_t conv_epi(const conv::Args& a, bool relu, hipStream_t st) {
-  if (a.R) return relu ? conv_go<BM, BN, WM, WN, KS, true, true>(a, st) : conv_go<BM, BN, WM, WN, KS, true, false>(a, st);
-  return relu ? conv_go<BM, BN, WM, WN, KS, false, true>(a, st) : conv_go<BM, BN, WM, WN, KS, false, false>(a, st);
+  if (a.R)
+    return relu ? conv_go<BM, BN, WM, WN, KH, KW, true, true>(a, st)
+                : conv_go<BM, BN, WM, WN, KH, KW, true, false>(a, st);
+  return relu ? conv_go<BM, BN, WM, WN, KH, KW, false, true>(a, st)
+              : conv_go<BM, BN, WM, WN, KH, KW, false, false>(a, st);
 }
 
-template <int KS>
+template <int KH, int KW>
 static hipError_t conv_tile(const conv::Args& a, int tile, bool relu, hipStream_t st) {
   switch (tile) {
-    case 0: return conv_epi<256, 128, 2, 2, KS>(a, relu, st);  // Cout % 128 == 0
-    case 1: return conv_epi<256, 64, 4, 1, KS>(a, relu, st);   // Cout == 64
-    case 2: return conv_epi<128, 128, 2, 2, KS>(a, relu, st);  // few pixels (late stages)
+    case 0: return conv_epi<256, 128, 2, 2, KH, KW>(a, relu, st);  // Cout % 128 == 0
+    case 1: return conv_epi<256, 64, 4, 1, KH, KW>(a, relu, st);   // Cout == 64
+    case 2: return conv_epi<128, 128, 2, 2, KH, KW>(a, relu, st);  // few pixels (late stages)
     default: return hipErrorInvalidValue;
   }
 }
 
-// tile: 0 = 256x128, 1 = 256x64, 2 = 128x128.
+// tile: 0 = 256x128, 1 = 256x64, 2 = 128x128. Kernel KH x KW (1x1, 3x3, 7x7, or the
+// pixel-pair stem's 7x4), stride / pad per direction.
 hipError_t conv2d_launch(const bf16* X, const bf16* Wt, const bf16* bias, const bf16* R, bf16* Y, const bf16* zero,
-                         int N, int H, int W, int lcin, int Ho, int Wo, int KS, int stride, int pad, int Cout, int Kp,
-                         bool relu, int tile, hipStream_t st) {
-  conv::Args a{X, Wt, bias, R, Y, zero, H, W, lcin, Ho, Wo, stride, pad, Cout, Kp, N * Ho * Wo, 0};
-  switch (KS) {
-    case 1: return conv_tile<1>(a, tile, relu, st);
-    case 3: return conv_tile<3>(a, tile, relu, st);
-    case 7: return conv_tile<7>(a, tile, relu, st);
-    default: return hipErrorInvalidValue;
-  }
+                         int N, int H, int W, int lcin, int Ho, int Wo, int KH, int KW, int stride_h, int stride_w,
+                         int pad_h, int pad_w, int Cout, int Kp, bool relu, int tile, hipStream_t st) {
+  conv::Args a{X, Wt, bias, R, Y, zero, H, W, lcin, Ho, Wo, stride_h, pad_h, Cout, Kp, N * Ho * Wo, 0,
+               stride_w, pad_w};
+  if (KH == 1 && KW == 1) return conv_tile<1, 1>(a, tile, relu, st);
+  if (KH == 3 && KW == 3) return conv_tile<3, 3>(a, tile, relu, st);
+  if (KH == 7 && KW == 7) return conv_tile<7, 7>(a, tile, relu, st);
+  if (KH == 7 && KW == 4) return conv_tile<7, 4>(a, tile, relu, st);
+  return hipErrorInvalidValue;
+}
+
+void normalize_pairs_launch(const uint8_t* in, bf16* out, int N, int H, int W, const float* sc, const float* bi,
+                            hipStream_t st) {
+  const int64_t total = (int64_t)N * (H + 6) * ((W + 6) / 2);
+  hipLaunchKernelGGL(conv::normalize_pairs_kernel, dim3(ew_grid(total, 256)), dim3(256), 0, st, in, out, N, H, W,
+                     sc[0], sc[1], sc[2], bi[0], bi[1], bi[2]);
 }
 
 void normalize_pad8_launch(const uint8_t* in, bf16* out, int64_t npix, const float* sc, const float* bi,

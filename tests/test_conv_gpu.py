@@ -81,3 +81,62 @@ def test_resnet50_own_conv_matches_miopen():
     b = lib.predict_uint8(u8).float()
     assert _rel(a, b) < 5e-2
     assert (a.argmax(1) == b.argmax(1)).float().mean().item() >= 0.75
+
+
+def _pairs_ref(img, mean, std):
+    """fp32 reference of normalize_pairs: [N,H,W,3] uint8 -> [N,H+6,(W+6)/2,8]."""
+    x = img.float() / 255.0
+    x = (x - torch.tensor(mean, device=img.device)) / torch.tensor(std, device=img.device)
+    x = F.pad(x, (0, 1, 3, 3, 3, 3))  # channel 3 = 0, 3-pixel border
+    n, hp, wp, _ = x.shape
+    return x.reshape(n, hp, wp // 2, 8)
+
+
+@pytest.mark.parametrize("shape", [(2, 224, 224), (3, 30, 42)])
+def test_normalize_pairs(shape):
+    from cluster_anywhere_amd.ops.vision import IMAGENET_MEAN, IMAGENET_STD, normalize_pairs
+
+    n, h, w = shape
+    img = torch.randint(0, 256, (n, h, w, 3), dtype=torch.uint8, device="cuda")
+    out = normalize_pairs(img)
+    ref = _pairs_ref(img, IMAGENET_MEAN, IMAGENET_STD)
+    assert out.shape == ref.shape
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("hw", [224, 64])
+def test_pixel_pair_stem_matches_fp32_conv(hw):
+    """The 7x7 / stride 2 / pad 3 stem as a 7x4 conv, stride (2, 1), over pixel pairs
+    (conv_weight_pairs + normalize_pairs + conv2d_nhwc_ex) vs the fp32 reference conv
+    of the real 3-channel input."""
+    from cluster_anywhere_amd.ops.vision import (IMAGENET_MEAN, IMAGENET_STD, conv2d_nhwc_ex, conv2d_nhwc_ref,
+                                                 conv_weight_pairs, normalize_pairs)
+
+    torch.manual_seed(0)
+    n = 2
+    img = torch.randint(0, 256, (n, hw, hw, 3), dtype=torch.uint8, device="cuda")
+    w4 = (torch.randn(64, 3, 7, 7, device="cuda") / 147 ** 0.5).bfloat16()
+    b = (torch.randn(64, device="cuda") * 0.1).bfloat16()
+    y = conv2d_nhwc_ex(normalize_pairs(img), conv_weight_pairs(w4.float()).bfloat16(), b, 7, 4, 2, 1, 0, 0, True)
+    x = img.float() / 255.0
+    x = ((x - torch.tensor(IMAGENET_MEAN, device="cuda")) / torch.tensor(IMAGENET_STD, device="cuda"))
+    ref = conv2d_nhwc_ref(x.bfloat16(), w4, b, 2, 3, True)
+    assert y.shape == ref.shape == (n, hw // 2, hw // 2, 64)
+    assert _rel(y, ref) < 1e-2
+
+
+def test_resnet_pixel_pair_stem_matches_pad8_stem():
+    """Whole own-kernel ResNet-50 with the pixel-pair stem vs the 8-channel stem."""
+    from cluster_anywhere_amd.models.resnet import resnet
+
+    torch.manual_seed(0)
+    f = resnet("resnet50").eval().fuse_for_inference(torch.bfloat16, "cuda")
+    if f.stem_pair is None:
+        pytest.skip("pixel-pair stem disabled")
+    img = torch.randint(0, 256, (4, 224, 224, 3), dtype=torch.uint8, device="cuda")
+    a = f.predict_uint8(img).float()
+    keep = f.stem_pair
+    f.stem_pair = None
+    b = f.predict_uint8(img).float()
+    f.stem_pair = keep
+    assert _rel(a, b) < 2e-2

@@ -135,3 +135,24 @@ def test_bias_act_gpu(res, relu):
     ref = ref.relu() if relu else ref
     bias_act_(y, b, r, relu)
     torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+
+
+def test_pixel_pair_stem_math_cpu():
+    """The pixel-pair rewrite of the stem (CPU, fp32, torch conv): a 7x4 conv with
+    stride (2, 1) over [N, H+6, (W+6)/2, 8] virtual pixels with conv_weight_pairs
+    weights equals the 7x7 / stride-2 / pad-3 conv of the 3-channel image."""
+    import torch.nn.functional as F
+
+    from cluster_anywhere_amd.ops.vision import conv_weight_pairs
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 3, 30, 42)
+    w = torch.randn(16, 3, 7, 7)
+    ref = F.conv2d(x, w, None, 2, 3)
+    xp = F.pad(x.permute(0, 2, 3, 1), (0, 1, 3, 3, 3, 3))  # [N, H+6, W+6, 4]
+    n, hp, wp, _ = xp.shape
+    xv = xp.reshape(n, hp, wp // 2, 8).permute(0, 3, 1, 2)  # [N, 8, H+6, (W+6)/2]
+    wv = conv_weight_pairs(w).reshape(16, 7, 4, 8).permute(0, 3, 1, 2)  # [Cout, 8, 7, 4]
+    out = F.conv2d(xv, wv, None, (2, 1), 0)
+    assert out.shape == ref.shape
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
