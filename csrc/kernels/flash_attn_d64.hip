@@ -682,7 +682,8 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
 // OPT (schedule variants, CAAMD_FA64_DKDV_OPT): bit 0 = the second half's Q / dO
 // row fragments loaded during the first half's VALU pass (into the registers the
 // first half's S / dP MFMAs just released); bit 1 = the transposed fragments of a
-// half requested before its S / dP MFMAs instead of after them.
+// half requested before its S / dP MFMAs instead of after them; bit 2 = the half's
+// lse2 / delta rows read (and retired) before its S / dP MFMAs.
 template <int ABL = 0, int OPT = 0>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ dout,
@@ -759,8 +760,14 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
       constexpr int qh = decltype(qh_c)::value;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        qr[s] = *(lds_bf16x8*)(qimg + qoff[s] + qh * 4096);
-        dr[s] = *(lds_bf16x8*)(qimg + IMG + qoff[s] + qh * 4096);
+        if constexpr (ABL & 16) {  // ablation: no row-fragment reads (stale registers)
+          bf16x8* q = qr;  // (a plain use, so the lambda captures the arrays)
+          bf16x8* d = dr;
+          asm volatile("" : "+v"(q[s]), "+v"(d[s]));
+        } else {
+          qr[s] = *(lds_bf16x8*)(qimg + qoff[s] + qh * 4096);
+          dr[s] = *(lds_bf16x8*)(qimg + IMG + qoff[s] + qh * 4096);
+        }
       }
     };
     load_rows(std::integral_constant<int, 0>{});
@@ -770,6 +777,16 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
       if constexpr (qh == 1 && !(OPT & 1)) load_rows(std::integral_constant<int, 1>{});
       TrFrag tv[2][2], tk[2][2];
       auto issue_tr = [&]() {
+        if constexpr (ABL & 8) {  // ablation: no transposed reads (stale registers)
+          TrFrag(*v)[2] = tv;  // (a plain use, so the lambda captures the arrays)
+          TrFrag(*k)[2] = tk;
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int d = 0; d < 2; ++d)
+              asm volatile("" : "+v"(v[s][d].lo), "+v"(v[s][d].hi), "+v"(k[s][d].lo), "+v"(k[s][d].hi));
+          return;
+        }
         static_for<2>([&](auto s_c) {
           constexpr int s = decltype(s_c)::value;
           tr_frag<qh * 32 + s * 16, 0>(tv[s][0], qimg_u + IMG, tb);
@@ -779,6 +796,22 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
         });
       };
       if constexpr (OPT & 2) issue_tr();
+      // OPT & 4: the half's lse2 / delta rows read with the row fragments, before the
+      // S / dP MFMAs; the asm wait (naming the registers) retires them there, so the
+      // VALU pass does not wait on LDS (the compiler's own wait for them would land
+      // behind the transposed reads and wait for those too)
+      f32x4 l4s[4], d4s[4];
+      if constexpr (OPT & 4) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int qi = qh * 32 + 8 * g + 4 * h;
+          l4s[g] = *reinterpret_cast<const f32x4*>(st + qi);
+          d4s[g] = *reinterpret_cast<const f32x4*>(st + 64 + qi);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(l4s[0]), "+v"(l4s[1]), "+v"(l4s[2]), "+v"(l4s[3]), "+v"(d4s[0]), "+v"(d4s[1]),
+                       "+v"(d4s[2]), "+v"(d4s[3])::"memory");
+      }
       __builtin_amdgcn_sched_barrier(0);
       f32x16 sacc = mfma32(qr[0], kf[0], zero16());
       f32x16 dp = mfma32(dr[0], vf[0], zero16());
@@ -794,8 +827,14 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int qi = qh * 32 + 8 * g + 4 * h;
-        const f32x4 l4 = *reinterpret_cast<const f32x4*>(st + qi);
-        const f32x4 d4 = *reinterpret_cast<const f32x4*>(st + 64 + qi);
+        f32x4 l4, d4;
+        if constexpr (OPT & 4) {
+          l4 = l4s[g];
+          d4 = d4s[g];
+        } else {
+          l4 = *reinterpret_cast<const f32x4*>(st + qi);
+          d4 = *reinterpret_cast<const f32x4*>(st + 64 + qi);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int i = 4 * g + j;
@@ -930,6 +969,9 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     case 1: kern = fa64::bwd_dkdv_kernel<0, 1>; break;
     case 2: kern = fa64::bwd_dkdv_kernel<0, 2>; break;
     case 3: kern = fa64::bwd_dkdv_kernel<0, 3>; break;
+    case 4: kern = fa64::bwd_dkdv_kernel<0, 4>; break;
+    case 5: kern = fa64::bwd_dkdv_kernel<0, 5>; break;
+    case 6: kern = fa64::bwd_dkdv_kernel<0, 6>; break;
     default: break;
   }
   switch (abl) {
@@ -938,6 +980,9 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     case 3: kern = fa64::bwd_dkdv_kernel<3>; break;
     case 4: kern = fa64::bwd_dkdv_kernel<4>; break;
     case 7: kern = fa64::bwd_dkdv_kernel<7>; break;
+    case 15: kern = fa64::bwd_dkdv_kernel<15>; break;
+    case 23: kern = fa64::bwd_dkdv_kernel<23>; break;
+    case 31: kern = fa64::bwd_dkdv_kernel<31>; break;
     default: break;
   }
   hipLaunchKernelGGL(kern, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
