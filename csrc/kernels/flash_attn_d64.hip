@@ -239,7 +239,40 @@ __device__ __forceinline__ int xcd_remap(int id, int n) {
 // ABL (timing ablations, tools/bench_attn.py with CAAMD_FA64_ABL; production 0):
 // bit 0 no DMA inside the loop (stale tiles), bit 1 no per-tile wait + barrier,
 // bit 2 no exp (p = s), bit 3 no tile compute at all.
-template <int QS, int ABL = 0, int NW = 4>
+// ----------------------------------------------------------------------------
+// A wave's 32 x 64 fp32 MFMA output (acc[d][4g + j] at row lane & 31, column d*32 + 8g
+// + 4h + j) written as bf16 rows through the wave's 4 KB of LDS (16-byte units XOR-
+// swizzled by row): eight lanes store one whole 128-byte row, so a store instruction
+// covers 8 full rows instead of 8 bytes in each of 32 rows (the direct per-lane stores
+// cost the dK / dV kernel 50 us of the 694 us backward; tools/gpu/r5_dkdv_store.sh).
+// `mul` scales the lane's row; rows >= nrows are not written; row i goes to base + i*rs.
+// The caller makes sure no wave still reads the LDS it hands over.
+__device__ __forceinline__ void store_rows_lds(const f32x16 (&acc)[2], float mul, lds_t* wb,
+                                               bf16* __restrict__ base, size_t rs, int nrows) {
+  typedef __attribute__((address_space(3))) bf16x4 lds_b4;
+  typedef __attribute__((address_space(3))) const bf16x8 lds_b8;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bf16x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = (bf16)(acc[d][4 * g + j] * mul);
+      *(lds_b4*)(wb + r * 128 + (((4 * d + g) ^ (r & 7)) << 4) + 8 * h) = a;
+    }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int c16 = lane & 7;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int row = 8 * it + (lane >> 3);
+    const bf16x8 v = *(lds_b8*)(wb + row * 128 + ((c16 ^ (row & 7)) << 4));
+    if (row < nrows) *reinterpret_cast<bf16x8*>(base + (size_t)row * rs + 8 * c16) = v;
+  }
+}
+
+template <int QS, int ABL = 0, int NW = 4, int STG = 1>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_kernel(const bf16* __restrict__ qp, const bf16* __restrict__ kp,
                                                      const bf16* __restrict__ vp, int q_rs, int kv_rs, int group,
                                                      bf16* __restrict__ out, float* __restrict__ lse, int T,
@@ -437,18 +470,25 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
   for (int qs = 0; qs < QS; ++qs) {
     const int q = q0w + qs * 32 + r;
     const float lt = sum_xor32(l[qs]);
+    const float inv_l = lt > 0.f ? 1.f / lt : 0.f;
+    if constexpr (STG) {
+      if (qs == 0) __syncthreads();  // every wave is past its last tile: the stage images are free
+      store_rows_lds(o[qs], inv_l, smem + wave * 4096, out + ((size_t)b * T + q0w + qs * 32) * H * D + (size_t)hh * D,
+                     (size_t)H * D, T - q0w - qs * 32);
+    }
     if (q < T) {
-      const float inv_l = lt > 0.f ? 1.f / lt : 0.f;
-      bf16* orow = out + ((size_t)b * T + q) * H * D + (size_t)hh * D;
+      if constexpr (!STG) {
+        bf16* orow = out + ((size_t)b * T + q) * H * D + (size_t)hh * D;
 #pragma unroll
-      for (int d = 0; d < 2; ++d)
+        for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 v;
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 v;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[qs][d][4 * g + j] * inv_l);
-          *reinterpret_cast<bf16x4*>(orow + d * 32 + 8 * g + 4 * h) = v;
-        }
+            for (int j = 0; j < 4; ++j) v[j] = (bf16)(o[qs][d][4 * g + j] * inv_l);
+            *reinterpret_cast<bf16x4*>(orow + d * 32 + 8 * g + 4 * h) = v;
+          }
+      }
       if (h == 0) lse[(size_t)bh * T + q] = (m[qs] + __log2f(lt)) * 0.69314718056f;
     }
   }
@@ -483,7 +523,7 @@ __device__ __forceinline__ void colsum_atomic(const f32x16 (&a)[2], float mul, f
 // backward dQ (+ Delta = rowsum(dO * O), lse2 = lse * log2 e for the dK/dV
 // kernel): 4 waves x 64 queries per block, 64-key tiles {K image, V image}.
 // ----------------------------------------------------------------------------
-template <int QS>
+template <int QS, int STG = 1>
 __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o,
                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                         float* __restrict__ delta, float* __restrict__ lse2o,
@@ -653,6 +693,14 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
     __shared__ float red[256];
     colsum_atomic(sum, scale, dbias + (size_t)hh * D, red);
   }
+  if constexpr (STG) {
+    __syncthreads();  // every wave is past its last tile: the stage images are free
+#pragma unroll
+    for (int qs = 0; qs < QS; ++qs)
+      store_rows_lds(dq[qs], scale, smem + wave * 4096, dqkv + ((size_t)b * T + q0w + qs * 32) * rs + (size_t)hh * D,
+                     rs, T - q0w - qs * 32);
+    return;
+  }
 #pragma unroll
   for (int qs = 0; qs < QS; ++qs) {
     const int q = q0w + qs * 32 + r;
@@ -678,12 +726,14 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
 // ----------------------------------------------------------------------------
 // ABL (timing ablations, tools/bench_attn.py with CAAMD_FA64_BWD_ABL; production 0):
 // bit 0 no DMA inside the loop (stale tiles), bit 1 no per-tile wait + barrier,
-// bit 2 no softmax / dS VALU (P = S, dS = dP).
+// bit 2 no softmax / dS VALU (P = S, dS = dP), bit 3 no transposed reads, bit 4 no
+// row-fragment reads, bit 5 no dK / dV stores.
 // OPT (schedule variants, CAAMD_FA64_DKDV_OPT): bit 0 = the second half's Q / dO
 // row fragments loaded during the first half's VALU pass (into the registers the
 // first half's S / dP MFMAs just released); bit 1 = the transposed fragments of a
 // half requested before its S / dP MFMAs instead of after them; bit 2 = the half's
-// lse2 / delta rows read (and retired) before its S / dP MFMAs.
+// lse2 / delta rows read (and retired) before its S / dP MFMAs; bit 3 = dK / dV
+// written through an LDS transpose as whole rows.
 template <int ABL = 0, int OPT = 0>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ dout,
@@ -899,7 +949,15 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
     colsum_atomic(k2, scale, dbias + (size_t)(H + hh) * D, red);
     colsum_atomic(v2, 1.f, dbias + (size_t)(2 * H + hh) * D, red);
   }
-  if (kv) {
+  if constexpr (OPT & 8) {
+    __syncthreads();  // every wave is past its last tile: the stage images are free
+    bf16* kr = dqkv + ((size_t)b * T + key0w) * rs + (size_t)(H + hh) * D;
+    store_rows_lds(dk, scale, smem + wave * 8192, kr, rs, T - key0w);
+    store_rows_lds(dv, 1.f, smem + wave * 8192 + 4096, kr + (size_t)H * D, rs, T - key0w);
+    return;
+  }
+  // ABL & 32: no dK / dV stores (kept behind a never-true test so the math stays live)
+  if (kv && (!(ABL & 32) || dk[0][0] == 12345.f)) {
     bf16* krow = dqkv + ((size_t)b * T + key) * rs + (size_t)(H + hh) * D;
     bf16* vrow = krow + (size_t)H * D;
 #pragma unroll
@@ -920,6 +978,16 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
 
 }  // namespace fa64
 
+// Outputs written through the LDS row transpose (fa64::store_rows_lds); CAAMD_FA64_STG=0
+// selects the direct per-lane stores (A/B)
+static bool fa64_staged_stores() {
+  static const bool on = [] {
+    const char* e = std::getenv("CAAMD_FA64_STG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int kv_rs, int group, bf16* out,
                      float* lse, int B, int T, int H, int causal, hipStream_t st) {
   // 128-query blocks of four waves, three waves per SIMD. (256-query blocks -- two
@@ -931,7 +999,7 @@ void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int 
     return e ? std::atoi(e) : 0;
   }();
   const int nqb = (T + 127) / 128;
-  auto kern = fa64::fwd_kernel<1, 0>;
+  auto kern = fa64_staged_stores() ? fa64::fwd_kernel<1, 0> : fa64::fwd_kernel<1, 0, 4, 0>;
   switch (abl) {
     case 1: kern = fa64::fwd_kernel<1, 1>; break;
     case 2: kern = fa64::fwd_kernel<1, 2>; break;
@@ -954,7 +1022,8 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
   float* delta = ws;
   float* lse2 = ws + (size_t)B * H * T;
   const int nqb = (T + 127) / 128;  // (a 256-query dQ block variant spilled and was removed in round 4)
-  hipLaunchKernelGGL(fa64::bwd_dq_kernel<1>, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout, lse,
+  auto dq_kern = fa64_staged_stores() ? fa64::bwd_dq_kernel<1> : fa64::bwd_dq_kernel<1, 0>;
+  hipLaunchKernelGGL(dq_kern, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout, lse,
                      delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
   static const int abl = [] {  // development timing ablations of dK/dV (tools/bench_attn.py)
     const char* e = std::getenv("CAAMD_FA64_BWD_ABL");
@@ -962,7 +1031,7 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
   }();
   static const int opt = [] {  // dK/dV schedule variants (see bwd_dkdv_kernel)
     const char* e = std::getenv("CAAMD_FA64_DKDV_OPT");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : (fa64_staged_stores() ? 8 : 0);
   }();
   auto kern = fa64::bwd_dkdv_kernel<0>;
   switch (opt) {
@@ -972,6 +1041,8 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     case 4: kern = fa64::bwd_dkdv_kernel<0, 4>; break;
     case 5: kern = fa64::bwd_dkdv_kernel<0, 5>; break;
     case 6: kern = fa64::bwd_dkdv_kernel<0, 6>; break;
+    case 8: kern = fa64::bwd_dkdv_kernel<0, 8>; break;
+    case 12: kern = fa64::bwd_dkdv_kernel<0, 12>; break;
     default: break;
   }
   switch (abl) {
@@ -983,6 +1054,9 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     case 15: kern = fa64::bwd_dkdv_kernel<15>; break;
     case 23: kern = fa64::bwd_dkdv_kernel<23>; break;
     case 31: kern = fa64::bwd_dkdv_kernel<31>; break;
+    case 32: kern = fa64::bwd_dkdv_kernel<32>; break;
+    case 63: kern = fa64::bwd_dkdv_kernel<63>; break;
+    case 95: kern = fa64::bwd_dkdv_kernel<31, 8>; break;  // stripped, staged stores
     default: break;
   }
   hipLaunchKernelGGL(kern, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
