@@ -326,8 +326,13 @@ class LLMEngine:
                                  bt.to(dev), ctx.to(dev), max_ctx)
 
     def _sample(self, logits: torch.Tensor, batch: List[_Seq]) -> List[int]:
-        logits = logits.float()
         temps = [s.params.temperature for s in batch]
+        if all(t <= 0 for t in temps) and logits.is_cuda and logits.dtype == torch.bfloat16 and logits.dim() == 2:
+            # greedy: row argmax on the bf16 logits in one HIP launch (no fp32 copy)
+            from ..ops._lib import kernels
+
+            return kernels().argmax_rows(logits).tolist()
+        logits = logits.float()
         if all(t <= 0 for t in temps):
             return logits.argmax(-1).tolist()
         out = logits.argmax(-1)

@@ -312,6 +312,11 @@ class Llama(nn.Module):
         dec = self._dec if (self._dec is not None and (tokens.shape[0] <= 128 or self._shared)) else None
         if dec is not None and dec["norm"]:
             return self._decode_folded(x, dec, cs, pos, slots, k_caches, v_caches, block_tables, ctx_lens, max_ctx)
+        if dec is not None and dec["attn"] is not None and tokens.shape[0] <= 128:
+            out = self._decode_reduce_norm(x, dec, cs, pos, slots, k_caches, v_caches, block_tables, ctx_lens,
+                                           max_ctx)
+            if out is not None:
+                return out
         for i, layer in enumerate(self.layers):
             h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
             if res is None:
@@ -333,6 +338,41 @@ class Llama(nn.Module):
                 x = L.decode_linear(L.silu_mul(L.decode_linear(h, layer.w_gate_up)), layer.w_down)
         h, _ = L.rms_norm(x, self.final_norm, cfg.norm_eps, res)
         if dec is not None and dec["head"] is not None:
+            return self._dg(h, dec["head"])
+        w = self.embed if self.lm_head is None else self.lm_head
+        return L.decode_linear(h, w)
+
+    def _decode_reduce_norm(self, x, dec, cs, pos, slots, k_caches, v_caches, block_tables, ctx_lens, max_ctx):
+        """Decode layers with the o / down projections' split-K combine, residual add
+        and the following RMSNorm in one launch each (``L.decode_gemm_norm``): per
+        layer qkv(+RoPE +cache append) -> paged attention -> o(+res, mlp_norm) ->
+        gate/up (SwiGLU) -> down(+res, next attn_norm / final_norm). ``res`` (the
+        residual stream) is updated in place. Returns None before any work when the
+        fused path does not apply to these shapes (the caller runs the plain loop)."""
+        cfg = self.cfg
+        H, KVH, eps = cfg.n_head, cfg.n_kv_head, cfg.norm_eps
+        n = len(self.layers)
+        res = x
+        h = None
+        for i, layer in enumerate(self.layers):
+            wq, wo = dec["attn"][i]
+            gu, dn = dec["layers"][i]
+            if i == 0:
+                if not (L.decode_gemm_ok(x.new_empty(x.shape[0], wo.shape[1]), wo)
+                        and L.decode_gemm_splits(wo.shape[0], wo.shape[1], L._cus(x.device)) > 1
+                        and L.decode_gemm_splits(dn.shape[0], dn.shape[1], L._cus(x.device)) > 1
+                        and wo.shape[0] <= 8192 and os.environ.get("CAAMD_DECODE_REDUCE_NORM", "1") != "0"):
+                    return None
+                h, _ = L.rms_norm(x, layer.attn_norm, eps)
+            qkv = L.decode_gemm_qkv_rope(h, wq, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
+            if qkv is None:
+                qkv = self._dg(h, wq)
+                L.rope_cache_(qkv, cs, pos, slots, k_caches[i], v_caches[i], H, KVH)
+            o = L.paged_decode_attention(qkv, k_caches[i], v_caches[i], block_tables, ctx_lens, max_ctx, H)
+            h = L.decode_gemm_norm(o, wo, res, layer.mlp_norm, eps)
+            nxt = self.layers[i + 1].attn_norm if i + 1 < n else self.final_norm
+            h = L.decode_gemm_norm(L.decode_gemm(h, gu, 2, packed=True), dn, res, nxt, eps)
+        if dec["head"] is not None:
             return self._dg(h, dec["head"])
         w = self.embed if self.lm_head is None else self.lm_head
         return L.decode_linear(h, w)

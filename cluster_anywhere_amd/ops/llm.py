@@ -161,6 +161,27 @@ def decode_gemm(x: torch.Tensor, w: torch.Tensor, epi: int = 0, residual: Option
     return y
 
 
+def decode_gemm_norm(x: torch.Tensor, w: torch.Tensor, res: torch.Tensor, norm_w: torch.Tensor,
+                     eps: float) -> Optional[torch.Tensor]:
+    """``res += x @ w.T`` (in place) and ``h = rmsnorm(res) * norm_w`` on the decode
+    GEMM (``w`` prepacked) with the split-K combine, the residual add and the norm in
+    ONE launch after the GEMM (``dg_reduce_norm_kernel``) instead of the reduce +
+    rmsnorm pair. The same numbers as ``rms_norm(decode_gemm(x, w), norm_w, eps, res)``
+    (the GEMM's sum is rounded to bf16 before the add). Returns ``h``, or None where
+    it does not apply (one split, N > 8192, ``CAAMD_DECODE_REDUCE_NORM=0``)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if (not decode_gemm_ok(x, w) or N > 8192 or res.shape != (M, N) or not res.is_contiguous()
+            or res.dtype != torch.bfloat16 or norm_w.dtype != torch.bfloat16
+            or _os.environ.get("CAAMD_DECODE_REDUCE_NORM", "1") == "0"):
+        return None
+    s = decode_gemm_splits(N, K, _cus(x.device))
+    if s < 2:
+        return None
+    part, _, _ = _dg_ws(x.device, (N // 128) * s * 16384, N // 128)
+    return kernels().decode_gemm_norm(x, w, part, s, res, norm_w.contiguous(), float(eps))
+
+
 def fold_norm(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
     """``w [N, K]`` with the RMSNorm weight ``g [K]`` multiplied into its columns
     (``rmsnorm(x) @ w.T == rsqrt-scaled x @ fold_norm(w, g).T``), in fp32 then

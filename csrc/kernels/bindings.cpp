@@ -56,6 +56,8 @@ void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
 void decode_gemm_config(int ext);
+hipError_t decode_gemm_norm_launch(const bf16* X, const bf16* W, float* part, int M, int N, int K, int ldx,
+                                   int splits, bf16* res, const bf16* nw, bf16* h, float eps, hipStream_t st);
 hipError_t decode_gemm_qkv_rope_launch(const bf16* X, const bf16* W, bf16* Y, float* part, int M, int N, int K,
                                        int ldx, int ldy, int splits, const float* cs, const int* pos,
                                        const int* slot, bf16* kc, bf16* vc, int H, int KVH, int BS,
@@ -512,6 +514,7 @@ Tensor flash_attn_bwd(const Tensor& qkv, const Tensor& out, const Tensor& dout, 
 namespace caamd {
 void rmsnorm_launch(const bf16*, const bf16*, bf16*, const bf16*, bf16*, int, int, float, hipStream_t);
 void silu_mul_launch(const bf16*, bf16*, int, int, hipStream_t);
+void argmax_rows_launch(const bf16* x, int M, int V, long long ld, long long* out, hipStream_t st);
 void rope_cache_launch(bf16*, const float*, const int*, const int*, bf16*, bf16*, int, int, int, int, int,
                        hipStream_t);
 bool paged_decode_launch(const bf16*, int, const bf16*, const bf16*, const int*, int, const int*, bf16*, float*,
@@ -574,6 +577,19 @@ void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& out, Tensor& part, Te
                                            (unsigned*)counters.data_ptr<int>(), (int)M, (int)N, (int)K,
                                            (int)x.stride(0), (int)splits, cur_stream());
   TORCH_CHECK(e == hipSuccess, "skinny_gemm launch failed: ", hipGetErrorString(e));
+}
+
+// greedy sampling: argmax over the last dim of bf16 logits [M, V] -> int64 [M]
+// (first maximum on ties)
+Tensor argmax_rows(const Tensor& x) {
+  CHECK_GPU(x);
+  CHECK_DT(x, at::kBFloat16);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) > 0, "argmax_rows: [M, V] with unit column stride");
+  Tensor out = torch::empty({x.size(0)}, x.options().dtype(at::kLong));
+  if (x.size(0) > 0)
+    caamd::argmax_rows_launch((const caamd::bf16*)x.data_ptr(), (int)x.size(0), (int)x.size(1),
+                              (long long)x.stride(0), (long long*)out.data_ptr<int64_t>(), cur_stream());
+  return out;
 }
 
 Tensor silu_mul(const Tensor& gu) {
@@ -1165,6 +1181,34 @@ static void decode_gemm(const Tensor& x, const Tensor& w, Tensor& y, c10::option
   TORCH_CHECK(e == hipSuccess, "decode_gemm launch failed: ", hipGetErrorString(e));
 }
 
+// o / down projection on the decode GEMM (w prepacked, splits > 1) with the split-K
+// combine, the residual add (res updated in place) and the next RMSNorm in one launch:
+// returns h = rmsnorm(res + x . w^T) * norm_w.
+static Tensor decode_gemm_norm(const Tensor& x, const Tensor& w, Tensor& part, int64_t splits, Tensor& res,
+                               const Tensor& norm_w, double eps) {
+  CHECK_BF16(x);
+  CHECK_BF16(w);
+  CHECK_BF16(res);
+  CHECK_BF16(norm_w);
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) >= K && w.size(1) == K && w.is_contiguous(),
+              "decode_gemm_norm: x, w");
+  TORCH_CHECK(M >= 1 && M <= 128 && K % 64 == 0 && N % 128 == 0 && N <= 8192, "decode_gemm_norm: shapes");
+  TORCH_CHECK(res.dim() == 2 && res.size(0) == M && res.size(1) == N && res.is_contiguous(), "decode_gemm_norm: res");
+  TORCH_CHECK(norm_w.numel() == N && norm_w.is_contiguous(), "decode_gemm_norm: norm weight");
+  TORCH_CHECK(splits >= 2 && (splits - 1) * ((K / 64 + splits - 1) / splits) < K / 64,
+              "decode_gemm_norm: 2 <= splits, every split non-empty");
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == at::kFloat && part.numel() >= splits * 128 * N,
+              "decode_gemm_norm: partial workspace too small");
+  Tensor h = torch::empty({M, N}, res.options());
+  hipError_t e = caamd::decode_gemm_norm_launch(
+      (const caamd::bf16*)x.data_ptr(), (const caamd::bf16*)w.data_ptr(), part.data_ptr<float>(), (int)M, (int)N,
+      (int)K, (int)x.stride(0), (int)splits, (caamd::bf16*)res.data_ptr(), (const caamd::bf16*)norm_w.data_ptr(),
+      (caamd::bf16*)h.data_ptr(), (float)eps, cur_stream());
+  TORCH_CHECK(e == hipSuccess, "decode_gemm_norm launch failed: ", hipGetErrorString(e));
+  return h;
+}
+
 // qkv projection on the decode GEMM (w prepacked, head_dim 128, splits > 1) with
 // RoPE and the paged-cache append fused into the split-K reduce launch:
 // y = rope(x . w^T); k / v rows of y also written to their cache slots.
@@ -1434,6 +1478,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm2_bf16", GUARDED(gemm2_bf16));
   m.def("decode_gemm", GUARDED(decode_gemm));
   m.def("decode_gemm_qkv_rope", GUARDED(decode_gemm_qkv_rope));
+  m.def("decode_gemm_norm", GUARDED(decode_gemm_norm));
   m.def("decode_gemm_config", [](int64_t ext) { caamd::decode_gemm_config((int)ext); });
   m.def("transpose_bf16", GUARDED(transpose_bf16));
   m.def("layernorm_fwd", GUARDED(layernorm_fwd));
@@ -1464,6 +1509,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("rmsnorm", GUARDED(rmsnorm), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("eps"),
         pybind11::arg("residual") = pybind11::none());
   m.def("silu_mul", GUARDED(silu_mul));
+  m.def("argmax_rows", GUARDED(argmax_rows));
   m.def("skinny_gemm", GUARDED(skinny_gemm));
   m.def("rope_cache_", GUARDED(rope_cache_));
   m.def("paged_decode", GUARDED(paged_decode), pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),

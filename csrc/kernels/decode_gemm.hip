@@ -112,7 +112,8 @@ struct Args {
   float* part;       // split-K partials: [slabs][splits][BN*128] floats
   unsigned* tick;    // split-K tickets: [slabs], zero between launches
   int M, N, K, ldx, ldy, splits, kchunk;
-  int ext;           // 1: split-K partials only; dg_reduce_kernel combines (own launch)
+  int ext;           // 1: split-K partials only, dg_reduce_kernel combines (own launch);
+                     // 2: row-major partials, dg_reduce_norm_kernel combines
   float* ssp;        // RMSNorm folded in: per-row sums of squares of X, [slabs][splits][128]
                      // (nullptr: plain GEMM); the norm weight is folded into W's columns
   float eps;
@@ -259,7 +260,19 @@ __global__ __launch_bounds__(WG, 1) void decode_gemm_kernel(Args p) {
     float* base = p.part + (size_t)slab * p.splits * (BN * 128);
     float* mine = base + (size_t)split * (BN * 128);
     if (rn && !consumer && lane < 32) p.ssp[((size_t)slab * p.splits + split) * 128 + srow] = ssq;
-    if (consumer) {
+    if (consumer && p.ext == 2) {
+      // row-major [splits][128][N] partials for dg_reduce_norm_kernel (a workgroup per
+      // row): for each accumulator value the 32 lanes of a half write 128 contiguous
+      // bytes of one row
+      float* rowp = p.part + (size_t)split * 128 * p.N + n0 + 32 * wave + r;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int m = 32 * mt + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (m < p.M) rowp[(size_t)m * p.N] = acc[mt][i];
+        }
+    } else if (consumer) {
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
@@ -419,6 +432,63 @@ __global__ __launch_bounds__(256) void dg_reduce_kernel(const float* __restrict_
   }
 }
 
+// Split-K combine + residual add + RMSNorm of the decode o / down projections (ext 2),
+// one launch instead of dg_reduce_kernel + rmsnorm_row_kernel (2 x ~5 us per
+// projection, profiles/llm_serving_prof_r4_final.md): one workgroup per row sums the
+// row's splits x N fp32 partials in split order, rounds to bf16 (the value the unfused
+// GEMM stored), adds the residual stream in place (res = bf16(x + res)) and writes
+// h = rmsnorm(res) * w -- the numerics of the two launches it replaces.
+template <int NV>
+__global__ __launch_bounds__(256) void dg_reduce_norm_kernel(const float* __restrict__ part, int splits, int N,
+                                                             bf16* __restrict__ res, const bf16* __restrict__ w,
+                                                             bf16* __restrict__ hout, float eps) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, t = threadIdx.x;
+  const int nchunk = N >> 3;
+  const size_t rbase = (size_t)row * N;
+  const size_t sstride = (size_t)128 * N;
+  float v[NV][8];
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int ch = t + c * 256;
+    if (ch < nchunk) {
+      const float* pp = part + rbase + ch * 8;
+      f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int k = 0; k < splits; ++k) {
+        a += *reinterpret_cast<const f32x4*>(pp + k * sstride);
+        b += *reinterpret_cast<const f32x4*>(pp + k * sstride + 4);
+      }
+      const bf16x8 rr = *reinterpret_cast<const bf16x8*>(res + rbase + ch * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float x = (float)(bf16)(j < 4 ? a[j] : b[j - 4]);
+        o[j] = (bf16)(x + (float)rr[j]);
+        v[c][j] = (float)o[j];
+        sq += v[c][j] * v[c][j];
+      }
+      *reinterpret_cast<bf16x8*>(res + rbase + ch * 8) = o;
+    }
+  }
+  sq = wave_sum(sq);
+  if ((t & 63) == 0) red[t >> 6] = sq;
+  __syncthreads();
+  const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)N + eps);
+#pragma unroll
+  for (int c = 0; c < NV; ++c) {
+    const int ch = t + c * 256;
+    if (ch < nchunk) {
+      const bf16x8 ww = *reinterpret_cast<const bf16x8*>(w + ch * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (bf16)(v[c][j] * rs * (float)ww[j]);
+      *reinterpret_cast<bf16x8*>(hout + rbase + ch * 8) = o;
+    }
+  }
+}
+
 // The qkv projection's reduce launch with RoPE + paged-cache append fused
 // (llm.hip rope_cache_kernel's math on the fp32 sums): head_dim 128 = one 128-column
 // slab = one head, so rotary pair (d, d + 64) is f32x4 idx and idx + 2048 of the
@@ -569,6 +639,25 @@ hipError_t decode_gemm_qkv_rope_launch(const bf16* X, const bf16* W, bf16* Y, fl
   launch_one<dg::EPI_STORE, true>(a, dim3(N / dg::BN, splits), st);
   hipLaunchKernelGGL(dg::dg_reduce_rope_kernel, dim3(N / dg::BN, 8), dim3(256), 0, st, part, Y, M, ldy, splits, cs,
                      pos, slot, kc, vc, H, KVH, BS, (const float*)ssp, K, eps);
+  return hipGetLastError();
+}
+
+
+// o / down projection + split-K combine + residual add + RMSNorm (w prepacked,
+// splits > 1, N % 8 == 0, N <= 8192): res [M, N] updated in place, h = rmsnorm(res) * nw.
+hipError_t decode_gemm_norm_launch(const bf16* X, const bf16* W, float* part, int M, int N, int K, int ldx,
+                                   int splits, bf16* res, const bf16* nw, bf16* h, float eps, hipStream_t st) {
+  const int kchunk = dg_kchunk(K, splits);
+  if (M < 1 || M > 128 || N % dg::BN || N > 8192 || splits < 2 || !kchunk) return hipErrorInvalidValue;
+  dg::Args a{X, W, nullptr, nullptr, part, nullptr, M, N, K, ldx, N, splits, kchunk, 2, nullptr, eps};
+  launch_one<dg::EPI_STORE, true>(a, dim3(N / dg::BN, splits), st);
+  const int nv = (N / 8 + 255) / 256;
+  if (nv <= 1)
+    hipLaunchKernelGGL(dg::dg_reduce_norm_kernel<1>, dim3(M), dim3(256), 0, st, part, splits, N, res, nw, h, eps);
+  else if (nv <= 2)
+    hipLaunchKernelGGL(dg::dg_reduce_norm_kernel<2>, dim3(M), dim3(256), 0, st, part, splits, N, res, nw, h, eps);
+  else
+    hipLaunchKernelGGL(dg::dg_reduce_norm_kernel<4>, dim3(M), dim3(256), 0, st, part, splits, N, res, nw, h, eps);
   return hipGetLastError();
 }
 

@@ -300,6 +300,70 @@ def test_llama_decode_folded_norms_match(M, monkeypatch):
     assert _rel(torch.stack(out["1"][1]), torch.stack(out["0"][1])) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(128, 4096, 4096), (128, 4096, 14336), (37, 1024, 2816), (5, 512, 1024)])
+def test_decode_gemm_norm(M, N, K):
+    """o / down projection with split-K combine + residual add + RMSNorm in one launch
+    after the GEMM (dg_reduce_norm_kernel) vs the two-launch path (decode GEMM with its
+    reduce launch, then rms_norm with the residual) and vs fp32 math."""
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.05
+    wp = L.pack_decode_weight(w)
+    g = (1 + 0.2 * torch.randn(N, device="cuda")).bfloat16()
+    r = torch.randn(M, N, device="cuda", dtype=torch.bfloat16)
+    res = r.clone()
+    h = L.decode_gemm_norm(x, wp, res, g, 1e-5)
+    assert h is not None
+    h2, res2 = L.rms_norm(L.decode_gemm(x, wp, 0, packed=True), g, 1e-5, r.clone())
+    assert _rel(res, res2.float()) < 1e-3 and _rel(h, h2.float()) < 1e-3
+    ref_res = x.float() @ w.float().t() + r.float()
+    ref_h = ref_res * torch.rsqrt(ref_res.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    assert _rel(res, ref_res) < 1e-2 and _rel(h, ref_h) < 1e-2
+
+
+@pytest.mark.parametrize("M", [128, 37])
+def test_llama_decode_reduce_norm_matches(M, monkeypatch):
+    """One decode step with the o / down reduce + residual + RMSNorm launches fused
+    (default) vs the reduce launch + rmsnorm launch path: same logits and caches."""
+    from cluster_anywhere_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(2)
+    m = Llama(LlamaConfig.named("llama-small")).to("cuda", torch.bfloat16).init_weights(std=0.02)
+    for lay in m.layers:
+        for g in (lay.attn_norm, lay.mlp_norm):
+            g.data = (1 + 0.2 * torch.randn_like(g.float())).bfloat16()
+    cfg, BS = m.cfg, 16
+    nb = M * 4 + 4
+    kc = [torch.randn(nb, cfg.n_kv_head, BS, cfg.head_dim, device="cuda", dtype=torch.bfloat16)
+          for _ in range(cfg.n_layer)]
+    vc = [torch.randn_like(t) for t in kc]
+    bt = torch.randperm(nb, device="cuda").int()[: M * 4].view(M, 4).contiguous()
+    ctx = torch.randint(1, 4 * BS + 1, (M,), device="cuda", dtype=torch.int32)
+    pos = (ctx - 1).int()
+    slots = (bt.gather(1, (pos // BS).long()[:, None]).squeeze(1) * BS + pos % BS).int()
+    tok = torch.randint(0, cfg.vocab_size, (M,), device="cuda")
+    assert m.prepare_decode() and m._dec["attn"] is not None and not m._dec["norm"]
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CAAMD_DECODE_REDUCE_NORM", fused)
+        k2, v2 = [t.clone() for t in kc], [t.clone() for t in vc]
+        out[fused] = (m.decode(tok, pos, slots, k2, v2, bt, ctx, 4 * BS).float(), k2, v2)
+    assert _rel(out["1"][0], out["0"][0]) < 1e-3
+    assert _rel(torch.stack(out["1"][1]), torch.stack(out["0"][1])) < 1e-3
+
+
+@pytest.mark.parametrize("M,V", [(128, 128256), (3, 1000), (1, 7)])
+def test_argmax_rows(M, V):
+    """Greedy sampler's HIP row argmax on bf16 logits vs torch.argmax (first maximum
+    on ties: bf16 logits tie often); also a strided row view."""
+    torch.manual_seed(V)
+    x = torch.randn(M, V + 8, device="cuda").bfloat16()
+    x[0, 5 % V] = x[0, (V - 1)] = 50.0  # a tie: the first index wins
+    for t in (x[:, :V].contiguous(), x[:, :V]):
+        got = L.kernels().argmax_rows(t)
+        assert torch.equal(got, t.float().argmax(-1)), (got, t.float().argmax(-1))
+
+
 def _rel2(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
