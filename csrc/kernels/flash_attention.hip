@@ -31,6 +31,8 @@ namespace caamd {
 // the first-generation D = 64 kernels below (A/B timing).
 void fa64_fwd_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
                      hipStream_t);
+void fa128_fwd_launch(const bf16*, const bf16*, const bf16*, int, int, int, bf16*, float*, int, int, int, int,
+                      hipStream_t);
 void fa64_bwd_launch(const bf16*, const bf16*, const bf16*, const float*, float*, bf16*, int, int, int, int,
                      hipStream_t, float*);
 static bool fa_v1() {
@@ -645,6 +647,10 @@ void fa_fwd_gqa_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, in
                        bf16* out, float* lse, int B, int T, int H, int D, int causal, hipStream_t st) {
   if (D == 64 && !fa_v1()) {
     fa64_fwd_launch(q, k, v, q_rs, kv_rs, group, out, lse, B, T, H, causal, st);
+    return;
+  }
+  if (D == 128 && !fa_v1()) {
+    fa128_fwd_launch(q, k, v, q_rs, kv_rs, group, out, lse, B, T, H, causal, st);
     return;
   }
   const int qblk = D == 64 ? qblk_for<64>() : qblk_for<128>();

@@ -495,6 +495,187 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
 }
 
 // ----------------------------------------------------------------------------
+// forward, head_dim 128 (Llama prefill: GQA through the q / kv row strides):
+// the D = 64 design with each 64-key K / V tile held as TWO swizzled 64-dim images
+// (dims 0-63, 64-127; the same DMA, row reads and transposed reads as D = 64).
+// 4 waves x 32 queries per block, two stages of {K0, K1, V0, V1} (64 KiB: two
+// blocks per CU), the next tile's DMA issued under the current tile's MFMAs.
+// Per tile and wave: 16 MFMAs for S (8 k-steps over the head dim) and 16 for
+// O^T += V^T P^T (4 32-dim blocks), i.e. twice the MFMA work per softmax element of
+// the D = 64 kernel. Replaces flash_attention.hip's first-generation
+// fa_fwd_kernel<128> (131.9 us per Llama-3-8B prefill chunk, B16 T512 H32 KVH8).
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void fwd128_kernel(const bf16* __restrict__ qp, const bf16* __restrict__ kp,
+                                                        const bf16* __restrict__ vp, int q_rs, int kv_rs, int group,
+                                                        bf16* __restrict__ out, float* __restrict__ lse, int T, int H,
+                                                        int nqb, float scale_log2, int causal) {
+  constexpr int DH = 128;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_t* smem = (lds_t*)smem_raw;
+  constexpr int STAGE = 4 * IMG;  // K0, K1, V0, V1
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = id / nqb;
+  const int qb = nqb - 1 - (id % nqb);  // heavy (late) query blocks first
+  const int b = bh / H, hh = bh % H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const size_t rs = (size_t)q_rs, krs = (size_t)kv_rs;
+  const bf16* qbase = qp + (size_t)b * T * rs + (size_t)hh * DH;
+  const bf16* kbase = kp + (size_t)b * T * krs + (size_t)(hh / group) * DH;
+  const bf16* vbase = vp + (size_t)b * T * krs + (size_t)(hh / group) * DH;
+  constexpr int QBLK = 128;
+  const int q0w = qb * QBLK + wave * 32;
+  const int qend = min(T, qb * QBLK + QBLK);
+  const int nkt = causal ? (qend + 63) / 64 : (T + 63) / 64;
+  auto issue = [&](int kt, lds_t* st) {
+    dma_tile(kbase, krs, kt * 64, T, st, wave, lane);
+    dma_tile(kbase + 64, krs, kt * 64, T, st + IMG, wave, lane);
+    dma_tile(vbase, krs, kt * 64, T, st + 2 * IMG, wave, lane);
+    dma_tile(vbase + 64, krs, kt * 64, T, st + 3 * IMG, wave, lane);
+  };
+  issue(0, smem);
+
+  int koff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) koff[s] = r * 128 + (((2 * s + h) ^ swz(r)) << 4);
+  const TrBase vtb = tr_base(lane);
+
+  bf16x8 qf[8];
+  f32x16 o[4];
+  const int q = q0w + r;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) {
+    if (q < T) qf[s] = *reinterpret_cast<const bf16x8*>(qbase + (size_t)q * rs + 16 * s + 8 * h);
+    else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)0.f;
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = zero16();
+  float m = -INFINITY, l = 0.f;
+  wait_dma();
+  __syncthreads();
+
+  auto tile = [&](auto need_mask_c, const lds_t* kimg, unsigned vimg, int k0) {
+    constexpr bool need_mask = decltype(need_mask_c)::value;
+    typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+    f32x16 sacc[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {  // head dims 64 * half .. + 63 (image `half`)
+        bf16x8 kf[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) kf[s] = *(lds_bf16x8*)(kimg + half * IMG + koff[s] + kb * 4096);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          sacc[kb] = mfma32(kf[s], qf[4 * half + s], (half == 0 && s == 0) ? zero16() : sacc[kb]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // V^T fragments of the first key half requested now, consumed after the softmax
+    TrFrag vt[2][4];
+    static_for<2>([&](auto s_c) {
+      constexpr int s = decltype(s_c)::value;
+      tr_frag<s * 16, 0>(vt[s][0], vimg, vtb);
+      tr_frag<s * 16, 1>(vt[s][1], vimg, vtb);
+      tr_frag<s * 16, 0>(vt[s][2], vimg + IMG, vtb);
+      tr_frag<s * 16, 1>(vt[s][3], vimg + IMG, vtb);
+    });
+    if constexpr (need_mask) {
+      const int lim = (causal ? min(q, T - 1) : T - 1) - k0 - 4 * h;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[kb][i] = (kb * 32 + crow(i, 0) > lim) ? -INFINITY : sacc[kb][i];
+    }
+    float mxa = sacc[0][0], mxb = sacc[1][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) {
+      mxa = fmaxf(mxa, sacc[0][i]);
+      mxb = fmaxf(mxb, sacc[1][i]);
+    }
+    float mx = fmaxf(mxa, mxb);
+    mx = max_xor32(mx) * scale_log2;
+    if (__builtin_amdgcn_ballot_w64(mx > m + kThr) != 0) {
+      asm volatile("");
+      const float mnew = fmaxf(m, mx);
+      const float alpha = m == -INFINITY ? 0.f : fexp2(m - mnew);
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+      m = mnew;
+    }
+    const float muse = m == -INFINITY ? 0.f : m;
+    float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p = fexp2(__builtin_fmaf(sacc[kb][i], scale_log2, -muse));
+        sacc[kb][i] = p;
+        rs4[i & 3] += p;
+      }
+    l += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
+    static_for<2>([&](auto kb_c) {
+      constexpr int kb = decltype(kb_c)::value;
+      tr_wait4(vt[0][0], vt[0][1], vt[0][2], vt[0][3]);
+      tr_wait4(vt[1][0], vt[1][1], vt[1][2], vt[1][3]);
+      TrFrag cur[2][4];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) cur[s][d] = vt[s][d];
+      if constexpr (kb == 0) {  // second key half's V^T under this half's MFMAs
+        static_for<2>([&](auto s_c) {
+          constexpr int s = decltype(s_c)::value;
+          tr_frag<32 + s * 16, 0>(vt[s][0], vimg, vtb);
+          tr_frag<32 + s * 16, 1>(vt[s][1], vimg, vtb);
+          tr_frag<32 + s * 16, 0>(vt[s][2], vimg + IMG, vtb);
+          tr_frag<32 + s * 16, 1>(vt[s][3], vimg + IMG, vtb);
+        });
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_frag(sacc[kb], s);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d] = mfma32(tr_join(cur[s][d]), pf, o[d]);
+      }
+    });
+  };
+
+  const unsigned smem_u = (unsigned)(size_t)smem;
+  auto iter = [&](int kt, auto mask_c) {
+    const int k0 = kt * 64;
+    const int st = kt & 1;
+    if (kt + 1 < nkt) issue(kt + 1, smem + (st ^ 1) * STAGE);  // stage st^1 was released by the last barrier
+    const bool active = !(causal && k0 > q0w + 31) && q0w < T;  // wave-uniform
+    if (active) tile(mask_c, smem + st * STAGE, smem_u + st * STAGE + 2 * IMG, k0);
+    wait_dma();
+    barrier_keep_dma();
+  };
+  {
+    const int qblk0 = qb * QBLK;
+    const int mfirst = min(nkt, min(T / 64, causal ? (qblk0 >= 63 ? (qblk0 - 63) / 64 + 1 : 0) : nkt));
+    int kt = 0;
+    for (; kt < mfirst; ++kt) iter(kt, std::false_type{});
+    for (; kt < nkt; ++kt) iter(kt, std::true_type{});
+  }
+  const float lt = sum_xor32(l);
+  const float inv_l = lt > 0.f ? 1.f / lt : 0.f;
+  // the last barrier: every wave is past its last tile, the stage images are free
+  const f32x16 lo[2] = {o[0], o[1]}, hi[2] = {o[2], o[3]};
+  bf16* ob = out + ((size_t)b * T + q0w) * H * DH + (size_t)hh * DH;
+  store_rows_lds(lo, inv_l, smem + wave * 4096, ob, (size_t)H * DH, T - q0w);
+  store_rows_lds(hi, inv_l, smem + wave * 4096, ob + 64, (size_t)H * DH, T - q0w);
+  if (q < T && h == 0) lse[(size_t)bh * T + q] = (m + __log2f(lt)) * 0.69314718056f;
+}
+
+// ----------------------------------------------------------------------------
 // Column sums of the block's 32-row output fragments (lane row = lane & 31, columns
 // d*32 + 8g + 4h + j for value 4g + j of acc[d], h = lane >> 5), added to out[col]:
 // the projection-bias gradient (colsum over tokens of dQ / dK / dV) taken from
@@ -986,6 +1167,21 @@ static bool fa64_staged_stores() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+// head_dim 128 forward (fwd128_kernel); GQA through the row strides and `group`
+void fa128_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int kv_rs, int group, bf16* out,
+                      float* lse, int B, int T, int H, int causal, hipStream_t st) {
+  const float scale_log2 = 1.44269504089f / sqrtf(128.f);
+  const int nqb = (T + 127) / 128;
+  static const bool attr = [] {
+    (void)hipFuncSetAttribute((const void*)fa64::fwd128_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              8 * fa64::IMG);
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(fa64::fwd128_kernel, dim3(B * H * nqb), dim3(256), 8 * fa64::IMG, st, q, k, v, q_rs, kv_rs,
+                     group, out, lse, T, H, nqb, scale_log2, causal);
 }
 
 void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int kv_rs, int group, bf16* out,

@@ -252,15 +252,17 @@ def test_flash_attention_fwd_bwd(C, B, T, H, D, causal):
     assert torch.allclose(lse, torch.logsumexp(s, -1), atol=2e-2, rtol=1e-3)
 
 
-@pytest.mark.parametrize("B,T,H,causal,amp", [(2, 512, 2, True, 3.0), (1, 320, 3, False, 3.0), (1, 1024, 2, True, 6.0)])
-def test_flash_attention_d64_spiky(C, B, T, H, causal, amp):
-    """Large-magnitude scores, so the D = 64 forward's lazy softmax rescale (raise
-    the reference max only when it grows by > 8 in log2 units) fires on many tiles;
-    keys are scaled up along the sequence so later tiles keep raising the max."""
+@pytest.mark.parametrize("B,T,H,causal,amp,D", [(2, 512, 2, True, 3.0, 64), (1, 320, 3, False, 3.0, 64),
+                                                 (1, 1024, 2, True, 6.0, 64), (2, 512, 2, True, 2.0, 128),
+                                                 (1, 333, 2, False, 2.0, 128)])
+def test_flash_attention_d64_spiky(C, B, T, H, causal, amp, D):
+    """Large-magnitude scores, so the second-generation forward's lazy softmax
+    rescale (raise the reference max only when it grows by > 8 in log2 units) fires
+    on many tiles; keys are scaled up along the sequence so later tiles keep raising
+    the max. D = 128 covers the head-dim-128 forward (fwd128_kernel)."""
     from cluster_anywhere_amd.ops.attention import attention_ref
     from cluster_anywhere_amd.ops.flash import flash_attention_qkv
 
-    D = 64
     torch.manual_seed(11)
     x = torch.randn(B, T, 3, H, D, device="cuda")
     ramp = torch.linspace(0.5, 2.0, T, device="cuda").view(1, T, 1, 1)
