@@ -52,14 +52,15 @@ def main():
         clk = gui / 8 / dur / 1e9 if gui and dur else None
         hit = (m["TCC_HIT_sum"] / max(1.0, m["TCC_HIT_sum"] + m["TCC_MISS_sum"])) if "TCC_HIT_sum" in m else None
         bank = (m["SQ_LDS_BANK_CONFLICT"] / max(1.0, m["SQ_LDS_IDX_ACTIVE"])) if "SQ_LDS_BANK_CONFLICT" in m else None
-        rows.append((key, n, dur, util, clk, hit, bank))
+        vpm = (m["SQ_INSTS_VALU"] / max(1.0, m["SQ_INSTS_MFMA"])) if "SQ_INSTS_MFMA" in m and "SQ_INSTS_VALU" in m else None
+        rows.append((key, n, dur, util, clk, hit, bank, vpm))
     rows.sort(key=lambda r: -((r[2] or 0) * r[1]))
     f = lambda x, fmt: "-" if x is None else fmt.format(x)
-    out = ["| kernel | WGs | dispatches | us (profiled) | MFMA util | clock GHz | L2 hit | LDS conflict/active |",
-           "|---|---|---|---|---|---|---|---|"]
-    for (k, g), n, dur, util, clk, hit, bank in rows:
+    out = ["| kernel | WGs | dispatches | us (profiled) | MFMA util | clock GHz | L2 hit | LDS conflict/active | VALU/MFMA |",
+           "|---|---|---|---|---|---|---|---|---|"]
+    for (k, g), n, dur, util, clk, hit, bank, vpm in rows:
         out.append(f"| `{k}` | {g} | {n} | {f(dur and dur * 1e6, '{:.1f}')} | {f(util, '{:.3f}')} | "
-                   f"{f(clk, '{:.2f}')} | {f(hit, '{:.3f}')} | {f(bank, '{:.3f}')} |")
+                   f"{f(clk, '{:.2f}')} | {f(hit, '{:.3f}')} | {f(bank, '{:.3f}')} | {f(vpm, '{:.2f}')} |")
     text = "\n".join(out)
     print(text)
     if a.md:
