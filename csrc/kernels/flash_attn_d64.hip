@@ -704,7 +704,7 @@ __device__ __forceinline__ void colsum_atomic(const f32x16 (&a)[2], float mul, f
 // backward dQ (+ Delta = rowsum(dO * O), lse2 = lse * log2 e for the dK/dV
 // kernel): 4 waves x 64 queries per block, 64-key tiles {K image, V image}.
 // ----------------------------------------------------------------------------
-template <int QS, int STG = 1>
+template <int QS, int STG = 1, int NEG = 0>
 __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o,
                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                         float* __restrict__ delta, float* __restrict__ lse2o,
@@ -760,8 +760,9 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
     dlt[qs] = dsum;
     lse2[qs] = q < T ? lse[(size_t)bh * T + q] * 1.44269504089f : 0.f;
     if (q < T && h == 0) {
-      delta[(size_t)bh * T + q] = dsum;
-      lse2o[(size_t)bh * T + q] = lse2[qs];
+      // NEG: negated for the dK/dV kernel's accumulator initialisation (OPT & 32)
+      delta[(size_t)bh * T + q] = NEG ? -dsum : dsum;
+      lse2o[(size_t)bh * T + q] = NEG ? -lse2[qs] : lse2[qs];
     }
     dq[qs][0] = dq[qs][1] = zero16();
   }
@@ -914,7 +915,9 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
 // first half's S / dP MFMAs just released); bit 1 = the transposed fragments of a
 // half requested before its S / dP MFMAs instead of after them; bit 2 = the half's
 // lse2 / delta rows read (and retired) before its S / dP MFMAs; bit 3 = dK / dV
-// written through an LDS transpose as whole rows.
+// written through an LDS transpose as whole rows; bit 5 = K pre-scaled by
+// log2(e)/sqrt(D) and the S / dP accumulators initialised with -lse2 / -delta (the dQ
+// kernel stores them negated), so the softmax pass is exp2 + one multiply per score.
 template <int ABL = 0, int OPT = 0>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ dout,
@@ -964,6 +967,15 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
 #pragma unroll
       for (int j = 0; j < 8; ++j) kf[s][j] = vf[s][j] = (bf16)0.f;
     }
+  }
+  if constexpr (OPT & 32) {
+    // K pre-scaled by log2(e) / sqrt(D) once per block: S' = Q (c K)^T - lse2 comes out
+    // of the MFMA chain (accumulator initialised with -lse2), so p = exp2(S') needs no
+    // FMA per score
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[s][j] = (bf16)((float)kf[s][j] * scale_log2);
   }
   f32x16 dk[2], dv[2];
   dk[0] = dk[1] = dv[0] = dv[1] = zero16();
@@ -1032,7 +1044,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
       // VALU pass does not wait on LDS (the compiler's own wait for them would land
       // behind the transposed reads and wait for those too)
       f32x4 l4s[4], d4s[4];
-      if constexpr (OPT & 4) {
+      if constexpr (OPT & (4 | 32)) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int qi = qh * 32 + 8 * g + 4 * h;
@@ -1043,9 +1055,19 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
                      : "+v"(l4s[0]), "+v"(l4s[1]), "+v"(l4s[2]), "+v"(l4s[3]), "+v"(d4s[0]), "+v"(d4s[1]),
                        "+v"(d4s[2]), "+v"(d4s[3])::"memory");
       }
+      f32x16 sinit = zero16(), dinit = zero16();
+      if constexpr (OPT & 32) {  // row constants as the initial accumulators: -lse2, -delta
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            sinit[4 * g + j] = l4s[g][j];
+            dinit[4 * g + j] = d4s[g][j];
+          }
+      }
       __builtin_amdgcn_sched_barrier(0);
-      f32x16 sacc = mfma32(qr[0], kf[0], zero16());
-      f32x16 dp = mfma32(dr[0], vf[0], zero16());
+      f32x16 sacc = mfma32(qr[0], kf[0], sinit);
+      f32x16 dp = mfma32(dr[0], vf[0], dinit);
 #pragma unroll
       for (int s = 1; s < 4; ++s) {
         sacc = mfma32(qr[s], kf[s], sacc);
@@ -1059,7 +1081,7 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
       for (int g = 0; g < 4; ++g) {
         const int qi = qh * 32 + 8 * g + 4 * h;
         f32x4 l4, d4;
-        if constexpr (OPT & 4) {
+        if constexpr (OPT & (4 | 32)) {
           l4 = l4s[g];
           d4 = d4s[g];
         } else {
@@ -1072,13 +1094,13 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
           if constexpr (ABL & 4) {
             continue;
           }
-          float p = fexp2(__builtin_fmaf(sacc[i], scale_log2, -l4[j]));
+          float p = (OPT & 32) ? fexp2(sacc[i]) : fexp2(__builtin_fmaf(sacc[i], scale_log2, -l4[j]));
           if constexpr (need_mask) {
             const int c = qh * 32 + 8 * g + j;
             p = (c < lo_lim || c > hi_lim) ? 0.f : p;
           }
           sacc[i] = p;
-          dp[i] = p * (dp[i] - d4[j]);
+          dp[i] = (OPT & 32) ? p * dp[i] : p * (dp[i] - d4[j]);
         }
       }
       tr_wait4(tv[0][0], tv[0][1], tk[0][0], tk[0][1]);
@@ -1218,17 +1240,19 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
   float* delta = ws;
   float* lse2 = ws + (size_t)B * H * T;
   const int nqb = (T + 127) / 128;  // (a 256-query dQ block variant spilled and was removed in round 4)
-  auto dq_kern = fa64_staged_stores() ? fa64::bwd_dq_kernel<1> : fa64::bwd_dq_kernel<1, 0>;
-  hipLaunchKernelGGL(dq_kern, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout, lse,
-                     delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
   static const int abl = [] {  // development timing ablations of dK/dV (tools/bench_attn.py)
     const char* e = std::getenv("CAAMD_FA64_BWD_ABL");
     return e ? std::atoi(e) : 0;
   }();
   static const int opt = [] {  // dK/dV schedule variants (see bwd_dkdv_kernel)
     const char* e = std::getenv("CAAMD_FA64_DKDV_OPT");
-    return e ? std::atoi(e) : (fa64_staged_stores() ? 8 : 0);
+    return e ? std::atoi(e) : (fa64_staged_stores() ? 40 : 32);
   }();
+  const bool neg = (opt & 32) && abl == 0;  // the dK/dV variant reads negated lse2 / delta
+  auto dq_kern = fa64_staged_stores() ? (neg ? fa64::bwd_dq_kernel<1, 1, 1> : fa64::bwd_dq_kernel<1>)
+                                      : (neg ? fa64::bwd_dq_kernel<1, 0, 1> : fa64::bwd_dq_kernel<1, 0>);
+  hipLaunchKernelGGL(dq_kern, dim3(B * H * nqb), dim3(256), 6 * fa64::IMG, st, qkv, out, dout, lse,
+                     delta, lse2, dqkv, T, H, nqb, scale_log2, scale, causal, dbias);
   auto kern = fa64::bwd_dkdv_kernel<0>;
   switch (opt) {
     case 1: kern = fa64::bwd_dkdv_kernel<0, 1>; break;
@@ -1239,6 +1263,9 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     case 6: kern = fa64::bwd_dkdv_kernel<0, 6>; break;
     case 8: kern = fa64::bwd_dkdv_kernel<0, 8>; break;
     case 12: kern = fa64::bwd_dkdv_kernel<0, 12>; break;
+    case 32: kern = fa64::bwd_dkdv_kernel<0, 32>; break;
+    case 40: kern = fa64::bwd_dkdv_kernel<0, 40>; break;
+    case 44: kern = fa64::bwd_dkdv_kernel<0, 44>; break;
     default: break;
   }
   switch (abl) {
