@@ -272,7 +272,7 @@ __device__ __forceinline__ void store_rows_lds(const f32x16 (&acc)[2], float mul
   }
 }
 
-template <int QS, int ABL = 0, int NW = 4, int STG = 1>
+template <int QS, int ABL = 0, int NW = 4, int STG = 1, int PRE = 0>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_kernel(const bf16* __restrict__ qp, const bf16* __restrict__ kp,
                                                      const bf16* __restrict__ vp, int q_rs, int kv_rs, int group,
                                                      bf16* __restrict__ out, float* __restrict__ lse, int T,
@@ -327,6 +327,21 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
     m[qs] = -INFINITY;
     l[qs] = 0.f;
   }
+  // PRE: Q pre-scaled by log2(e)/sqrt(D) and the S accumulators started from
+  // -(reference max) (minit, a splat kept in registers and rewritten only when the
+  // lazy rescale raises the max): the MFMA chain leaves exp2's argument, p = exp2(S')
+  // needs no FMA per score
+  f32x16 minit[QS];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int qs = 0; qs < QS; ++qs) {
+      minit[qs] = zero16();
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[qs][s][j] = (bf16)((float)qf[qs][s][j] * scale_log2);
+    }
+  }
   wait_dma();
   __syncthreads();
 
@@ -347,7 +362,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
       for (int s = 0; s < 4; ++s) kf[s] = *(lds_bf16x8*)(kimg + koff[s] + kb * 4096);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[0], qf[qs][0], zero16());
+      for (int qs = 0; qs < QS; ++qs) sacc[qs][kb] = mfma32(kf[0], qf[qs][0], PRE ? minit[qs] : zero16());
 #pragma unroll
       for (int s = 1; s < 4; ++s)
 #pragma unroll
@@ -379,6 +394,38 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
         mxb = fmaxf(mxb, sacc[qs][1][i]);
       }
       float mx = fmaxf(mxa, mxb);
+      float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (PRE) {
+        // sacc = c S - muse (muse = the reference max, 0 before the first tile)
+        mx = max_xor32(mx);
+        if (__builtin_amdgcn_ballot_w64(mx > kThr || (m[qs] == -INFINITY && mx > -INFINITY)) != 0) {
+          asm volatile("");  // a real (rarely taken) branch
+          const float muse_old = m[qs] == -INFINITY ? 0.f : m[qs];
+          const float mnew = fmaxf(m[qs], mx + muse_old);
+          const float alpha = m[qs] == -INFINITY ? 0.f : fexp2(m[qs] - mnew);
+          l[qs] *= alpha;
+#pragma unroll
+          for (int d = 0; d < 2; ++d)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[qs][d][i] *= alpha;
+          m[qs] = mnew;
+          const float shift = (mnew == -INFINITY ? 0.f : mnew) - muse_old;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sacc[qs][kb][i] -= shift;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) minit[qs][i] = mnew == -INFINITY ? 0.f : -mnew;
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float p = fexp2(sacc[qs][kb][i]);
+            sacc[qs][kb][i] = p;
+            rs4[i & 3] += p;
+          }
+      } else {
       mx = max_xor32(mx) * scale_log2;  // scale > 0 commutes with max
       // lazy rescale: raise the reference max only when it grew by > kThr somewhere
       if (__builtin_amdgcn_ballot_w64(mx > m[qs] + kThr) != 0) {
@@ -393,7 +440,6 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
         m[qs] = mnew;
       }
       const float muse = m[qs] == -INFINITY ? 0.f : m[qs];
-      float rs4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -403,6 +449,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
           sacc[qs][kb][i] = p;
           rs4[i & 3] += p;
         }
+      }
       l[qs] += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);  // this lane's key half only
     }
     // O^T += V^T P^T ; each V^T fragment feeds both query sub-blocks
@@ -1217,7 +1264,12 @@ void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int 
     return e ? std::atoi(e) : 0;
   }();
   const int nqb = (T + 127) / 128;
-  auto kern = fa64_staged_stores() ? fa64::fwd_kernel<1, 0> : fa64::fwd_kernel<1, 0, 4, 0>;
+  static const bool pre = [] {  // CAAMD_FA64_FWD_PRE=0: the FMA-per-score forward (A/B)
+    const char* e = std::getenv("CAAMD_FA64_FWD_PRE");
+    return !(e && e[0] == '0');
+  }();
+  auto kern = fa64_staged_stores() ? (pre ? fa64::fwd_kernel<1, 0, 4, 1, 1> : fa64::fwd_kernel<1, 0>)
+                                   : (pre ? fa64::fwd_kernel<1, 0, 4, 0, 1> : fa64::fwd_kernel<1, 0, 4, 0>);
   switch (abl) {
     case 1: kern = fa64::fwd_kernel<1, 1>; break;
     case 2: kern = fa64::fwd_kernel<1, 2>; break;
