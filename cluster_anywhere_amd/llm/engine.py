@@ -138,6 +138,16 @@ class LLMEngine:
         # (batch size, seconds) of every decode step: forward + sampling, host included
         self.decode_times: List[tuple] = []
         self._pinned: Dict[int, Dict[str, torch.Tensor]] = {}
+        # one-step-ahead decode (greedy batches on HIP graphs): step t + 1 is launched
+        # with step t's argmax still on the GPU, and step t's tokens are read back and
+        # processed while t + 1 runs, so the host work of a step (reading tokens,
+        # appending, building the next inputs) overlaps the GPU (CAAMD_LLM_ASYNC=0: off)
+        import os as _os
+
+        self._async = self.use_graphs and _os.environ.get("CAAMD_LLM_ASYNC", "1") != "0"
+        self._inflight: Optional[dict] = None
+        self._async_flip = 0
+        self._last_finish: Optional[float] = None
         self._gen = torch.Generator(device=self.device)
         self._gen.manual_seed(0)
 
@@ -242,15 +252,19 @@ class LLMEngine:
         self.stats["prefill_tokens"] += sum(s.ctx for s in batch)
         return logits
 
-    def _decode_inputs(self, batch: List[_Seq], B: int):
+    def _decode_inputs(self, batch: List[_Seq], B: int, pending: int = 0, key=None):
         """Decode inputs built with numpy in (pinned, reused) host buffers: no
-        per-sequence tensor construction, and the H2D copies are truly async."""
+        per-sequence tensor construction, and the H2D copies are truly async.
+        ``pending``: tokens already generated on the GPU but not yet appended (the
+        one-step-ahead path); ``key`` selects the pinned buffer set (that path
+        alternates two, so a set is never rewritten while its copies are queued)."""
         import numpy as np
 
-        buf = self._pinned.get(B)
+        key = B if key is None else key
+        buf = self._pinned.get(key)
         if buf is None:
             pin = self.device.type == "cuda"
-            buf = self._pinned[B] = {
+            buf = self._pinned[key] = {
                 "toks": torch.zeros(B, dtype=torch.long, pin_memory=pin),
                 "pos": torch.zeros(B, dtype=torch.int32, pin_memory=pin),
                 "slots": torch.full((B,), -1, dtype=torch.int32, pin_memory=pin),
@@ -258,9 +272,10 @@ class LLMEngine:
                 "bt": torch.zeros(B, self.max_blocks_per_seq, dtype=torch.int32, pin_memory=pin)}
         n = len(batch)
         toks, pos, slots, ctx, bt = (buf[k].numpy() for k in ("toks", "pos", "slots", "ctx", "bt"))
-        c = np.fromiter((s.ctx for s in batch), np.int32, n)
+        c = np.fromiter((s.ctx for s in batch), np.int32, n) + pending
         p = c - 1  # position of the newest (not yet cached) token
-        toks[:n] = np.fromiter((s.last_token for s in batch), np.int64, n)
+        if not pending:
+            toks[:n] = np.fromiter((s.last_token for s in batch), np.int64, n)
         toks[n:] = 0
         pos[:n], pos[n:] = p, 0
         ctx[:n], ctx[n:] = c, 0
@@ -325,6 +340,77 @@ class LLMEngine:
         return self.model.decode(toks.to(dev), pos.to(dev), slots.to(dev), self.k_caches, self.v_caches,
                                  bt.to(dev), ctx.to(dev), max_ctx)
 
+    # ------------------------------------------------------- one step ahead
+    def _async_ok(self, batch: List[_Seq]) -> bool:
+        from ..ops._lib import kernels
+
+        return (self._async and len(batch) <= self.max_num_seqs and all(s.params.temperature <= 0 for s in batch)
+                and hasattr(kernels(), "argmax_rows"))
+
+    def _launch_ahead(self, prev: Optional[dict]) -> Optional[dict]:
+        """Launch one greedy decode step for the running sequences without waiting
+        for ``prev`` (the step in flight, if any): its tokens are gathered on the GPU
+        as this step's input. Returns the in-flight record, or None when the step
+        cannot be launched ahead (a cache block is missing, or nothing would run)."""
+        from ..ops._lib import kernels
+
+        pending = 1 if prev is not None else 0
+        # sequences that reach max_tokens with prev's token are done: no further step
+        batch = [s for s in self.running if len(s.out) + pending < s.params.max_tokens]
+        if not batch or not self._async_ok(batch):
+            return None
+        for s in batch:  # blocks for the token this step writes (position ctx - 1 + pending)
+            need = self._blocks_needed(s.ctx + pending + 1) - len(s.blocks)
+            if need > 0:
+                got = self.alloc.allocate(need)
+                if got is None:
+                    return None
+                s.blocks.extend(got)
+        n = len(batch)
+        B = self._bucket(n)
+        graph, st, out = self._graph_for(B)
+        self._async_flip ^= 1
+        toks, pos, slots, bt, ctx = self._decode_inputs(batch, B, pending, key=(B, self._async_flip))
+        dev = self.device
+        if prev is not None:
+            where = {id(s): i for i, s in enumerate(prev["batch"])}
+            idx = [where[id(s)] for s in batch]
+            if idx == list(range(n)):
+                st["toks"][:n].copy_(prev["toks_dev"][:n])
+            else:
+                st["toks"][:n].copy_(prev["toks_dev"][torch.tensor(idx, device=dev)])
+        else:
+            st["toks"].copy_(toks, non_blocking=True)
+        st["pos"].copy_(pos, non_blocking=True)
+        st["slots"].copy_(slots, non_blocking=True)
+        st["bt"].copy_(bt, non_blocking=True)
+        st["ctx"].copy_(ctx, non_blocking=True)
+        graph.replay()
+        toks_dev = kernels().argmax_rows(out[:n])
+        host = self._pinned.setdefault(("out", B, self._async_flip),
+                                       torch.empty(B, dtype=torch.long, pin_memory=True))
+        host[:n].copy_(toks_dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.stats["decode_tokens"] += n
+        return {"batch": batch, "toks_dev": toks_dev, "host": host, "event": ev}
+
+    def _finish_ahead(self, inf: dict) -> List[RequestOutput]:
+        """Read back an in-flight step's tokens and append them; sequences that
+        finished (or were aborted) in the meantime drop their extra token."""
+        inf["event"].synchronize()
+        batch = inf["batch"]
+        toks = inf["host"][: len(batch)].tolist()
+        now_p = time.perf_counter()
+        if self._last_finish is not None:
+            self.decode_times.append((len(batch), now_p - self._last_finish))
+        self._last_finish = now_p
+        live = {id(x) for x in self.running}
+        keep = [(s, t) for s, t in zip(batch, toks) if s.finish_reason is None and id(s) in live]
+        if not keep:
+            return []
+        return self._append([s for s, _ in keep], [t for _, t in keep], time.time())
+
     def _sample(self, logits: torch.Tensor, batch: List[_Seq]) -> List[int]:
         temps = [s.params.temperature for s in batch]
         if all(t <= 0 for t in temps) and logits.is_cuda and logits.dtype == torch.bfloat16 and logits.dim() == 2:
@@ -387,6 +473,16 @@ class LLMEngine:
         every running sequence. Returns the sequences that produced a token."""
         with self.lock:
             self.stats["steps"] += 1
+            if self._inflight is not None:
+                inf, self._inflight = self._inflight, None
+                # keep one step ahead while no waiting request could be admitted
+                admit = bool(self.waiting) and len(self.running) < self.max_num_seqs
+                if not admit:
+                    self._inflight = self._launch_ahead(inf)
+                outs = self._finish_ahead(inf)
+                if self._inflight is None:
+                    self._last_finish = None
+                return outs
             batch = self._schedule_prefill()
             if batch:
                 logits = self._run_prefill(batch)
@@ -399,6 +495,11 @@ class LLMEngine:
             batch = list(self.running)
             if not batch:
                 return []
+            if self._async_ok(batch) and not (self.waiting and len(self.running) < self.max_num_seqs):
+                self._inflight = self._launch_ahead(None)
+                if self._inflight is not None:
+                    self._last_finish = time.perf_counter()
+                    return []
             t0 = time.perf_counter()
             logits = self._run_decode(batch)
             toks = self._sample(logits, batch)

@@ -137,6 +137,42 @@ def test_llama_engine_gpu():
     assert agree > 0.75 and bool((gap <= 0.05 * spread).all()), (agree, (gap / spread).max().item())
 
 
+def test_llama_engine_one_step_ahead_matches_sync():
+    """The one-step-ahead greedy decode (step t + 1 launched before step t's tokens
+    are read back) gives the same tokens as the synchronous loop: more prompts than
+    sequence slots (draining for admissions), different max_tokens, and stop tokens
+    that end sequences while their next step is already in flight."""
+    from cluster_anywhere_amd.llm import LLMEngine, SamplingParams
+    from cluster_anywhere_amd.models.llama import Llama, LlamaConfig
+
+    torch.manual_seed(3)
+    cfg = LlamaConfig.named("llama-small")
+    m = Llama(cfg).to("cuda", torch.bfloat16).init_weights(std=0.02)
+    g = torch.Generator().manual_seed(5)
+    prompts = [torch.randint(1, cfg.vocab_size, (int(n),), generator=g).tolist()
+               for n in torch.randint(3, 90, (11,), generator=g)]
+
+    def run(async_mode, stops):
+        e = LLMEngine(m, max_num_seqs=4, max_model_len=512, num_blocks=512, use_graphs=True)
+        e._async = async_mode
+        ids = [e.add_request(p, SamplingParams(max_tokens=6 + 3 * (i % 4), stop_token_ids=stops.get(i, [])))
+               for i, p in enumerate(prompts)]
+        final = {}
+        while e.has_unfinished():
+            for o in e.step():
+                if o.finished:
+                    final[o.request_id] = o
+        assert e._inflight is None
+        return [(final[i].output_token_ids, final[i].finish_reason) for i in ids]
+
+    plain = run(False, {})
+    stops = {i: [plain[i][0][2]] for i in range(0, len(prompts), 2)}  # every other request stops early
+    ref = run(False, stops)
+    assert any(r == "stop" for _, r in ref)
+    assert run(True, stops) == ref
+    assert run(True, {}) == plain
+
+
 @pytest.mark.parametrize("M", [1, 7, 32, 100, 128])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (1024, 14336), (28672, 4096), (64, 512)])
 def test_skinny_decode_gemm(C, M, N, K):
