@@ -348,6 +348,20 @@ def gemm(a: torch.Tensor, b: torch.Tensor, layout: int = 0, *, algo: Optional[in
 # epilogues, so prefill keeps no second copy of the weights and no [M, 2F]
 # intermediate.
 PREFILL_ALGO = int(os.environ.get("CAAMD_PREFILL_ALGO", "9"))  # 256 x 256: four phases, DMA over two (tools/bench_prefill_gemm.py)
+_PREFILL_ALGO_FORCED = "CAAMD_PREFILL_ALGO" in os.environ
+
+
+def prefill_algo(M: int, N: int, K: int, epi: int) -> int:
+    """Full-line kernel variant per prefill projection. Measured at the serving
+    bench's 8192-token chunks (tools/bench_prefill_gemm.py --tokens 8192,
+    profiles/prefill_algo_8192_r5.jsonl): qkv 380.7 -> 312.2 us and o 234.4 -> 221.5 us
+    with DMA over three phases (3009), gate/up + SwiGLU 1578.9 -> 1466.9 us and down
+    736.9 -> 727.2 us with two phases (4009); above 8192 tokens the round-4 choice (9)."""
+    if _PREFILL_ALGO_FORCED or M > 8192:
+        return PREFILL_ALGO
+    if epi == EPI_SWIGLU or K >= 8192:
+        return 4009
+    return 3009
 
 
 def prefill_ok(M: int, N: int, K: int) -> bool:
@@ -365,7 +379,7 @@ def prefill_linear(x2: torch.Tensor, wp: torch.Tensor, *, epi: int = EPI_BF16, o
         raise ValueError(f"prefill_linear: M % 256, N % 256, K % 64 must be 0 (M={M} N={N} K={K})")
     if out is None:
         out = torch.empty(M, N // 2 if epi == EPI_SWIGLU else N, device=x2.device, dtype=torch.bfloat16)
-    algo = PREFILL_ALGO
+    algo = prefill_algo(M, N, K, epi)
     full, S = tail_plan(M, N, K, 256, 256, x2.device, algo)
     ws = cnt = None
     if S > 1:

@@ -62,7 +62,7 @@ def main():
                           "pfs": round(fl / us / 1e9, 3)}), flush=True)
         wp = L.pack_decode_weight(L.interleave_gate_up(w) if epi == 5 else w)
         for algo in [int(t) for t in a.algos.split(",")]:
-            G.PREFILL_ALGO = algo
+            G.PREFILL_ALGO, G._PREFILL_ALGO_FORCED = algo, True
             out = r.clone()
             if epi == 5:
                 fn = lambda: G.prefill_linear(x, wp, epi=G.EPI_SWIGLU)  # noqa: E731
