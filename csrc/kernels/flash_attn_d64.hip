@@ -552,6 +552,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 4 : (QS == 2 ? 2 : 3)) void fwd_
 // the D = 64 kernel. Replaces flash_attention.hip's first-generation
 // fa_fwd_kernel<128> (131.9 us per Llama-3-8B prefill chunk, B16 T512 H32 KVH8).
 // ----------------------------------------------------------------------------
+template <int PRE = 1>
 __global__ __launch_bounds__(256, 2) void fwd128_kernel(const bf16* __restrict__ qp, const bf16* __restrict__ kp,
                                                         const bf16* __restrict__ vp, int q_rs, int kv_rs, int group,
                                                         bf16* __restrict__ out, float* __restrict__ lse, int T, int H,
@@ -601,6 +602,15 @@ __global__ __launch_bounds__(256, 2) void fwd128_kernel(const bf16* __restrict__
 #pragma unroll
   for (int d = 0; d < 4; ++d) o[d] = zero16();
   float m = -INFINITY, l = 0.f;
+  // PRE (as fwd_kernel): Q pre-scaled by log2(e)/sqrt(D), S accumulators start from
+  // -(reference max), p = exp2(S') with no FMA per score
+  f32x16 minit = zero16();
+  if constexpr (PRE) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qf[s][j] = (bf16)((float)qf[s][j] * scale_log2);
+  }
   wait_dma();
   __syncthreads();
 
@@ -618,7 +628,7 @@ __global__ __launch_bounds__(256, 2) void fwd128_kernel(const bf16* __restrict__
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-          sacc[kb] = mfma32(kf[s], qf[4 * half + s], (half == 0 && s == 0) ? zero16() : sacc[kb]);
+          sacc[kb] = mfma32(kf[s], qf[4 * half + s], (half == 0 && s == 0) ? (PRE ? minit : zero16()) : sacc[kb]);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
@@ -645,6 +655,37 @@ __global__ __launch_bounds__(256, 2) void fwd128_kernel(const bf16* __restrict__
       mxb = fmaxf(mxb, sacc[1][i]);
     }
     float mx = fmaxf(mxa, mxb);
+    float rs4[4] = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (PRE) {
+      mx = max_xor32(mx);  // relative to the current reference max (0 before the first)
+      if (__builtin_amdgcn_ballot_w64(mx > kThr || (m == -INFINITY && mx > -INFINITY)) != 0) {
+        asm volatile("");
+        const float muse_old = m == -INFINITY ? 0.f : m;
+        const float mnew = fmaxf(m, mx + muse_old);
+        const float alpha = m == -INFINITY ? 0.f : fexp2(m - mnew);
+        l *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[d][i] *= alpha;
+        m = mnew;
+        const float shift = (mnew == -INFINITY ? 0.f : mnew) - muse_old;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sacc[kb][i] -= shift;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) minit[i] = mnew == -INFINITY ? 0.f : -mnew;
+      }
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = fexp2(sacc[kb][i]);
+          sacc[kb][i] = p;
+          rs4[i & 3] += p;
+        }
+    } else {
     mx = max_xor32(mx) * scale_log2;
     if (__builtin_amdgcn_ballot_w64(mx > m + kThr) != 0) {
       asm volatile("");
@@ -658,7 +699,6 @@ __global__ __launch_bounds__(256, 2) void fwd128_kernel(const bf16* __restrict__
       m = mnew;
     }
     const float muse = m == -INFINITY ? 0.f : m;
-    float rs4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -667,6 +707,7 @@ __global__ __launch_bounds__(256, 2) void fwd128_kernel(const bf16* __restrict__
         sacc[kb][i] = p;
         rs4[i & 3] += p;
       }
+    }
     l += (rs4[0] + rs4[1]) + (rs4[2] + rs4[3]);
     static_for<2>([&](auto kb_c) {
       constexpr int kb = decltype(kb_c)::value;
@@ -1243,13 +1284,20 @@ void fa128_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int
                       float* lse, int B, int T, int H, int causal, hipStream_t st) {
   const float scale_log2 = 1.44269504089f / sqrtf(128.f);
   const int nqb = (T + 127) / 128;
+  static const bool pre = [] {  // CAAMD_FA64_FWD_PRE=0: FMA per score (A/B)
+    const char* e = std::getenv("CAAMD_FA64_FWD_PRE");
+    return !(e && e[0] == '0');
+  }();
+  auto kern = pre ? fa64::fwd128_kernel<1> : fa64::fwd128_kernel<0>;
   static const bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)fa64::fwd128_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)fa64::fwd128_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              8 * fa64::IMG);
+    (void)hipFuncSetAttribute((const void*)fa64::fwd128_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               8 * fa64::IMG);
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL(fa64::fwd128_kernel, dim3(B * H * nqb), dim3(256), 8 * fa64::IMG, st, q, k, v, q_rs, kv_rs,
+  hipLaunchKernelGGL(kern, dim3(B * H * nqb), dim3(256), 8 * fa64::IMG, st, q, k, v, q_rs, kv_rs,
                      group, out, lse, T, H, nqb, scale_log2, causal);
 }
 
