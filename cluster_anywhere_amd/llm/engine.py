@@ -383,6 +383,8 @@ class LLMEngine:
         dev = self.device
         if prev is not None:
             where = {id(s): i for i, s in enumerate(prev["batch"])}
+            if any(id(s) not in where for s in batch):  # (cannot happen: joins only after a drain)
+                return None
             idx = [where[id(s)] for s in batch]
             if idx == list(range(n)):
                 st["toks"][:n].copy_(prev["toks_dev"][:n])
