@@ -1046,15 +1046,36 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
   if (qt0 + 1 < nqt) issue(qt0 + 1, smem + STAGE);
 
   bf16x8 kf[4], vf[4];
+  if constexpr (OPT & 64) {
+    // the block's 128 K rows by LDS-DMA into the third stage (whole 128-byte rows, 8
+    // lanes a row) instead of per-lane 16-byte loads that touch 32 rows per instruction;
+    // read back as row fragments before that stage's first tile is issued
+    dma_tile(kbase, rs, kb0 * 128, T, smem + 2 * STAGE, wave, lane);
+    dma_tile(kbase, rs, kb0 * 128 + 64, T, smem + 2 * STAGE + IMG, wave, lane);
+  }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     if (kv) {
-      kf[s] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)key * rs + 16 * s + 8 * h);
+      if constexpr (!(OPT & 64)) kf[s] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)key * rs + 16 * s + 8 * h);
       vf[s] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)key * rs + 16 * s + 8 * h);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) kf[s][j] = vf[s][j] = (bf16)0.f;
     }
+  }
+  if constexpr (OPT & 64) {
+    wait_dma();
+    __syncthreads();
+    typedef __attribute__((address_space(3))) const bf16x8 lds_kf;
+    const lds_t* kimg = smem + 2 * STAGE + (wave >> 1) * IMG;
+    const int row = (wave & 1) * 32 + r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 v = *(lds_kf*)(kimg + row * 128 + (((2 * s + h) ^ swz(row)) << 4));
+      if (kv) kf[s] = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave has its K fragments: the stage is free for tile qt0 + 2
   }
   if constexpr (OPT & 32) {
     // K pre-scaled by log2(e) / sqrt(D) once per block: S' = Q (c K)^T - lse2 comes out
@@ -1366,6 +1387,7 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     case 32: kern = fa64::bwd_dkdv_kernel<0, 32>; break;
     case 40: kern = fa64::bwd_dkdv_kernel<0, 40>; break;
     case 44: kern = fa64::bwd_dkdv_kernel<0, 44>; break;
+    case 104: kern = fa64::bwd_dkdv_kernel<0, 104>; break;
     default: break;
   }
   switch (abl) {
