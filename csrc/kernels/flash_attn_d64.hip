@@ -1005,7 +1005,8 @@ __global__ __launch_bounds__(256, QS == 2 ? 2 : 3) void bwd_dq_kernel(const bf16
 // lse2 / delta rows read (and retired) before its S / dP MFMAs; bit 3 = dK / dV
 // written through an LDS transpose as whole rows; bit 5 = K pre-scaled by
 // log2(e)/sqrt(D) and the S / dP accumulators initialised with -lse2 / -delta (the dQ
-// kernel stores them negated), so the softmax pass is exp2 + one multiply per score.
+// kernel stores them negated), so the softmax pass is exp2 + one multiply per score;
+// bit 6 = the block's K rows by LDS-DMA through the third stage in the prologue.
 template <int ABL = 0, int OPT = 0>
 __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict__ qkv,
                                                           const bf16* __restrict__ dout,
@@ -1367,7 +1368,7 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
   }();
   static const int opt = [] {  // dK/dV schedule variants (see bwd_dkdv_kernel)
     const char* e = std::getenv("CAAMD_FA64_DKDV_OPT");
-    return e ? std::atoi(e) : (fa64_staged_stores() ? 40 : 32);
+    return e ? std::atoi(e) : (fa64_staged_stores() ? 104 : 32);
   }();
   const bool neg = (opt & 32) && abl == 0;  // the dK/dV variant reads negated lse2 / delta
   auto dq_kern = fa64_staged_stores() ? (neg ? fa64::bwd_dq_kernel<1, 1, 1> : fa64::bwd_dq_kernel<1>)
