@@ -398,8 +398,9 @@ class LLMEngine:
         st["ctx"].copy_(ctx, non_blocking=True)
         graph.replay()
         toks_dev = kernels().argmax_rows(out[:n])
-        host = self._pinned.setdefault(("out", B, self._async_flip),
-                                       torch.empty(B, dtype=torch.long, pin_memory=True))
+        host = self._pinned.get(("out", B, self._async_flip))
+        if host is None:  # (setdefault would allocate pinned memory on every step)
+            host = self._pinned[("out", B, self._async_flip)] = torch.empty(B, dtype=torch.long, pin_memory=True)
         host[:n].copy_(toks_dev, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
