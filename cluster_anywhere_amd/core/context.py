@@ -25,3 +25,17 @@ def current_task() -> "TaskContext":
 
 def set_current_task(ctx):
     _tls.ctx = ctx
+
+
+# the placement-group strategy tuple of this process's actor (set at actor creation):
+# its method calls -- including ones running on thread pools or event loops, which
+# have no task context of their own -- belong to the actor's placement group
+actor_pg = None
+
+
+def current_pg():
+    """``("pg", pg_id, bundle, capture)`` of the running task, else of this actor."""
+    ctx = getattr(_tls, "ctx", None)
+    if ctx is not None and getattr(ctx, "pg", None):
+        return ctx.pg
+    return actor_pg

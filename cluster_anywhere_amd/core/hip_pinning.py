@@ -84,6 +84,20 @@ def pin_object_store(max_bytes: Optional[int] = None) -> bool:
         return True
 
 
+_async_started = False
+
+
+def pin_object_store_async() -> None:
+    """Start :func:`pin_object_store` once, on a background thread (callers take the
+    staging copy until :func:`arena_contains` says the arena is registered)."""
+    global _async_started
+    with _lock:
+        if _async_started or _tried:
+            return
+        _async_started = True
+    threading.Thread(target=pin_object_store, name="caamd-pin-arena", daemon=True).start()
+
+
 def arena_contains(arr) -> bool:
     """True if ``arr``'s buffer lies inside ONE registered chunk (a copy must not
     span two registrations)."""

@@ -147,9 +147,9 @@ def _strategy_tuple(o: Dict[str, Any]):
         st = PlacementGroupSchedulingStrategy(pg, o.get("placement_group_bundle_index", -1),
                                               o.get("placement_group_capture_child_tasks"))
     if st is None or st == "DEFAULT":
-        ctx = context.current_task()
-        if ctx is not None and ctx.pg is not None and len(ctx.pg) > 3 and ctx.pg[3]:
-            return ("pg", ctx.pg[1], -1, True)
+        cur = context.current_pg()
+        if cur is not None and len(cur) > 3 and cur[3]:
+            return ("pg", cur[1], -1, True)
         return None
     if st == "SPREAD":
         return ("spread",)

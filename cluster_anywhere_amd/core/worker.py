@@ -1260,6 +1260,7 @@ class CoreWorker:
                 cls = self._function(spec)
                 self.actor_id = spec.actor_id
                 self.actor_opts = spec.actor_opts or {}
+                context.actor_pg = spec.strategy if spec.strategy and spec.strategy[0] == "pg" else None
                 context.current_task().actor_id = spec.actor_id
                 self.actor_instance = cls(*args, **kwargs)
                 self._setup_actor_concurrency(cls)

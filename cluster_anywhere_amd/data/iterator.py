@@ -131,19 +131,43 @@ class DataIterator:
         device = torch.device(device) if isinstance(device, str) else device
         gpu = device.type == "cuda"
 
+        registered = False
+        if gpu:
+            # batches whose numpy buffer lies in the HIP-registered object-store arena
+            # are copied straight from shared memory (no pin_memory() staging copy);
+            # the arena is registered in the background, batches take the staging
+            # copy until it is
+            from ..core import hip_pinning
+
+            registered = True
+            hip_pinning.pin_object_store_async()
+
         def to_host(batch):
             if collate_fn is not None:
                 return collate_fn(batch)
+            from ..core.hip_pinning import arena_contains
+
             out = {}
             for k, v in batch.items():
                 if v.dtype == object:
                     out[k] = v
                     continue
-                t = torch.from_numpy(np.ascontiguousarray(v))
                 dt = dtypes.get(k) if isinstance(dtypes, dict) else dtypes
-                if dt is not None:
-                    t = t.to(dt)
-                if gpu:
+                direct = registered and v.flags["C_CONTIGUOUS"] and arena_contains(v)
+                if direct:
+                    import warnings
+
+                    with warnings.catch_warnings():  # read-only shm view; only ever read
+                        warnings.simplefilter("ignore", UserWarning)
+                        t = torch.from_numpy(v)
+                    if dt is not None and t.dtype != dt:
+                        t = t.to(dt)  # the conversion makes an ordinary host tensor
+                        direct = False
+                else:
+                    t = torch.from_numpy(np.ascontiguousarray(v))
+                    if dt is not None:
+                        t = t.to(dt)
+                if gpu and not direct:
                     t = t.pin_memory()
                 out[k] = t
             return out
@@ -157,27 +181,25 @@ class DataIterator:
         if not gpu:
             yield from host_batches
             return
-        stream = torch.cuda.Stream(device)
+        # copies run one batch ahead on a side stream; hand_over() makes the compute
+        # stream wait for them and record_stream()s every device tensor, so a dropped
+        # batch's HBM is not reused by the next copy while compute still reads it
+        from ..util.device_transfer import SideStreamMover
 
-        def move(b):
-            with torch.cuda.stream(stream):
-                if isinstance(b, dict):
-                    return {k: (v.to(device, non_blocking=True) if isinstance(v, torch.Tensor) else v)
-                            for k, v in b.items()}
-                if isinstance(b, torch.Tensor):
-                    return b.to(device, non_blocking=True)
-                return b
-
-        nxt = None
-        for hb in host_batches:
-            cur = move(hb)
+        mover = SideStreamMover(device)
+        try:
+            nxt = None
+            for hb in host_batches:
+                # hand the staged batch over BEFORE enqueuing the next copy, so the
+                # compute stream waits for that batch's copy only
+                ready = mover.hand_over(nxt) if nxt is not None else None
+                nxt = mover.stage(hb)
+                if ready is not None:
+                    yield ready
             if nxt is not None:
-                torch.cuda.current_stream(device).wait_stream(stream)
-                yield nxt
-            nxt = cur
-        if nxt is not None:
-            torch.cuda.current_stream(device).wait_stream(stream)
-            yield nxt
+                yield mover.hand_over(nxt)
+        finally:
+            mover.close()
 
     def materialize(self):
         from .dataset import Dataset

@@ -51,7 +51,8 @@ def start(http_options: Union[None, dict, HTTPOptions] = None, detached: bool = 
         http_options = http_options or HTTPOptions()
         P = ActorClass(HTTPProxy, {})
         proxy = P.options(num_cpus=0, max_concurrency=8, name="SERVE_PROXY", namespace=NAMESPACE,
-                          lifetime="detached").remote(http_options.host, http_options.port)
+                          lifetime="detached").remote(http_options.host, http_options.port,
+                                                      http_options.request_timeout_s)
         port = core.get(proxy.ready.remote())
         core.get(ctl.set_proxy.remote(proxy, port))
     return ctl
@@ -132,6 +133,19 @@ def run(target: Union[Application, Deployment], *, name: str = "default", route_
         target = target.bind()
     if not isinstance(target, Application):
         raise TypeError("serve.run() expects an Application (Deployment.bind(...))")
+    if not name:
+        from .exceptions import RayServeException
+
+        raise RayServeException("Application name must a non-empty string.")
+    import os
+
+    if os.environ.get("RAY_SERVE_FORCE_LOCAL_TESTING_MODE", "0") == "1":
+        _local_testing_mode = True
+    if _local_testing_mode:
+        # every deployment in this process, no cluster needed (api.py:438-454)
+        from .local_testing_mode import run_local
+
+        return run_local(target, name)
     if target.deployment.route_prefix is not None and route_prefix == "/":
         route_prefix = target.deployment.route_prefix
     ctl = start(proxy_location="HeadOnly" if http and route_prefix is not None else "Disabled")

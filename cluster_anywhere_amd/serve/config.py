@@ -72,6 +72,26 @@ class DeploymentConfig:
     max_replicas_per_node: Optional[int] = None
     version: Optional[str] = None
 
+    def __post_init__(self):
+        # reference: serve/_private/config.py:432 (_validate_max_replicas_per_node),
+        # schema.py:411-420 (not together with placement_group_bundles)
+        if self.max_queued_requests is not None and self.max_queued_requests != -1 and self.max_queued_requests < 1:
+            raise ValueError("max_queued_requests must be -1 (no limit) or a positive integer")
+        if self.max_ongoing_requests is not None and self.max_ongoing_requests < 1:
+            raise ValueError("max_ongoing_requests must be a positive integer")
+        if self.max_replicas_per_node is not None:
+            if not (1 <= int(self.max_replicas_per_node) <= 100):
+                raise ValueError("max_replicas_per_node must be between 1 and 100")
+            if self.placement_group_bundles is not None:
+                raise ValueError("Setting max_replicas_per_node is not allowed when "
+                                 "placement_group_bundles is provided.")
+        if self.placement_group_bundles is not None:
+            from ..util.placement_group import VALID_STRATEGIES, _validate_bundles
+
+            _validate_bundles(self.placement_group_bundles)
+            if self.placement_group_strategy not in VALID_STRATEGIES:
+                raise ValueError(f"Invalid placement group strategy {self.placement_group_strategy}")
+
     def initial_replicas(self) -> int:
         a = self.autoscaling_config
         if a is not None:

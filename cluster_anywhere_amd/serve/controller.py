@@ -33,6 +33,7 @@ CONTROLLER_NAME = "SERVE_CONTROLLER"
 NAMESPACE = "serve"
 CHECKPOINT_KEY = b"serve:controller_checkpoint"
 REPLICA_PREFIX = "SERVE_REPLICA::"
+REPLICA_PG_PREFIX = "SERVE_REPLICA_PG::"
 
 
 class _ReplicaState:
@@ -47,6 +48,8 @@ class _ReplicaState:
         self.metrics_ref = None
         self.started = time.time()
         self.stop_ref = None
+        self.node_id: Optional[str] = None  # known at start (max_replicas_per_node) or from metrics
+        self.pg = None  # per-replica placement group (placement_group_bundles)
 
 
 class _DeploymentState:
@@ -145,7 +148,15 @@ class ServeController:
                         h = core.get_actor(REPLICA_PREFIX + tag, namespace=NAMESPACE)
                     except ValueError:
                         continue  # gone with the old controller's node / killed: replaced below
-                    st.replicas.append(_ReplicaState(tag, h))  # STARTING until ready() answers
+                    r = _ReplicaState(tag, h)  # STARTING until ready() answers
+                    if d["config"].placement_group_bundles:
+                        try:
+                            from ..util.placement_group import get_placement_group
+
+                            r.pg = get_placement_group(REPLICA_PG_PREFIX + tag)
+                        except Exception:
+                            pass
+                    st.replicas.append(r)
                 deps[dn] = st
             self.apps[n] = {"route_prefix": a["route_prefix"], "ingress": a["ingress"],
                             "deployments": deps, "created": a["created"]}
@@ -218,7 +229,7 @@ class ServeController:
                 return None
             st = a["deployments"][deployment]
             return (st.version, [(r.tag, r.handle, list(r.metrics.get("models", []))) for r in st.running()],
-                    st.config.max_ongoing_requests)
+                    st.config.max_ongoing_requests, st.config.max_queued_requests)
 
     def get_routes(self):
         with self.lock:
@@ -243,7 +254,8 @@ class ServeController:
                     deps[dn] = {"status": st.status(), "target_replicas": st.target_replicas,
                                 "running_replicas": len(st.running()),
                                 "replica_states": {r.tag: r.state for r in st.replicas},
-                                "message": st.error or ""}
+                                "replica_nodes": {r.tag: r.node_id for r in st.replicas},
+                                "message": st.error or getattr(st, "pending_reason", None) or ""}
                 sts = [d["status"] for d in deps.values()]
                 if any(s == "DEPLOY_FAILED" for s in sts):
                     ast = "DEPLOY_FAILED"
@@ -279,11 +291,18 @@ class ServeController:
     def get_deploy_config(self):
         return getattr(self, "deploy_config", None)
 
-    def record_handle_metrics(self, app, deployment, queued):
+    def record_handle_metrics(self, app, deployment, queued, router_id: str = ""):
+        """Requests waiting in a handle router's queue (no replica slot free): counted
+        by the autoscaler on top of the replicas' ongoing requests (reference:
+        autoscaling_state.py, handle queued metrics)."""
         with self.lock:
             a = self.apps.get(app)
             if a and deployment in a["deployments"]:
-                a["deployments"][deployment].handle_queued = queued
+                st = a["deployments"][deployment]
+                q = getattr(st, "router_queued", None)
+                if q is None:
+                    q = st.router_queued = {}
+                q[router_id] = (int(queued), time.time())
         return True
 
     def shutdown(self):
@@ -331,13 +350,69 @@ class ServeController:
                 traceback.print_exc()
             time.sleep(0.1)
 
+    def _pick_node(self, st: _DeploymentState, opts: Dict[str, Any]) -> Optional[str]:
+        """``max_replicas_per_node``: an alive node holding fewer than that many live
+        replicas of this deployment whose free resources fit the replica actor (the
+        emptiest such node first), or None (the replica waits; reference:
+        deployment_scheduler.py:143-176 -- there an implicit per-node resource of 1.0
+        of which each replica takes 1 / max_replicas_per_node)."""
+        cap = st.config.max_replicas_per_node
+        count: Dict[str, int] = {}
+        for r in st.replicas:
+            if r.state in ("STARTING", "RUNNING") and r.node_id:
+                count[r.node_id] = count.get(r.node_id, 0) + 1
+        need = {"CPU": float(opts.get("num_cpus", 0) or 0), "GPU": float(opts.get("num_gpus", 0) or 0)}
+        for k, v in (opts.get("resources") or {}).items():
+            need[k] = float(v)
+        try:
+            avail = core.available_resources_per_node()
+        except Exception:
+            avail = {}
+        best = None
+        for n in core.nodes():
+            if not n.get("Alive", True):
+                continue
+            nid = n["NodeID"]
+            c = count.get(nid, 0)
+            if c >= cap:
+                continue
+            free = avail.get(nid, n.get("Resources", {}))
+            if any(v > 0 and free.get(k, 0.0) + 1e-9 < v for k, v in need.items()):
+                continue
+            if best is None or c < best[0]:
+                best = (c, nid)
+        return best[1] if best else None
+
     def _start_replica(self, st: _DeploymentState):
         from ..core.actor import ActorClass
         from .replica import ServeReplica
 
-        st.counter += 1
+        cfg = st.config
         tag = f"{st.app}#{st.name}#{uuid.uuid4().hex[:6]}"
-        opts = dict(st.config.ray_actor_options or {})
+        opts = dict(cfg.ray_actor_options or {})
+        node = pg = None
+        if cfg.max_replicas_per_node:
+            node = self._pick_node(st, opts)
+            if node is None:
+                st.pending_reason = (f"no node can take another replica (max_replicas_per_node="
+                                     f"{cfg.max_replicas_per_node})")
+                return False
+            from ..util.scheduling_strategies import NodeAffinitySchedulingStrategy
+
+            opts["scheduling_strategy"] = NodeAffinitySchedulingStrategy(node, soft=False)
+        elif cfg.placement_group_bundles:
+            # one gang per replica, the replica actor in bundle 0, its tasks / child
+            # actors (e.g. the ranks of a multi-GPU model) in the PG's other bundles
+            # (reference: deployment_scheduler.py:143-176, replica.py placement group)
+            from ..util.placement_group import placement_group
+            from ..util.scheduling_strategies import PlacementGroupSchedulingStrategy
+
+            pg = placement_group(cfg.placement_group_bundles, strategy=cfg.placement_group_strategy or "PACK",
+                                 name=REPLICA_PG_PREFIX + tag, lifetime="detached")
+            opts["scheduling_strategy"] = PlacementGroupSchedulingStrategy(
+                pg, placement_group_bundle_index=0, placement_group_capture_child_tasks=True)
+        st.pending_reason = None
+        st.counter += 1
         opts.setdefault("num_cpus", 0)
         opts["max_concurrency"] = max(16, st.config.max_ongoing_requests * 2)
         opts["max_restarts"] = 0
@@ -349,7 +424,10 @@ class ServeController:
         Replica = ActorClass(ServeReplica, {})
         h = Replica.options(**opts).remote(st.app, st.name, tag, st.target, st.init_args, st.init_kwargs,
                                            st.config.user_config, st.config.max_ongoing_requests)
-        st.replicas.append(_ReplicaState(tag, h))
+        r = _ReplicaState(tag, h)
+        r.node_id, r.pg = node, pg
+        st.replicas.append(r)
+        return True
 
     def _stop_replica(self, st: _DeploymentState, r: _ReplicaState):
         if r.state != "STOPPING":
@@ -386,7 +464,8 @@ class ServeController:
         live = [r for r in st.replicas if r.state in ("STARTING", "RUNNING")]
         if len(live) < target and not (st.error and len(live) == 0 and st.counter > 3 * max(1, target)):
             for _ in range(target - len(live)):
-                self._start_replica(st)
+                if not self._start_replica(st):
+                    break  # no node may take one now (max_replicas_per_node): retried next pass
         elif len(live) > target:
             # drain the least loaded / newest replicas first
             order = sorted(live, key=lambda r: (r.state == "RUNNING", -r.started))
@@ -423,6 +502,8 @@ class ServeController:
                         m = core.get(r.metrics_ref)
                         models_changed = m.get("models") != r.metrics.get("models")
                         r.metrics = m
+                        if m.get("node_id"):
+                            r.node_id = m["node_id"]
                         if models_changed:
                             st.version += 1
                     except RayError:
@@ -439,7 +520,8 @@ class ServeController:
     def _autoscale(self, st: _DeploymentState, now: float):
         cfg = st.config.autoscaling_config
         run = st.running()
-        total = sum(r.metrics.get("ongoing", 0) for r in run) + getattr(st, "handle_queued", 0)
+        queued = sum(n for n, t in getattr(st, "router_queued", {}).values() if now - t < 2.0)
+        total = sum(r.metrics.get("ongoing", 0) for r in run) + queued
         st.metric_hist.append((now, total))
         st.metric_hist = [(t, v) for t, v in st.metric_hist if now - t <= cfg.look_back_period_s]
         avg = sum(v for _, v in st.metric_hist) / max(1, len(st.metric_hist))
@@ -461,3 +543,11 @@ class ServeController:
             core.kill(r.handle)
         except Exception:
             pass
+        if r.pg is not None:
+            try:
+                from ..util.placement_group import remove_placement_group
+
+                remove_placement_group(r.pg)
+            except Exception:
+                pass
+            r.pg = None

@@ -11,6 +11,7 @@ refreshed from the controller when its version changes (polled at most every
 from __future__ import annotations
 
 import asyncio
+import collections
 import concurrent.futures
 import random
 import threading
@@ -30,15 +31,29 @@ def _controller():
 
 
 class _Router:
+    """Per-process router of one deployment. A request takes a replica slot only
+    while that replica has fewer than ``max_ongoing_requests`` requests of this
+    router in flight; otherwise it waits in the router's queue (FIFO) and is
+    assigned by the router's drain thread when a slot frees or replicas are added.
+    With ``max_queued_requests`` != -1 a request that would make the queue longer
+    than that is rejected at once with :class:`BackPressureError` (reference:
+    serve/_private/router.py:125-136)."""
+
     def __init__(self, app: str, deployment: str):
         self.app, self.deployment = app, deployment
         self.replicas: List[tuple] = []  # (tag, handle, models)
         self.version = -1
         self.inflight: Dict[str, int] = {}
         self.max_ongoing = 5
+        self.max_queued = -1
         self.last_refresh = 0.0
         self.lock = threading.Lock()
+        self.wake = threading.Condition(self.lock)
+        self.pending: "collections.deque" = collections.deque()  # (model_id, Future)
+        self.drainer: Optional[threading.Thread] = None
         self.rng = random.Random()
+        self.router_id = uuid.uuid4().hex[:8]
+        self._reported = (0, 0.0)
 
     def _refresh(self, force=False):
         now = time.time()
@@ -53,14 +68,17 @@ class _Router:
             raise
         if snap is None:
             raise KeyError(f"deployment {self.deployment!r} of application {self.app!r} does not exist")
-        version, reps, self.max_ongoing = snap
+        version, reps, self.max_ongoing = snap[:3]
+        self.max_queued = snap[3] if len(snap) > 3 else -1
         if version != self.version:
-            self.version = version
-            self.replicas = reps
-            for tag, _, _ in reps:
-                self.inflight.setdefault(tag, 0)
+            with self.lock:
+                self.version = version
+                self.replicas = reps
+                for tag, _, _ in reps:
+                    self.inflight.setdefault(tag, 0)
+                self.wake.notify_all()
 
-    def choose(self, model_id: str = "", timeout_s: float = 60.0):
+    def _wait_for_replicas(self, timeout_s: float):
         deadline = time.time() + timeout_s
         while True:
             try:
@@ -71,30 +89,120 @@ class _Router:
                 if time.time() > deadline:
                     raise
             if self.replicas:
-                break
+                return
             if time.time() > deadline:
                 raise TimeoutError(f"no running replica of {self.app}/{self.deployment}")
             time.sleep(0.05)
+
+    def _pick_locked(self, model_id: str):
+        """A replica with a free slot (power of two choices over those), or None."""
         cands = self.replicas
+        if not cands:
+            return None
         if model_id:
             having = [r for r in cands if model_id in r[2]]
             if having:
                 cands = having
-            else:
+            elif len(cands) > 1:
                 # deterministic placement for a new model: same replica for same id
-                cands = [cands[hash(model_id) % len(cands)]] if len(cands) > 1 else cands
-        with self.lock:
-            if len(cands) == 1:
-                pick = cands[0]
-            else:
-                a, b = self.rng.sample(cands, 2)
-                pick = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
-            self.inflight[pick[0]] = self.inflight.get(pick[0], 0) + 1
+                cands = [cands[hash(model_id) % len(cands)]]
+        cap = max(1, int(self.max_ongoing or 1))
+        free = [r for r in cands if self.inflight.get(r[0], 0) < cap]
+        if not free:
+            return None
+        if len(free) == 1:
+            pick = free[0]
+        else:
+            a, b = self.rng.sample(free, 2)
+            pick = a if self.inflight.get(a[0], 0) <= self.inflight.get(b[0], 0) else b
+        self.inflight[pick[0]] = self.inflight.get(pick[0], 0) + 1
         return pick
+
+    def assign(self, model_id: str = "", timeout_s: float = 60.0) -> concurrent.futures.Future:
+        """Future of ``(tag, handle, models)``: resolved at once when a replica has a
+        free slot and nothing is queued, else when the drain thread assigns it."""
+        from .exceptions import BackPressureError
+
+        self._wait_for_replicas(timeout_s)
+        self._refresh()
+        fut: concurrent.futures.Future = concurrent.futures.Future()
+        with self.lock:
+            if not self.pending:
+                pick = self._pick_locked(model_id)
+                if pick is not None:
+                    fut.set_result(pick)
+                    return fut
+            if self.max_queued is not None and self.max_queued >= 0 and len(self.pending) >= self.max_queued:
+                raise BackPressureError(len(self.pending), self.max_queued)
+            self.pending.append((model_id, fut))
+            if self.drainer is None or not self.drainer.is_alive():
+                self.drainer = threading.Thread(target=self._drain_loop, daemon=True,
+                                                name=f"serve-router-{self.deployment}")
+                self.drainer.start()
+            self.wake.notify_all()
+        return fut
+
+    def choose(self, model_id: str = "", timeout_s: float = 60.0):
+        return self.assign(model_id, timeout_s).result(timeout_s)
+
+    def num_queued(self) -> int:
+        with self.lock:
+            return sum(1 for _, f in self.pending if not f.done())
+
+    def _report_queued(self, n: int):
+        """Tell the controller how many requests wait here (autoscaling input)."""
+        now = time.time()
+        if n == self._reported[0] and now - self._reported[1] < 0.5:
+            return
+        self._reported = (n, now)
+        try:
+            _controller().record_handle_metrics.remote(self.app, self.deployment, n, self.router_id)
+        except Exception:
+            pass
+
+    def _drain_loop(self):
+        # assignments are handed out here, never in the thread that completed a
+        # response (a core callback thread), so callers' submissions run off it
+        while True:
+            self._report_queued(len(self.pending))
+            ready = []
+            with self.lock:
+                while self.pending:
+                    model_id, f = self.pending[0]
+                    if f.done():  # cancelled while queued
+                        self.pending.popleft()
+                        continue
+                    pick = self._pick_locked(model_id)
+                    if pick is None:
+                        break
+                    self.pending.popleft()
+                    ready.append((f, pick))
+                if not self.pending and not ready:
+                    self.drainer = None
+                    done = True
+                else:
+                    done = False
+                if not ready and not done:
+                    self.wake.wait(0.05)
+            if done:
+                self._report_queued(0)
+                return
+            for f, pick in ready:
+                if f.set_running_or_notify_cancel():
+                    f.set_result(pick)
+                else:
+                    self.done(pick[0])
+            if not ready:
+                try:
+                    self._refresh()  # replicas added by autoscaling / recovery free slots too
+                except Exception:
+                    pass
 
     def done(self, tag):
         with self.lock:
             self.inflight[tag] = max(0, self.inflight.get(tag, 0) - 1)
+            if self.pending:
+                self.wake.notify_all()
 
     def drop_actor(self, actor_id):
         with self.lock:
@@ -154,19 +262,45 @@ def _unwrap(x):
 
 
 class DeploymentResponse:
-    def __init__(self, router: _Router, tag: str, ref, resend):
+    """Result of ``handle.remote()``. ``_assigned`` resolves to ``(tag, ref)`` once the
+    router gave the request a replica slot (at once, or later from its queue)."""
+
+    def __init__(self, router: _Router, assigned: concurrent.futures.Future, resend, request_id: str = ""):
         self._router = router
-        self._tag = tag
-        self._ref = ref
+        self._assigned = assigned
         self._resend = resend
+        self._request_id = request_id
         self._fut = None
         self._lock = threading.Lock()
 
     def _future(self) -> concurrent.futures.Future:
         with self._lock:
             if self._fut is None:
-                self._fut = self._ref.future()
-                self._fut.add_done_callback(lambda f, t=self._tag, r=self._router: r.done(t))
+                outer: concurrent.futures.Future = concurrent.futures.Future()
+                router = self._router
+
+                def on_ref(af):
+                    try:
+                        tag, ref = af.result()
+                    except BaseException as e:  # noqa: BLE001 (cancelled / submission failed)
+                        if isinstance(e, concurrent.futures.CancelledError):
+                            from .exceptions import RequestCancelledError
+
+                            e = RequestCancelledError(self._request_id)
+                        outer.set_exception(e)
+                        return
+
+                    def fin(g, t=tag):
+                        router.done(t)
+                        try:
+                            outer.set_result(g.result())
+                        except BaseException as e:  # noqa: BLE001
+                            outer.set_exception(e)
+
+                    ref.future().add_done_callback(fin)
+
+                self._assigned.add_done_callback(on_ref)
+                self._fut = outer
             return self._fut
 
     def result(self, timeout_s: Optional[float] = None, _retries: int = 1):
@@ -200,23 +334,27 @@ class DeploymentResponse:
             return await self._resend()._await_retrying(retries - 1)
 
     def _to_object_ref(self):
-        return self._ref
+        return self._assigned.result()[1]
 
     async def _to_object_ref_async(self):
-        return self._ref
+        return (await asyncio.wrap_future(self._assigned))[1]
 
     def _to_object_ref_sync(self):
-        return self._ref
+        return self._to_object_ref()
 
     def cancel(self):
+        """Cancel a queued request (it never reaches a replica) or the replica call."""
+        if self._assigned.cancel():
+            return
         try:
-            core.cancel(self._ref)
+            if self._assigned.done() and self._assigned.exception() is None:
+                core.cancel(self._assigned.result()[1])
         except Exception:
             pass
 
     @property
     def request_id(self):
-        return self._ref.hex()
+        return self._request_id
 
 
 class DeploymentResponseGenerator:
@@ -298,9 +436,33 @@ class DeploymentHandle:
             return DeploymentResponseGenerator(router, tag, gen)
 
         def send():
-            tag, h, _ = router.choose(self._model_id)
-            ref = h.handle_request.remote(meta, *args, **kwargs)
-            return DeploymentResponse(router, tag, ref, send)
+            assigned = router.assign(self._model_id)  # BackPressureError when the queue is full
+            out: concurrent.futures.Future = concurrent.futures.Future()
+
+            def submit(af):
+                try:
+                    tag, h, _ = af.result()
+                except BaseException as e:  # noqa: BLE001 (cancelled while queued)
+                    if isinstance(e, concurrent.futures.CancelledError):
+                        out.cancel()
+                    else:
+                        out.set_exception(e)
+                    return
+                if not out.set_running_or_notify_cancel():  # cancelled meanwhile
+                    router.done(tag)
+                    return
+                try:
+                    out.set_result((tag, h.handle_request.remote(meta, *args, **kwargs)))
+                except BaseException as e:  # noqa: BLE001
+                    router.done(tag)
+                    out.set_exception(e)
+
+            assigned.add_done_callback(submit)
+            resp = DeploymentResponse(router, out, send, meta["request_id"])
+            if not assigned.done():
+                # cancelling the response cancels the queued assignment
+                out.add_done_callback(lambda f, a=assigned: f.cancelled() and a.cancel())
+            return resp
 
         resp = send()
         resp._future()  # start tracking completion now (in-flight accounting)

@@ -27,9 +27,16 @@ def _free_port(host="127.0.0.1"):
 
 
 class HTTPProxy:
-    def __init__(self, host: str = "127.0.0.1", port: int = 8000):
+    def __init__(self, host: str = "127.0.0.1", port: int = 8000, request_timeout_s=None):
+        import os
+
         import uvicorn
 
+        # end-to-end limit per request (reference: proxy.py:143-147, 1026-1033: 408 and
+        # the replica call cancelled); also from RAY_SERVE_REQUEST_PROCESSING_TIMEOUT_S
+        if request_timeout_s is None:
+            request_timeout_s = float(os.environ.get("RAY_SERVE_REQUEST_PROCESSING_TIMEOUT_S", "0")) or None
+        self.request_timeout_s = request_timeout_s if request_timeout_s and request_timeout_s > 0 else None
         self.host = host
         self.port = port or _free_port(host)
         self.routes = {}
@@ -102,19 +109,42 @@ class HTTPProxy:
                "headers": headers, "body": b"".join(chunks), "route_prefix": prefix or "/",
                "request_id": uuid.uuid4().hex[:12], "model_id": model_id}
         self.num_requests += 1
+        timeout = self.request_timeout_s
+        state = {"started": False}
+        work = asyncio.ensure_future(self._forward(app_name, ingress, model_id, req, send, state))
+        try:
+            await asyncio.wait_for(asyncio.shield(work), timeout)
+        except asyncio.TimeoutError:
+            # cancel the queued assignment / replica call, then answer 408 if nothing
+            # was sent yet (a streaming response already under way is just ended)
+            work.cancel()
+            try:
+                await work
+            except BaseException:  # noqa: BLE001
+                pass
+            msg = f"Request {req['request_id']} timed out after {timeout}s.".encode()
+            if not state["started"]:
+                await _respond(send, 408, msg)
+            else:
+                await send({"type": "http.response.body", "body": b"", "more_body": False})
+
+    async def _forward(self, app_name, ingress, model_id, req, send, state):
+        from ..exceptions import RayActorError
+        from .exceptions import BackPressureError, DeploymentUnavailableError
         from .handle import _router
 
         router = _router(app_name, ingress)
         loop = asyncio.get_event_loop()
-        from ..exceptions import RayActorError
-
         # the replica streams the response back (handle_http_stream): a complete
         # response is one item; a streaming one (SSE, StreamingResponse) is relayed
         # chunk by chunk as the app produces it
-        gen = first = tag = None
+        gen = first = tag = af = None
         try:
             for attempt in range(3):
-                tag, h, _ = await loop.run_in_executor(None, router.choose, model_id)
+                # a slot on a replica with fewer than max_ongoing_requests in flight;
+                # queued in the router otherwise (BackPressureError when its queue is full)
+                af = await loop.run_in_executor(None, router.assign, model_id)
+                tag, h, _ = await asyncio.wrap_future(af)
                 try:
                     gen = h.handle_http_stream.options(num_returns="streaming").remote(req)
                     first = await (await gen.__anext__())
@@ -122,10 +152,17 @@ class HTTPProxy:
                 except RayActorError:
                     # the replica went away (redeploy / downscale / crash): re-resolve and retry
                     router.done(tag)
-                    tag = None
+                    tag = gen = None
                     if attempt == 2:
                         raise
                     router.invalidate()
+        except asyncio.CancelledError:
+            self._cancel(router, af, tag, gen)
+            raise
+        except (BackPressureError, DeploymentUnavailableError) as e:
+            if tag is not None:
+                router.done(tag)
+            return await _respond(send, 503, e.message.encode())
         except Exception as e:  # noqa
             if tag is not None:
                 router.done(tag)
@@ -133,6 +170,7 @@ class HTTPProxy:
         try:
             if first[0] == "full":
                 _, status, hdrs, body = first
+                state["started"] = True
                 await send({"type": "http.response.start", "status": status,
                             "headers": [(k.encode(), v.encode()) for k, v in hdrs
                                         if k.lower() != "content-length"]
@@ -140,15 +178,36 @@ class HTTPProxy:
                 await send({"type": "http.response.body", "body": body})
                 return
             _, status, hdrs = first
+            state["started"] = True
             await send({"type": "http.response.start", "status": status,
                         "headers": [(k.encode(), v.encode()) for k, v in hdrs if k.lower() != "content-length"]})
             try:
                 async for ref in gen:
                     item = await ref
                     await send({"type": "http.response.body", "body": item[1], "more_body": True})
-            finally:
-                await send({"type": "http.response.body", "body": b"", "more_body": False})
+            except asyncio.CancelledError:
+                self._cancel(router, None, None, gen)
+                raise
+            await send({"type": "http.response.body", "body": b"", "more_body": False})
         finally:
+            router.done(tag)
+
+    @staticmethod
+    def _cancel(router, af, tag, gen):
+        from ..core import api as core
+
+        if af is not None and not af.cancel():
+            # assigned meanwhile: the slot is ours to give back
+            if tag is None and not af.cancelled() and af.exception() is None:
+                tag = af.result()[0]
+        elif af is not None:
+            return  # still queued: it never reached a replica
+        if gen is not None:
+            try:
+                core.cancel(gen)
+            except Exception:
+                pass
+        if tag is not None:
             router.done(tag)
 
     def stats(self):

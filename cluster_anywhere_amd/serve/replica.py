@@ -358,8 +358,15 @@ class ServeReplica:
             self.ongoing -= 1
 
     async def get_metrics(self):
+        if not hasattr(self, "_node_id"):
+            try:
+                from ..runtime_context import get_runtime_context
+
+                self._node_id = get_runtime_context().get_node_id()
+            except Exception:
+                self._node_id = None
         return {"ongoing": self.ongoing, "total": self.total, "models": loaded_model_ids(self.callable),
-                "time": time.time()}
+                "time": time.time(), "node_id": self._node_id}
 
     async def check_health(self):
         fn = getattr(self.callable, "check_health", None)

@@ -280,29 +280,32 @@ class _DeviceLoader:
         return b
 
     def __iter__(self):
-        import torch
-
         if self.device.type != "cuda":
             for b in self.loader:
                 yield self._move(b)
             return
-        stream = torch.cuda.Stream(self.device)
+        # side-stream copies one batch ahead; hand_over() = wait_stream + record_stream
+        # on every moved tensor (train_loop_utils.py:688-703): without the record, a
+        # batch the loop drops goes back to the side stream's pool while the compute
+        # stream may still read it, and the next prefetch copy overwrites it
+        from ...util.device_transfer import SideStreamMover
+
+        mover = SideStreamMover(self.device)
         it = iter(self.loader)
-        nxt = None
         try:
-            with torch.cuda.stream(stream):
-                nxt = self._move(next(it))
-        except StopIteration:
-            return
-        while nxt is not None:
-            torch.cuda.current_stream(self.device).wait_stream(stream)
-            cur = nxt
             try:
-                with torch.cuda.stream(stream):
-                    nxt = self._move(next(it))
+                nxt = mover.stage(next(it))
             except StopIteration:
-                nxt = None
-            yield cur
+                return
+            while nxt is not None:
+                cur = mover.hand_over(nxt)  # before the next copy is enqueued
+                try:
+                    nxt = mover.stage(next(it))
+                except StopIteration:
+                    nxt = None
+                yield cur
+        finally:
+            mover.close()
 
 
 def prepare_data_loader(data_loader, add_dist_sampler: bool = True, move_to_device: bool = True,

@@ -117,10 +117,12 @@ def placement_group_table(pg: Optional[PlacementGroup] = None) -> dict:
 
 
 def get_current_placement_group() -> Optional[PlacementGroup]:
-    ctx = context.current_task()
-    if ctx is None or not ctx.pg:
+    """The placement group of the running task, or of this actor (also inside its
+    methods' thread pools / event loops)."""
+    cur = context.current_pg()
+    if not cur:
         return None
-    return PlacementGroup(PlacementGroupID(ctx.pg[1]))
+    return PlacementGroup(PlacementGroupID(cur[1]))
 
 
 def check_placement_group_index(pg: PlacementGroup, bundle_index: int):
