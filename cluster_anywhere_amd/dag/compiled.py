@@ -36,6 +36,7 @@ import asyncio
 import inspect
 import os
 import threading
+import time
 import traceback
 from typing import Any, Dict, List, Optional
 
@@ -91,6 +92,33 @@ class CompiledDAGRef:
         return f"CompiledDAGRef(seq={self._seq})"
 
 
+class CompiledDAGFuture:
+    """``await dag.execute_async(...)`` returns this; ``await fut`` gives the result
+    (reference: compiled_dag_node.py:2417-2434, compiled_dag_ref.py CompiledDAGFuture)."""
+
+    def __init__(self, fut, multi):
+        self._fut, self._multi = fut, multi
+        self._done = False
+
+    def __await__(self):
+        if self._done:
+            raise ValueError("a CompiledDAGFuture can be awaited only once")
+        self._done = True
+        vals = yield from self._fut.__await__()
+        return _unpack(vals, self._multi)
+
+    def __repr__(self):
+        return f"CompiledDAGFuture(done={self._fut.done()})"
+
+
+def _unpack(vals, multi):
+    for v in vals:
+        if isinstance(v, _DagError):
+            e = v.err
+            raise e.as_instanceof_cause() if hasattr(e, "as_instanceof_cause") else e
+    return vals if multi else vals[0]
+
+
 # --------------------------------------------------------------------- actor side
 def _split_tensors(value):
     """Replace torch tensors at the top level of value (or in a list/tuple/dict)
@@ -132,6 +160,24 @@ def _slots(skel):
 
 
 class _ActorLoop:
+    """One actor's resident execution loop.
+
+    With ``overlap_gpu_communication`` (reference: compiled_dag_node.py:192-226, 540)
+    a GPU actor moves its edge transfers onto a communication stream of its own,
+    ordered against compute by events, so the host loop never waits for them:
+      * RCCL sends are enqueued on the comm stream behind an event recorded after the
+        producing compute and are not waited for (NCCL records the tensors on its
+        stream, so dropping them is safe); RCCL recvs run on the comm stream and the
+        compute stream waits on them GPU-side;
+      * an IPC producer copies into the shared HBM buffer on the comm stream, and a
+        writer thread publishes the ring message once that copy's event completed
+        (FIFO with every other write, so ring order is unchanged) while the loop
+        goes on to the next compute;
+      * an IPC consumer copies out on the comm stream and waits for that copy only
+        before its NEXT read of the same edge (the producer reuses a buffer only
+        after that read).
+    """
+
     def __init__(self, instance, plan):
         self.inst = instance
         self.plan = plan
@@ -140,6 +186,54 @@ class _ActorLoop:
         self.ipc_out = {}   # (out key, tensor index) -> [buffers]
         self.ipc_seq = {}   # out key -> executions written
         self.ipc_maps = {}  # (channel name, tensor index, buffer) -> mapped uint8 tensor
+        self.overlap = bool(plan.get("overlap"))
+        self.comm = None         # comm stream (overlap mode, GPU actors)
+        self.writer = None       # writer thread + its FIFO (overlap mode)
+        self.pending_read = {}   # channel name -> event of the last copy-out from it
+        self.pending_sends = []  # (works, tensors) of un-waited RCCL sends
+
+    def _comm_stream(self):
+        import torch
+
+        if not self.overlap or not torch.cuda.is_available():
+            return None
+        if self.comm is None:
+            self.comm = torch.cuda.Stream()
+        return self.comm
+
+    def _start_writer(self):
+        import queue
+
+        self.wq = queue.Queue()
+        self.writer_err = None
+
+        def run():
+            while True:
+                item = self.wq.get()
+                if item is None:
+                    return
+                ev, ch, msg = item
+                try:
+                    if ev is not None:
+                        ev.synchronize()
+                    ch.write(msg)
+                except Exception as e:  # noqa: BLE001 (channel closed at teardown)
+                    self.writer_err = e
+                    return
+
+        self.writer = threading.Thread(target=run, name="caamd-cdag-writer", daemon=True)
+        self.writer.start()
+
+    def _post(self, ch, msg, ev=None):
+        """Write a ring message: in order through the writer thread in overlap mode."""
+        if self.writer is None:
+            if ev is not None:
+                ev.synchronize()
+            ch.write(msg)
+            return
+        if self.writer_err is not None:
+            raise ChannelClosedError(str(self.writer_err))
+        self.wq.put((ev, ch, msg))
 
     def _setup_group(self):
         from ..util.collective import collective as col
@@ -163,6 +257,9 @@ class _ActorLoop:
                        else torch.device("cpu"))
 
     def _read(self, ch, reader, producer_rank):
+        ev = self.pending_read.pop(ch.name, None)
+        if ev is not None:
+            ev.synchronize()  # the previous copy-out of this edge is done: its buffer may be reused
         v = ch.read(reader)
         if producer_rank == "ipc" and not isinstance(v, (_Stop, _DagError)):
             return self._read_ipc(ch, v)
@@ -170,10 +267,22 @@ class _ActorLoop:
             import torch
 
             slots = _slots(v)
-            bufs = [torch.empty(s.shape, dtype=s.dtype, device=self.device) for s in slots]
-            works = [self.group.pg.recv([b], producer_rank, 0) for b in bufs]
-            for w in works:
-                w.wait()
+            comm = self._comm_stream() if self.device.type == "cuda" else None
+            if comm is None:
+                bufs = [torch.empty(s.shape, dtype=s.dtype, device=self.device) for s in slots]
+                works = [self.group.pg.recv([b], producer_rank, 0) for b in bufs]
+                for w in works:
+                    w.wait()
+            else:
+                cur = torch.cuda.current_stream()
+                with torch.cuda.stream(comm):
+                    bufs = [torch.empty(s.shape, dtype=s.dtype, device=self.device) for s in slots]
+                    works = [self.group.pg.recv([b], producer_rank, 0) for b in bufs]
+                    for w in works:
+                        w.wait()  # NCCL: the comm stream waits, not the host
+                cur.wait_stream(comm)
+                for b in bufs:
+                    b.record_stream(cur)
             v = _fill_tensors(v, {s.i: b for s, b in zip(slots, bufs)})
         return v
 
@@ -189,6 +298,10 @@ class _ActorLoop:
         nbuf = out["ipc_depth"] + 1
         j = seq % nbuf
 
+        comm = self._comm_stream()
+        if comm is not None:
+            comm.wait_stream(torch.cuda.current_stream())  # the producing compute first
+
         def sub_all(skel, tensors):
             def sub(v):
                 if not isinstance(v, _TensorSlot):
@@ -202,7 +315,12 @@ class _ActorLoop:
                 if bufs[j] is None or bufs[j].numel() < nbytes or bufs[j].device != t.device:
                     bufs[j] = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=t.device)
                     handle = reduce_ipc(bufs[j])
-                bufs[j][:nbytes].copy_(t.reshape(-1).view(torch.uint8))
+                if comm is not None:
+                    with torch.cuda.stream(comm):
+                        bufs[j][:nbytes].copy_(t.reshape(-1).view(torch.uint8))
+                    t.record_stream(comm)
+                else:
+                    bufs[j][:nbytes].copy_(t.reshape(-1).view(torch.uint8))
                 return _IpcSlot(v.i, t.shape, t.dtype, j, handle)
 
             if isinstance(skel, (list, tuple)):
@@ -213,9 +331,13 @@ class _ActorLoop:
 
         skel, tensors = _split_tensors(value)
         msg = sub_all(skel, tensors)
+        ev = None
         if any(t.is_cuda for t in tensors):
-            torch.cuda.current_stream().synchronize()  # data in HBM before the consumer sees the slot
-        out["chan"].write(msg)
+            # data in HBM before the consumer sees the slot: the writer thread waits for
+            # the copy's event in overlap mode, the loop itself otherwise
+            ev = torch.cuda.Event()
+            ev.record(comm if comm is not None else torch.cuda.current_stream())
+        self._post(out["chan"], msg, ev)
 
     def _read_ipc(self, ch, v):
         import torch
@@ -232,9 +354,17 @@ class _ActorLoop:
             for d in x.shape:
                 n *= d
             nbytes = n * torch.empty((), dtype=x.dtype).element_size()
-            t = src[:nbytes].view(x.dtype).view(x.shape).clone()
-            return t
+            if comm is not None:
+                with torch.cuda.stream(comm):
+                    t = src[:nbytes].view(x.dtype).view(x.shape).clone()
+                t.record_stream(cur)
+                return t
+            return src[:nbytes].view(x.dtype).view(x.shape).clone()
 
+        comm = self._comm_stream()
+        cur = torch.cuda.current_stream() if comm is not None else None
+        if comm is not None:
+            comm.wait_stream(cur)  # earlier compute may still read this actor's last copies
         if isinstance(v, (list, tuple)):
             out = type(v)(sub(x) for x in v)
         elif isinstance(v, dict):
@@ -242,8 +372,16 @@ class _ActorLoop:
         else:
             out = sub(v)
         if torch.cuda.is_available() and self.ipc_maps:
-            # copies done before the next read lets the producer reuse the buffer
-            torch.cuda.current_stream().synchronize()
+            if comm is not None:
+                # compute waits GPU-side; the host waits for the copy only before the
+                # next read of this edge (the producer reuses the buffer after it)
+                ev = torch.cuda.Event()
+                ev.record(comm)
+                cur.wait_event(ev)
+                self.pending_read[ch.name] = ev
+            else:
+                # copies done before the next read lets the producer reuse the buffer
+                torch.cuda.current_stream().synchronize()
         return out
 
     def _collective(self, spec, x):
@@ -278,12 +416,43 @@ class _ActorLoop:
         ch, dst_ranks = out["chan"], out.get("dst_ranks")
         if dst_ranks and not isinstance(value, (_Stop, _DagError)):
             skel, tensors = _split_tensors(value)
-            ch.write(skel)
-            works = [self.group.pg.send([t], r, 0) for r in dst_ranks for t in tensors]
-            for w in works:
-                w.wait()
+            self._post(ch, skel)
+            comm = self._comm_stream() if self.device.type == "cuda" else None
+            if comm is None:
+                works = [self.group.pg.send([t], r, 0) for r in dst_ranks for t in tensors]
+                for w in works:
+                    w.wait()
+                return
+            import torch
+
+            comm.wait_stream(torch.cuda.current_stream())  # behind the producing compute
+            with torch.cuda.stream(comm):
+                works = [self.group.pg.send([t], r, 0) for r in dst_ranks for t in tensors]
+            self.pending_sends.append((works, tensors))
+            while len(self.pending_sends) > int(self.plan.get("depth", 8)):
+                old_works, _ = self.pending_sends.pop(0)
+                with torch.cuda.stream(comm):
+                    for w in old_works:
+                        w.wait()
         else:
-            ch.write(value)
+            self._post(ch, value)
+
+    def _drain(self):
+        """Overlap mode: every queued ring write and comm-stream transfer completes."""
+        if self.pending_sends:
+            import torch
+
+            with torch.cuda.stream(self.comm):
+                for works, _ in self.pending_sends:
+                    for w in works:
+                        w.wait()
+            self.pending_sends = []
+        if self.comm is not None:
+            self.comm.synchronize()
+        if self.writer is not None:
+            self.wq.put(None)
+            self.writer.join(30)
+            self.writer = None
 
     def _call(self, method, a, k):
         fn = getattr(self.inst, method)
@@ -299,9 +468,20 @@ class _ActorLoop:
         return r
 
     def run(self):
+        try:
+            self._run()
+        finally:
+            try:
+                self._drain()
+            except Exception:
+                pass
+
+    def _run(self):
         from ..exceptions import RayTaskError
 
         try:
+            if self.overlap and self._comm_stream() is not None:
+                self._start_writer()
             self._setup_group()
         except Exception:  # pragma: no cover - surfaced through the graph outputs
             err = _DagError(RayTaskError("compiled-graph setup", traceback.format_exc()))
@@ -358,6 +538,7 @@ class _ActorLoop:
                     except ChannelClosedError:
                         return
             if stop:
+                self._drain()  # in-flight transfers land before the groups go away
                 from ..util import collective as col
 
                 names = list(self.cgroups) + ([self.plan["group"]["name"]] if self.group is not None else [])
@@ -415,7 +596,8 @@ class CompiledDAG:
         return super().__new__(cls)
 
     def __init__(self, root, _max_inflight_executions: Optional[int] = None,
-                 _buffer_size_bytes: Optional[int] = None, **_kw):
+                 _buffer_size_bytes: Optional[int] = None, enable_asyncio: bool = False,
+                 _overlap_gpu_communication: Optional[bool] = None, **_kw):
         from . import (ClassMethodNode, ClassNode, InputAttributeNode, InputNode,
                        MultiOutputNode)
         from ..core.api import get
@@ -491,7 +673,13 @@ class CompiledDAG:
         for o in outputs:
             self._out_specs.append((chans[id(o)], consumers[id(o)].index("driver")))
 
-        plans = {a: {"tasks": [], "group": None, "cgroups": []} for a in range(len(actors))}
+        if _overlap_gpu_communication is None:
+            from .context import DAGContext
+
+            _overlap_gpu_communication = DAGContext.get_current().overlap_gpu_communication
+        self._overlap = bool(_overlap_gpu_communication)
+        plans = {a: {"tasks": [], "group": None, "cgroups": [], "overlap": self._overlap,
+                     "depth": self._slots} for a in range(len(actors))}
         if backend:
             for a in plans:
                 plans[a]["group"] = {"world": len(actors), "rank": a, "backend": backend,
@@ -557,11 +745,82 @@ class CompiledDAG:
         self._results: Dict[int, Any] = {}
         self._lock = threading.Lock()
         self._torn_down = False
+        self._asyncio = bool(enable_asyncio)
+        if self._asyncio:
+            # results are read by one thread, in submission order, and handed to the
+            # futures' event loops (reference: compiled_dag_node.py:798,849,2417-2434)
+            self._afuts: Dict[int, Any] = {}
+            self._acv = threading.Condition(self._lock)
+            self._aspace: Dict[int, Any] = {}  # id(loop) -> asyncio.Event (a slot freed)
+            self._alocks: Dict[int, Any] = {}
+            self._reader = threading.Thread(target=self._async_reader, name="caamd-cdag-reader", daemon=True)
+            self._reader.start()
+
+    # -- asyncio execution -----------------------------------------------------------
+    async def execute_async(self, *args, **kwargs) -> "CompiledDAGFuture":
+        """Submit one execution without blocking the event loop; ``await`` the returned
+        future for its result. At most ``_max_inflight_executions`` are in flight: a
+        further submission waits (asynchronously) for the oldest to be read."""
+        if not self._asyncio:
+            raise RuntimeError("execute_async() needs experimental_compile(enable_asyncio=True)")
+        if self._torn_down:
+            raise RuntimeError("compiled graph was torn down")
+        loop = asyncio.get_running_loop()
+        lk = self._alocks.setdefault(id(loop), asyncio.Lock())
+        async with lk:  # submission order = result order
+            while True:
+                with self._lock:
+                    if self._submitted - self._fetched < self._slots:
+                        fut = loop.create_future()
+                        seq = self._submitted
+                        self._afuts[seq] = (loop, fut)
+                        self._input.write((args, kwargs))  # never blocks: the ring has a free slot
+                        self._submitted += 1
+                        self._acv.notify_all()
+                        break
+                    ev = self._aspace.setdefault(id(loop), (loop, asyncio.Event()))[1]
+                    ev.clear()
+                await ev.wait()
+        return CompiledDAGFuture(fut, self._multi)
+
+    def _async_reader(self):
+        def deliver(fut, vals):
+            if not fut.done():
+                fut.set_result(vals)
+
+        while True:
+            with self._lock:
+                while self._fetched >= self._submitted and not self._torn_down:
+                    self._acv.wait(0.1)
+                if self._torn_down:
+                    return
+            vals = []
+            try:
+                for ch, r in self._out_specs:
+                    while True:
+                        try:
+                            vals.append(ch.read(r, 0.1))
+                            break
+                        except TimeoutError:
+                            if self._torn_down:
+                                return
+            except ChannelClosedError:
+                return
+            with self._lock:
+                seq = self._fetched
+                self._fetched += 1
+                loop, fut = self._afuts.pop(seq)
+            loop.call_soon_threadsafe(deliver, fut, vals)
+            for lp, ev in list(self._aspace.values()):  # a ring slot freed
+                lp.call_soon_threadsafe(ev.set)
 
     # -- execution ---------------------------------------------------------------
     def execute(self, *args, **kwargs) -> CompiledDAGRef:
         if self._torn_down:
             raise RuntimeError("compiled graph was torn down")
+        if self._asyncio:
+            raise RuntimeError("this graph was compiled with enable_asyncio=True: use "
+                               "`await dag.execute_async(...)`")
         with self._lock:
             # keep at most `slots` executions in flight: drain the oldest first
             while self._submitted - self._fetched >= self._slots:
@@ -583,16 +842,24 @@ class CompiledDAG:
                     raise ValueError("result already fetched")
                 self._read_one(timeout)
             vals = self._results.pop(seq)
-        for v in vals:
-            if isinstance(v, _DagError):
-                e = v.err
-                raise e.as_instanceof_cause() if hasattr(e, "as_instanceof_cause") else e
-        return vals if self._multi else vals[0]
+        return _unpack(vals, self._multi)
 
     def teardown(self, timeout: float = 30.0):
         if self._torn_down:
             return
+        if self._asyncio:
+            # let the reader deliver what is in flight, then stop it
+            deadline = time.time() + timeout
+            while time.time() < deadline:
+                with self._lock:
+                    if self._fetched >= self._submitted:
+                        break
+                time.sleep(0.01)
         self._torn_down = True
+        if self._asyncio:
+            with self._lock:
+                self._acv.notify_all()
+            self._reader.join(timeout)
         try:
             self._input.write(_Stop(), timeout=timeout)
             # drain until every output ring delivered the stop sentinel

@@ -162,3 +162,62 @@ def test_compiled_replay_with_task_nodes(cluster):
         dag = s.fwd.bind(inc.bind(inp))
     cdag = dag.experimental_compile()
     assert ray.get(cdag.execute(1)) == 6
+
+
+def test_compiled_asyncio_pipelines_eight_in_flight(cluster):
+    """experimental_compile(enable_asyncio=True) + await dag.execute_async()
+    (reference: compiled_dag_node.py:798,2417-2434; dag/tests/experimental/
+    test_accelerated_dag.py::test_asyncio): 8 executions in flight at once from one
+    event loop, more submissions than the ring depth, results in order, errors
+    re-raised at await, sync execute() refused."""
+    import asyncio
+
+    a, b = Stage.remote(2), Stage.remote(5)
+    with InputNode() as inp:
+        dag = b.fwd.bind(a.fwd.bind(inp))
+    cdag = dag.experimental_compile(enable_asyncio=True, _max_inflight_executions=8)
+    with pytest.raises(RuntimeError, match="execute_async"):
+        cdag.execute(1)
+
+    async def main():
+        futs = [await cdag.execute_async(i) for i in range(8)]  # fills the ring, no await of results
+        first = await asyncio.gather(*futs)
+        # 24 more from concurrent producers: submissions beyond the depth wait for slots
+        async def one(i):
+            fut = await cdag.execute_async(i)
+            return await fut
+
+        more = await asyncio.gather(*[one(i) for i in range(8, 32)])
+        with pytest.raises(ValueError, match="negative input"):
+            await (await cdag.execute_async(-1))
+        after = await (await cdag.execute_async(3))
+        return first, more, after
+
+    first, more, after = asyncio.run(main())
+    assert first == [10 * i for i in range(8)]
+    assert more == [10 * i for i in range(8, 32)]
+    assert after == 30
+    cdag.teardown()
+
+
+def test_compiled_overlap_flag_cpu_is_equivalent(cluster):
+    """overlap_gpu_communication on CPU actors (gloo edges) changes nothing but the
+    schedule: same results (the comm stream and the writer thread exist only on GPU
+    actors; a CPU actor runs the synchronous loop)."""
+    from cluster_anywhere_amd.dag.context import DAGContext
+
+    p, q, r = TensorStage.remote(), TensorStage.remote(), TensorStage.remote()
+    with InputNode() as inp:
+        t = p.make.bind(inp).with_tensor_transport("gloo")
+        d = q.double.bind(t).with_tensor_transport("gloo")
+        dag = r.total.bind(d)
+    ctx = DAGContext.get_current()
+    ctx.overlap_gpu_communication = True
+    try:
+        cdag = dag.experimental_compile()
+    finally:
+        ctx.overlap_gpu_communication = False
+    assert cdag._overlap
+    for n in (4, 100, 1000):
+        assert ray.get(cdag.execute(n), timeout=60) == (float(n * (n - 1)), n)
+    cdag.teardown()
