@@ -174,6 +174,20 @@ def is_initialized() -> bool:
     return context.worker is not None or context.local_mode
 
 
+def _spill_config(kwargs):
+    """``init(_system_config={"object_spilling_config": dict or JSON})`` (reference:
+    _private/external_storage.py setup_external_storage), else CAAMD_OBJECT_SPILLING_CONFIG.
+    Validated here so a bad config fails ``init`` rather than the first spill."""
+    from .external_storage import parse_config
+
+    sc = kwargs.get("_system_config") or {}
+    cfg = sc.get("object_spilling_config", os.environ.get("CAAMD_OBJECT_SPILLING_CONFIG"))
+    cfg = parse_config(cfg)
+    if cfg is not None and cfg["type"] not in ("filesystem", "smart_open", "uri", "fsspec", "pyarrow"):
+        raise ValueError(f"unsupported object_spilling_config type {cfg['type']!r}")
+    return cfg
+
+
 def _gcs_storage(kwargs) -> Optional[str]:
     """Durable GCS table log for head fault tolerance: ``init(_gcs_storage=path)``,
     ``init(_system_config={"gcs_storage": path})`` or ``CAAMD_GCS_STORAGE``."""
@@ -252,7 +266,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                             namespace=namespace or "default",
                             worker_env=_worker_env_from(runtime_env),
                             listen_tcp=kwargs.get("_listen_tcp"), labels=kwargs.get("labels"),
-                            gcs_storage=_gcs_storage(kwargs))
+                            gcs_storage=_gcs_storage(kwargs), spill_config=_spill_config(kwargs))
                 head.start()
                 _head = head
                 address = head.sock_path
@@ -266,6 +280,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
                     "namespace": namespace or "default", "worker_env": _worker_env_from(runtime_env),
                     "listen_tcp": kwargs.get("_listen_tcp"), "parent_pid": os.getpid(),
                     "labels": kwargs.get("labels") or {}, "gcs_storage": _gcs_storage(kwargs),
+                    "spill_config": _spill_config(kwargs),
                     "sys_path": [p for p in sys.path if p and os.path.isdir(p)]})
                 address = info["unix"]
                 tcp = info.get("address")

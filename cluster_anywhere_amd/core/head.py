@@ -154,7 +154,7 @@ class Head:
                  worker_env: Optional[Dict[str, str]] = None, prestart: int = 0,
                  spill_dir: Optional[str] = None, labels: Optional[Dict[str, str]] = None,
                  gcs_storage: Optional[str] = None, reattach: bool = False,
-                 reconnect_s: Optional[float] = None):
+                 reconnect_s: Optional[float] = None, spill_config=None):
         from .. import _native
 
         self.session_dir = session_dir
@@ -187,6 +187,13 @@ class Head:
         self.namespace = namespace
         self.worker_env = worker_env or {}
         self.spill_dir = spill_dir or os.path.join(session_dir, "spill")
+        # where evicted objects go: the session dir, or _system_config
+        # object_spilling_config (several directories round-robin, or a URI)
+        from .external_storage import setup_external_storage
+
+        self.spill_store = setup_external_storage(
+            spill_config if spill_config is not None else os.environ.get("CAAMD_OBJECT_SPILLING_CONFIG"),
+            os.path.basename(os.path.normpath(session_dir)) or "session", self.spill_dir)
         self.sock_path = os.path.join(session_dir, "head.sock")
         if len(self.sock_path) > 100:  # AF_UNIX path limit (108 bytes)
             import tempfile
@@ -644,10 +651,7 @@ class Head:
                 except Exception:
                     pass
         if e.spilled_path:
-            try:
-                os.unlink(e.spilled_path)
-            except OSError:
-                pass
+            self.spill_store.delete(e.spilled_path)
         for r in e.contained:
             ce = self.objects.get(r)
             if ce is not None:
@@ -784,8 +788,7 @@ class Head:
         return ("err_store" if e.is_error else "store", e.size)
 
     def _restore(self, oid, e):
-        with open(e.spilled_path, "rb") as f:
-            data = f.read()
+        data = self.spill_store.restore(e.spilled_path)
         off = self.store.create(oid, len(data), 0)
         if off < 0:
             self._evict(len(data))
@@ -793,8 +796,9 @@ class Head:
         if off >= 0:
             self.store.buffer(off, len(data), False)[:] = data
             self.store.seal(oid)
-            os.unlink(e.spilled_path)
+            self.spill_store.delete(e.spilled_path)
             e.spilled_path = None
+            self.events.append(("restore", oid.hex(), len(data), time.time()))
         else:
             e.inline = data  # last resort: serve through the control plane
 
@@ -806,7 +810,6 @@ class Head:
         are spilled only when nothing else can make room (otherwise two readers of
         spilled objects evict each other's copies between the head's reply and the
         reader's mapping)."""
-        os.makedirs(self.spill_dir, exist_ok=True)
         now = time.time()
         grace = self._restored_grace
         for o in [o for o, t in grace.items() if t <= now]:
@@ -825,9 +828,7 @@ class Head:
             pb = self.store.get_pinned(oid)
             if pb is None:
                 continue
-            path = os.path.join(self.spill_dir, oid.hex())
-            with open(path, "wb") as f:
-                f.write(memoryview(pb))
+            path = self.spill_store.spill(oid.hex(), memoryview(pb))
             del pb
             self.store.remove(oid)
             e.spilled_path = path
@@ -2768,6 +2769,10 @@ class Head:
             self.thread.join(timeout=5)
         if getattr(self, "_zygote", None) is not None:
             self._zygote.stop()
+        try:
+            self.spill_store.destroy()
+        except Exception:
+            pass
         try:
             self.lsock.close()
             os.unlink(self.sock_path)

@@ -32,7 +32,8 @@ def embedded(cfg_json: str):
     head = Head(cfg["session_dir"], bytes.fromhex(cfg["node_id"]), cfg["resources"], cfg["store_name"],
                 int(cfg["store_bytes"]), cfg["gpus"], namespace=cfg.get("namespace") or "default",
                 worker_env=cfg.get("worker_env") or {}, listen_tcp=cfg.get("listen_tcp"),
-                labels=cfg.get("labels"), gcs_storage=cfg.get("gcs_storage"))
+                labels=cfg.get("labels"), gcs_storage=cfg.get("gcs_storage"),
+                spill_config=cfg.get("spill_config"))
     head.start()
     print(json.dumps({"pid": os.getpid(), "unix": head.sock_path, "address": head.tcp_address,
                       "session_dir": head.session_dir, "node_id": head.head_hex}), flush=True)
@@ -85,6 +86,7 @@ def main(argv=None):
     ap.add_argument("--gcs-storage", default=None,
                     help="durable GCS table log (head fault tolerance): a head restarted with the same "
                          "path restores the KV, function table, jobs, detached actors and placement groups")
+    ap.add_argument("--system-config", default=None, help="JSON _system_config (object_spilling_config)")
     a = ap.parse_args(argv)
 
     from .api import _default_cpus, _default_store_bytes, _mem_bytes, detect_gpus
@@ -119,7 +121,8 @@ def main(argv=None):
         reattach = True
     head = Head(session_dir, node_id, res, store_name, store_bytes, gpus,
                 listen_tcp=f"{a.host}:{port}", labels=json.loads(a.labels), gcs_storage=a.gcs_storage,
-                reattach=reattach, reconnect_s=float(os.environ.get("CAAMD_HEAD_RECONNECT_S", "60")))
+                reattach=reattach, reconnect_s=float(os.environ.get("CAAMD_HEAD_RECONNECT_S", "60")),
+                spill_config=json.loads(a.system_config).get("object_spilling_config") if a.system_config else None)
     head.start()
     url = None
     if a.include_dashboard.lower() in ("1", "true", "yes"):

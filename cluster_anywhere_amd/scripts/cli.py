@@ -56,6 +56,8 @@ def cmd_start(a):
             argv += ["--temp-dir", a.temp_dir]
         if a.gcs_storage:
             argv += ["--gcs-storage", a.gcs_storage]
+        if a.system_config:
+            argv += ["--system-config", a.system_config]
     elif a.address:
         argv = [sys.executable, "-m", "cluster_anywhere_amd.core.node_agent", "--address", a.address,
                 "--resources", a.resources, "--node-ip-address", a.node_ip_address]
@@ -341,6 +343,9 @@ def main(argv=None):
     s.add_argument("--temp-dir", default=None)
     s.add_argument("--gcs-storage", default=None,
                    help="head fault tolerance: durable GCS table log reloaded by a head restarted on it")
+    s.add_argument("--system-config", default=None,
+                   help='JSON, e.g. {"object_spilling_config": {"type": "filesystem", '
+                        '"params": {"directory_path": ["/mnt/a", "/mnt/b"]}}}')
     s.add_argument("--block", action="store_true")
     s.set_defaults(fn=cmd_start)
     s = sub.add_parser("stop")

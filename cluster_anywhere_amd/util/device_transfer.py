@@ -23,7 +23,10 @@ on the compute stream:
 from __future__ import annotations
 
 import collections
+import os
 from typing import Any
+
+_NO_RECORD = os.environ.get("CAAMD_XFER_NO_RECORD_STREAM", "0") == "1"
 
 
 def _map(obj, fn):
@@ -73,6 +76,8 @@ class SideStreamMover:
 
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(self.stream)
+        if _NO_RECORD:  # negative control for tests/test_device_transfer_gpu.py only
+            return dev_batch
 
         def rec(t):
             if t.device.type == "cuda":

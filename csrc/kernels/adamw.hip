@@ -129,7 +129,9 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
 }
 
 // bit 0: non-temporal (3.3 vs 4.8 TB/s: slower), bit 1: 2 vectors per thread per
-// iteration (8.82-8.91 vs 9.08 ms over 1.56 B params: the default); tools/bench_adamw.py
+// iteration (8.82-8.91 vs 9.08 ms over 1.56 B params: the default), bit 2: no
+// grid-stride loop (grid covers the buffer once), bit 3: 4 vectors per thread;
+// tools/bench_adamw.py
 static int g_adam_variant = 2;
 void adamw_config(int variant) { g_adam_variant = variant; }
 
@@ -149,12 +151,16 @@ void adamw_launch(float* p, float* m, float* v, const void* g, bool g_bf16, bf16
                   hipStream_t st) {
   AdamHyper h{lr, beta1, beta2, eps, wd, bc1, bc2, inv_world, max_norm};
   const int64_t nvec = n / 8;
-  const int grid = ew_grid(nvec, 256);
+  // bit 2: one pass, no grid-stride loop (a block per 256 x UNR vectors)
+  const int unr = (g_adam_variant & 2) ? 2 : ((g_adam_variant & 8) ? 4 : 1);
+  const int64_t full = (nvec + 256LL * unr - 1) / (256LL * unr);
+  const int grid = (g_adam_variant & 4) ? (int)std::min<int64_t>(full, 1 << 30) : ew_grid(nvec, 256);
 #define CA_ADAM2(GT, W, NT, U)                                                                   \
   hipLaunchKernelGGL((adamw_kernel<GT, W, NT, U>), dim3(grid), dim3(256), 0, st, p, m, v, (const GT*)g, \
                      pbf, nvec, h, sumsq, wd_mask)
 #define CA_ADAM(GT, W)                                          \
   do {                                                          \
+    if (g_adam_variant & 8) { CA_ADAM2(GT, W, false, 4); break; } \
     switch (g_adam_variant & 3) {                               \
       case 1: CA_ADAM2(GT, W, true, 1); break;                  \
       case 2: CA_ADAM2(GT, W, false, 2); break;                 \

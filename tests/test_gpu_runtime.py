@@ -263,7 +263,7 @@ def test_compiled_dag_ipc_asyncio_overlap(cluster):
     try:
         outs = asyncio.run(main())
         for i, (s, tag) in enumerate(outs):
-            assert tag == float(i) and s == pytest.approx(2.0 * base * i, rel=1e-9)
+            assert tag == float(i) and s == pytest.approx(2.0 * base * i, rel=1e-6)
     finally:
         cdag.teardown()
     for a in (c, m, p):
