@@ -29,6 +29,42 @@ SCRIPT_MODE = 0
 WORKER_MODE = 1
 
 
+_GFX_ACCELERATOR = {  # KFD gfx_target_version -> reference accelerator type name
+    90500: "AMD-Instinct-MI355X-OAM", 90402: "AMD-Instinct-MI300X-OAM", 90400: "AMD-Instinct-MI300X-OAM",
+    90010: "AMD-Instinct-MI250X-MI250", 90008: "AMD-Instinct-MI100"}
+
+
+def detect_accelerator_type() -> Optional[str]:
+    """This node's AMD accelerator type (reference: _private/accelerators/amd_gpu.py
+    get_current_node_accelerator_type), from the KFD topology; ``CAAMD_ACCELERATOR_TYPE``
+    overrides. The node then advertises the resource ``accelerator_type:<type>``
+    that ``@remote(accelerator_type=...)`` and ``ScalingConfig(accelerator_type=...)``
+    request 0.001 of. gfx950 parts (MI350X / MI355X) report as MI355X."""
+    if os.environ.get("CAAMD_ACCELERATOR_TYPE"):
+        return os.environ["CAAMD_ACCELERATOR_TYPE"]
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for d in sorted(os.listdir(base)):
+            try:
+                with open(os.path.join(base, d, "properties")) as f:
+                    props = dict(line.split() for line in f if len(line.split()) == 2)
+            except (OSError, ValueError):
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                v = int(props.get("gfx_target_version", "0"))
+                return _GFX_ACCELERATOR.get(v, f"AMD-gfx{v // 10000}{(v // 100) % 100:x}{v % 100:x}")
+    except OSError:
+        pass
+    return None
+
+
+def accelerator_resources(gpus) -> Dict[str, float]:
+    if not gpus:
+        return {}
+    t = detect_accelerator_type()
+    return {f"accelerator_type:{t}": 1.0} if t else {}
+
+
 def detect_gpus() -> List[int]:
     """MI355X GPUs visible to this process, without initialising HIP.
 
@@ -251,6 +287,7 @@ def init(address: Optional[str] = None, *, num_cpus: Optional[int] = None,
             res = {"CPU": float(num_cpus if num_cpus is not None else _default_cpus())}
             if gpus:
                 res["GPU"] = float(len(gpus))
+            res.update(accelerator_resources(gpus))
             res["memory"] = float(_mem_bytes())
             _sweep_stale_stores()  # before sizing the store from the free /dev/shm space
             store_bytes = int(object_store_memory or _default_store_bytes())

@@ -99,6 +99,9 @@ def main(argv=None):
     res = {"CPU": float(a.num_cpus if a.num_cpus is not None else _default_cpus()), "memory": float(_mem_bytes())}
     if gpus:
         res["GPU"] = float(len(gpus))
+        from .api import accelerator_resources
+
+        res.update(accelerator_resources(gpus))
     store_bytes = int(a.object_store_memory or _default_store_bytes())
     res["object_store_memory"] = float(store_bytes)
     res[f"node:{a.host}"] = 1.0

@@ -40,10 +40,34 @@ class ScalingConfig:
         r.setdefault("CPU", 1.0)
         if self.use_gpu:
             r.setdefault("GPU", 1.0)
-        return {k: float(v) for k, v in r.items()}
+        if self.accelerator_type:
+            # a node advertising accelerator_type:<X> (core/api.py detect_accelerator_type)
+            # -- reference: air/config.py:209-215
+            r.setdefault(f"accelerator_type:{self.accelerator_type}", 0.001)
+        return {k: float(v) for k, v in r.items() if v != 0 or k == "CPU"}
+
+    @property
+    def _trainer_resources_not_none(self) -> Dict[str, float]:
+        """What the run's coordinator reserves next to its workers (reference:
+        air/config.py:217-233): ``trainer_resources`` as given; by default nothing
+        when the run has workers (the coordinator is the driver / a light actor)."""
+        if self.trainer_resources is None:
+            return {} if self.num_workers else {"CPU": 1.0}
+        return {k: float(v) for k, v in self.trainer_resources.items() if v}
 
     def as_placement_group_bundles(self) -> List[Dict[str, float]]:
-        return [self._resources_per_worker_not_none for _ in range(self.total_workers)]
+        """The run's gang: the coordinator's bundle first when it reserves anything
+        (reference: ScalingConfig.as_placement_group_factory), then one per worker."""
+        head = [self._trainer_resources_not_none] if self._trainer_resources_not_none else []
+        return head + [self._resources_per_worker_not_none for _ in range(self.total_workers)]
+
+    @property
+    def total_resources(self) -> Dict[str, float]:
+        out: Dict[str, float] = {}
+        for b in self.as_placement_group_bundles():
+            for k, v in b.items():
+                out[k] = out.get(k, 0.0) + v
+        return out
 
     @property
     def num_cpus_per_worker(self):

@@ -419,19 +419,24 @@ class _WorkerGroup:
         sc = self.trainer.scaling_config
         n = self.n
         res = sc._resources_per_worker_not_none
-        bundles = [dict(res) for _ in range(n)]
+        # bundle 0 reserves trainer_resources for the coordinator when it asks for any
+        # (reference: air/config.py:156-161, as_placement_group_factory); the workers
+        # take the bundles after it
+        coord = sc._trainer_resources_not_none
+        off = 1 if coord else 0
+        bundles = ([dict(coord)] if coord else []) + [dict(res) for _ in range(n)]
         self.pg = pg = placement_group(bundles, strategy=sc.placement_strategy)
         ready, _ = core.wait([pg.ready()], timeout=float(os.environ.get("CAAMD_TRAIN_PG_TIMEOUT", "600")))
         if not ready:
             remove_placement_group(pg)
             self.pg = None
-            raise RuntimeError(f"could not reserve {n} training workers with {bundles[0]} each "
+            raise RuntimeError(f"could not reserve {n} training workers with {res} each "
                                f"(cluster: {core.available_resources()})")
         Worker = ActorClass(_TrainWorker, {})
         for i in range(n):
             opts = dict(num_cpus=res.get("CPU", 1), num_gpus=res.get("GPU", 0),
                         resources={k: v for k, v in res.items() if k not in ("CPU", "GPU")},
-                        scheduling_strategy=PlacementGroupSchedulingStrategy(pg, i),
+                        scheduling_strategy=PlacementGroupSchedulingStrategy(pg, i + off),
                         runtime_env={"env_vars": {"CAAMD_NOSET_ROCR_VISIBLE_DEVICES": "1",
                                                   "HSA_ENABLE_IPC_MODE_LEGACY": "0"}})
             self.workers.append(Worker.options(**opts).remote())

@@ -276,8 +276,7 @@ class TuneController:
 
         if isinstance(self.trainable, DataParallelTrainer):
             sc = (config or {}).get("scaling_config") or self.trainable.scaling_config
-            per = sc._resources_per_worker_not_none
-            return {k: v * sc.total_workers for k, v in per.items()}
+            return dict(sc.total_resources)  # workers + the coordinator's trainer_resources
         return trainable_resources(self.trainable, config)
 
     def _max_concurrent(self):
