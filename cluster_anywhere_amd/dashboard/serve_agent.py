@@ -23,6 +23,7 @@ import os
 import subprocess
 import sys
 import threading
+import time
 from typing import Any, Dict, Optional
 
 
@@ -50,13 +51,41 @@ class ServeAgentClient:
                 try:
                     self.proc.stdin.write(json.dumps({"op": op, "body": body}) + "\n")
                     self.proc.stdin.flush()
-                    line = self.proc.stdout.readline()
+                    line = self._readline(self.timeout_s)
+                except TimeoutError:
+                    # a deploy hung in the agent: kill it (the next request starts a
+                    # fresh one) instead of holding the lock for every later call
+                    self.close()
+                    return {"ok": False, "status": 504,
+                            "error": f"serve agent did not answer within {self.timeout_s}s"}
                 except (BrokenPipeError, OSError):
                     line = ""
                 if line:
                     return json.loads(line)
                 self.close()  # died: restart once
             return {"ok": False, "status": 503, "error": "serve agent unavailable"}
+
+    def _readline(self, timeout_s: float) -> str:
+        """One reply line, waiting at most ``timeout_s`` (select on the pipe)."""
+        import select
+
+        f = self.proc.stdout
+        deadline = time.time() + timeout_s
+        buf = ""
+        fd = f.fileno()
+        while True:
+            left = deadline - time.time()
+            if left <= 0:
+                raise TimeoutError
+            r, _, _ = select.select([fd], [], [], left)
+            if not r:
+                raise TimeoutError
+            chunk = os.read(fd, 1 << 16).decode()
+            if not chunk:
+                return buf  # EOF: the agent died
+            buf += chunk
+            if "\n" in buf:  # one request in flight at a time: nothing follows the reply
+                return buf.split("\n", 1)[0] + "\n"
 
     def close(self):
         p, self.proc = self.proc, None

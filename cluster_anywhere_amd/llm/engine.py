@@ -492,6 +492,14 @@ class LLMEngine:
                 if not admit:
                     self._inflight = self._launch_ahead(inf)
                 outs = self._finish_ahead(inf)
+                if self._inflight is not None and all(s.finish_reason is not None
+                                                      for s in self._inflight["batch"]):
+                    # every sequence of the step launched ahead has finished (e.g. all on
+                    # stop tokens): nothing will read it -- drain it now, so it is not
+                    # finished inside the next request's first step (a bogus decode-time
+                    # entry spanning the idle gap)
+                    self._inflight["event"].synchronize()
+                    self._inflight = None
                 if self._inflight is None:
                     self._last_finish = None
                 return outs

@@ -371,9 +371,14 @@ class _LearnerActor:
         if staged is not None:
             shard = {k: v.to(self.learner.device, copy=True) for k, v in shard.items()}
         del b, staged
-        if i == 0:
-            self._staged = None  # peers keep their IPC mappings alive (torch IPC refcounts)
+        # rank 0 keeps _staged: peers may still be copying their shards out of it
+        # (one IPC share read by n-1 consumers); the group releases it once every
+        # update_shard returned (release_staged), or the next stage_ipc replaces it
         return self.learner.update(shard, mbs, num_epochs, shuffle)
+
+    def release_staged(self):
+        self._staged = None
+        return True
 
     def update_shard_host(self, batch, i, n, mbs, num_epochs, shuffle):
         return self.learner.update(_shard_nested(batch, i, n), mbs, num_epochs, shuffle)
@@ -525,6 +530,11 @@ class LearnerGroup:
                         for i, a in enumerate(self.actors)]
 
             res = self._run(calls)
+            if t == "ipc":
+                try:  # every peer's update_shard has returned: rank 0 may free the batch
+                    self.actors[0].release_staged.remote()
+                except Exception:
+                    pass
         self._checkpoint()
         return _mean_nested(res)
 

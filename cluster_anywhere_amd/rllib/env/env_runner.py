@@ -445,6 +445,10 @@ class EnvRunnerGroup:
             self.local.set_weights(state, extra)
             return
         self._weights = (core.put(state, _tensor_transport=transport), extra)
+        # an "ipc" ref carries HIP IPC handles into THESE device tensors: keep them
+        # alive while the ref is what restarted runners receive (_catch_up), so their
+        # HBM is not handed to other tensors by the caching allocator in between
+        self._weights_keep = state if transport == "ipc" else None
         self._fanout("set_weights", *self._weights)
 
     def sync_weights_to(self, state, indices: List[int], extra: Optional[Dict] = None):
@@ -453,6 +457,7 @@ class EnvRunnerGroup:
         from ...core import api as core
 
         self._weights = (core.put(state), extra)
+        self._weights_keep = None  # a host-copy ref: nothing on the device to pin
         self._fanout("set_weights", *self._weights, indices=[i for i in indices if self.healthy[i]])
 
     def sync_connector_states(self):

@@ -162,7 +162,7 @@ class Tuner:
         if self._storage is not None:
             # remote storage (URI / storage_filesystem): the experiment is staged in a
             # local directory of the driver and mirrored to the storage filesystem
-            d = os.path.join(_staging_root(), name)
+            d = os.path.join(_fresh_staging_dir(), name)
         else:
             d = os.path.join(self.run_config.storage_path, name)
         os.makedirs(d, exist_ok=True)
@@ -230,7 +230,7 @@ class Tuner:
 
             fs, fs_path = get_fs_and_path(path, storage_filesystem)
             fs_path = fs_path.rstrip("/")
-            local = os.path.join(_staging_root(), os.path.basename(fs_path))
+            local = os.path.join(_fresh_staging_dir(), os.path.basename(fs_path))
             download_dir(fs, fs_path, local)
             remote_root = (path.rstrip("/").rsplit("/", 1)[0] if "://" in path
                            else os.path.dirname(fs_path) if storage_filesystem is None else fs_path.rsplit("/", 1)[0])
@@ -346,6 +346,27 @@ def _staging_root() -> str:
     import tempfile
 
     return os.environ.get("CAAMD_TUNE_STAGING_DIR") or os.path.join(tempfile.gettempdir(), "caamd_tune_staging")
+
+
+_staged_dirs: List[str] = []
+
+
+def _fresh_staging_dir() -> str:
+    """A new local staging directory per fit / restore: a reused one would mirror a
+    previous run's (or a concurrent tuner's) trial dirs to the new remote experiment
+    and merge a restore's download into stale files. Removed at exit
+    (the results of the run live in the storage filesystem)."""
+    import atexit
+    import shutil
+    import tempfile
+
+    root = _staging_root()
+    os.makedirs(root, exist_ok=True)
+    d = tempfile.mkdtemp(prefix="run_", dir=root)
+    if not _staged_dirs:
+        atexit.register(lambda: [shutil.rmtree(x, ignore_errors=True) for x in _staged_dirs])
+    _staged_dirs.append(d)
+    return d
 
 
 def _remote_storage(run_config):

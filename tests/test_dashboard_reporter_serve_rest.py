@@ -173,3 +173,25 @@ def test_serve_rest_round_trip(cluster):
     except urllib.error.HTTPError as e:
         assert e.code == 400
     assert json.loads(_get(url))["applications"] == {}
+
+
+def test_serve_agent_request_times_out_and_restarts():
+    """a hung agent answers 504 within the client's timeout (the lock is
+    not held forever) and is replaced on the next request."""
+    import subprocess
+    import sys
+    import time
+
+    from cluster_anywhere_amd.dashboard.serve_agent import ServeAgentClient
+
+    c = ServeAgentClient("unused", timeout_s=0.5)
+    hung = subprocess.Popen([sys.executable, "-c", "import sys, time; sys.stdin.readline(); time.sleep(60)"],
+                            stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
+    c.proc = hung
+    started = []
+    c._ensure = lambda: started.append(1) if c.proc is None else None
+    t0 = time.time()
+    r = c.request("status")
+    assert r["status"] == 504 and time.time() - t0 < 5
+    assert hung.poll() is not None  # killed
+    assert c.proc is None

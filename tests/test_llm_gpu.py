@@ -172,6 +172,31 @@ def test_llama_engine_one_step_ahead_matches_sync():
     assert run(True, stops) == ref
     assert run(True, {}) == plain
 
+    # every request ends on a stop token (none on max_tokens) -- the step
+    # launched ahead for them must be drained at once, not finished inside the next
+    # request's first step (which would log a bogus decode time over the idle gap)
+    e = LLMEngine(m, max_num_seqs=4, max_model_len=512, num_blocks=512, use_graphs=True)
+    e._async = True
+    few = prompts[:3]
+    outs = e.generate(few, SamplingParams(max_tokens=40, stop_token_ids=[]))
+    stop_ids = {i: [o.output_token_ids[3]] for i, o in enumerate(outs)}
+    e2 = LLMEngine(m, max_num_seqs=4, max_model_len=512, num_blocks=512, use_graphs=True)
+    e2._async = True
+    ids = [e2.add_request(p, SamplingParams(max_tokens=40, stop_token_ids=stop_ids[i])) for i, p in enumerate(few)]
+    done = {}
+    while e2.has_unfinished():
+        for o in e2.step():
+            if o.finished:
+                done[o.request_id] = o
+    assert all(done[i].finish_reason == "stop" for i in ids)
+    assert e2._inflight is None and e2._last_finish is None
+    n_times = len(e2.decode_times)
+    import time as _t
+
+    _t.sleep(0.3)
+    e2.generate([few[0]], SamplingParams(max_tokens=4))
+    assert all(dt < 0.25 for _, dt in e2.decode_times[n_times:]), e2.decode_times[n_times:]
+
 
 @pytest.mark.parametrize("M", [1, 7, 32, 100, 128])
 @pytest.mark.parametrize("N,K", [(6144, 4096), (4096, 4096), (1024, 14336), (28672, 4096), (64, 512)])

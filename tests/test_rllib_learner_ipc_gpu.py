@@ -28,3 +28,16 @@ def test_ipc_transport_matches_pickle(cluster):
     for a, b in zip(w_p, w_i):
         for k in a:
             torch.testing.assert_close(a[k], b[k], rtol=1e-6, atol=1e-6)
+
+
+def test_ipc_transport_three_learners_matches_pickle(cluster):
+    """with n >= 3 learners one IPC share of rank 0's staged
+    batch is read by n - 1 peers; rank 0 keeps it until every update_shard returned
+    (release_staged), so no peer copies out of freed / reused HBM."""
+    extra = {"num_gpus_per_learner": 0.3, "learner_dist_backend": "gloo"}
+    st_p, w_p = _train("pickle", extra, num_learners=3)
+    st_i, w_i = _train("ipc", extra, num_learners=3)
+    assert abs(st_p["loss"] - st_i["loss"]) < 1e-5
+    for a, b in zip(w_p, w_i):
+        for k in a:
+            torch.testing.assert_close(a[k], b[k], rtol=1e-6, atol=1e-6)

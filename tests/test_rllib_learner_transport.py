@@ -40,8 +40,8 @@ def _batch(n=64):
     return {"x": x, "y": (x @ np.arange(8, dtype=np.float32)).astype(np.float32)}
 
 
-def _train(transport, cfg_extra=None, updates=3):
-    cfg = {"num_learners": 2, "lr": 1e-2, "seed": 0, "learner_batch_transport": transport,
+def _train(transport, cfg_extra=None, updates=3, num_learners=2):
+    cfg = {"num_learners": num_learners, "lr": 1e-2, "seed": 0, "learner_batch_transport": transport,
            "num_gpus_per_learner": 0, **(cfg_extra or {})}
     g = LearnerGroup(_MSE, cfg, _factory, None, None)
     try:
