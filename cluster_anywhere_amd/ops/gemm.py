@@ -24,6 +24,7 @@ import os
 from typing import Optional, Tuple
 
 import torch
+import torch.nn.functional as F
 
 from ._lib import kernels
 
@@ -287,7 +288,22 @@ def _run(a, b, c, epi, bias=None, z=None, zout=None, dbias=None):
     return run_pp(a, b, c, 0, epi, bm, bn, bias, z, zout, dbias)
 
 
+# Plain (no-epilogue) NT GEMMs routed to the library (hipBLASLt / rocBLAS through
+# torch, with the shipped TunableOp selections of ops/gemm_tuning.py): a comma list of
+# "NxK" output-width x depth pairs, e.g. CAAMD_LIB_NT=1600x6400,4800x1600. Default:
+# none (every GEMM of the step on gemm.hip). tools/gemm_vs_blaslt.py compares the two
+# per shape; the fused-epilogue GEMMs and the weight gradients stay on gemm.hip.
+_LIB_NT = {tuple(int(v) for v in p.split("x")) for p in os.environ.get("CAAMD_LIB_NT", "").split(",")
+           if "x" in p}
+
+
+def _lib(N: int, K: int) -> bool:
+    return bool(_LIB_NT) and (N, K) in _LIB_NT
+
+
 def linear_nt(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if _lib(w.shape[0], w.shape[1]):
+        return F.linear(x2, w, b)
     out = torch.empty(x2.shape[0], w.shape[0], device=x2.device, dtype=torch.bfloat16)
     return _run(x2, w, out, EPI_BF16, bias=b)
 
@@ -302,6 +318,8 @@ def linear_gelu(x2: torch.Tensor, w: torch.Tensor, b: torch.Tensor):
 
 def dgrad(dy2: torch.Tensor, wt: torch.Tensor) -> torch.Tensor:
     """dx = dy @ W given wt = W^T ([K_in, N_out], row-major)."""
+    if _lib(wt.shape[0], wt.shape[1]):
+        return F.linear(dy2, wt)
     out = torch.empty(dy2.shape[0], wt.shape[0], device=dy2.device, dtype=torch.bfloat16)
     return _run(dy2, wt, out, EPI_BF16)
 

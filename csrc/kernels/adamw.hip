@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, float
 // iteration (8.82-8.91 vs 9.08 ms over 1.56 B params: the default), bit 2: no
 // grid-stride loop (grid covers the buffer once), bit 3: 4 vectors per thread;
 // tools/bench_adamw.py
-static int g_adam_variant = 2;
+static int g_adam_variant = 4;
 void adamw_config(int variant) { g_adam_variant = variant; }
 
 void grad_sumsq_launch(const void* g, bool g_bf16, int64_t n, float* out, hipStream_t st) {
