@@ -130,9 +130,6 @@ class LLMEngine:
             from ..ops.gemm_tuning import use_tuned_gemms
 
             use_tuned_gemms()  # shipped per-shape hipBLASLt selections (prefill GEMMs)
-            from ..ops.llm import skinny_workspace
-
-            skinny_workspace(self.device)  # decode-GEMM split-K workspace, before any graph capture
         self.graphs: Dict[int, tuple] = {}
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "preemptions": 0, "steps": 0}
         # (batch size, seconds) of every decode step: forward + sampling, host included

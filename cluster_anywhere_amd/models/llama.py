@@ -321,7 +321,7 @@ class Llama(nn.Module):
             h, res = L.rms_norm(x, layer.attn_norm, cfg.norm_eps, res)
             if res is None:
                 res = x
-            # decode GEMMs stream the weights once: the skinny MFMA kernel (<= 128 rows)
+            # decode GEMMs stream the weights once: decode_gemm.hip (<= 128 rows)
             att = dec["attn"][i] if (dec is not None and dec["attn"] is not None) else None
             qkv = L.decode_gemm_qkv_rope(h, att[0], cs, pos, slots, k_caches[i], v_caches[i], H, KVH) \
                 if att else None

@@ -30,11 +30,6 @@ from ._lib import kernels
 
 ALGO = int(os.environ.get("CAAMD_GEMM_ALGO", "2"))
 ENABLED = os.environ.get("CAAMD_MFMA_GEMM", "1") == "1"
-# second-generation kernel (gemm2.hip: 256 x 160 tiles, two workgroups per CU, split-K tail)
-# (opt-in: its mainloop measured ~1.3x slower per MFMA than the ping-pong kernel's,
-# profiles/gemm2_vs_pp.jsonl, so the step keeps gemm.hip + the split tail below)
-GEN2 = os.environ.get("CAAMD_GEMM_GEN", "1") == "2"
-MAX_SPLIT = int(os.environ.get("CAAMD_GEMM2_MAX_SPLIT", "4"))
 # split-K tail of the ping-pong kernel: tiles past the last full round of CUs are
 # split over K-slices so that round is not half empty (N = 1600: 640 tiles = 2.5 rounds)
 TAIL = os.environ.get("CAAMD_GEMM_TAIL", "1") == "1"
@@ -83,21 +78,6 @@ _PLANS: dict = {}
 _WS: dict = {}
 
 
-def _slots(dev: torch.device) -> int:
-    """Workgroups of gemm2 resident at once: two per CU."""
-    return 2 * torch.cuda.get_device_properties(dev).multi_processor_count
-
-
-def plan2(M: int, N: int, K: int, dev: torch.device, max_split: Optional[int] = None):
-    """(full tiles, tail split S, grid, workspace floats, tickets) for a gemm2 launch."""
-    ms = MAX_SPLIT if max_split is None else max_split
-    key = (M, N, K, dev.index, ms)
-    p = _PLANS.get(key)
-    if p is None:
-        p = _PLANS[key] = tuple(kernels().gemm2_plan(M, N, K, _slots(dev), ms))
-    return p
-
-
 def _workspace(dev: torch.device, floats: int, tickets: int):
     """Per-device split-K slab workspace + zeroed ticket counters (the kernel's last
     arriver resets its ticket, so the counters stay zero between launches)."""
@@ -107,22 +87,6 @@ def _workspace(dev: torch.device, floats: int, tickets: int):
         cnt = torch.zeros(max(tickets, 4096), device=dev, dtype=torch.int32)
         _WS[dev.index] = (ws, cnt)
     return ws, cnt
-
-
-def gen2_ok(M: int, N: int, K: int) -> bool:
-    return ENABLED and GEN2 and M % 8 == 0 and N % 160 == 0 and K % 32 == 0 and K > 0
-
-
-def run2(a, b, c, layout, epi, bias=None, z=None, zout=None, dbias=None, max_split=None):
-    """gemm2 launch: layout 0 a[M,K] b[N,K]; layout 2 a[K,M] b[K,N]."""
-    M, N = c.shape
-    K = a.shape[0] if layout == 2 else a.shape[1]
-    full, S, grid, wsf, tickets = plan2(M, N, K, c.device, max_split)
-    ws = cnt = None
-    if S > 1:
-        ws, cnt = _workspace(c.device, wsf, tickets)
-    kernels().gemm2_bf16(a, b, c, layout, epi, bias, z, zout, dbias, ws, cnt, full, S, grid)
-    return c
 
 
 # De-phased full-line launches (CAAMD_GEMM_DEPHASE=1, experimental): on grids that are a
@@ -282,8 +246,6 @@ def run_tn(a, b, c, accumulate: bool, bm: int = 256, slices: int = 1, inkernel: 
 def _run(a, b, c, epi, bias=None, z=None, zout=None, dbias=None):
     M, N = c.shape
     K = a.shape[1]
-    if gen2_ok(M, N, K) and M % 256 == 0:
-        return run2(a, b, c, 0, epi, bias, z, zout, dbias)
     bm, bn = tile_for(M, N, K)
     return run_pp(a, b, c, 0, epi, bm, bn, bias, z, zout, dbias)
 

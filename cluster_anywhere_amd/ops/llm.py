@@ -39,60 +39,6 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5,
 
 # ------------------------------------------------------------------ SwiGLU
 # ---------------------------------------------------------------- decode GEMM
-_SKINNY_WS = {}
-
-
-def skinny_workspace(device, floats: int = 8 << 20, slabs: int = 4096):
-    """Per-device split-K workspace (fp32 partial tiles) and arrival counters of the
-    decode GEMM. Allocated once (before any HIP-graph capture) and reused: every
-    launch leaves the counters zeroed."""
-    dev = torch.device(device)
-    key = (dev.type, dev.index if dev.index is not None else torch.cuda.current_device())
-    ws = _SKINNY_WS.get(key)
-    if ws is None:
-        ws = (torch.empty(floats, device=dev, dtype=torch.float32), torch.zeros(slabs, device=dev, dtype=torch.int32))
-        _SKINNY_WS[key] = ws
-    return ws
-
-
-def skinny_splits(N: int, K: int) -> int:
-    """Split-K factor of the decode GEMM. Measured on MI355X at M = 128
-    (tools/bench_decode_gemm.py, CAAMD_SKINNY_SPLITS sweep): 2 for N <= 8192 at
-    K = 4096, else 4 where K allows (the last-arriver reduction of 8 splits costs
-    more than it hides), 1 for the vocabulary projection."""
-    forced = int(_os.environ.get("CAAMD_SKINNY_SPLITS", "0"))
-    if forced and K % (128 * forced) == 0:
-        return forced
-    if N >= 65536:
-        return 1
-    s = 2 if (N <= 8192 and K <= 4096) else 4
-    while s > 1 and K % (128 * s):
-        s //= 2
-    return s
-
-
-def skinny_ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2
-            and 1 <= x.shape[0] <= 128 and x.stride(1) == 1 and w.is_contiguous() and w.shape[0] % 64 == 0
-            and x.shape[1] == w.shape[1] and x.shape[1] % 128 == 0)
-
-
-def skinny_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """``x @ w.T`` on the weight-streaming MFMA kernel (``skinny_gemm.hip``); the
-    shapes must satisfy ``skinny_ok`` (raises otherwise)."""
-    if not skinny_ok(x, w):
-        raise ValueError(f"skinny_gemm: unsupported shapes {tuple(x.shape)} x {tuple(w.shape)}")
-    M, K = x.shape
-    N = w.shape[0]
-    s = skinny_splits(N, K)
-    part, cnt = skinny_workspace(x.device)
-    if s > 1 and part.numel() < s * N * 128:
-        s = 1
-    out = torch.empty(M, N, device=x.device, dtype=torch.bfloat16)
-    kernels().skinny_gemm(x, w, out, part, cnt, s)
-    return out
-
-
 # ---------------------------------------------------- decode GEMM v3 (decode_gemm.hip)
 _DG_WS: dict = {}
 
@@ -263,16 +209,9 @@ def interleave_gate_up(w: torch.Tensor) -> torch.Tensor:
 
 
 def decode_linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """``x @ w.T`` for decode-sized batches: the skinny MFMA kernel when enabled
-    (``CAAMD_SKINNY_GEMM=1``) and the shapes fit, else torch / hipBLASLt."""
-    if _SKINNY_ON and use_gpu_kernel(x, w) and skinny_ok(x, w):
-        return skinny_linear(x, w)
+    """``x @ w.T`` for decode-sized batches on a weight without a packed decode copy
+    (torch / hipBLASLt); the packed projections run on ``decode_gemm`` (v3)."""
     return F.linear(x, w)
-
-
-# opt-in: at batch 128 the kernel measured level with hipBLASLt's tuned selections
-# per GEMM (PERF.md, "Decode GEMM"), so serving keeps hipBLASLt unless this is set
-_SKINNY_ON = _os.environ.get("CAAMD_SKINNY_GEMM", "0") == "1"
 
 
 def silu_mul_ref(gu):

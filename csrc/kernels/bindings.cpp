@@ -65,11 +65,6 @@ hipError_t decode_gemm_qkv_rope_launch(const bf16* X, const bf16* W, bf16* Y, fl
 hipError_t decode_gemm_launch(int epi, const bf16* X, const bf16* W, bf16* Y, const bf16* R, float* part,
                               unsigned* tick, int M, int N, int K, int ldx, int ldy, int splits, bool packed,
                               float* ssp, float eps, hipStream_t st);
-void gemm2_plan(int M, int N, int K, int slots, int max_split, int* full, int* S, int* grid,
-                long long* ws_floats, int* tickets);
-hipError_t gemm2_launch(int layout, int epi, const bf16* A, const bf16* B, bf16* C, const bf16* bias,
-                        const bf16* Z, bf16* Zout, float* dbias, float* ws, int* cnt, int M, int N, int K,
-                        int lda, int ldb, int ldc, int full, int S, int grid, hipStream_t st);
 void rl_gemm(int layout, const bf16* A, const bf16* B, void* C, const bf16* bias, const bf16* aux, int M, int N,
              int K, int lda, int ldb, int ldc, int epi, int splits, hipStream_t st);
 void rl_im2col(const void* x, bool u8, bf16* col, int B, int H, int W, int C, int KH, int KW, int S, float scale,
@@ -550,35 +545,6 @@ std::vector<Tensor> rmsnorm(const Tensor& x, const Tensor& w, double eps, const 
   return {y, s_out};
 }
 
-namespace caamd {
-hipError_t skinny_gemm_launch(const bf16*, const bf16*, bf16*, float*, unsigned*, int, int, int, int, int,
-                              hipStream_t);
-}
-
-// decode GEMM: out[M, N] = x[M, K] . w[N, K]^T for M <= 128 (skinny_gemm.hip)
-void skinny_gemm(const Tensor& x, const Tensor& w, Tensor& out, Tensor& part, Tensor& counters, int64_t splits) {
-  CHECK_BF16(x);
-  CHECK_BF16(w);
-  CHECK_BF16(out);
-  CHECK_F32(part);
-  TORCH_CHECK(counters.is_cuda() && counters.scalar_type() == at::kInt && counters.is_contiguous(),
-              "skinny_gemm: counters must be a contiguous int32 CUDA tensor");
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && out.dim() == 2, "skinny_gemm: 2-D operands");
-  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
-  TORCH_CHECK(w.size(1) == K && w.is_contiguous(), "skinny_gemm: w must be a contiguous [N, K]");
-  TORCH_CHECK(x.stride(1) == 1 && x.stride(0) >= K, "skinny_gemm: x rows must be dense");
-  TORCH_CHECK(out.size(0) == M && out.size(1) == N && out.is_contiguous(), "skinny_gemm: out must be [M, N]");
-  TORCH_CHECK(M >= 1 && M <= 128, "skinny_gemm: 1 <= M <= 128");
-  TORCH_CHECK(N % 64 == 0, "skinny_gemm: N % 64 == 0");
-  TORCH_CHECK(splits >= 1 && K % (128 * splits) == 0, "skinny_gemm: K % (128 * splits) == 0");
-  TORCH_CHECK(splits == 1 || part.numel() >= splits * N * 128, "skinny_gemm: workspace too small");
-  TORCH_CHECK(counters.numel() >= N / 64, "skinny_gemm: counters too small");
-  hipError_t e = caamd::skinny_gemm_launch(bp(x), bp(w), bp(out), part.data_ptr<float>(),
-                                           (unsigned*)counters.data_ptr<int>(), (int)M, (int)N, (int)K,
-                                           (int)x.stride(0), (int)splits, cur_stream());
-  TORCH_CHECK(e == hipSuccess, "skinny_gemm launch failed: ", hipGetErrorString(e));
-}
-
 // greedy sampling: argmax over the last dim of bf16 logits [M, V] -> int64 [M]
 // (first maximum on ties)
 Tensor argmax_rows(const Tensor& x) {
@@ -1055,80 +1021,6 @@ static void gemm_tn64(Tensor a, Tensor b, Tensor c, int64_t bm, bool accumulate,
   TORCH_CHECK(e == hipSuccess, "gemm_tn64 launch failed: ", hipGetErrorString(e));
 }
 
-// ---- second-generation GEMM (gemm2.hip): 256 x 160 tiles, 2 workgroups per CU -------------
-// layout 0: a[M,K] b[N,K] · 2: a[K,M] b[K,N]. epi 0: c = acc(+bias) · 1: c += acc(+bias)
-// 3: zout = acc+bias, c = gelu(zout) · 4: c = acc*gelu'(z), dbias += colsum(c)
-static std::vector<int64_t> gemm2_plan_(int64_t M, int64_t N, int64_t K, int64_t slots, int64_t max_split) {
-  int full, S, grid, tickets;
-  long long wsf;
-  caamd::gemm2_plan((int)M, (int)N, (int)K, (int)slots, (int)max_split, &full, &S, &grid, &wsf, &tickets);
-  return {full, S, grid, (int64_t)wsf, tickets};
-}
-
-static void gemm2_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi, c10::optional<Tensor> bias,
-                       c10::optional<Tensor> z, c10::optional<Tensor> zout, c10::optional<Tensor> dbias,
-                       c10::optional<Tensor> ws, c10::optional<Tensor> cnt, int64_t full, int64_t S,
-                       int64_t grid) {
-  CHECK_BF16(a);
-  CHECK_BF16(b);
-  CHECK_BF16(c);
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm2: 2-D operands");
-  TORCH_CHECK(layout == 0 || layout == 2, "gemm2: layout 0 (NT) or 2 (TN)");
-  const int64_t M = layout == 2 ? a.size(1) : a.size(0);
-  const int64_t K = layout == 2 ? a.size(0) : a.size(1);
-  const int64_t N = layout == 0 ? b.size(0) : b.size(1);
-  const int64_t Kb = layout == 0 ? b.size(1) : b.size(0);
-  TORCH_CHECK(Kb == K, "gemm2: K mismatch");
-  TORCH_CHECK(c.size(0) == M && c.size(1) == N, "gemm2: output shape mismatch");
-  TORCH_CHECK(M % 8 == 0 && M >= 8 && N % 160 == 0 && K % 32 == 0 && K > 0, "gemm2: M%8, N%160, K%32 must be 0");
-  TORCH_CHECK(M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "gemm2: size");
-  const int64_t tiles = ((M + 255) / 256) * (N / 160);
-  TORCH_CHECK(S >= 1 && full >= 0 && full <= tiles, "gemm2: bad plan");
-  TORCH_CHECK(grid == (S > 1 ? full + (tiles - full) * S : tiles), "gemm2: grid does not match the plan");
-  TORCH_CHECK(S == 1 || (full % 8 == 0 && (grid - full) % 8 == 0), "gemm2: tail plan must be XCD-divisible");
-  using caamd::bf16;
-  const bf16* bp = nullptr;
-  if (bias.has_value()) {
-    CHECK_BF16(*bias);
-    TORCH_CHECK(bias->numel() == N, "gemm2: bias size");
-    bp = (const bf16*)bias->data_ptr();
-  }
-  const bf16* zp = nullptr;
-  bf16* zop = nullptr;
-  float* dbp = nullptr;
-  if (epi == 3) {
-    TORCH_CHECK(layout == 0 && zout.has_value() && bp, "gemm2: bias_gelu needs layout 0, bias and zout");
-    CHECK_BF16(*zout);
-    TORCH_CHECK(zout->sizes() == c.sizes(), "gemm2: zout shape");
-    zop = (bf16*)zout->data_ptr();
-  } else if (epi == 4) {
-    TORCH_CHECK(layout == 0 && z.has_value() && dbias.has_value(), "gemm2: dgelu needs layout 0, z, dbias");
-    CHECK_BF16(*z);
-    CHECK_F32(*dbias);
-    TORCH_CHECK(z->sizes() == c.sizes() && dbias->numel() == N, "gemm2: z / dbias shape");
-    zp = (const bf16*)z->data_ptr();
-    dbp = dbias->data_ptr<float>();
-  } else {
-    TORCH_CHECK(epi == 0 || epi == 1, "gemm2: bad epilogue");
-  }
-  float* wsp = nullptr;
-  int* cp = nullptr;
-  if (S > 1) {
-    TORCH_CHECK(ws.has_value() && cnt.has_value(), "gemm2: split tail needs ws and cnt");
-    CHECK_F32(*ws);
-    TORCH_CHECK(cnt->is_cuda() && cnt->scalar_type() == at::kInt && cnt->is_contiguous(), "gemm2: cnt int32");
-    TORCH_CHECK(ws->numel() >= (tiles - full) * S * 256 * 160, "gemm2: workspace too small");
-    TORCH_CHECK(cnt->numel() >= tiles - full, "gemm2: too few tickets");
-    wsp = ws->data_ptr<float>();
-    cp = cnt->data_ptr<int>();
-  }
-  hipError_t e = caamd::gemm2_launch((int)layout, (int)epi, (const bf16*)a.data_ptr(), (const bf16*)b.data_ptr(),
-                                     (bf16*)c.data_ptr(), bp, zp, zop, dbp, wsp, cp, (int)M, (int)N, (int)K,
-                                     (int)a.size(1), (int)b.size(1), (int)N, (int)full, (int)S, (int)grid,
-                                     cur_stream());
-  TORCH_CHECK(e == hipSuccess, "gemm2 launch failed: ", hipGetErrorString(e));
-}
-
 // ---- decode GEMM v3 (decode_gemm.hip): y = x . w^T for M <= 128, weight-streaming --------
 // epi 0: y = acc · 1: y = acc + residual · 2: SwiGLU over 64-row-interleaved gate/up weights
 // (y has N/2 columns)
@@ -1474,8 +1366,6 @@ PYBIND11_MODULE(_C, m) {
     caamd::gemm_tail_plan((int)tiles, (int)K, (int)ks, (int)slots, (int)max_split, &full, &S);
     return std::vector<int64_t>{full, S};
   });
-  m.def("gemm2_plan", GUARDED(gemm2_plan_));
-  m.def("gemm2_bf16", GUARDED(gemm2_bf16));
   m.def("decode_gemm", GUARDED(decode_gemm));
   m.def("decode_gemm_qkv_rope", GUARDED(decode_gemm_qkv_rope));
   m.def("decode_gemm_norm", GUARDED(decode_gemm_norm));
@@ -1510,7 +1400,6 @@ PYBIND11_MODULE(_C, m) {
         pybind11::arg("residual") = pybind11::none());
   m.def("silu_mul", GUARDED(silu_mul));
   m.def("argmax_rows", GUARDED(argmax_rows));
-  m.def("skinny_gemm", GUARDED(skinny_gemm));
   m.def("rope_cache_", GUARDED(rope_cache_));
   m.def("paged_decode", GUARDED(paged_decode), pybind11::arg("q"), pybind11::arg("k_cache"), pybind11::arg("v_cache"),
         pybind11::arg("block_tables"), pybind11::arg("ctx_lens"), pybind11::arg("max_ctx"), pybind11::arg("H"),

@@ -1,5 +1,5 @@
-"""Decode GEMM v3 (decode_gemm.hip) vs hipBLASLt (tuned selections) vs the first
-decode kernel (skinny_gemm.hip) on Llama-3-8B's decode shapes, batch 128, cache-cold
+"""Decode GEMM v3 (decode_gemm.hip) vs hipBLASLt (tuned selections) on Llama-3-8B's
+decode shapes, batch 128, cache-cold
 weights (rotated over >= 1 GB so each call streams from HBM, as in a decode step),
 plus numerics vs fp32 (store, residual and SwiGLU epilogues, split and unsplit).
 Prints one JSON line per shape."""
@@ -80,7 +80,7 @@ def check():
 
 
 def bench():
-    tot = {"hipblaslt": 0.0, "v1": 0.0, "v3": 0.0, "v3p": 0.0}
+    tot = {"hipblaslt": 0.0, "v3": 0.0, "v3p": 0.0}
     for name, N, K in (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
                        ("lm_head", 128256, 4096)):
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
@@ -94,7 +94,6 @@ def bench():
             return ws[it[0]]
 
         a = timeit(lambda: F.linear(x, nxt()))
-        b = timeit(lambda: L.skinny_linear(x, nxt())) if L.skinny_ok(x, w) else float("nan")
         c = timeit(lambda: L.decode_gemm(x, nxt()))
         wps = [L.pack_decode_weight(t) for t in ws]
         itp = [0]
@@ -105,7 +104,7 @@ def bench():
 
         d = timeit(lambda: L.decode_gemm(x, nxtp(), packed=True))
         row = {"gemm": name, "M": M, "N": N, "K": K, "splits": L.decode_gemm_splits(N, K),
-               "hipblaslt_us": round(a, 1), "v1_us": round(b, 1), "v3_us": round(c, 1), "v3p_us": round(d, 1),
+               "hipblaslt_us": round(a, 1), "v3_us": round(c, 1), "v3p_us": round(d, 1),
                "v3_TBps": round(N * K * 2 / c / 1e6, 2), "hipblaslt_TBps": round(N * K * 2 / a / 1e6, 2)}
         if name == "gate_up":
             wsi = [L.interleave_gate_up(t) for t in ws]
@@ -125,7 +124,6 @@ def bench():
         if name != "lm_head":
             tot["hipblaslt"] += a
             tot["v3"] += c
-            tot["v1"] += b
             tot["v3p"] += d
         print(json.dumps(row), flush=True)
     print(json.dumps({"layer_total_us": {k: round(v, 1) for k, v in tot.items()}}), flush=True)
