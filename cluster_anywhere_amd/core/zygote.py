@@ -108,6 +108,19 @@ def zygote_main(sock_path: str):
         pass
     from . import worker  # noqa: F401  (the worker runtime, pre-imported)
 
+    # Warm the RNG seeding paths the children run: numpy's first seed-from-entropy
+    # imports and initialises its entropy machinery (secrets / hashlib), ~140 ms that
+    # every forked worker otherwise paid again between fork and main() (measured on
+    # the CPU container: actor .remote() -> __init__ 125-170 ms, 140 of it here)
+    import random
+
+    random.seed()
+    numpy.random.seed(None)
+    try:
+        torch.seed()  # (lazy: queues the device seeding, no HIP initialisation)
+    except Exception:
+        pass
+
     signal.signal(signal.SIGCHLD, _reap)
     try:
         os.unlink(sock_path)
