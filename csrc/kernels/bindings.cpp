@@ -37,6 +37,7 @@ void maxpool3s2_launch(const bf16* x, bf16* y, int N, int H, int W, int C, int H
 bool xent_fused_launch(bf16*, const int64_t*, float*, float*, const float*, int, int, int, hipStream_t);
 void grad_sumsq_launch(const void*, bool, int64_t, float*, hipStream_t);
 void adamw_config(int variant);
+void fa64_set_pair(int v);
 void adamw_launch(float*, float*, float*, const void*, bool, bf16*, int64_t, float, float, float,
                   float, float, float, float, float, float, const float*, const uint8_t*,
                   hipStream_t);
@@ -1390,6 +1391,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("xent_fused_", GUARDED(xent_fused_));
   m.def("grad_sumsq", GUARDED(grad_sumsq));
   m.def("adamw_config", [](int64_t variant) { caamd::adamw_config((int)variant); });
+  m.def("fa64_set_pair", [](int64_t v) { caamd::fa64_set_pair((int)v); });
   m.def("adamw_step", GUARDED(adamw_step));
   m.def("gae", GUARDED(gae));
   m.def("vtrace", GUARDED(vtrace));

@@ -1289,6 +1289,264 @@ __global__ __launch_bounds__(256, 2) void bwd_dkdv_kernel(const bf16* __restrict
   }
 }
 
+// ----------------------------------------------------------------------------
+// dK, dV with PAIRED key blocks (fewer, longer blocks): one workgroup walks key block
+// j and key block nkb - 1 - j of one (batch, head) as ONE continuous stream of
+// 64-query tiles. Under the causal mask key block j needs nqt - 2j tiles, so every
+// pair carries nqt + 2 tiles (uniform work, half the blocks of the one-item kernel);
+// the LDS-DMA ring keeps prefetching across the seam between the two items, item B's
+// K / V rows sit in registers from the prologue on, and item A's dK / dV leave
+// through a 16 KB staging region of their own while item B's first tiles are
+// already in flight. Per tile the body is bwd_dkdv_kernel's production schedule
+// (OPT 104: K pre-scaled, S / dP accumulators started from -lse2 / -delta, K of the
+// first item by LDS-DMA, dK / dV stored as whole rows through LDS).
+// Measured lever: tools/lab/mfma_dep_bench.hip -- the dK/dV MFMA chain runs ~95 %
+// busy inside one long block; the one-item kernel's 6,400 short blocks pay a
+// prologue load and an epilogue store each (PERF.md round 5).
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void bwd_dkdv_pair_kernel(const bf16* __restrict__ qkv,
+                                                               const bf16* __restrict__ dout,
+                                                               const float* __restrict__ lse2g,
+                                                               const float* __restrict__ delta,
+                                                               bf16* __restrict__ dqkv, int T, int H, int nkb,
+                                                               int npair, float scale_log2, float scale, int causal,
+                                                               float* __restrict__ dbias) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  lds_t* smem = (lds_t*)smem_raw;
+  constexpr int STAGE = 2 * IMG + 512;
+  lds_t* stg_out = smem + 3 * STAGE;  // 16 KB: 4 KB per wave, dK then dV of a finished item
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = id / npair;
+  const int pj = id % npair;
+  const int kbs[2] = {pj, nkb - 1 - pj};
+  const int nitem = kbs[1] == kbs[0] ? 1 : 2;
+  const int b = bh / H, hh = bh % H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const size_t rs = (size_t)3 * H * D, ors = (size_t)H * D;
+  const bf16* qbase = qkv + (size_t)b * T * rs + (size_t)hh * D;
+  const bf16* kbase = qbase + (size_t)H * D;
+  const bf16* vbase = kbase + (size_t)H * D;
+  const bf16* dobase = dout + (size_t)b * T * ors + (size_t)hh * D;
+  const float* l2b = lse2g + (size_t)bh * T;
+  const float* dlb = delta + (size_t)bh * T;
+  const int nqt = (T + 63) / 64;
+  const int nfull = T / 64;
+  // tile stream: item 0's tiles [qt0(0), nqt), then item 1's [qt0(1), nqt)
+  auto qt0_of = [&](int it) { return causal ? (kbs[it] * 128) / 64 : 0; };
+  const int qt0A = qt0_of(0);
+  const int cntA = max(0, nqt - qt0A);
+  const int cnt = cntA + (nitem == 2 ? max(0, nqt - qt0_of(1)) : 0);
+  auto qt_of = [&](int g) { return g < cntA ? qt0A + g : qt0_of(1) + (g - cntA); };
+
+  auto issue = [&](int g, lds_t* buf) {
+    const int qt = qt_of(g);
+    dma_tile(qbase, rs, qt * 64, T, buf, wave, lane);
+    dma_tile(dobase, ors, qt * 64, T, buf + IMG, wave, lane);
+    if (wave == 0) dma_stats(l2b, qt * 64, T, buf + 2 * IMG, lane);
+    else if (wave == 1) dma_stats(dlb, qt * 64, T, buf + 2 * IMG + 256, lane);
+  };
+  if (cnt > 0) issue(0, smem);
+  if (cnt > 1) issue(1, smem + STAGE);
+
+  // K / V rows: item 0's K by LDS-DMA through the third stage and its V by per-lane
+  // 16-byte loads; item 1's K / V by per-lane loads issued at the seam (they land
+  // while item 0's dK / dV are written out)
+  bf16x8 kf[4], vf[4];
+  int key0w = kbs[0] * 128 + wave * 32;
+  int key = key0w + r;
+  bool kv = key < T;
+  dma_tile(kbase, rs, kbs[0] * 128, T, smem + 2 * STAGE, wave, lane);
+  dma_tile(kbase, rs, kbs[0] * 128 + 64, T, smem + 2 * STAGE + IMG, wave, lane);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (kv) {
+      vf[s] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)key * rs + 16 * s + 8 * h);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kf[s][j] = vf[s][j] = (bf16)0.f;
+    }
+  }
+  wait_dma();
+  __syncthreads();
+  {
+    typedef __attribute__((address_space(3))) const bf16x8 lds_kf;
+    const lds_t* kimg = smem + 2 * STAGE + (wave >> 1) * IMG;
+    const int row = (wave & 1) * 32 + r;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 v = *(lds_kf*)(kimg + row * 128 + (((2 * s + h) ^ swz(row)) << 4));
+      if (kv) kf[s] = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  __syncthreads();  // every wave has its K fragments: the stage is free for tile 2
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kf[s][j] = (bf16)((float)kf[s][j] * scale_log2);
+  f32x16 dk[2], dv[2];
+  dk[0] = dk[1] = dv[0] = dv[1] = zero16();
+  int qoff[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qoff[s] = r * 128 + (((2 * s + h) ^ swz(r)) << 4);
+  const TrBase tb = tr_base(lane);
+
+  auto tile = [&](auto need_mask_c, const lds_t* qimg, unsigned qimg_u, int q0) {
+    constexpr bool need_mask = decltype(need_mask_c)::value;
+    typedef __attribute__((address_space(3))) const bf16x8 lds_bf16x8;
+    const float* st = (const float*)(qimg + 2 * IMG);
+    const int lo_lim = causal ? key - q0 - 4 * h : -0x7fffffff;
+    const int hi_lim = T - 1 - q0 - 4 * h;
+    bf16x8 qr[4], dr[4];
+    auto load_rows = [&](int qh) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        qr[s] = *(lds_bf16x8*)(qimg + qoff[s] + qh * 4096);
+        dr[s] = *(lds_bf16x8*)(qimg + IMG + qoff[s] + qh * 4096);
+      }
+    };
+    load_rows(0);
+    static_for<2>([&](auto qh_c) {
+      constexpr int qh = decltype(qh_c)::value;
+      if constexpr (qh == 1) load_rows(1);
+      TrFrag tv[2][2], tk[2][2];
+      f32x4 l4s[4], d4s[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int qi = qh * 32 + 8 * g + 4 * h;
+        l4s[g] = *reinterpret_cast<const f32x4*>(st + qi);
+        d4s[g] = *reinterpret_cast<const f32x4*>(st + 64 + qi);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(l4s[0]), "+v"(l4s[1]), "+v"(l4s[2]), "+v"(l4s[3]), "+v"(d4s[0]), "+v"(d4s[1]),
+                     "+v"(d4s[2]), "+v"(d4s[3])::"memory");
+      f32x16 sinit, dinit;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sinit[4 * g + j] = l4s[g][j];
+          dinit[4 * g + j] = d4s[g][j];
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x16 sacc = mfma32(qr[0], kf[0], sinit);
+      f32x16 dp = mfma32(dr[0], vf[0], dinit);
+#pragma unroll
+      for (int s = 1; s < 4; ++s) {
+        sacc = mfma32(qr[s], kf[s], sacc);
+        dp = mfma32(dr[s], vf[s], dp);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<2>([&](auto s_c) {
+        constexpr int s = decltype(s_c)::value;
+        tr_frag<qh * 32 + s * 16, 0>(tv[s][0], qimg_u + IMG, tb);
+        tr_frag<qh * 32 + s * 16, 1>(tv[s][1], qimg_u + IMG, tb);
+        tr_frag<qh * 32 + s * 16, 0>(tk[s][0], qimg_u, tb);
+        tr_frag<qh * 32 + s * 16, 1>(tk[s][1], qimg_u, tb);
+      });
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int i = 4 * g + j;
+          float p = fexp2(sacc[i]);
+          if constexpr (need_mask) {
+            const int c = qh * 32 + 8 * g + j;
+            p = (c < lo_lim || c > hi_lim) ? 0.f : p;
+          }
+          sacc[i] = p;
+          dp[i] = p * dp[i];
+        }
+      }
+      tr_wait4(tv[0][0], tv[0][1], tk[0][0], tk[0][1]);
+      tr_wait4(tv[1][0], tv[1][1], tk[1][0], tk[1][1]);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pf = acc_frag(sacc, s), sf = acc_frag(dp, s);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = mfma32(tr_join(tv[s][d]), pf, dv[d]);
+          dk[d] = mfma32(tr_join(tk[s][d]), sf, dk[d]);
+        }
+      }
+    });
+  };
+
+  // dK / dV of the finished item (keys key0w .. key0w + 31 of this wave): through the
+  // wave's 4 KB of the staging region, dK then dV (the region is this wave's only)
+  auto finish_item = [&]() {
+    if (dbias) {
+      __shared__ float red[256];
+      f32x16 k2[2], v2[2];
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        k2[d] = kv ? dk[d] : zero16();
+        v2[d] = kv ? dv[d] : zero16();
+      }
+      colsum_atomic(k2, scale, dbias + (size_t)(H + hh) * D, red);
+      colsum_atomic(v2, 1.f, dbias + (size_t)(2 * H + hh) * D, red);
+    }
+    bf16* kr = dqkv + ((size_t)b * T + key0w) * rs + (size_t)(H + hh) * D;
+    lds_t* wb = stg_out + wave * 4096;
+    store_rows_lds(dk, scale, wb, kr, rs, T - key0w);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's row reads of dK done
+    __builtin_amdgcn_wave_barrier();
+    store_rows_lds(dv, 1.f, wb, kr + (size_t)H * D, rs, T - key0w);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  };
+
+  const unsigned smem_u = (unsigned)(size_t)smem;
+  // one tile of the stream: prefetch stream tile g + 2, compute tile g (= query tile qt)
+  auto iter = [&](int g, int qt, auto mask_c) {
+    const int q0 = qt * 64;
+    const bool ahead = g + 2 < cnt;
+    if (ahead) issue(g + 2, smem + ((g + 2) % 3) * STAGE);
+    if (!(causal && q0 + 63 < key0w) && key0w < T)  // wave-uniform
+      tile(mask_c, smem + (g % 3) * STAGE, smem_u + (g % 3) * STAGE, q0);
+    if (wave < 2) wait_next<5>(ahead);
+    else wait_next<4>(ahead);
+    barrier_keep_dma();
+  };
+  int g = 0;
+  for (int it = 0; it < nitem; ++it) {
+    if (it == 1) {  // seam: item 0 done, item 1's first tiles are already in the ring
+      const int keyB = kbs[1] * 128 + wave * 32 + r;
+      const bool kvB = keyB < T;
+      bf16x8 kn[4], vn[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (kvB) {
+          kn[s] = *reinterpret_cast<const bf16x8*>(kbase + (size_t)keyB * rs + 16 * s + 8 * h);
+          vn[s] = *reinterpret_cast<const bf16x8*>(vbase + (size_t)keyB * rs + 16 * s + 8 * h);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) kn[s][j] = vn[s][j] = (bf16)0.f;
+        }
+      }
+      finish_item();
+      key0w = kbs[1] * 128 + wave * 32;
+      key = keyB;
+      kv = kvB;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kf[s][j] = (bf16)((float)kn[s][j] * scale_log2);
+        vf[s] = vn[s];
+      }
+      dk[0] = dk[1] = dv[0] = dv[1] = zero16();
+    }
+    const int q0t = qt0_of(it);
+    const int pro = min(nqt, q0t + 2);  // the causal diagonal tiles need the mask
+    int qt = q0t;
+    for (; qt < pro; ++qt, ++g) iter(g, qt, std::true_type{});
+    for (; qt < nfull; ++qt, ++g) iter(g, qt, std::false_type{});
+    for (; qt < nqt; ++qt, ++g) iter(g, qt, std::true_type{});
+  }
+  finish_item();
+}
+
 }  // namespace fa64
 
 // Outputs written through the LDS row transpose (fa64::store_rows_lds); CAAMD_FA64_STG=0
@@ -1353,6 +1611,16 @@ void fa64_fwd_launch(const bf16* q, const bf16* k, const bf16* v, int q_rs, int 
                      H, nqb, scale_log2, causal);
 }
 
+static int g_fa64_pair = -1;  // -1: from CAAMD_FA64_PAIR (default on)
+static bool fa64_pair_mode() {
+  if (g_fa64_pair < 0) {
+    const char* e = std::getenv("CAAMD_FA64_PAIR");
+    g_fa64_pair = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_fa64_pair != 0;
+}
+void fa64_set_pair(int v) { g_fa64_pair = v ? 1 : 0; }
+
 // ws: 2 * B * H * T floats (delta, then lse * log2 e)
 void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const float* lse, float* ws, bf16* dqkv,
                      int B, int T, int H, int causal, hipStream_t st, float* dbias) {
@@ -1404,6 +1672,20 @@ void fa64_bwd_launch(const bf16* qkv, const bf16* out, const bf16* dout, const f
     case 63: kern = fa64::bwd_dkdv_kernel<63>; break;
     case 95: kern = fa64::bwd_dkdv_kernel<31, 8>; break;  // stripped, staged stores
     default: break;
+  }
+  // paired key blocks (bwd_dkdv_pair_kernel): CAAMD_FA64_PAIR=0 (or fa64_set_pair(0))
+  // -> one key block per workgroup
+  if (fa64_pair_mode() && opt == 104 && abl == 0 && causal) {
+    const int npair = (nkb + 1) / 2;
+    static const bool attr = [] {
+      (void)hipFuncSetAttribute((const void*)fa64::bwd_dkdv_pair_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 6 * fa64::IMG + 1536 + 16384);
+      return true;
+    }();
+    (void)attr;
+    hipLaunchKernelGGL(fa64::bwd_dkdv_pair_kernel, dim3(B * H * npair), dim3(256), 6 * fa64::IMG + 1536 + 16384, st,
+                       qkv, dout, lse2, delta, dqkv, T, H, nkb, npair, scale_log2, scale, causal, dbias);
+    return;
   }
   hipLaunchKernelGGL(kern, dim3(B * H * nkb), dim3(256), 6 * fa64::IMG + 1536, st, qkv, dout,
                      lse2, delta, dqkv, T, H, nkb, scale_log2, scale, causal, dbias);

@@ -425,3 +425,24 @@ def test_bias_grad_rowsum(C, rows, N, accumulate):
     ref = dy.float().sum(0) + (out.float() if accumulate else 0.0)
     C.bias_grad_(dy, out, accumulate)
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2 * max(1.0, rows ** 0.5 / 10))
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 1024, 5), (1, 200, 3), (2, 640, 2), (1, 64, 2)])
+def test_flash_bwd_paired_dkdv_bit_exact(C, B, T, H):
+    """The paired-key-block dK/dV kernel (one workgroup walks key blocks j and
+    nkb-1-j as one tile stream) adds every key's contributions in the same tile
+    order as the one-block-per-key-block kernel: dqkv bit-identical (odd and even
+    key-block counts, partial last blocks, a single block)."""
+    torch.manual_seed(11)
+    D = 64
+    qkv = (torch.randn(B, T, 3 * H * D, device="cuda") * 0.7).bfloat16()
+    out, lse = C.flash_attn_fwd(qkv, H, True)
+    dout = torch.randn_like(out)
+    try:
+        C.fa64_set_pair(1)
+        paired = C.flash_attn_bwd(qkv, out, dout, lse, H, True)
+        C.fa64_set_pair(0)
+        single = C.flash_attn_bwd(qkv, out, dout, lse, H, True)
+    finally:
+        C.fa64_set_pair(1)
+    assert torch.equal(paired, single)
