@@ -53,7 +53,7 @@ from typing import Dict, List, Optional
 
 from .head import NORMAL
 
-DEPTH = int(os.environ.get("CAAMD_LEASE_DEPTH", "16"))
+DEPTH = int(os.environ.get("CAAMD_LEASE_DEPTH", "64"))
 LINGER = float(os.environ.get("CAAMD_LEASE_LINGER_S", "0.02"))
 SLICE = float(os.environ.get("CAAMD_LEASE_SLICE_S", "0.25"))
 MAX_WANT = int(os.environ.get("CAAMD_LEASE_MAX_WANT", "16"))
