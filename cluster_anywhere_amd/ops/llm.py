@@ -41,6 +41,9 @@ def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5,
 # ---------------------------------------------------------------- decode GEMM
 # ---------------------------------------------------- decode GEMM v3 (decode_gemm.hip)
 _DG_WS: dict = {}
+# split-count overrides for A/B runs: CAAMD_DG_SPLITS="4096x4096:4,6144x4096:6" (N x K : splits)
+_DG_SPLITS = {tuple(int(v) for v in p.split(":")[0].split("x")): int(p.split(":")[1])
+              for p in _os.environ.get("CAAMD_DG_SPLITS", "").split(",") if ":" in p}
 
 
 def decode_gemm_splits(N: int, K: int, cus: int = 256) -> int:
@@ -49,6 +52,9 @@ def decode_gemm_splits(N: int, K: int, cus: int = 256) -> int:
     not divide K: Llama-3-8B qkv (48 slabs, K 4096) runs 5 splits on 240 CUs instead
     of 4 on 192 (measured level, 19.4 vs 19.3-19.5 us: that GEMM is bound by each
     CU's LDS-DMA intake, not by the idle CUs; profiles/decode_ragged_split_r4.txt)."""
+    forced = _DG_SPLITS.get((N, K))
+    if forced:
+        return forced
     slabs = N // 128
     steps = K // 64
     s = max(1, min(cus // max(1, slabs), K // 256))
