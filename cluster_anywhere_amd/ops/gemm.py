@@ -12,11 +12,12 @@ every GPT-2-XL projection at micro-batch x seq = 32768 tokens. Anything else
 
 Tile choice: 256 x 320 (divides 1600/4800/6400) with the ping-pong pipeline
 (``algo=2``: BK=32, 4-deep LDS ring, LDS-DMA two K-steps ahead, counted vmcnt, staggered wave rows), else 256 x 256.
-NT GEMMs with N or K >= 4096 (fc / fc2 / qkv forward and dgrad) take the full-line
-kernel instead (``algo=4009``: BK=64, one 128-byte line per row and K-tile, two LDS
-buffers, DMA of K-tile t+1 issued in the first of two MFMA phases of t): 2-4 %
-faster on those shapes, 2 % slower on the 1600 x 1600 projection
-(``profiles/gemm_k64_r4.jsonl``).
+NT GEMMs with N or K >= 1536 (fc / fc2 / qkv / proj forward and dgrad) take the
+full-line kernel instead (``algo=4009``: BK=64, one 128-byte line per row and K-tile,
+two LDS buffers, DMA of K-tile t+1 issued in the first of two MFMA phases of t): 2-4 %
+faster on the large shapes in round 4 (``profiles/gemm_k64_r4.jsonl``); since round 6
+also on the 1600 x 1600 projection (149-152 vs 154-168 us,
+``profiles/gemm_algo_ab_r6.jsonl``).
 """
 from __future__ import annotations
 
@@ -36,6 +37,10 @@ TAIL = os.environ.get("CAAMD_GEMM_TAIL", "1") == "1"
 # full-line BK=64 kernel (algo 4009) on the large NT shapes (CAAMD_GEMM_K64=0: off)
 K64 = os.environ.get("CAAMD_GEMM_K64", "1") == "1"
 K64_ALGO = 4009
+# smallest max(N, K) routed to the full-line kernel: the 1600 x 1600 attention projection
+# (fwd and dgrad, 640 tiles) runs 149-152 us there vs 154-168 on the ping-pong kernel
+# (tools/gemm_algo_ab.py, profiles/gemm_algo_ab_r6.jsonl); the rule was 4096 until round 6
+K64_MIN = int(os.environ.get("CAAMD_GEMM_K64_MIN", "1536"))
 
 
 # 256 x 256 tiles on the full-line kernel too (the LM-head logits GEMM: vocab 50432 is
@@ -45,7 +50,7 @@ K64_256 = os.environ.get("CAAMD_GEMM_K64_256", "1") == "1"
 
 def k64_ok(layout: int, epi: int, bm: int, bn: int, N: int, K: int) -> bool:
     tiles = (bm, bn) == (256, 320) or (K64_256 and (bm, bn) == (256, 256))
-    return (K64 and layout == 0 and tiles and epi != EPI_F32 and max(N, K) >= 4096 and K % 64 == 0)
+    return (K64 and layout == 0 and tiles and epi != EPI_F32 and max(N, K) >= K64_MIN and K % 64 == 0)
 MAX_TAIL_SPLIT = int(os.environ.get("CAAMD_GEMM_TAIL_SPLIT", "4"))
 
 EPI_BF16, EPI_BF16_ACC, EPI_F32, EPI_BIAS_GELU, EPI_DGELU, EPI_SWIGLU = range(6)

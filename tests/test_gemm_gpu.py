@@ -166,13 +166,14 @@ def test_gemm_k64_variants(algo, K):
 
 
 def test_gemm_k64_epilogues_and_dispatch():
-    """The dispatcher sends NT GEMMs with max(N, K) >= 4096 to algo 4009; its bias,
+    """The dispatcher sends NT GEMMs with max(N, K) >= 1536 to algo 4009; its bias,
     bias+GELU and dGELU+bias-grad epilogues vs fp32, and the result equals an explicit
     algo-4009 launch."""
     from cluster_anywhere_amd.ops import gemm as G
     from cluster_anywhere_amd.ops import kernels
 
-    assert G.k64_ok(0, G.EPI_BF16, 256, 320, 4800, 1600) and not G.k64_ok(0, G.EPI_BF16, 256, 320, 1600, 1600)
+    assert G.k64_ok(0, G.EPI_BF16, 256, 320, 4800, 1600) and G.k64_ok(0, G.EPI_BF16, 256, 320, 1600, 1600)
+    assert not G.k64_ok(0, G.EPI_BF16, 256, 320, 1280, 1280)
     M, K, N = 512, 640, 4160  # N = 13 x 320 >= 4096
     x, w = _mk((M, K), 23), _mk((N, K), 24) * 0.05
     b = _mk((N,), 25)
