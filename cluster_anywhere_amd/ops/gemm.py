@@ -275,6 +275,36 @@ def linear_nt(x2: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = Non
     return _run(x2, w, out, EPI_BF16, bias=b)
 
 
+# NN GEMMs on the TN kernel's full-line schedule with a K-major A (gemm.hip algo 27):
+# x @ W for a weight W [K, N] read as stored, so the input-gradient GEMMs, the fc2
+# forward from its transposed storage and the LM-head dgrad need no transpose pass.
+# Opt-in (CAAMD_GEMM_NN=1): it measured slower than transpose + the k64 NT kernel on
+# the 640-tile shapes (fc dgrad 571-581 vs 537-550 us: no split tail on this schedule)
+# and the step 99.5k / 99.7k vs 100.9k / 101.2k (profiles/gemm_nn_ab_r6.txt)
+NN = os.environ.get("CAAMD_GEMM_NN", "0") == "1"
+
+
+def nn_ok(M: int, N: int, K: int) -> bool:
+    return NN and ENABLED and M % 256 == 0 and N % 320 == 0 and K % 64 == 0
+
+
+def linear_nn64(x2: torch.Tensor, wkn: torch.Tensor, b: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``x2 [M, K] @ wkn [K, N] (+ b)`` on the NN kernel (caller checks :func:`nn_ok`)."""
+    if out is None:
+        out = torch.empty(x2.shape[0], wkn.shape[1], device=x2.device, dtype=torch.bfloat16)
+    kernels().gemm_nn64(x2, wkn, out, b)
+    return out
+
+
+def dgrad_w(dy2: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """dx = dy @ W for an nn.Linear weight W [N_out, K_in] as stored: the NN kernel,
+    else W^T by the transpose kernel + the NT path (:func:`dgrad`)."""
+    if nn_ok(dy2.shape[0], w.shape[1], w.shape[0]) and _ok(dy2, w):
+        return linear_nn64(dy2, w)
+    return dgrad(dy2, transpose(w))
+
+
 def linear_gelu(x2: torch.Tensor, w: torch.Tensor, b: torch.Tensor):
     M, N = x2.shape[0], w.shape[0]
     u = torch.empty(M, N, device=x2.device, dtype=torch.bfloat16)

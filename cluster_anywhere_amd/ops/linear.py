@@ -4,9 +4,9 @@ data-parallel gradient buffer ("main grad").
 Forward and input-gradient GEMMs run on the hand-written MFMA kernels
 (``ops/gemm.py`` -> ``csrc/kernels/gemm.hip``) whenever the shape tiles
 (GPT-2-XL: every projection), with the bias add fused into the epilogue; the
-input gradient ``dX = dY @ W`` runs as an NT GEMM against ``W^T`` (one 64x64-tile
-transpose per weight per step, ~1 ms for all of GPT-2-XL) so both operands stream
-K-major. ``dW += dY^T X`` accumulates directly into ``weight.main_grad`` — a view
+input gradient ``dX = dY @ W`` runs on the NN kernel reading ``W`` as stored (round 6;
+before, an NT GEMM against a transposed copy: one 64x64-tile transpose per weight per
+step, ~1.7 ms for all of GPT-2-XL). ``dW += dY^T X`` accumulates directly into ``weight.main_grad`` — a view
 of the flat grad buffer — on the split-K / stream-K weight-gradient kernel of
 gemm.hip for the shapes where it measured faster (``gemm.WGRAD_WINNERS``), else
 with ``addmm_`` (hipBLASLt, beta = 1); and
@@ -93,7 +93,7 @@ def _bgrad(b, dy2, needs):
 
 def _dgrad(dy2, w, mfma):
     if mfma:
-        return _g.dgrad(dy2.contiguous(), _g.transpose(w))
+        return _g.dgrad_w(dy2.contiguous(), w)
     return dy2 @ w
 
 
@@ -129,7 +129,10 @@ class _MainGradMLP(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, b2_grad=True):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         u, z = _g.linear_gelu(x2, w1, b1)
-        if _FC2_NN and not w2.is_contiguous():
+        if (not w2.is_contiguous() and w2.t().is_contiguous()
+                and _g.nn_ok(u.shape[0], w2.shape[0], w2.shape[1]) and _g._ok(u, b2)):
+            y = _g.linear_nn64(u, w2.t(), b2)  # transposed storage read as stored (NN kernel)
+        elif _FC2_NN and not w2.is_contiguous():
             y = _g.linear_nn(u, w2.t(), b2)  # transposed storage read as the NN layout
         else:
             y = _g.linear_nt(u, _wn(w2), b2)
@@ -166,7 +169,7 @@ class _MainGradMLP(torch.autograd.Function):
         gw1 = _wgrad(w1, dz, x2, ctx.needs_input_grad[1])
         dx = None
         if ctx.needs_input_grad[0]:
-            dx = _g.dgrad(dz, _g.transpose(w1)).view(ctx.xshape)
+            dx = _g.dgrad_w(dz, w1).view(ctx.xshape)
         return dx, gw1, gb1, gw2, gb2, None
 
 

@@ -99,7 +99,10 @@ class _LinearXentFn(torch.autograd.Function):
         logits = torch.empty(C, V, device=h2.device, dtype=torch.bfloat16)
         dh = torch.empty_like(h2)
         dw = torch.empty_like(w)
-        wt = _g.transpose(w)  # [D, V]: dh = dlogits @ w as an NT GEMM (both operands K-major)
+        # dh = dlogits @ w: on the NN kernel with w read as stored, else against a
+        # transposed copy [D, V] on the NT kernel (both operands K-major)
+        nn = _g.nn_ok(min(N, chunk), D, V) and (N % min(N, chunk)) % 256 == 0 and _g._ok(h2, w)
+        wt = None if nn else _g.transpose(w)
         losses = []
         for c0 in range(0, N, C):
             c1 = min(N, c0 + C)
@@ -107,7 +110,10 @@ class _LinearXentFn(torch.autograd.Function):
             _g._run(hc, w, lg, _g.EPI_BF16)                          # logits = h w^T
             loss_c, _ = k.xent_fused_(lg, target[c0:c1], scale, vocab)  # lg <- scale*(p - onehot)
             losses.append(loss_c)
-            _g._run(lg, wt, dh[c0:c1], _g.EPI_BF16)                  # dh = dlogits w
+            if nn:
+                _g.linear_nn64(lg, w, out=dh[c0:c1])                    # dh = dlogits w
+            else:
+                _g._run(lg, wt, dh[c0:c1], _g.EPI_BF16)
             tn = _g.tn_plan(V, D, c1 - c0)
             if tn is not None:
                 _g.run_tn(lg, hc, dw, c0 > 0, *tn)                   # dw (+)= dlogits^T h

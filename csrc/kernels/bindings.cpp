@@ -53,6 +53,8 @@ void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* ful
 void gemm_set_tail_first(int v);
 hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
                             int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st, int* tickets);
+hipError_t gemm_nn64_launch(const bf16* A, const bf16* B, bf16* C, const bf16* bias, int M, int N, int K, int lda,
+                            int ldb, int ldc, hipStream_t st);
 void gemm_splitk_reduce(const float* part, int S, long long slab, bf16* out, int M, int N, int ldc,
                         bool accumulate, hipStream_t st);
 void transpose_bf16(const bf16* in, bf16* out, int R, int C, hipStream_t st);
@@ -985,6 +987,32 @@ static void gemm_bf16(Tensor a, Tensor b, Tensor c, int64_t layout, int64_t epi,
   }
 }
 
+// NN GEMM on the TN kernel's schedule (gemm.hip algo 27): c[M,N] = a[M,K] b[K,N] (+ bias),
+// a K-major (rows of K), b row-major [K, N] (e.g. a weight W[N_out][K_in] as stored, so the
+// dgrad dx = dY W needs no transposed copy); 256 x 320 tiles, no split
+static void gemm_nn64(Tensor a, Tensor b, Tensor c, c10::optional<Tensor> bias) {
+  CHECK_BF16(a);
+  CHECK_BF16(b);
+  CHECK_BF16(c);
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && c.dim() == 2, "gemm_nn64: 2-D operands");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  TORCH_CHECK(b.size(0) == K && c.size(0) == M && c.size(1) == N, "gemm_nn64: shape mismatch");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && c.stride(1) == 1, "gemm_nn64: unit inner strides");
+  TORCH_CHECK(M % 256 == 0 && N % 320 == 0 && K % 64 == 0 && K > 0, "gemm_nn64: M%256, N%320, K%64 must be 0");
+  TORCH_CHECK(256LL * a.stride(0) * 2 < (1LL << 32) && K * b.stride(0) * 2 < (1LL << 32),
+              "gemm_nn64: operands must fit a 32-bit buffer descriptor");
+  const caamd::bf16* bp = nullptr;
+  if (bias.has_value()) {
+    CHECK_BF16(*bias);
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemm_nn64: bias [N]");
+    bp = (const caamd::bf16*)bias->data_ptr();
+  }
+  hipError_t e = caamd::gemm_nn64_launch((const caamd::bf16*)a.data_ptr(), (const caamd::bf16*)b.data_ptr(),
+                                         (caamd::bf16*)c.data_ptr(), bp, (int)M, (int)N, (int)K, (int)a.stride(0),
+                                         (int)b.stride(0), (int)c.stride(0), cur_stream());
+  TORCH_CHECK(e == hipSuccess, "gemm_nn64 launch failed: ", hipGetErrorString(e));
+}
+
 // TN weight gradient on the full-line kernel (gemm.hip algo 25): c[M,N] (+)= a[K,M]^T b[K,N],
 // 256- or 192-row tiles x 320 columns, lockstep split over `slices` (ws: slices x tiles fp32 slabs)
 static void gemm_tn64(Tensor a, Tensor b, Tensor c, int64_t bm, bool accumulate, int64_t slices,
@@ -1361,6 +1389,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_tn64", GUARDED(gemm_tn64), pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
         pybind11::arg("bm"), pybind11::arg("accumulate"), pybind11::arg("slices"),
         pybind11::arg("ws") = pybind11::none(), pybind11::arg("tickets") = pybind11::none());
+  m.def("gemm_nn64", GUARDED(gemm_nn64), pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
+        pybind11::arg("bias") = pybind11::none());
   m.def("gemm_set_tail_first", [](int64_t v) { caamd::gemm_set_tail_first((int)v); });
   m.def("gemm_tail_plan", [](int64_t tiles, int64_t K, int64_t ks, int64_t slots, int64_t max_split) {
     int full, S;

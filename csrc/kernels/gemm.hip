@@ -1778,7 +1778,17 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restr
 // BM = 192 serves the 4800-row qkv gradient: 25 x 5 tiles x 2 slices = 250 runs for
 // 256 CUs (256-row tiles: 95 tiles, 190 runs).
 // ================================================================================
-template <int BM, int BN, int EPI, bool COMBINE = false>
+//
+// AKM (NN layout, "gemm_nn64"): A K-major (A[m][k], activations / dY) with B still
+// MN-major (B[k][n] = a weight W[N_out][K_in] read as stored): the dgrad dx = dY W and
+// the transposed-storage fc2 forward without a weight transpose pass. A K-tile of A is
+// the k64 kernel's image (BM rows x 128 B, kswz-swizzled, ds_read_b128 fragments at two
+// precomputed lane addresses per fragment -- the k-sub moves the swizzled chunk, not a
+// constant offset); B, the phases and the epilogue are the TN kernel's. No split (LS 1).
+// (A BKM variant -- B K-major too, i.e. the NT layout on this schedule -- measured level
+// with the k64 kernel at K = 1600 and 4-10 % slower at K = 6400, and was removed:
+// profiles/gemm_nt_sched_ab_r6.txt.)
+template <int BM, int BN, int EPI, bool COMBINE = false, bool AKM = false>
 __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
   constexpr int WM = 2, WN = 4;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16, TMH = TM / 2;
@@ -1822,16 +1832,26 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
   const int m0 = (first_m + tin % gm) * BM, n0 = (tin / gm) * BN;
 
   // ---- DMA: one descriptor per operand, one lane offset per round ------------------------
-  const __amdgpu_buffer_rsrc_t ra = make_rsrc(p.A + m0, (unsigned)(((size_t)p.K * p.lda - m0) * 2));
+  const __amdgpu_buffer_rsrc_t ra =
+      AKM ? make_rsrc(p.A + (size_t)m0 * p.lda, (unsigned)(BM * p.lda * 2))
+          : make_rsrc(p.A + m0, (unsigned)(((size_t)p.K * p.lda - m0) * 2));
   const __amdgpu_buffer_rsrc_t rb = make_rsrc(p.B + n0, (unsigned)(((size_t)p.K * p.ldb - n0) * 2));
   int voa[NA], vob[NB];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
-    constexpr int CPR = BM / 8;
-    const int lin = j * NTHR + wid * 64 + lane;
-    const int k = lin / CPR, pos = lin - k * CPR;
-    const int col = min(m0 + (pos ^ mswz<BM>(k)) * 8, p.M - 8) - m0;  // ragged M: clamp
-    voa[j] = (k * p.lda + col) * 2;
+    if constexpr (AKM) {
+      // round j: rows 64 j + 8 wid + (lane >> 3), 16-B chunk (lane & 7) ^ kswz(row) of the
+      // K-tile's 128-B row segment; kswz does not see the 64 j part of the row, so every
+      // round uses round 0's lane offset and its 64 j rows go into soffset (dma_round)
+      const int row = wid * 8 + (lane >> 3);
+      voa[j] = (row * p.lda + ((lane & 7) ^ kswz(row)) * 8) * 2;
+    } else {
+      constexpr int CPR = BM / 8;
+      const int lin = j * NTHR + wid * 64 + lane;
+      const int k = lin / CPR, pos = lin - k * CPR;
+      const int col = min(m0 + (pos ^ mswz<BM>(k)) * 8, p.M - 8) - m0;  // ragged M: clamp
+      voa[j] = (k * p.lda + col) * 2;
+    }
   }
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -1840,10 +1860,11 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
     const int k = lin / CPR, pos = lin - k * CPR;
     vob[j] = (k * p.ldb + (pos ^ mswz<BN>(k)) * 8) * 2;
   }
-  const int arow = 64 * p.lda * 2, brow = 64 * p.ldb * 2;  // bytes per K-tile
+  const int arow = AKM ? 128 : 64 * p.lda * 2, brow = 64 * p.ldb * 2;  // bytes per K-tile
   auto dma_round = [&](int t, int stage, int j) {
     if (j < NA)
-      dma_lds16(ra, smem + stage * A_ST + (j * NTHR + wid * 64) * 16, voa[j], (t0 + t) * arow);
+      dma_lds16(ra, smem + stage * A_ST + (j * NTHR + wid * 64) * 16, AKM ? voa[0] : voa[j],
+                (t0 + t) * arow + (AKM ? j * 64 * p.lda * 2 : 0));
     else
       dma_lds16(rb, smem + B_BASE + stage * B_ST + ((j - NA) * NTHR + wid * 64) * 16, vob[j - NA],
                 (t0 + t) * brow);
@@ -1851,6 +1872,10 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
 
   // ---- fragment lane addresses (tr16 reads of k rows 8g+q and 8g+4+q) ----------------------
   unsigned fa[TM], fb[TN];
+  // AKM: k-sub 0 row-read lane address per fragment; k-sub 1 reads chunk c ^ 4, i.e.
+  // the address XOR 64 (the image base -- the start of the dynamic LDS -- and every row
+  // are 128-B aligned)
+  unsigned fk[AKM ? TM : 1];
   {
     const int g4 = lane >> 4, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
     const int kk = 8 * g4 + q;
@@ -1858,8 +1883,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
     const unsigned base = (unsigned)(size_t)smem;
 #pragma unroll
     for (int f = 0; f < TM; ++f) {
-      const int chunk = (wr * TM * 16 + f * 16 + 4 * pp) >> 3;
-      fa[f] = base + kk * (BM * 2) + (chunk ^ mswz<BM>(kk)) * 16 + within;
+      if constexpr (AKM) {
+        const int row = wr * TM * 16 + f * 16 + i16;
+        fk[f] = base + row * 128 + ((g4 ^ kswz(row)) << 4);
+        fa[f] = 0;
+      } else {
+        const int chunk = (wr * TM * 16 + f * 16 + 4 * pp) >> 3;
+        fa[f] = base + kk * (BM * 2) + (chunk ^ mswz<BM>(kk)) * 16 + within;
+      }
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -1907,18 +1938,27 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
       }
 #pragma unroll
       for (int i = 0; i < TMH; ++i) {
-        s16x4 lo, hi;
-        const unsigned a = fa[mh * TMH + i];
-        if (ks == 0) {
-          TN64_TR(lo, a, S * A_ST);
-          TN64_TR(hi, a, S * A_ST + 4 * BM * 2);
+        if constexpr (AKM) {
+          unsigned a = fk[mh * TMH + i];
+          if (ks == 1) {
+            asm volatile("" : "+v"(a));  // keeps the XOR here (hoisted, 8 more live VGPRs spilled)
+            a ^= 64u;
+          }
+          asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(af[i]) : "v"(a), "i"(S * A_ST) : "memory");
         } else {
-          TN64_TR(lo, a, S * A_ST + 32 * BM * 2);
-          TN64_TR(hi, a, S * A_ST + 32 * BM * 2 + 4 * BM * 2);
+          s16x4 lo, hi;
+          const unsigned a = fa[mh * TMH + i];
+          if (ks == 0) {
+            TN64_TR(lo, a, S * A_ST);
+            TN64_TR(hi, a, S * A_ST + 4 * BM * 2);
+          } else {
+            TN64_TR(lo, a, S * A_ST + 32 * BM * 2);
+            TN64_TR(hi, a, S * A_ST + 32 * BM * 2 + 4 * BM * 2);
+          }
+          typedef short s16x8 __attribute__((ext_vector_type(8)));
+          s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          af[i] = __builtin_bit_cast(bf16x8_t, v);
         }
-        typedef short s16x8 __attribute__((ext_vector_type(8)));
-        s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        af[i] = __builtin_bit_cast(bf16x8_t, v);
       }
       if (q == 3 && !lo_grp) wait_vm<0>();  // lagging row: K-tile t+1 landed
       // the asm reads are invisible to the compiler's counters: wait here, naming the
@@ -2061,7 +2101,27 @@ static hipError_t launch_tn64(const Args& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int EPI>
+static hipError_t launch_nn64(const Args& a, hipStream_t st) {
+  constexpr int BM = 256, BN = 320;
+  auto k = gemm_tn64_kernel<BM, BN, EPI, false, true>;
+  constexpr int lds = 2 * 64 * (BM + BN) * 2;
+  ensure_lds((const void*)k, lds);
+  hipLaunchKernelGGL(k, dim3(a.tiles_m * a.tiles_n), dim3(NTHR), lds, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace gemm
+
+// NN GEMM on the full-line TN schedule (algo 27): C[M][N] = A[M][K] B[K][N] (+ bias[N]),
+// A K-major, B row-major (a weight read as stored: no transpose pass); M % 256 == 0,
+// N % 320 == 0, K % 64 == 0 (validated by the binding).
+hipError_t gemm_nn64_launch(const bf16* A, const bf16* B, bf16* C, const bf16* bias, int M, int N, int K, int lda,
+                            int ldb, int ldc, hipStream_t st) {
+  gemm::Args a{A, B, C, bias, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, 1,
+               M / 256, N / 320, 0, 27, 0, 0, nullptr, nullptr, 0, 0, 0};
+  return gemm::launch_nn64<gemm::EPI_BF16>(a, st);
+}
 
 // TN weight-gradient GEMM on the full-line kernel (algo 25): c[M][N] (+)= a[K][M]^T b[K][N],
 // lockstep split over `slices` (> 1: fp32 slabs in ws, combined by a reduce launch).

@@ -313,3 +313,32 @@ def test_wgrad_tn64_strided_views_and_dispatch():
         c = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
         G.run_tn(dy, x, c, True, *plan)
         assert _rel(c, dy.float().t() @ x.float()) < 5e-3
+
+
+@pytest.mark.parametrize("M,K,N,bias", [(256, 64, 320, False), (512, 640, 320, True), (256, 4800, 1600, False),
+                                        (768, 1600, 640, True)])
+def test_gemm_nn64_vs_fp32(M, K, N, bias):
+    """NN kernel (TN schedule with a K-major A, gemm.hip algo 27): x [M, K] @ W [K, N]
+    (+ bias) with W read as stored, vs fp32; and the dgrad routing through it equals the
+    transpose + NT path within bf16 rounding."""
+    from cluster_anywhere_amd.ops import gemm as G
+
+    x, w = _mk((M, K), 31), _mk((K, N), 32) * 0.05
+    b = _mk((N,), 33) if bias else None
+    ref = x.float() @ w.float() + (b.float() if bias else 0.0)
+    y = G.linear_nn64(x, w, b)
+    assert _rel(y, ref) < 5e-3
+    # dgrad: dx = dy @ Wl for an nn.Linear weight Wl [N_out = K, K_in = N]
+    y2 = G.dgrad_w(x, w)
+    assert _rel(y2, x.float() @ w.float()) < 5e-3
+    y3 = G.dgrad(x, G.transpose(w))
+    assert _rel(y2, y3.float()) < 5e-3
+
+
+def test_gemm_nn64_rejects_bad_shapes():
+    from cluster_anywhere_amd.ops import kernels
+
+    x, w = _mk((200, 64), 1), _mk((64, 320), 2)
+    c = torch.empty(200, 320, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        kernels().gemm_nn64(x, w, c, None)  # M % 256 != 0
