@@ -594,7 +594,11 @@ void ln_bwd_launch(const bf16* dy, const bf16* x, const bf16* g, const float* me
                    bf16* db, int rows, int D, hipStream_t st, bf16* dxsum, int acc_gb) {
   if (dxsum && ln_bwd_cs_ok(D)) {
     const int nb = ln_bwd_cs_blocks(rows);
-    if (dres)
+    // variant 2: four rows per iteration (more loads in flight), variant 3 (default): two
+    if (dres && g_ln_bwd_variant == 2)
+      hipLaunchKernelGGL((ln_bwd_cs_kernel<LN_CS_RB, true, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd,
+                         dres, dx, partial, rows, D);
+    else if (dres)
       hipLaunchKernelGGL((ln_bwd_cs_kernel<2, true, true>), dim3(nb), dim3(256), 0, st, dy, x, g, mean, rstd, dres,
                          dx, partial, rows, D);
     else

@@ -47,6 +47,30 @@ def main():
                           "TB_s": round(4 * R * D * 2 / us / 1e6, 2), "dx_maxerr": err, "dgamma_relerr": gerr,
                           "dbeta_relerr": berr}),
               flush=True)
+    # the training step's form: + the column sums of dx (the residual branch's bias
+    # gradient) accumulated into a main-grad vector, dgamma / dbeta into main grads
+    dxsum = torch.zeros(D, device="cuda", dtype=torch.bfloat16)
+    gm = torch.zeros(D, device="cuda", dtype=torch.bfloat16)
+    bm = torch.zeros(D, device="cuda", dtype=torch.bfloat16)
+    for variant, blocks in ((3, 0), (2, 0), (3, 4096), (2, 4096), (3, 1024), (2, 1024), (3, 0)):
+        C.ln_bwd_config(variant, blocks)
+        dxsum.zero_()
+        dx = C.layernorm_bwd(dy, x, g, mean, rstd, dres, dxsum, gm, bm)[0]
+        err = float((dx.float() - ref_dx).abs().max())
+        serr = float((dxsum.float() - ref_dx.sum(0)).abs().max() / ref_dx.sum(0).abs().max())
+        for _ in range(3):
+            C.layernorm_bwd(dy, x, g, mean, rstd, dres, dxsum, gm, bm)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(50):
+            C.layernorm_bwd(dy, x, g, mean, rstd, dres, dxsum, gm, bm)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) / 50 * 1e3
+        print(json.dumps({"path": "dxsum", "variant": variant, "max_blocks": blocks, "us": round(us, 1),
+                          "TB_s": round(4 * R * D * 2 / us / 1e6, 2), "dx_maxerr": err, "dxsum_relerr": serr}),
+              flush=True)
     C.ln_bwd_config(3, 0)  # the library default
 
 
