@@ -35,9 +35,10 @@ def kernels():
                 "cluster_anywhere_amd HIP kernels (_C) are not built; run "
                 "`python -m cluster_anywhere_amd._build`"
             ) from e
-    v = os.environ.get("CAAMD_LN_BWD_VARIANT")  # A/B switch for the LayerNorm backward kernel
-    if v is not None and hasattr(_C, "ln_bwd_config"):
-        _C.ln_bwd_config(int(v), 0)
+    # A/B switches for the LayerNorm backward kernel: variant and grid cap (0: the default)
+    v, nb = os.environ.get("CAAMD_LN_BWD_VARIANT"), os.environ.get("CAAMD_LN_BWD_BLOCKS")
+    if (v is not None or nb is not None) and hasattr(_C, "ln_bwd_config"):
+        _C.ln_bwd_config(int(v or 3), int(nb or 0))
     return _C
 
 

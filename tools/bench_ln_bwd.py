@@ -52,7 +52,8 @@ def main():
     dxsum = torch.zeros(D, device="cuda", dtype=torch.bfloat16)
     gm = torch.zeros(D, device="cuda", dtype=torch.bfloat16)
     bm = torch.zeros(D, device="cuda", dtype=torch.bfloat16)
-    for variant, blocks in ((3, 0), (2, 0), (3, 4096), (2, 4096), (3, 1024), (2, 1024), (3, 0)):
+    caps = [int(c) for c in os.environ.get("LN_BWD_CAPS", "0,4096,1024").split(",")]
+    for variant, blocks in [(v, c) for c in caps for v in (3, 2)] + [(3, 0)]:
         C.ln_bwd_config(variant, blocks)
         dxsum.zero_()
         dx = C.layernorm_bwd(dy, x, g, mean, rstd, dres, dxsum, gm, bm)[0]
