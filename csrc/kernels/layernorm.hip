@@ -572,7 +572,11 @@ void ln_fwd_launch(const bf16* x, const bf16* r, bf16* s, const bf16* g, const b
 constexpr int LN_CS_RB = 4;
 
 int ln_bwd_cs_blocks(int rows) {
-  const int cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : 2048;
+  // 1024: every block resident at once (4 per CU at ~100 VGPRs; 2048 blocks ran 1.6
+  // rounds) and half the partial rows for colsum3: 96 vs 106-113 us standalone in the
+  // step form, step 101.1k / 101.0k vs 100.9k / 100.5k (profiles/ln_bwd_dxsum_r6.jsonl,
+  // profiles/step_ab_ln_bwd_cap_r6.txt)
+  const int cap = g_ln_bwd_blocks > 0 ? g_ln_bwd_blocks : 1024;
   const int ng = (rows + LN_CS_RB - 1) / LN_CS_RB;
   return ng < cap ? ng : cap;
 }
