@@ -8,6 +8,8 @@
 //        columns (j >= V) get 0. Rows with target < 0 (ignore_index) get 0.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace caamd {
 
 constexpr int kXentThreads = 256;
@@ -97,10 +99,12 @@ __global__ __launch_bounds__(kXentThreads) void xent_bwd_kernel(
 //   max -> sum exp -> lse -> loss[row], then dlogits = scale * (softmax - onehot)
 // in place. `scale` is a device scalar (1 / #valid targets for a mean loss), so no
 // host sync is needed to know the loss normaliser.
-constexpr int kXentFusedThreads = 1024;
-
-template <int NCH>
-__global__ __launch_bounds__(kXentFusedThreads) void xent_fused_kernel(
+// TPB threads per block: 512 (the default) lets two blocks share a CU at the GPT-2 row
+// width -- at 1024 threads and ~84 VGPRs only one 16-wave block fits, and its two
+// block-wide reductions leave the CU idle (3.7 TB/s); CAAMD_XENT_TPB=1024 is the
+// previous launch (A/B).
+template <int NCH, int kXentFusedThreads>
+__device__ __forceinline__ void xent_fused_body(
     bf16* __restrict__ logits, const int64_t* __restrict__ target, float* __restrict__ loss,
     float* __restrict__ lse_out, const float* __restrict__ scale, int V, int stride) {
   __shared__ float red[kXentFusedThreads / 64];
@@ -188,19 +192,41 @@ __global__ __launch_bounds__(kXentFusedThreads) void xent_fused_kernel(
   }
 }
 
+template <int NCH>
+__global__ __launch_bounds__(1024) void xent_fused_kernel(bf16* __restrict__ logits, const int64_t* __restrict__ target,
+                                                          float* __restrict__ loss, float* __restrict__ lse_out,
+                                                          const float* __restrict__ scale, int V, int stride) {
+  xent_fused_body<NCH, 1024>(logits, target, loss, lse_out, scale, V, stride);
+}
+// 512 threads, at most 128 VGPRs (4 waves per SIMD): two blocks per CU
+template <int NCH>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void xent_fused512_kernel(
+    bf16* __restrict__ logits, const int64_t* __restrict__ target, float* __restrict__ loss,
+    float* __restrict__ lse_out, const float* __restrict__ scale, int V, int stride) {
+  xent_fused_body<NCH, 512>(logits, target, loss, lse_out, scale, V, stride);
+}
+
 bool xent_fused_launch(bf16* logits, const int64_t* target, float* loss, float* lse, const float* scale,
                        int rows, int V, int stride, hipStream_t st) {
   const int nvec = stride >> 3;
-  const int nch = (nvec + kXentFusedThreads - 1) / kXentFusedThreads;
-#define XENT_FUSED(N)                                                                                 \
-  hipLaunchKernelGGL(xent_fused_kernel<N>, dim3(rows), dim3(kXentFusedThreads), 0, st, logits, target, \
-                     loss, lse, scale, V, stride)
-  if (nch <= 1) XENT_FUSED(1);
-  else if (nch <= 2) XENT_FUSED(2);
-  else if (nch <= 4) XENT_FUSED(4);
-  else if (nch <= 7) XENT_FUSED(7);
-  else if (nch <= 8) XENT_FUSED(8);
-  else if (nch <= 16) XENT_FUSED(16);
+  static const int tpb_env = [] {
+    const char* e = std::getenv("CAAMD_XENT_TPB");
+    return e ? std::atoi(e) : 512;
+  }();
+  if (tpb_env == 512 && nvec > 4 * 1024 && nvec <= 13 * 512) {  // wide rows: 512-thread blocks
+    hipLaunchKernelGGL(xent_fused512_kernel<13>, dim3(rows), dim3(512), 0, st, logits, target, loss, lse, scale, V,
+                       stride);
+    return true;
+  }
+#define XENT_FUSED(N, T)                                                                                    \
+  hipLaunchKernelGGL(xent_fused_kernel<N>, dim3(rows), dim3(T), 0, st, logits, target, loss, lse, scale, V, stride)
+  const int nch = (nvec + 1023) / 1024;
+  if (nch <= 1) XENT_FUSED(1, 1024);
+  else if (nch <= 2) XENT_FUSED(2, 1024);
+  else if (nch <= 4) XENT_FUSED(4, 1024);
+  else if (nch <= 7) XENT_FUSED(7, 1024);
+  else if (nch <= 8) XENT_FUSED(8, 1024);
+  else if (nch <= 16) XENT_FUSED(16, 1024);
   else return false;
 #undef XENT_FUSED
   return true;
