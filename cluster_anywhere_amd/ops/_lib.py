@@ -39,6 +39,9 @@ def kernels():
     v, nb = os.environ.get("CAAMD_LN_BWD_VARIANT"), os.environ.get("CAAMD_LN_BWD_BLOCKS")
     if (v is not None or nb is not None) and hasattr(_C, "ln_bwd_config"):
         _C.ln_bwd_config(int(v or 3), int(nb or 0))
+    gm = os.environ.get("CAAMD_GEMM_GROUP_M")  # A/B switch: m-tiles per tile-order group of the k64 GEMM
+    if gm is not None and hasattr(_C, "gemm_set_group_m"):
+        _C.gemm_set_group_m(int(gm))
     return _C
 
 
