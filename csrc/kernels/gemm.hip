@@ -2138,7 +2138,10 @@ hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* 
 }
 
 // Host entry: shapes are validated by the caller (bindings.cpp).
-static int g_group_m = 0;  // 0: the kernels' default tile-order group (8 m-tiles)
+// 0: the default tile-order group -- 4 m-tiles at M >= 16384 (the training step's 32768
+// rows: 101.4-102.0k vs 101.1k tok/s at 8, 100.7-101.3k at 2, 100.0-100.3k at 16 on one
+// box, profiles/step_ab_group_m_r6.txt), 8 below (the serving prefill chunks, as tuned)
+static int g_group_m = 0;
 void gemm_set_group_m(int g) { g_group_m = g; }
 static int g_tail_first = 0;  // algo 9 split tails dispatched first (see Args::tail_first)
 void gemm_set_tail_first(int v) { g_tail_first = v; }
@@ -2149,7 +2152,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int tfull, int tS, float* tws, int* tcnt, int bpack) {
   gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk,
                (algo == 5 || algo == 15) ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt,
-               bpack, g_group_m, g_tail_first};
+               bpack, g_group_m > 0 ? g_group_m : (M >= 16384 ? 4 : 8), g_tail_first};
   if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
   if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);
   if (bm == 128 && bn == 320) return gemm::launch_epi<128, 320>(layout, epi, a, st);
