@@ -42,6 +42,9 @@ def kernels():
     gm = os.environ.get("CAAMD_GEMM_GROUP_M")  # A/B switch: m-tiles per tile-order group of the k64 GEMM
     if gm is not None and hasattr(_C, "gemm_set_group_m"):
         _C.gemm_set_group_m(int(gm))
+    tg = os.environ.get("CAAMD_TN_GROUP_M")  # the same for the TN weight-gradient kernel
+    if tg is not None and hasattr(_C, "gemm_set_tn_group_m"):
+        _C.gemm_set_tn_group_m(int(tg))
     return _C
 
 

@@ -52,6 +52,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
 void gemm_tail_plan(int tiles, int K, int ks, int slots, int max_split, int* full, int* S);
 void gemm_set_tail_first(int v);
 void gemm_set_group_m(int g);
+void gemm_set_tn_group_m(int g);
 hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
                             int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st, int* tickets);
 hipError_t gemm_nn64_launch(const bf16* A, const bf16* B, bf16* C, const bf16* bias, int M, int N, int K, int lda,
@@ -1393,6 +1394,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_nn64", GUARDED(gemm_nn64), pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c"),
         pybind11::arg("bias") = pybind11::none());
   m.def("gemm_set_tail_first", [](int64_t v) { caamd::gemm_set_tail_first((int)v); });
+  m.def("gemm_set_tn_group_m", [](int64_t g) {  // m-tiles per tile-order group of the TN wgrad kernel (0: 8)
+    TORCH_CHECK(g >= 0 && g <= 64, "gemm_set_tn_group_m: 0..64");
+    caamd::gemm_set_tn_group_m((int)g);
+  });
   m.def("gemm_set_group_m", [](int64_t g) {  // m-tiles per tile-order group of the k64 kernel (0: 8)
     TORCH_CHECK(g >= 0 && g <= 64, "gemm_set_group_m: 0..64");
     caamd::gemm_set_group_m((int)g);

@@ -1242,7 +1242,9 @@ __global__ __launch_bounds__(256) void sk_reduce_kernel(Args p, int LS) {
   q /= TN;
   const int i = q % TM, wid = q / TM;
   const int wr = wid >> 2, wc = wid & 3;
-  constexpr int GROUP_M = 8;  // tile -> (m0, n0) exactly as gemm_sk_kernel
+  // tile -> (m0, n0) exactly as the producing kernel: gemm_sk_kernel (8; its launches
+  // pass group_m 0) or gemm_tn64_kernel (p.group_m, gemm_set_tn_group_m)
+  const int GROUP_M = p.group_m > 0 ? p.group_m : 8;
   const int group_sz = GROUP_M * p.tiles_n;
   const int gq = tile / group_sz;
   const int first_m = gq * GROUP_M;
@@ -1823,7 +1825,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_tn64_kernel(Args p) {
   const int nkt = p.K / 64;
   const int t0 = (int)((long long)sl * nkt / LS);
   const int nk = (int)((long long)(sl + 1) * nkt / LS) - t0;
-  constexpr int GROUP_M = 8;  // tile order as gemm_sk_kernel / sk_reduce_kernel
+  const int GROUP_M = p.group_m > 0 ? p.group_m : 8;  // tile order as sk_reduce_kernel
   const int group_sz = GROUP_M * p.tiles_n;
   const int gq = tile / group_sz;
   const int first_m = gq * GROUP_M;
@@ -2123,13 +2125,16 @@ hipError_t gemm_nn64_launch(const bf16* A, const bf16* B, bf16* C, const bf16* b
   return gemm::launch_nn64<gemm::EPI_BF16>(a, st);
 }
 
+static int g_tn_group_m = 0;  // m-tiles per tile-order group of the TN kernel (0: 8)
+void gemm_set_tn_group_m(int g) { g_tn_group_m = g; }
+
 // TN weight-gradient GEMM on the full-line kernel (algo 25): c[M][N] (+)= a[K][M]^T b[K][N],
 // lockstep split over `slices` (> 1: fp32 slabs in ws, combined by a reduce launch).
 hipError_t gemm_tn64_launch(int bm, bool accumulate, const bf16* A, const bf16* B, bf16* C, int M, int N, int K,
                             int lda, int ldb, int ldc, int slices, float* ws, hipStream_t st, int* tickets) {
   // tickets != null: the last arriving slice of each tile combines (algo 26), else a reduce launch (25)
   gemm::Args a{A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, lda, ldb, ldc, 1,
-               (M + bm - 1) / bm, N / 320, 0, tickets ? 26 : 25, slices, 0, ws, tickets, 0, 0, 0};
+               (M + bm - 1) / bm, N / 320, 0, tickets ? 26 : 25, slices, 0, ws, tickets, 0, g_tn_group_m, 0};
   if (bm == 256) return accumulate ? gemm::launch_tn64<256, gemm::EPI_BF16_ACC>(a, st)
                                    : gemm::launch_tn64<256, gemm::EPI_BF16>(a, st);
   if (bm == 192) return accumulate ? gemm::launch_tn64<192, gemm::EPI_BF16_ACC>(a, st)
@@ -2152,7 +2157,7 @@ hipError_t gemm_launch(int layout, int epi, int bm, int bn, const bf16* A, const
                        int tfull, int tS, float* tws, int* tcnt, int bpack) {
   gemm::Args a{A, B, C, bias, Z, Zout, dbias, M, N, K, lda, ldb, ldc, splitk,
                (algo == 5 || algo == 15) ? (M + bm - 1) / bm : M / bm, N / bn, (long long)M * ldc, algo, tfull, tS, tws, tcnt,
-               bpack, g_group_m > 0 ? g_group_m : (M >= 16384 ? 4 : 8), g_tail_first};
+               bpack, algo % 10 != 9 ? 0 : (g_group_m > 0 ? g_group_m : (M >= 16384 ? 4 : 8)), g_tail_first};
   if (bm == 256 && bn == 256) return gemm::launch_epi<256, 256>(layout, epi, a, st);
   if (bm == 256 && bn == 320) return gemm::launch_epi<256, 320>(layout, epi, a, st);
   if (bm == 128 && bn == 320) return gemm::launch_epi<128, 320>(layout, epi, a, st);
