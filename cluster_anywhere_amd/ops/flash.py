@@ -29,13 +29,21 @@ class _FlashQKV(torch.autograd.Function):
             return kernels().flash_attn_bwd(qkv, out, dout.contiguous(), lse, ctx.n_head, ctx.causal), None, None, None
         # the qkv projection's bias gradient = column sums of dqkv, taken from the
         # backward kernels' registers (fp32 atomics) instead of a re-read of dqkv
-        db = torch.zeros(qkv.shape[-1], device=qkv.device, dtype=torch.float32)
-        dqkv = kernels().flash_attn_bwd(qkv, out, dout.contiguous(), lse, ctx.n_head, ctx.causal, db)
-        mg = getattr(b, "main_grad", None)
-        if mg is not None:
-            from .linear import _ready
+        from .linear import _dbias_acc, _ready
 
-            mg.add_(db)
+        mg = getattr(b, "main_grad", None)
+        # bf16 main gradient: accumulate into the persistent zeroed fp32 vector that
+        # drain_f32_ empties (one launch) instead of zeros() + add_ (two)
+        drain = (mg is not None and mg.dtype == torch.bfloat16 and mg.is_contiguous()
+                 and mg.device == qkv.device)
+        db = (_dbias_acc(qkv.device, qkv.shape[-1]) if drain
+              else torch.zeros(qkv.shape[-1], device=qkv.device, dtype=torch.float32))
+        dqkv = kernels().flash_attn_bwd(qkv, out, dout.contiguous(), lse, ctx.n_head, ctx.causal, db)
+        if mg is not None:
+            if drain:
+                kernels().drain_f32_(db, mg)
+            else:
+                mg.add_(db)
             _ready(b)
             return dqkv, None, None, None
         return dqkv, None, None, (db.to(b.dtype) if ctx.needs_input_grad[3] else None)

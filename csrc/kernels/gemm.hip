@@ -259,20 +259,28 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
   // (dGELU only: for the accumulate epilogue the extra live registers pushed the
   // stream-K weight-gradient kernel's main loop into scratch spills -- 3x slower)
   constexpr bool PRE = EPI == EPI_DGELU;
-  bf16x8_t pre[PRE ? RITERS : 1];
+  // dGELU: the second half's Z loads are issued right after the first half is staged
+  // (its accumulators are dead by then), so their latency overlaps the first half's
+  // row loop instead of sitting between the two halves: fc-shape dGELU 660-663 ->
+  // 649-651 us, bitwise equal (profiles/gemm_epi_ab_r6.jsonl)
+  constexpr bool PRE2 = PRE;
+  bf16x8_t pre[PRE2 ? 2 : 1][PRE ? RITERS : 1];
+  auto zload = [&](int hh, int slot) {
+    if (tid < ACTIVE && !(ABL & 8)) {
+      const bf16* src = p.Z;
+#pragma unroll
+      for (int it = 0; it < RITERS; ++it) {
+        const int ir = it * RG + rg;
+        const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
+        const int m = m0 + wr_ * (TM * 16) + hh * (TMH * 16) + rem;
+        if (ir < HR && m < p.M) pre[slot][it] = *reinterpret_cast<const bf16x8_t*>(src + (size_t)m * p.ldc + n);
+      }
+    }
+  };
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     if constexpr (PRE) {
-      if (tid < ACTIVE && !(ABL & 8)) {
-        const bf16* src = p.Z;
-#pragma unroll
-        for (int it = 0; it < RITERS; ++it) {
-          const int ir = it * RG + rg;
-          const int wr_ = ir / (TMH * 16), rem = ir - wr_ * (TMH * 16);
-          const int m = m0 + wr_ * (TM * 16) + h * (TMH * 16) + rem;
-          if (ir < HR && m < p.M) pre[it] = *reinterpret_cast<const bf16x8_t*>(src + (size_t)m * p.ldc + n);
-        }
-      }
+      if (!PRE2 || h == 0) zload(h, 0);
     }
 #if CAAMD_EPI_SYNC
     __syncthreads();
@@ -296,6 +304,9 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
 #else
     lds_barrier();  // image written
 #endif
+    if constexpr (PRE2) {
+      if (h == 0) zload(1, 1);
+    }
     if constexpr (ABL & 8) continue;
     if (tid >= ACTIVE) continue;
     if constexpr (EPI == EPI_SWIGLU) {
@@ -351,7 +362,7 @@ __device__ __forceinline__ void epilogue_staged(const Args& p, f32x4 (&acc)[TM][
         }
         *reinterpret_cast<bf16x8_t*>(p.Zout + off) = z;
       } else if constexpr (EPI == EPI_DGELU) {
-        const bf16x8_t z = pre[it];
+        const bf16x8_t z = pre[PRE2 ? h : 0][it];
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
           o[r] = (bf16)(f[r] * gelu_tanh_grad((float)z[r]));
@@ -1606,6 +1617,10 @@ static hipError_t launch_k64(const Args& a, hipStream_t st) {
       default: break;
     }
 #undef K64_ABL
+  }
+  if constexpr (BM == 256 && BN == 320 && (EPI == EPI_BIAS_GELU || EPI == EPI_DGELU)) {
+    // epilogue ablation (full-line variant 4 only): 8 = no epilogue (tools/gemm_epi_ab.py)
+    if (v == 4 && abl == 8) return launch_k64_v<BM, BN, EPI, 8, 1, 2>(a, st);
   }
   return hipErrorInvalidValue;
 }
