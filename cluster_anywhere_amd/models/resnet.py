@@ -176,6 +176,19 @@ class _FConv:
         # own-kernel form: [Cout, Kp] (k = (kh*KS + kw)*Cin + ci), Cin padded for the stem
         self.w2d = conv_weight_nhwc(self.w.float(), cin_pad).to(dtype) if own else None
 
+    @classmethod
+    def folded(cls, w, b, stride, relu, own=False, cin_pad=0):
+        """From an already folded weight ``w`` [Cout, Cin, K, K] (model dtype) and bias:
+        the same tensors as ``__init__`` (the own-kernel form is built from the model-dtype
+        weight directly, which equals the fp32 round trip bit for bit)."""
+        self = cls.__new__(cls)
+        self.w = w.contiguous(memory_format=torch.channels_last)
+        self.b = b
+        k = w.shape[-1]
+        self.stride, self.pad, self.relu, self.ks = (stride, stride), (k // 2, k // 2), relu, k
+        self.w2d = conv_weight_nhwc(w, cin_pad) if own else None
+        return self
+
     def __call__(self, x, residual=None):
         # bias-free MIOpen conv + ONE fused epilogue kernel (bias, residual, ReLU)
         y = F.conv2d(x, self.w, None, self.stride, self.pad)
@@ -190,7 +203,7 @@ class _FConv:
 class FusedResNet(nn.Module):
     """BN-folded bf16 channels_last inference form of a :class:`ResNet`."""
 
-    def __init__(self, net: ResNet, dtype, device, own_conv: Optional[bool] = None):
+    def __init__(self, net: Optional[ResNet], dtype, device, own_conv: Optional[bool] = None, _parts=None):
         super().__init__()
         device = device or next(net.parameters()).device
         self.dtype, self.device = dtype, torch.device(device)
@@ -202,22 +215,25 @@ class FusedResNet(nn.Module):
 
             kernels()  # fail loudly if the HIP extension is missing
         o = self.own
-        self.stem = _FConv(net.conv1, net.bn1, True, dtype, device, own=o, cin_pad=8)
+        if _parts is not None:  # FusedResNet.random: folded parts, no nn.Module in between
+            self.stem, self.blocks, self.fc_w, self.fc_b = _parts(o)
+        else:
+            self.stem = _FConv(net.conv1, net.bn1, True, dtype, device, own=o, cin_pad=8)
+            self.blocks: List[tuple] = []
+            for b in net.blocks:
+                convs = [_FConv(c, bn, r, dtype, device, own=o) for c, bn, r in b.convs()]
+                down = _FConv(b.down[0], b.down[1], False, dtype, device, own=o) if b.down is not None else None
+                self.blocks.append((convs, down))
+            self.fc_w = net.fc.weight.detach().to(device=device, dtype=dtype)
+            self.fc_b = net.fc.bias.detach().to(device=device, dtype=dtype)
         # pixel-pair stem (conv.hip normalize_pairs_kernel): the 7x7 / 3-channel stem as a
         # 7x4-tap convolution over two-pixel virtual pixels, K = 224 instead of 416
         self.stem_pair = None
-        if o and PAIR_STEM and net.conv1.kernel_size == (7, 7) and net.conv1.in_channels == 3 \
-                and net.conv1.stride == (2, 2) and net.conv1.padding == (3, 3):
+        if o and PAIR_STEM and self.stem.w.shape[1:] == (3, 7, 7) and self.stem.stride == (2, 2) \
+                and self.stem.pad == (3, 3):
             from ..ops.vision import conv_weight_pairs
 
             self.stem_pair = conv_weight_pairs(self.stem.w.float()).to(dtype)
-        self.blocks: List[tuple] = []
-        for b in net.blocks:
-            convs = [_FConv(c, bn, r, dtype, device, own=o) for c, bn, r in b.convs()]
-            down = _FConv(b.down[0], b.down[1], False, dtype, device, own=o) if b.down is not None else None
-            self.blocks.append((convs, down))
-        self.fc_w = net.fc.weight.detach().to(device=device, dtype=dtype)
-        self.fc_b = net.fc.bias.detach().to(device=device, dtype=dtype)
         self.num_classes = self.fc_w.shape[0]
         # classifier on the framework's MFMA GEMM (ops/gemm.py, 256 x 256 tiles) at
         # batch sizes that are a multiple of 256: the weight is padded to a multiple of
@@ -234,6 +250,63 @@ class FusedResNet(nn.Module):
                 bp = torch.full((n_pad,), float("-inf"), device=device, dtype=dtype)
                 bp[: self.num_classes] = self.fc_b
                 self.fc_wp, self.fc_bp = wp, bp
+
+    @classmethod
+    @torch.no_grad()
+    def random(cls, name: str = "resnet50", dtype=torch.bfloat16, device=None, num_classes: int = 1000,
+               own_conv: Optional[bool] = None) -> "FusedResNet":
+        """The fused form of a freshly initialised :func:`resnet` (kaiming-normal fan-out
+        convolutions, identity BatchNorm folded in, nn.Linear's default uniform
+        classifier) drawn directly: every conv weight is a view of ONE normal draw,
+        scaled per layer (the BN fold's 1/sqrt(1 + eps) included) by one multi-tensor
+        multiply and rounded to the model dtype in one pass; biases are zeros. The
+        module route (``resnet(name)`` + ``fuse_for_inference``) costs ~300 init and
+        ~580 fold launches, 0.19-0.24 s of a fresh GPU actor's start-up
+        (PERF.md "Data start-up"). Same distributions, a different random stream."""
+        import math
+
+        device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        block, counts = _CFG[name]
+        # (cout, cin, k, stride, relu) in a fixed order: stem, then per block its convs
+        # and its projection shortcut
+        specs = [(64, 3, 7, 2, True)]
+        layout, cin = [], 64
+        for i, (n, wd) in enumerate(zip(counts, (64, 128, 256, 512))):
+            for j in range(n):
+                stride = 2 if (j == 0 and i > 0) else 1
+                cout = wd * block.expansion
+                if block is Bottleneck:
+                    cs = [(wd, cin, 1, 1, True), (wd, wd, 3, stride, True), (cout, wd, 1, 1, False)]
+                else:
+                    cs = [(wd, cin, 3, stride, True), (cout, wd, 3, 1, False)]
+                down = (cout, cin, 1, stride, False) if (stride != 1 or cin != cout) else None
+                layout.append((len(specs), len(cs), down is not None))
+                specs += cs + ([down] if down else [])
+                cin = cout
+        eps = 1e-5  # nn.BatchNorm2d's default; identity statistics fold to 1/sqrt(1 + eps)
+        sizes = [co * ci * k * k for co, ci, k, _, _ in specs]
+        flat = torch.randn(sum(sizes), device=device)
+        views = list(torch.split(flat, sizes))
+        torch._foreach_mul_(views, [math.sqrt(2.0 / (co * k * k)) / math.sqrt(1.0 + eps)
+                                    for co, _, k, _, _ in specs])
+        flat_t = flat.to(dtype)
+        ws = [v.view(co, ci, k, k) for v, (co, ci, k, _, _) in zip(torch.split(flat_t, sizes), specs)]
+        zeros = torch.zeros(max(co for co, *_ in specs), device=device, dtype=dtype)
+        bound = 1.0 / math.sqrt(cin)
+        u = torch.rand(num_classes * cin + num_classes, device=device).mul_(2 * bound).sub_(bound).to(dtype)
+        fc_w, fc_b = u[: num_classes * cin].view(num_classes, cin), u[num_classes * cin:]
+
+        def parts(own):
+            def fc(i, cin_pad=0):
+                co, _, _, stride, relu = specs[i]
+                return _FConv.folded(ws[i], zeros[:co], stride, relu, own=own, cin_pad=cin_pad)
+
+            blocks = []
+            for first, nc, has_down in layout:
+                blocks.append(([fc(first + t) for t in range(nc)], fc(first + nc) if has_down else None))
+            return fc(0, cin_pad=8), blocks, fc_w, fc_b
+
+        return cls(None, dtype, device, own_conv, _parts=parts)
 
     @torch.no_grad()
     def forward(self, x):
@@ -327,13 +400,18 @@ class ResNetPredictor:
         if self._pin_at_init:
             self._start_pinning()
         t1 = time.perf_counter()
-        if dev.type == "cuda":
-            with torch.device(dev):  # random init straight in HBM
-                net = resnet(name).eval()
+        if dev.type == "cuda" and os.environ.get("CAAMD_PREDICTOR_MODULE_INIT", "0") != "1":
+            # the fused weights drawn directly in HBM (FusedResNet.random)
+            t2 = t1
+            self.model = FusedResNet.random(name, torch.bfloat16, dev)
         else:
-            net = resnet(name).eval()
-        t2 = time.perf_counter()
-        self.model = net.fuse_for_inference(torch.bfloat16 if dev.type == "cuda" else torch.float32, dev)
+            if dev.type == "cuda":
+                with torch.device(dev):  # random init straight in HBM
+                    net = resnet(name).eval()
+            else:
+                net = resnet(name).eval()
+            t2 = time.perf_counter()
+            self.model = net.fuse_for_inference(torch.bfloat16 if dev.type == "cuda" else torch.float32, dev)
         self.graph = None
         self._pending_capture = self._ran_eager = self._early_pin = False
         self.init_profile.update(cuda_init_s=t1 - t0, model_init_s=t2 - t1, fuse_s=time.perf_counter() - t2)

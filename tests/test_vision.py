@@ -35,6 +35,36 @@ def test_bn_folding_matches_reference():
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("name", ["resnet18", "resnet50"])
+def test_fused_random_matches_module_route(name):
+    """FusedResNet.random (the GPU predictor's start-up path) builds the same fused
+    network as resnet(name) + fuse_for_inference: conv shapes, strides, paddings,
+    ReLU flags, shortcut placement, classifier shape, and weight scales of the same
+    kaiming-normal init (the random streams differ)."""
+    from cluster_anywhere_amd.models.resnet import FusedResNet
+
+    torch.manual_seed(0)
+    fr = FusedResNet.random(name, torch.float32, "cpu")
+    ref = resnet(name).eval().fuse_for_inference(torch.float32, "cpu")
+
+    def convs(f):
+        out = [f.stem]
+        for cs, down in f.blocks:
+            out += cs + ([down] if down is not None else [])
+        return out
+
+    a, b = convs(fr), convs(ref)
+    assert len(a) == len(b) and [d is None for _, d in fr.blocks] == [d is None for _, d in ref.blocks]
+    for x, y in zip(a, b):
+        assert (x.w.shape, x.b.shape, x.stride, x.pad, x.relu, x.ks) == (y.w.shape, y.b.shape, y.stride, y.pad, y.relu, y.ks)
+        assert 0.85 < (x.w.float().std() / y.w.float().std()).item() < 1.15
+        assert torch.count_nonzero(x.b) == 0
+    assert fr.fc_w.shape == ref.fc_w.shape and fr.fc_b.shape == ref.fc_b.shape
+    assert fr.fc_w.abs().max() <= 1.0 / fr.fc_w.shape[1] ** 0.5 + 1e-6
+    x = torch.randint(0, 256, (2, 64, 64, 3), dtype=torch.uint8)
+    assert fr.predict_uint8(x).shape == (2, 1000)
+
+
 def test_predictor_cpu_batches():
     p = ResNetPredictor("resnet18", batch_size=4, hw=32, device="cpu")
     imgs = np.random.randint(0, 256, (10, 32, 32, 3), dtype=np.uint8)
