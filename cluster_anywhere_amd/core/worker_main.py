@@ -58,8 +58,15 @@ def _prewarm_hip():
     it), then ``torch.cuda.init()`` finishes the torch side. Only when torch is already
     in the process (forked from the zygote, so importing it costs nothing) and a device
     is visible (counting devices does not initialise HIP); torch's lazy-init lock makes
-    the user's own calls wait for it. CAAMD_WORKER_HIP_PREWARM=0 turns it off."""
+    the user's own calls wait for it. Only for workers isolated to their GPUs
+    (ROCR_VISIBLE_DEVICES set by the head, so device 0 is the leased one); Train
+    worker groups see the whole node and are left alone. CAAMD_WORKER_HIP_PREWARM=0
+    turns it off."""
     if os.environ.get("CAAMD_WORKER_HIP_PREWARM", "1") == "0" or not os.environ.get("CAAMD_GPU_IDS"):
+        return
+    if os.environ.get("CAAMD_NOSET_ROCR_VISIBLE_DEVICES") or not os.environ.get("ROCR_VISIBLE_DEVICES"):
+        # every GPU of the node visible (Train worker groups, for RCCL P2P): device 0 is
+        # not this worker's device, and a context there would be one per worker
         return
     torch = sys.modules.get("torch")
     if torch is None:

@@ -26,6 +26,13 @@ def test_prewarm_skips_without_lease_or_device(monkeypatch):
     monkeypatch.setenv("CAAMD_WORKER_HIP_PREWARM", "0")
     wm._prewarm_hip()  # opted out
     monkeypatch.setenv("CAAMD_WORKER_HIP_PREWARM", "1")
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    wm._prewarm_hip()  # leased, but every GPU visible (no isolation)
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0")
+    monkeypatch.setenv("CAAMD_NOSET_ROCR_VISIBLE_DEVICES", "1")
+    wm._prewarm_hip()  # Train worker group (NOSET)
+    monkeypatch.delenv("CAAMD_NOSET_ROCR_VISIBLE_DEVICES")
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
-    wm._prewarm_hip()  # leased, but no device visible
+    wm._prewarm_hip()  # isolated, but no device visible
     assert len(_prewarm_threads()) == before
