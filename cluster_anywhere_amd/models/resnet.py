@@ -233,7 +233,8 @@ class FusedResNet(nn.Module):
                 and self.stem.pad == (3, 3):
             from ..ops.vision import conv_weight_pairs
 
-            self.stem_pair = conv_weight_pairs(self.stem.w.float()).to(dtype)
+            # bf16 in, bf16 out: the same values as the fp32 round trip, no cast kernels
+            self.stem_pair = conv_weight_pairs(self.stem.w).to(dtype)
         self.num_classes = self.fc_w.shape[0]
         # classifier on the framework's MFMA GEMM (ops/gemm.py, 256 x 256 tiles) at
         # batch sizes that are a multiple of 256: the weight is padded to a multiple of
