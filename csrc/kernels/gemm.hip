@@ -1735,30 +1735,42 @@ static hipError_t launch_epi(int layout, int epi, const Args& a, hipStream_t st)
 
 // ---- bf16 transpose (W -> W^T for the dgrad GEMM's K-major B operand) ---------------
 // 64 x 64 tiles through LDS: coalesced 16-byte loads of input rows, 16-byte stores of
-// output rows (each thread gathers 8 input rows of one column from LDS).
+// output rows. LDS in dwords (bf16 pairs): each thread writes its 8 input elements as
+// 4 dwords and gathers, for one PAIR of input columns, 8 rows as 8 dwords (row stride 33
+// dwords: the 64 lanes of a gather hit 64 distinct banks), then splits low / high
+// halves into two output rows -- half the LDS instructions of a bf16-granular tile.
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const bf16* __restrict__ in,
                                                              bf16* __restrict__ out, int R, int C) {
-  __shared__ bf16 tile[64][66];
+  __shared__ unsigned tile[64][33];
   const int tiles_c = C / 64;
   const int tr = blockIdx.x / tiles_c, tc = blockIdx.x % tiles_c;
   const int t = threadIdx.x;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int r = h * 32 + (t >> 3), c = (t & 7) * 8;
-    bf16x8_t v = *reinterpret_cast<const bf16x8_t*>(in + (size_t)(tr * 64 + r) * C + tc * 64 + c);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) tile[r][c + j] = v[j];
+    const uint4 v = *reinterpret_cast<const uint4*>(in + (size_t)(tr * 64 + r) * C + tc * 64 + c);
+    tile[r][c / 2 + 0] = v.x;
+    tile[r][c / 2 + 1] = v.y;
+    tile[r][c / 2 + 2] = v.z;
+    tile[r][c / 2 + 3] = v.w;
   }
   __syncthreads();
+  const int cp = t >> 3;        // input column pair -> output rows 2 cp, 2 cp + 1
+  const int orr = (t & 7) * 8;  // output column chunk = input rows orr .. orr + 7
+  unsigned w[8];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int oc = h * 32 + (t >> 3);  // output row = input column
-    const int orr = (t & 7) * 8;       // output column chunk = input rows
-    bf16x8_t v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = tile[orr + j][oc];
-    *reinterpret_cast<bf16x8_t*>(out + (size_t)(tc * 64 + oc) * R + tr * 64 + orr) = v;
-  }
+  for (int j = 0; j < 8; ++j) w[j] = tile[orr + j][cp];
+  uint4 lo, hi;  // output row 2 cp: the low halves; row 2 cp + 1: the high halves
+  lo.x = __builtin_amdgcn_perm(w[1], w[0], 0x05040100u);
+  lo.y = __builtin_amdgcn_perm(w[3], w[2], 0x05040100u);
+  lo.z = __builtin_amdgcn_perm(w[5], w[4], 0x05040100u);
+  lo.w = __builtin_amdgcn_perm(w[7], w[6], 0x05040100u);
+  hi.x = __builtin_amdgcn_perm(w[1], w[0], 0x07060302u);
+  hi.y = __builtin_amdgcn_perm(w[3], w[2], 0x07060302u);
+  hi.z = __builtin_amdgcn_perm(w[5], w[4], 0x07060302u);
+  hi.w = __builtin_amdgcn_perm(w[7], w[6], 0x07060302u);
+  *reinterpret_cast<uint4*>(out + (size_t)(tc * 64 + 2 * cp) * R + tr * 64 + orr) = lo;
+  *reinterpret_cast<uint4*>(out + (size_t)(tc * 64 + 2 * cp + 1) * R + tr * 64 + orr) = hi;
 }
 
 // ================================================================================
