@@ -568,16 +568,19 @@ static void launch_cfg(const dg::Args& a, dim3 grid, hipStream_t st) {
   hipLaunchKernelGGL((dg::decode_gemm_kernel<EPI, PK, NWS, NXS>), grid, dim3(dg::WG), lds, st, a);
 }
 
-// ring depths (W images, X images): CAAMD_DG_RING = 0 -> (6, 3), 1 -> (8, 2), 2 -> (4, 4)
+// ring depths (W images, X images): (4, 4) by default -- three K-steps of each stream
+// in flight -- or CAAMD_DG_RING = 0 -> (6, 3), 1 -> (8, 2). Serving bench, alternating
+// on two boxes: steady TPOT 6.28-6.32 vs 6.42-6.44 ms and 6.38-6.43 vs 6.41-6.43 ms for
+// (4, 4) vs (6, 3); (5, 5) and (6, 4) 6.46-6.51, (4, 6) level (profiles/decode_ring_ab_r6.txt)
 template <int EPI, bool PK>
 static void launch_one(const dg::Args& a, dim3 grid, hipStream_t st) {
   static const int ring = [] {
     const char* e = getenv("CAAMD_DG_RING");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   if (ring == 1) launch_cfg<EPI, PK, 8, 2>(a, grid, st);
-  else if (ring == 2) launch_cfg<EPI, PK, 4, 4>(a, grid, st);
-  else launch_cfg<EPI, PK, 6, 3>(a, grid, st);
+  else if (ring == 0) launch_cfg<EPI, PK, 6, 3>(a, grid, st);
+  else launch_cfg<EPI, PK, 4, 4>(a, grid, st);
 }
 
 static int g_dg_ext = [] {
